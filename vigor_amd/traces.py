@@ -1,0 +1,173 @@
+"""Synthetic packet traces shaped like the reference benchmark (host side).
+
+Workload definition follows SURVEY.md §8(d), derived from the reference's
+MoonGen script (bench/bench.lua:45-71 packetConfigs/packetInit, 108-138
+throughput task) and run-benchmark.sh:47 (60 B frames + 4 B FCS):
+
+* 60 B UDP frame in a 64 B slot; eth dst 00:..:00, src FF:..:FF, type 0x0800;
+  IPv4 ihl 5, total_length 46, ttl 64, proto 17, valid header checksum;
+  UDP dst_port 0, length 26, checksum 0 (bench.lua:128 offloads only the IP
+  checksum); 18 zero payload bytes.
+* L4 flows (vignat): flow i has src_ip 10.0.0.0 + (i >> 16), src_port
+  i & 0xFFFF (bench.lua:54 generalised past 65,536 flows), dst 0.0.0.0:0.
+* L3 flows (viglb): src_ip 11.0.0.0 + i (bench.lua:51).
+* L2 (vigbridge): station k = 02:00:00:kk:kk:kk.
+* Packet p belongs to flow p mod N (round robin, bench.lua:125) or to
+  splitmix64(0x5EED, p) mod N (uniform).
+* now_p = 1e9 + p nanoseconds.
+
+Everything is vectorised numpy; arrays are frames[n*slot] u8, len[n] u16,
+in_dev[n] u16, now[n] i64.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+ETH_IPV4 = b"\x08\x00"
+NOW0 = 1_000_000_000
+
+
+def ip4(a: int, b: int, c: int, d: int) -> int:
+    """Address as the host-order integer nf_parse_ipv4addr builds
+    (nf-parse.h:21-32): a.b.c.d -> a<<24|b<<16|c<<8|d."""
+    return (a << 24) | (b << 16) | (c << 8) | d
+
+
+def mac(s: str) -> bytes:
+    return bytes(int(x, 16) for x in s.split(":"))
+
+
+def splitmix64(seed: int, p: np.ndarray) -> np.ndarray:
+    z = (np.uint64(seed) + (p.astype(np.uint64) + np.uint64(1)) *
+         np.uint64(0x9E3779B97F4A7C15))
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def flow_order(n_packets: int, n_flows: int, order: str = "rr",
+               seed: int = 0x5EED, start: int = 0) -> np.ndarray:
+    p = np.arange(start, start + n_packets, dtype=np.int64)
+    if order == "rr":
+        return (p % n_flows).astype(np.int64)
+    if order == "uniform":
+        with np.errstate(over="ignore"):
+            return (splitmix64(seed, p) % np.uint64(n_flows)).astype(np.int64)
+    raise ValueError(order)
+
+
+def _be16(v: np.ndarray) -> np.ndarray:
+    v = v.astype(np.uint32)
+    return np.stack([(v >> 8) & 0xFF, v & 0xFF], axis=-1).astype(np.uint8)
+
+
+def _be32(v: np.ndarray) -> np.ndarray:
+    v = v.astype(np.uint64)
+    return np.stack([(v >> 24) & 0xFF, (v >> 16) & 0xFF, (v >> 8) & 0xFF,
+                     v & 0xFF], axis=-1).astype(np.uint8)
+
+
+def ipv4_header_checksum(hdr: np.ndarray) -> np.ndarray:
+    """Valid RFC 791 checksum (as the tester's NIC offload writes it) for
+    n x 20-byte headers whose checksum field is zero. Returns n x 2 bytes."""
+    w = hdr.reshape(-1, 10, 2).astype(np.uint32)
+    s = (w[:, :, 0] << 8 | w[:, :, 1]).sum(axis=1)
+    s = (s & 0xFFFF) + (s >> 16)
+    s = (s & 0xFFFF) + (s >> 16)
+    c = (~s) & 0xFFFF
+    return _be16(c)
+
+
+def udp_frames(src_ip: np.ndarray, dst_ip: np.ndarray, src_port: np.ndarray,
+               dst_port: np.ndarray, slot: int = 64, frame_len: int = 60,
+               proto: int = 17,
+               eth_src: bytes = b"\xff" * 6, eth_dst: bytes = b"\x00" * 6):
+    """Build n UDP (or TCP when proto=6, same layout) frames of frame_len bytes
+    in slot-byte slots. Addresses/ports are numeric, written network order."""
+    n = src_ip.shape[0]
+    assert frame_len >= 42 and slot >= frame_len
+    f = np.zeros((n, slot), dtype=np.uint8)
+    f[:, 0:6] = np.frombuffer(eth_dst, np.uint8)
+    f[:, 6:12] = np.frombuffer(eth_src, np.uint8)
+    f[:, 12:14] = np.frombuffer(ETH_IPV4, np.uint8)
+    tot = frame_len - 14
+    f[:, 14] = 0x45
+    f[:, 16:18] = _be16(np.full(n, tot))
+    f[:, 22] = 64
+    f[:, 23] = proto
+    f[:, 26:30] = _be32(src_ip)
+    f[:, 30:34] = _be32(dst_ip)
+    f[:, 24:26] = ipv4_header_checksum(f[:, 14:34])
+    f[:, 34:36] = _be16(src_port)
+    f[:, 36:38] = _be16(dst_port)
+    if proto == 17:
+        f[:, 38:40] = _be16(np.full(n, tot - 20))
+    lens = np.full(n, frame_len, dtype=np.uint16)
+    return f.reshape(-1), lens
+
+
+def nat_lan_trace(n_packets: int, n_flows: int, order: str = "rr",
+                  slot: int = 64, lan_dev: int = 0, start: int = 0,
+                  seed: int = 0x5EED):
+    """vignat LAN->WAN trace (config 1/2/5 shape)."""
+    fl = flow_order(n_packets, n_flows, order, seed, start)
+    src_ip = ip4(10, 0, 0, 0) + (fl >> 16)
+    src_port = fl & 0xFFFF
+    z = np.zeros_like(fl)
+    frames, lens = udp_frames(src_ip, z, src_port, z, slot=slot)
+    in_dev = np.full(n_packets, lan_dev, dtype=np.uint16)
+    now = (NOW0 + np.arange(start, start + n_packets, dtype=np.int64))
+    return frames, lens, in_dev, now
+
+
+def bridge_trace(n_packets: int, n_stations: int, slot: int = 64,
+                 start: int = 0, flood_pattern: bool = False):
+    """vigbridge config 3: frame p from station p mod N (on port (k & 1)) to
+    station (p + N/2) mod N; flood_pattern: dst = 0xFF0000000000 + k
+    (bench.lua:47-48), never learned."""
+    p = np.arange(start, start + n_packets, dtype=np.int64)
+    src_k = p % n_stations
+    dst_k = (p + n_stations // 2) % n_stations
+    frames, lens = udp_frames(np.full(n_packets, ip4(10, 0, 0, 1)),
+                              np.zeros(n_packets, np.int64),
+                              np.zeros(n_packets, np.int64),
+                              np.zeros(n_packets, np.int64), slot=slot)
+    f = frames.reshape(n_packets, slot)
+    f[:, 6:9] = np.array([0x02, 0, 0], np.uint8)
+    f[:, 9:12] = _be32(src_k)[:, 1:]
+    if flood_pattern:
+        f[:, 0:6] = np.concatenate(
+            [np.full((n_packets, 1), 0xFF, np.uint8),
+             np.zeros((n_packets, 1), np.uint8), _be32(src_k)], axis=1)
+    else:
+        f[:, 0:3] = np.array([0x02, 0, 0], np.uint8)
+        f[:, 3:6] = _be32(dst_k)[:, 1:]
+    in_dev = (src_k & 1).astype(np.uint16)
+    now = NOW0 + p
+    return frames, lens, in_dev, now
+
+
+def lb_traffic(n_packets: int, n_flows: int, wan_dev: int = 2, slot: int = 64,
+               order: str = "rr", start: int = 0, seed: int = 0x5EED):
+    """viglb config 4 WAN traffic: flow i = src_ip 11.0.0.0 + i."""
+    fl = flow_order(n_packets, n_flows, order, seed, start)
+    src_ip = ip4(11, 0, 0, 0) + fl
+    z = np.zeros_like(fl)
+    frames, lens = udp_frames(src_ip, z, z, z, slot=slot)
+    in_dev = np.full(n_packets, wan_dev, dtype=np.uint16)
+    now = NOW0 + np.arange(start, start + n_packets, dtype=np.int64)
+    return frames, lens, in_dev, now
+
+
+def lb_heartbeats(n_backends: int, slot: int = 64, t0: int = NOW0 - 1000):
+    """Backend b: src_ip 192.168.(b>>8).(b&255) on port b & 1."""
+    b = np.arange(n_backends, dtype=np.int64)
+    src_ip = ip4(192, 168, 0, 0) + b
+    z = np.zeros_like(b)
+    frames, lens = udp_frames(src_ip, z, z, z, slot=slot)
+    f = frames.reshape(n_backends, slot)
+    f[:, 6:8] = np.array([0x02, 0xBE], np.uint8)
+    f[:, 8:12] = _be32(b)
+    in_dev = (b & 1).astype(np.uint16)
+    now = t0 + b
+    return frames, lens, in_dev, now
