@@ -1,0 +1,222 @@
+"""Headline benchmark: vignat device-resident classification throughput.
+
+BASELINE.json metric: "Mpackets/s device-resident, 64B vignat @1M flows;
+%HBM roofline", measured on configs[1]: vignat 64 B, 1M flows, 1xMI355X
+(parse + CRC32C hash + map probe + state update + checksum rewrite).
+
+A step = one pass of the hot path (vp_process_device) over one batch of
+B synthetic 64 B packets already resident in HBM (traces.nat_lan_trace
+shape: round-robin over 1M flows, now_p = 1e9 + p ns).
+Every timed step reads its own pre-generated batch, so no input restore sits
+inside the timed region. A warm-up pass allocates all 1M flows first (its
+rate is reported as new_flow_mpps).
+
+N > 1 (torch.distributed, one rank per GPU): each rank runs its own NF
+replica over its own flows (weak scaling, no data-path collective;
+DESIGN.md §6). value = all ranks' packets / max-over-ranks time.
+
+Also reported:
+  roofline      algorithmic HBM-read bytes per packet (92 B)
+                x packets per launch / average classify-kernel time (HIP
+                events on the context's stream), vs 8 TB/s
+  cpu_baseline  the oracle (clean-room C restatement of nf.c + vignat) on
+                one host core, warm 1M-flow table, bounded sample
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import vigor_amd  # noqa: E402
+from vigor_amd import traces as T  # noqa: E402
+
+METRIC = "Mpackets/s device-resident, 64B vignat @1M flows; %HBM roofline"
+ALG_BYTES = 92          # 64 frame + 4 len/port + 16 key + 4 tag + 4 value
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SLOT = 64
+DEV_MACS = [T.mac("02:00:00:00:00:00"), T.mac("02:00:00:00:00:01")]
+NAT_ARGS = ["--expire", "60000000", "--starting-port", "0", "--wan", "1",
+            "--extip", "192.168.4.2", "--eth-dest", "0,90:e2:ba:55:12:20",
+            "--eth-dest", "1,90:e2:ba:55:12:21"]
+
+
+class FlowBank:
+    """Per-flow header bytes of the synthetic trace, on the device."""
+
+    def __init__(self, n_flows: int, flow_base: int, dev):
+        fl = np.arange(flow_base, flow_base + n_flows, dtype=np.int64)
+        src = T.ip4(10, 0, 0, 0) + (fl >> 16)
+        sp = fl & 0xFFFF
+        z = np.zeros_like(fl)
+        f, _ = T.udp_frames(src, z, sp, z, slot=SLOT)
+        f = f.reshape(n_flows, SLOT)
+        self.template = torch.from_numpy(f[0].copy()).to(dev)
+        self.var = torch.from_numpy(np.ascontiguousarray(
+            np.concatenate([f[:, 24:30], f[:, 34:36]], axis=1))).to(dev)
+        self.n = n_flows
+
+    def fill(self, frames: torch.Tensor, start: int):
+        B = frames.shape[0] // SLOT
+        fv = frames.view(B, SLOT)
+        fv.copy_(self.template.expand(B, SLOT))
+        fl = torch.arange(start, start + B, device=frames.device) % self.n
+        v = self.var.index_select(0, fl)
+        fv[:, 24:30] = v[:, 0:6]
+        fv[:, 34:36] = v[:, 6:8]
+
+
+def cpu_baseline(n_flows: int, sample: int):
+    """The oracle on one core over the same trace shape: warm every flow,
+    then time `sample` steady-state packets."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import orc
+
+    cfg = orc.nat_cfg(wan=1, ext_ip=T.ip4(192, 168, 4, 2),
+                      expire_us=60_000_000, max_flows=n_flows,
+                      device_macs=DEV_MACS,
+                      endpoint_macs=[T.mac("90:e2:ba:55:12:20"),
+                                     T.mac("90:e2:ba:55:12:21")])
+    o = orc.Oracle("nat", cfg)
+    fr, ln, dv, now = T.nat_lan_trace(n_flows, n_flows)
+    o.run(fr, ln, dv, now, SLOT)
+    chunk = 1 << 22
+    total, t = 0, 0.0
+    while total < sample:
+        fr, ln, dv, now = T.nat_lan_trace(chunk, n_flows, start=n_flows + total)
+        t0 = time.perf_counter()
+        o.run(fr, ln, dv, now, SLOT)
+        t += time.perf_counter() - t0
+        total += chunk
+    return total / t / 1e6, total
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1 << 24)
+    ap.add_argument("--flows", type=int, default=1 << 20)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 24)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    cfg = vigor_amd.nat_config_from_args(
+        NAT_ARGS + ["--max-flows", str(args.flows)], 2, DEV_MACS)
+    nat = vigor_amd.Nat(cfg, gpu=local)
+    bank = FlowBank(args.flows, rank * args.flows, dev)
+    B = args.batch
+    lens = torch.full((B,), 60, dtype=torch.int16, device=dev)
+    in_dev = torch.zeros(B, dtype=torch.int16, device=dev)
+    out = torch.zeros(B, dtype=torch.int16, device=dev)
+
+    def step(frames, start):
+        nat.process_device(frames, lens, in_dev, out, SLOT,
+                           now0=T.NOW0 + start, now_step=1)
+
+    # warm-up: first pass allocates every flow
+    wbuf = torch.empty(B * SLOT, dtype=torch.uint8, device=dev)
+    new_flow_mpps = None
+    for w in range(args.warmup):
+        bank.fill(wbuf, w * B)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        step(wbuf, w * B)
+        torch.cuda.synchronize()
+        if w == 0:
+            new_flow_mpps = B / (time.perf_counter() - t0) / 1e6
+    assert nat.live_count() == min(args.flows, B * max(1, args.warmup))
+    del wbuf
+    bufs = []
+    for k in range(args.steps):
+        b = torch.empty(B * SLOT, dtype=torch.uint8, device=dev)
+        bank.fill(b, (args.warmup + k) * B)
+        bufs.append(b)
+    torch.cuda.synchronize()
+
+    kms = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(bufs[k], (args.warmup + k) * B)
+        kms.append(nat.last_kernel_ms())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # every packet hit (steady state) and went out on the WAN port
+    assert int((out != 1).sum().item()) == 0
+
+    total_pkts = B * args.steps * world
+    mpps = total_pkts / elapsed / 1e6
+    launches = sum(k for _, k in kms)
+    kernel_s = sum(m for m, _ in kms) / 1e3
+    per_launch_s = kernel_s / max(1, launches)
+    pkts_per_launch = B * args.steps / max(1, launches)
+    achieved = ALG_BYTES * pkts_per_launch / per_launch_s / 1e9
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu and world == 1:
+            cmpps, sample = cpu_baseline(args.flows, args.cpu_sample)
+            cpu = {"value": round(cmpps, 3), "unit": "Mpps", "cores": 1,
+                   "kind": "port",
+                   "sample": "%d steady-state packets of the same trace "
+                             "(64B, %d flows warm, round robin), oracle/"
+                             "liborc.so, 1 thread" % (sample, args.flows)}
+        line = {
+            "metric": METRIC, "value": round(mpps, 2), "unit": "Mpps",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "vignat 64B, 1M flows, 1xMI355X "
+                                   "(parse+hash+map-probe kernel, checksum "
+                                   "rewrite)" if args.flows == 1 << 20 else
+                                   "vignat 64B, %d flows" % args.flows,
+                       "flows_per_gpu": args.flows, "batch_packets": B,
+                       "frame_bytes": 60, "slot_bytes": SLOT,
+                       "parallelism": "replicas%d" % world if world > 1
+                       else "single"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None,
+                         "kernel": "nat_classify",
+                         "kernel_ms_per_launch": round(per_launch_s * 1e3, 4),
+                         "alg_bytes_per_packet": ALG_BYTES,
+                         "kernel_mpps": round(pkts_per_launch / per_launch_s
+                                              / 1e6, 1)},
+            "cpu_baseline": cpu,
+            "new_flow_mpps": round(new_flow_mpps, 2) if new_flow_mpps else None,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

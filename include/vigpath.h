@@ -1,0 +1,162 @@
+/*
+ * vigpath — MI355X-native implementation of Vigor's per-packet receive path
+ * (parse -> CRC32C flow hash -> libVig map probe -> state update -> header
+ * rewrite + IPv4/L4 checksum) for vignat, vigbridge and viglb.
+ *
+ * C ABI only: plain pointers and sizes, no HIP or torch types. Two layers:
+ *
+ *  1. The reference's own operator surface, nf.h (reference nf.h:8-18):
+ *       bool nf_init(void);
+ *       int  nf_process(uint16_t device, uint8_t *buffer,
+ *                       uint16_t packet_length, vigor_time_t now);
+ *       void nf_config_init(int argc, char **argv); nf_config_usage();
+ *       nf_config_print(); FLOOD_FRAME
+ *     exported by the per-NF shim libraries libvignat_nf.so /
+ *     libvigbridge_nf.so / libviglb_nf.so (one NF per binary, as the
+ *     reference builds one NF per binary, Makefile.dpdk). They link unchanged
+ *     against the reference's nf.c (nf.c:143-216). See INTEGRATION.md.
+ *
+ *  2. The batch interface those shims sit on (libvigpath.so), which is what a
+ *     batching caller (nf.c's VIGOR_BATCH_SIZE path, nf.c:178-215, or a GPU
+ *     host loop) binds. It replaces the per-packet loop
+ *     `for each mbuf: nf_process(...)` (nf.c:150-176) with one call per
+ *     batch whose results are identical to calling nf_process on every
+ *     packet in order.
+ *
+ * Error convention: 0 on success, a negative errno-style code on failure;
+ * never aborts. "Drop" keeps the reference encoding: out_dev == in_dev.
+ */
+#ifndef VIGPATH_H
+#define VIGPATH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VP_FLOOD_FRAME ((uint16_t)-1) /* nf.h:8 FLOOD_FRAME */
+#define VP_MAX_DEVICES 32
+
+/* error codes (negated errno values) */
+#define VP_OK 0
+#define VP_EINVAL (-22)
+#define VP_ENOMEM (-12)
+#define VP_EIO (-5)       /* HIP runtime failure */
+#define VP_ENOTSUP (-95)  /* outside the supported domain */
+
+typedef struct vp_ctx vp_ctx;
+
+/* ------------------------------------------------------------ configs --
+ * Field meanings and units are exactly the reference's struct nf_config. */
+
+/* vignat/nat_config.h:5-31 (+ the device MACs nf_config_init reads through
+ * rte_eth_macaddr_get, nat_config.c:34-37). */
+typedef struct vp_nat_config {
+  uint16_t wan_device;
+  uint16_t lan_main_device;
+  uint16_t start_port;
+  uint32_t external_addr;   /* host-order value, as nf_parse_ipv4addr makes */
+  uint32_t expiration_time; /* microseconds */
+  uint32_t max_flows;       /* power of two (map.c:73, -DCAPACITY_POW2) */
+  uint16_t n_devices;       /* rte_eth_dev_count_avail() */
+  uint8_t device_macs[VP_MAX_DEVICES][6];
+  uint8_t endpoint_macs[VP_MAX_DEVICES][6];
+} vp_nat_config;
+
+/* vigbridge/bridge_config.h:8-18; the --config static table is passed as
+ * rules instead of a file name (bridge_main.c:130-230 parses the file into
+ * exactly these triples). */
+typedef struct vp_bridge_rule {
+  uint8_t mac[6];
+  int32_t device_from;
+  int32_t device_to; /* -2 filters (bridge_main.c:322-325) */
+} vp_bridge_rule;
+typedef struct vp_bridge_config {
+  uint32_t expiration_time; /* microseconds */
+  uint32_t dyn_capacity;    /* power of two */
+  uint16_t n_devices;
+  uint32_t n_static;
+  const vp_bridge_rule *static_rules;
+} vp_bridge_config;
+
+/* viglb/lb_config.h:8-38 */
+typedef struct vp_lb_config {
+  uint32_t flow_capacity;           /* power of two */
+  uint32_t flow_expiration_time;    /* microseconds */
+  uint32_t backend_capacity;        /* power of two, < cht_height */
+  uint32_t cht_height;              /* prime */
+  uint32_t backend_expiration_time; /* microseconds */
+  uint16_t wan_device;
+  uint16_t n_devices;
+  uint8_t device_macs[VP_MAX_DEVICES][6];
+} vp_lb_config;
+
+/* Create an NF instance whose state lives in HBM of HIP device `gpu`.
+ * Returns 0 and *out, or VP_EINVAL for a configuration the reference's
+ * nf_init would reject (non power-of-two capacities, ...). */
+int vp_nat_create(const vp_nat_config *cfg, int gpu, vp_ctx **out);
+int vp_bridge_create(const vp_bridge_config *cfg, int gpu, vp_ctx **out);
+int vp_lb_create(const vp_lb_config *cfg, int gpu, vp_ctx **out);
+void vp_destroy(vp_ctx *ctx);
+
+/* ------------------------------------------------------------ batches -- */
+
+/* A batch already resident in device memory (all pointers are device
+ * pointers). Frames sit `slot` bytes apart and are rewritten in place, like
+ * the mbuf data nf_process mutates (nf.c:154-156). `slot` must be a multiple
+ * of 16 and >= 64. Bytes past a frame's slot read as 0.
+ * Time: if `now` is NULL, packet i has now0 + i * now_step (ns); otherwise
+ * now[i]. Times must be non-decreasing (nf.c takes them from
+ * CLOCK_MONOTONIC, vigor-time.c:56-66) and >= 0 (nat_flowmanager.c:58). */
+typedef struct vp_dev_batch {
+  uint8_t *frames;
+  uint32_t slot;
+  uint32_t n;
+  const uint16_t *len;
+  const uint16_t *in_dev;
+  const int64_t *now;
+  int64_t now0;
+  int64_t now_step;
+  uint16_t *out_dev; /* nf_process's return value, stored as u16 (nf.c:156) */
+} vp_dev_batch;
+
+/* Process one device-resident batch on HIP stream `stream` (a hipStream_t,
+ * or NULL for the context's own stream). Synchronous: returns after the
+ * results are in device memory and the NF state is updated. */
+int vp_process_device(vp_ctx *ctx, const vp_dev_batch *batch, void *stream);
+
+/* Host-resident batch shaped like a DPDK rx burst: frames[i] -> mbuf data of
+ * len[i] bytes (rte_pktmbuf_mtod, nf.c:154), rewritten in place. Staged
+ * through pinned memory with hipMemcpyAsync. */
+int vp_process_batch(vp_ctx *ctx, uint32_t n, const uint16_t *in_dev,
+                     uint8_t *const *frames, const uint16_t *len,
+                     const int64_t *now, uint16_t *out_dev);
+
+/* Host-resident contiguous batch (frames `slot` bytes apart). */
+int vp_process_host(vp_ctx *ctx, uint32_t n, const uint16_t *in_dev,
+                    uint8_t *frames, uint32_t slot, const uint16_t *len,
+                    const int64_t *now, uint16_t *out_dev);
+
+/* ------------------------------------------------------- observability -- */
+
+/* vignat state by flow index i < max_flows: alloc[i] (dchain allocated?),
+ * ts[i] (timestamp, only meaningful when allocated), key[16*i] (the FlowId
+ * bytes, vignat/flow.h:3-10 layout, padding zero). */
+int vp_nat_dump(vp_ctx *ctx, uint8_t *alloc, int64_t *ts, uint8_t *keys);
+
+/* Number of live flows / learned MACs / flows+backends. */
+int64_t vp_live_count(vp_ctx *ctx);
+
+/* Per-context kernel timing of the last vp_process_device call: time of the
+ * dominant classification kernel in ms (HIP events on the stream it ran on),
+ * summed over its launches, and the number of launches. */
+int vp_last_kernel_ms(vp_ctx *ctx, float *ms, int *launches);
+
+/* Build identification (e.g. "vigpath gfx950"). */
+const char *vp_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -18,6 +18,7 @@ import numpy as np
 import pytest
 
 import orc
+from tracegen import mixed_nat_trace
 from vigor_amd import traces as T
 
 HAVE_REF = os.path.isdir("/root/reference/libvig/verified")
@@ -225,43 +226,6 @@ def test_cht_matches_reference(height, cap):
 
 
 # ------------------------------------------------------ whole-NF vs ref --
-
-def mixed_nat_trace(rng, n, n_flows, slot=64, max_idx=64):
-    """LAN packets over n_flows plus WAN replies to existing/unknown ports,
-    some malformed frames, monotone time with ties."""
-    fl = rng.integers(0, n_flows, n)
-    sip = T.ip4(10, 0, 0, 0) + fl
-    dip = T.ip4(8, 8, 0, 0) + (fl % 7)
-    sp = 1000 + fl % 13
-    dp = np.full(n, 53)
-    proto = np.where(fl % 5 == 0, 6, 17)
-    frames = np.zeros((n, slot), np.uint8)
-    lens = np.zeros(n, np.uint16)
-    for p_ in (6, 17):
-        m = proto == p_
-        f, ln = T.udp_frames(sip[m], dip[m], sp[m], dp[m], slot=slot, proto=p_)
-        frames[m] = f.reshape(-1, slot)
-        lens[m] = ln
-    in_dev = np.zeros(n, np.uint16)
-    wan = rng.random(n) < 0.3
-    in_dev[wan] = 1
-    # WAN replies: swap addresses, dst port = an index (raw LE u16 on wire)
-    idx = rng.integers(0, max_idx, n).astype(np.uint16)
-    w = frames[wan]
-    w[:, 26:30], w[:, 30:34] = frames[wan][:, 30:34], frames[wan][:, 26:30]
-    w[:, 34:36] = frames[wan][:, 36:38]
-    w[:, 36] = (idx[wan] & 0xFF).astype(np.uint8)
-    w[:, 37] = (idx[wan] >> 8).astype(np.uint8)
-    frames[wan] = w
-    # malformed: non-IPv4, short total_length, ihl<5, non tcp/udp
-    bad = rng.random(n)
-    frames[bad < 0.02, 12] = 0x86
-    frames[(bad >= 0.02) & (bad < 0.04), 17] = 200
-    frames[(bad >= 0.04) & (bad < 0.05), 14] = 0x44
-    frames[(bad >= 0.05) & (bad < 0.06), 23] = 1
-    now = T.NOW0 + np.cumsum(rng.integers(0, 3, n))
-    return frames.reshape(-1), lens, in_dev, now.astype(np.int64)
-
 
 @needs_ref
 @pytest.mark.parametrize("seed,max_flows,expire_us,n_flows",

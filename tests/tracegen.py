@@ -1,0 +1,78 @@
+"""Adversarial trace builders shared by the oracle and GPU parity tests."""
+import numpy as np
+
+from vigor_amd import traces as T
+
+
+def mixed_nat_trace(rng, n, n_flows, slot=64, max_idx=64):
+    """LAN packets over n_flows plus WAN replies to existing/unknown ports,
+    some malformed frames, monotone time with ties."""
+    fl = rng.integers(0, n_flows, n)
+    sip = T.ip4(10, 0, 0, 0) + fl
+    dip = T.ip4(8, 8, 0, 0) + (fl % 7)
+    sp = 1000 + fl % 13
+    dp = np.full(n, 53)
+    proto = np.where(fl % 5 == 0, 6, 17)
+    frames = np.zeros((n, slot), np.uint8)
+    lens = np.zeros(n, np.uint16)
+    for p_ in (6, 17):
+        m = proto == p_
+        f, ln = T.udp_frames(sip[m], dip[m], sp[m], dp[m], slot=slot, proto=p_)
+        frames[m] = f.reshape(-1, slot)
+        lens[m] = ln
+    in_dev = np.zeros(n, np.uint16)
+    wan = rng.random(n) < 0.3
+    in_dev[wan] = 1
+    # WAN replies: swap addresses, dst port = an index (raw LE u16 on wire)
+    idx = rng.integers(0, max_idx, n).astype(np.uint16)
+    w = frames[wan]
+    w[:, 26:30], w[:, 30:34] = frames[wan][:, 30:34], frames[wan][:, 26:30]
+    w[:, 34:36] = frames[wan][:, 36:38]
+    w[:, 36] = (idx[wan] & 0xFF).astype(np.uint8)
+    w[:, 37] = (idx[wan] >> 8).astype(np.uint8)
+    frames[wan] = w
+    # malformed: non-IPv4, short total_length, ihl<5, non tcp/udp
+    bad = rng.random(n)
+    frames[bad < 0.02, 12] = 0x86
+    frames[(bad >= 0.02) & (bad < 0.04), 17] = 200
+    frames[(bad >= 0.04) & (bad < 0.05), 14] = 0x44
+    frames[(bad >= 0.05) & (bad < 0.06), 23] = 1
+    now = T.NOW0 + np.cumsum(rng.integers(0, 3, n))
+    return frames.reshape(-1), lens, in_dev, now.astype(np.int64)
+
+
+def edge_nat_trace(rng, n, n_flows, slot=128, long_frames=False):
+    """Header edge cases of nf-util.h:116-162 / nf-util.c:45-64: IP options
+    (borrowed or not), odd and short lengths, total_length < 20 or beyond the
+    packet, pkt_len < 14 (u16 wrap), TCP and UDP, long frames."""
+    fl = rng.integers(0, n_flows, n)
+    frames = np.zeros((n, slot), np.uint8)
+    lens = np.zeros(n, np.uint16)
+    in_dev = np.where(rng.random(n) < 0.2, 1, 0).astype(np.uint16)
+    maxlen = min(slot, 1514 if long_frames else slot)
+    for i in range(n):
+        ihl = 5 if rng.random() < 0.6 else int(rng.integers(0, 16))
+        proto = int(rng.choice([6, 17, 17, 1]))
+        flen = int(rng.integers(14, maxlen + 1)) if rng.random() < 0.7 else \
+            int(rng.integers(0, 64))
+        f = frames[i]
+        f[:slot] = rng.integers(0, 256, slot, dtype=np.uint8)  # dirty bytes
+        f[12:14] = (8, 0) if rng.random() < 0.95 else (0x86, 0xDD)
+        f[14] = 0x40 | ihl
+        tl = max(0, flen - 14) if rng.random() < 0.7 else \
+            int(rng.integers(0, 2 * maxlen))
+        f[16:18] = (tl >> 8, tl & 0xFF)
+        f[23] = proto
+        k = int(fl[i])
+        f[26:30] = (10, 0, (k >> 8) & 0xFF, k & 0xFF)
+        f[30:34] = (8, 8, 8, k % 3)
+        l4 = 14 + 4 * max(ihl, 5)
+        if l4 + 4 <= slot:
+            f[l4:l4 + 2] = (0, 53)
+            if in_dev[i] == 1:  # WAN: dst port = small index, raw LE
+                idx = int(rng.integers(0, 70))
+                f[l4 + 2:l4 + 4] = (idx & 0xFF, idx >> 8)
+            else:
+                f[l4 + 2:l4 + 4] = (k >> 8, k & 0xFF)
+        lens[i] = flen
+    return frames.reshape(-1), lens, in_dev

@@ -1,0 +1,127 @@
+"""vigor_amd — MI355X-native Vigor per-packet path (host-side mirror).
+
+Thin ctypes layer over libvigpath.so (include/vigpath.h), the C-ABI the HIP
+kernels sit behind. There is no CPU fallback: if the library or a GPU is
+missing, every entry point raises. The CPU restatement used to check results
+lives in oracle/ and is test infrastructure only.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+LIB_PATH = os.path.join(PKG, "libvigpath.so")
+MAX_DEV = 32
+FLOOD_FRAME = 0xFFFF
+
+VP_OK, VP_EINVAL, VP_ENOMEM, VP_EIO, VP_ENOTSUP = 0, -22, -12, -5, -95
+_ERR = {VP_EINVAL: "EINVAL", VP_ENOMEM: "ENOMEM", VP_EIO: "EIO (HIP)",
+        VP_ENOTSUP: "ENOTSUP"}
+
+
+class VigpathError(RuntimeError):
+    def __init__(self, rc: int, what: str):
+        super().__init__(f"{what}: {_ERR.get(rc, rc)}")
+        self.rc = rc
+
+
+MacTable = (C.c_uint8 * 6) * MAX_DEV
+
+
+class NatConfigC(C.Structure):
+    """vp_nat_config (vignat/nat_config.h:5-31)."""
+    _fields_ = [("wan_device", C.c_uint16), ("lan_main_device", C.c_uint16),
+                ("start_port", C.c_uint16), ("external_addr", C.c_uint32),
+                ("expiration_time", C.c_uint32), ("max_flows", C.c_uint32),
+                ("n_devices", C.c_uint16), ("device_macs", MacTable),
+                ("endpoint_macs", MacTable)]
+
+
+class BridgeRuleC(C.Structure):
+    _fields_ = [("mac", C.c_uint8 * 6), ("device_from", C.c_int32),
+                ("device_to", C.c_int32)]
+
+
+class BridgeConfigC(C.Structure):
+    """vp_bridge_config (vigbridge/bridge_config.h:8-18)."""
+    _fields_ = [("expiration_time", C.c_uint32), ("dyn_capacity", C.c_uint32),
+                ("n_devices", C.c_uint16), ("n_static", C.c_uint32),
+                ("static_rules", C.POINTER(BridgeRuleC))]
+
+
+class LbConfigC(C.Structure):
+    """vp_lb_config (viglb/lb_config.h:8-38)."""
+    _fields_ = [("flow_capacity", C.c_uint32),
+                ("flow_expiration_time", C.c_uint32),
+                ("backend_capacity", C.c_uint32), ("cht_height", C.c_uint32),
+                ("backend_expiration_time", C.c_uint32),
+                ("wan_device", C.c_uint16), ("n_devices", C.c_uint16),
+                ("device_macs", MacTable)]
+
+
+class DevBatchC(C.Structure):
+    _fields_ = [("frames", C.c_void_p), ("slot", C.c_uint32), ("n", C.c_uint32),
+                ("len", C.c_void_p), ("in_dev", C.c_void_p),
+                ("now", C.c_void_p), ("now0", C.c_int64),
+                ("now_step", C.c_int64), ("out_dev", C.c_void_p)]
+
+
+# every symbol include/vigpath.h declares
+EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_destroy",
+           "vp_process_device", "vp_process_batch", "vp_process_host",
+           "vp_nat_dump", "vp_live_count", "vp_last_kernel_ms", "vp_version"]
+
+_lib = None
+
+
+def lib():
+    """Load libvigpath.so; raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} missing: run __graft_entry__.build()")
+    L = C.CDLL(LIB_PATH)
+    L.vp_version.restype = C.c_char_p
+    for name in ("vp_nat_create", "vp_bridge_create", "vp_lb_create"):
+        getattr(L, name).restype = C.c_int
+    L.vp_nat_create.argtypes = [C.POINTER(NatConfigC), C.c_int,
+                                C.POINTER(C.c_void_p)]
+    L.vp_bridge_create.argtypes = [C.POINTER(BridgeConfigC), C.c_int,
+                                   C.POINTER(C.c_void_p)]
+    L.vp_lb_create.argtypes = [C.POINTER(LbConfigC), C.c_int,
+                               C.POINTER(C.c_void_p)]
+    L.vp_destroy.argtypes = [C.c_void_p]
+    L.vp_destroy.restype = None
+    L.vp_process_device.argtypes = [C.c_void_p, C.POINTER(DevBatchC),
+                                    C.c_void_p]
+    L.vp_process_device.restype = C.c_int
+    L.vp_process_host.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p,
+                                  C.c_void_p, C.c_uint32, C.c_void_p,
+                                  C.c_void_p, C.c_void_p]
+    L.vp_process_host.restype = C.c_int
+    L.vp_process_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p,
+                                   C.POINTER(C.c_void_p), C.c_void_p,
+                                   C.c_void_p, C.c_void_p]
+    L.vp_process_batch.restype = C.c_int
+    L.vp_nat_dump.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.vp_nat_dump.restype = C.c_int
+    L.vp_live_count.argtypes = [C.c_void_p]
+    L.vp_live_count.restype = C.c_int64
+    L.vp_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float),
+                                    C.POINTER(C.c_int)]
+    L.vp_last_kernel_ms.restype = C.c_int
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise VigpathError(rc, what)
+
+
+from .nf import Bridge, Lb, Nat, NfBase  # noqa: E402,F401
+from .config import (bridge_config_from_args, lb_config_from_args,  # noqa
+                     nat_config_from_args)

@@ -1,0 +1,247 @@
+// Device-side building blocks shared by the NF kernels (gfx950, wave64).
+//
+// Semantics restate, per function, the reference's per-packet path (paths
+// relative to the reference repository):
+//   packet cursor + header parse   nf-util.h:116-162, packet-io.c:40-111
+//   L3/L4 predicates               nf-util.c:21-31
+//   checksum rewrite               nf-util.c:45-64 + DPDK 20.08 rte_ip.h
+//   CRC32C key hash                codegen/main.ml:328-401 (generated
+//                                  <Struct>_hash), libvig/verified/ether.c:61-90
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vp {
+
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;  // slot index field: never used
+constexpr uint32_t kTomb = 0xFFFFFFFEu;   // slot index field: erased
+constexpr uint32_t kNone = 0xFFFFFFFFu;   // slot_of[]: index not allocated
+
+__host__ __device__ inline uint16_t bswap16(uint16_t v) {
+  return (uint16_t)((v >> 8) | (v << 8));
+}
+
+// ---------------------------------------------------------------- frames --
+// A frame is `cap` bytes of a slot. Reads past the slot are 0 and writes past
+// it are dropped: the reference touches mbuf bytes past pkt_len for some
+// malformed headers; within the slot we read the same bytes it would.
+struct GFrame {
+  uint8_t *b;
+  uint32_t cap;
+  __device__ uint8_t r8(uint32_t o) const { return o < cap ? b[o] : 0; }
+  __device__ uint16_t r16(uint32_t o) const {
+    return (uint16_t)(r8(o) | (r8(o + 1) << 8));
+  }
+  __device__ uint32_t r32(uint32_t o) const {
+    return (uint32_t)r16(o) | ((uint32_t)r16(o + 2) << 16);
+  }
+  __device__ void w8(uint32_t o, uint8_t v) const {
+    if (o < cap) b[o] = v;
+  }
+  __device__ void w16(uint32_t o, uint16_t v) const {
+    w8(o, (uint8_t)v);
+    w8(o + 1, (uint8_t)(v >> 8));
+  }
+  __device__ void w32(uint32_t o, uint32_t v) const {
+    w16(o, (uint16_t)v);
+    w16(o + 2, (uint16_t)(v >> 16));
+  }
+};
+
+struct L34 {
+  uint32_t ip;  // offset of the IPv4 header
+  uint32_t l4;  // offset of the TCP/UDP header (after borrowed options)
+  bool ok;
+};
+
+// nf_then_get_rte_ether_header + nf_then_get_rte_ipv4_header +
+// nf_then_get_tcpudp_header (nf-util.h:116-162). `total` is the packet-io
+// cursor's total length (the mbuf pkt_len); lengths wrap like the
+// reference's size_t -> u32 -> u16 narrowing.
+__device__ inline L34 parse_l34(const GFrame &f, uint32_t total) {
+  L34 r{14, 0, false};
+  uint32_t read = 14;
+  uint16_t unread = (uint16_t)(total - read);
+  bool is_ip = f.r16(12) == bswap16(0x0800);
+  if (!is_ip | (unread < 20)) return r;
+  read += 20;
+  uint8_t ihl = f.r8(14) & 0x0F;
+  uint16_t tl = bswap16(f.r16(16));
+  if ((ihl < 5) | (unread < tl)) return r;
+  uint16_t opt = (uint16_t)((ihl - 5) * 4);
+  if ((opt != 0) & ((uint32_t)unread - 20u >= opt)) read += opt;
+  uint8_t proto = f.r8(23);
+  if (!((proto == 6) | (proto == 17)) | ((uint32_t)(total - read) < 4u))
+    return r;
+  r.l4 = read;
+  r.ok = true;
+  return r;
+}
+
+// DPDK 20.08 __rte_raw_cksum + __rte_raw_cksum_reduce.
+__device__ inline uint32_t fold16(uint32_t s) {
+  s = (s >> 16) + (s & 0xFFFF);
+  s = (s >> 16) + (s & 0xFFFF);
+  return s;
+}
+__device__ inline uint32_t raw_cksum(const GFrame &f, uint32_t off,
+                                     uint32_t len) {
+  uint32_t sum = 0, i = 0;
+  for (; i + 1 < len; i += 2) sum += f.r16(off + i);
+  if (len & 1) sum += f.r8(off + i);
+  return fold16(sum);
+}
+// rte_ipv4_phdr_cksum: {src, dst, 0, proto, be16(l4_len)} as 6 LE words.
+__device__ inline uint32_t phdr_cksum(uint32_t src, uint32_t dst, uint8_t proto,
+                                      uint32_t l4_len) {
+  uint32_t s = (src & 0xFFFF) + (src >> 16) + (dst & 0xFFFF) + (dst >> 16) +
+               ((uint32_t)proto << 8) + (((l4_len >> 8) & 0xFF) |
+                                         ((l4_len & 0xFF) << 8));
+  return fold16(s);
+}
+// rte_ipv4_udptcp_cksum given the folded L4 byte sum.
+__device__ inline uint16_t finish_l4(uint32_t l4sum, uint32_t ph) {
+  uint32_t c = l4sum + ph;
+  c = ((c & 0xFFFF0000u) >> 16) + (c & 0xFFFF);
+  c = (~c) & 0xFFFF;
+  if (c == 0) c = 0xFFFF;  // DPDK 20.08: for TCP too (TCP-zero edge unpinned)
+  return (uint16_t)c;
+}
+
+// nf_set_rte_ipv4_udptcp_checksum (nf-util.c:45-64), generic byte form.
+__device__ inline void set_checksums(const GFrame &f, uint32_t ip,
+                                     uint32_t l4) {
+  f.w16(ip + 10, 0);
+  uint8_t proto = f.r8(ip + 9);
+  uint32_t at = proto == 6 ? l4 + 16 : l4 + 6;
+  if (proto == 6 || proto == 17) {
+    f.w16(at, 0);
+    uint32_t l3 = bswap16(f.r16(ip + 2));
+    uint16_t c = 0;
+    if (l3 >= 20) {
+      uint32_t l4len = l3 - 20;
+      c = finish_l4(raw_cksum(f, l4, l4len),
+                    phdr_cksum(f.r32(ip + 12), f.r32(ip + 16), proto, l4len));
+    }
+    f.w16(at, c);
+  }
+  f.w16(ip + 10, (uint16_t)~raw_cksum(f, ip, 20));
+}
+
+__device__ inline void set_macs(const GFrame &f, const uint32_t mw[3]) {
+  // mw = the 12 header bytes d_addr[6] s_addr[6] as 3 LE words
+  for (int k = 0; k < 3; k++) f.w32(4 * k, mw[k]);
+}
+
+// ------------------------------------------------------------ fast frames --
+// The 64-byte slot held in 16 registers (LE words). Only compile-time word
+// indices are used so nothing spills to scratch.
+struct RFrame {
+  uint32_t w[16];
+  __device__ uint32_t u16at(int o) const {  // o even, compile-time
+    return (o & 2) ? (w[o >> 2] >> 16) : (w[o >> 2] & 0xFFFF);
+  }
+  __device__ void set16(int o, uint32_t v) {
+    if (o & 2)
+      w[o >> 2] = (w[o >> 2] & 0x0000FFFFu) | (v << 16);
+    else
+      w[o >> 2] = (w[o >> 2] & 0xFFFF0000u) | (v & 0xFFFF);
+  }
+  // raw u32 at an offset == 2 (mod 4)
+  __device__ uint32_t u32at2(int o) const {
+    return (w[o >> 2] >> 16) | (w[(o >> 2) + 1] << 16);
+  }
+  __device__ void set32at2(int o, uint32_t v) {
+    w[o >> 2] = (w[o >> 2] & 0x0000FFFFu) | (v << 16);
+    w[(o >> 2) + 1] = (w[(o >> 2) + 1] & 0xFFFF0000u) | (v >> 16);
+  }
+};
+
+// Checksums of a 64-byte IHL=5 frame with total_length <= 50 (so every byte
+// the L4 sum covers lies in the slot). Same arithmetic as set_checksums.
+__device__ inline void fast_checksums(RFrame &f, uint32_t proto, uint32_t tl) {
+  f.set16(24, 0);
+  if (proto == 6 || proto == 17) {
+    const bool tcp = proto == 6;
+    if (tcp) f.set16(50, 0); else f.set16(40, 0);
+    uint32_t c = 0;
+    if (tl >= 20) {
+      const uint32_t L = tl - 20, end = 34 + L;
+      uint32_t s = 0;
+#pragma unroll
+      for (int k = 0; k < 15; k++) {
+        const int o = 34 + 2 * k;
+        uint32_t word = f.u16at(o);
+        uint32_t m = ((uint32_t)o + 2 <= end) ? 0xFFFFu
+                     : (((uint32_t)o + 1 == end) ? 0xFFu : 0u);
+        s += word & m;
+      }
+      c = finish_l4(fold16(s), phdr_cksum(f.u32at2(26), f.u32at2(30),
+                                          (uint8_t)proto, L));
+    }
+    if (tcp) f.set16(50, c); else f.set16(40, c);
+  }
+  uint32_t s = 0;
+#pragma unroll
+  for (int o = 14; o < 34; o += 2) s += f.u16at(o);
+  f.set16(24, (~fold16(s)) & 0xFFFF);
+}
+
+// ------------------------------------------------------------------ CRC --
+// CRC-32C as SSE4.2 `crc32 r32` computes it (boilerplate-util.h:9): reflected
+// polynomial 0x82F63B78, the operand's 4 LE bytes, no pre/post inversion.
+__host__ __device__ inline uint32_t crc32c_byte(uint32_t crc, uint8_t b) {
+  crc ^= b;
+  for (int k = 0; k < 8; k++) crc = (crc >> 1) ^ (0x82F63B78u & (0u - (crc & 1u)));
+  return crc;
+}
+__host__ __device__ inline uint32_t crc32c_u32(uint32_t crc, uint32_t v) {
+  for (int k = 0; k < 4; k++) crc = crc32c_byte(crc, (uint8_t)(v >> (8 * k)));
+  return crc;
+}
+
+// Seed 0 and no final XOR make the chained hash GF(2)-linear in the message
+// bytes, so a hash over a fixed field layout is the XOR of one 256-entry
+// table per non-zero byte position: T_p[b] = CRC of the message whose only
+// non-zero byte is b at position p. Built on the host, staged in LDS.
+inline void build_position_table(uint32_t *tab, int pos, int msg_len) {
+  for (int b = 0; b < 256; b++) {
+    uint32_t c = 0;
+    for (int k = pos; k < msg_len; k++)
+      c = crc32c_byte(c, k == pos ? (uint8_t)b : 0);
+    tab[b] = c;
+  }
+}
+
+// ------------------------------------------------------------- flow slot --
+// One open-addressing slot of the device flow table, 32 B (one half of a
+// 64-byte memory request). The key is stored in the slot so a hit costs one
+// random line. ts is the libVig dchain timestamp of the flow index stored
+// here (double-chain.c:16-19 keeps it per index; the GPU keeps it per slot).
+struct __align__(32) FlowSlot {
+  uint32_t k[4];  // 16 key bytes, reference struct layout, padding zero
+  uint32_t hash;
+  uint32_t index;  // kEmpty / kTomb / dchain index
+  uint64_t ts;     // vigor_time_t, >= 0
+};
+
+__device__ inline bool key_eq(const uint32_t a[4], const uint32_t b[4]) {
+  return ((a[0] ^ b[0]) | (a[1] ^ b[1]) | (a[2] ^ b[2]) | (a[3] ^ b[3])) == 0;
+}
+
+// Wave-aggregated append: one atomic per wave for all active lanes that set
+// `want`; returns this lane's position (valid only where want).
+__device__ inline uint32_t wave_append(uint32_t *counter, bool want) {
+  uint64_t mask = __ballot(want);
+  if (mask == 0) return 0;
+  uint32_t lane = __lane_id();
+  uint32_t leader = __ffsll((unsigned long long)mask) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
+  base = __shfl(base, leader);
+  uint64_t below = mask & ((1ull << lane) - 1ull);
+  return base + (uint32_t)__popcll(below);
+}
+
+}  // namespace vp

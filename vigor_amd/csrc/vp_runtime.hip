@@ -1,0 +1,346 @@
+// C-ABI entry points of libvigpath.so (include/vigpath.h): context
+// lifetime, workspace, host<->device batch staging and dispatch per NF.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "vp_internal.h"
+
+namespace vp {
+
+int hip_fail(hipError_t e, const char *what, const char *file, int line) {
+  if (getenv("VIGPATH_DEBUG"))
+    fprintf(stderr, "vigpath: %s failed: %s (%s:%d)\n", what,
+            hipGetErrorString(e), file, line);
+  return e == hipErrorOutOfMemory ? VP_ENOMEM : VP_EIO;
+}
+
+int nat_process_device(vp_ctx *c, const vp_dev_batch *b);
+int nat_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *keys);
+void build_flowid_tables(std::vector<uint32_t> &tab);
+
+static bool is_pow2(uint32_t v) { return v && !(v & (v - 1)); }
+
+template <class T>
+static int dalloc(T **p, size_t count) {
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc((void **)p, sizeof(T) * count);
+  return e == hipSuccess ? 0 : hip_fail(e, "hipMalloc", __FILE__, __LINE__);
+}
+
+int ws_reserve(vp_ctx *c, uint32_t n) {
+  Workspace &w = c->ws;
+  if (n <= w.cap_n) return 0;
+  uint32_t cap = std::max<uint32_t>(n, 1024);
+  hipFree(w.miss);
+  hipFree(w.miss_sorted);
+  hipFree(w.defer);
+  hipFree(w.mkey);
+  hipFree(w.mhash);
+  hipFree(w.first);
+  hipFree(w.rank);
+  hipFree(w.rep);
+  hipFree(w.assign);
+  hipFree(w.scratch);
+  int rc = 0;
+  uint64_t ss = 1;
+  while (ss < 2ull * cap) ss <<= 1;
+  if ((rc = dalloc(&w.miss, cap)) || (rc = dalloc(&w.miss_sorted, cap)) ||
+      (rc = dalloc(&w.defer, cap)) || (rc = dalloc(&w.mkey, 4ull * cap)) ||
+      (rc = dalloc(&w.mhash, cap)) || (rc = dalloc(&w.first, cap)) ||
+      (rc = dalloc(&w.rank, cap)) || (rc = dalloc(&w.rep, cap)) ||
+      (rc = dalloc(&w.assign, cap)) || (rc = dalloc(&w.scratch, ss))) {
+    w.cap_n = 0;
+    return rc;
+  }
+  w.cap_n = cap;
+  return 0;
+}
+
+static int table_alloc(vp_ctx *c, uint32_t cap) {
+  FlowTable &t = c->ft;
+  // >= 2x the index range: load factor <= 1/2 (+ tombstones <= 1/4, rebuild)
+  uint64_t ns = 1024;
+  while (ns < 2ull * cap) ns <<= 1;
+  t.tmask = (uint32_t)(ns - 1);
+  t.cap = cap;
+  int rc;
+  if ((rc = dalloc(&t.slots, ns)) || (rc = dalloc(&t.slot_of, cap)) ||
+      (rc = dalloc(&t.birth, cap)) || (rc = dalloc(&t.tseq, cap)) ||
+      (rc = dalloc(&t.stack, cap)) || (rc = dalloc(&t.ctl, 1)))
+    return rc;
+  VP_HIP(hipMemset(t.slots, 0xFF, sizeof(FlowSlot) * ns));
+  VP_HIP(hipMemset(t.slot_of, 0xFF, sizeof(uint32_t) * (size_t)cap));
+  VP_HIP(hipMemset(t.birth, 0, sizeof(uint64_t) * (size_t)cap));
+  VP_HIP(hipMemset(t.tseq, 0, sizeof(uint64_t) * (size_t)cap));
+  VP_HIP(hipMemset(t.ctl, 0, sizeof(Ctl)));
+  Workspace &w = c->ws;
+  w.exp_cap = cap;
+  if ((rc = dalloc(&w.ekey, cap)) || (rc = dalloc(&w.ekey2, cap)) ||
+      (rc = dalloc(&w.eidx, cap)) || (rc = dalloc(&w.eidx2, cap)))
+    return rc;
+  t.ts_floor = ~0ull;
+  return 0;
+}
+
+static void mac_words(const uint8_t d[6], const uint8_t s[6], uint32_t w[3]) {
+  uint8_t b[12];
+  memcpy(b, d, 6);
+  memcpy(b + 6, s, 6);
+  for (int k = 0; k < 3; k++)
+    w[k] = b[4 * k] | (b[4 * k + 1] << 8) | (b[4 * k + 2] << 16) |
+           ((uint32_t)b[4 * k + 3] << 24);
+}
+
+static int ctx_common(vp_ctx *c, int gpu) {
+  c->gpu = gpu;
+  VP_HIP(hipSetDevice(gpu));
+  VP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  VP_HIP(hipEventCreate(&c->ev0));
+  VP_HIP(hipEventCreate(&c->ev1));
+  return 0;
+}
+
+static void free_all(vp_ctx *c) {
+  if (!c) return;
+  if (c->gpu >= 0) hipSetDevice(c->gpu);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  FlowTable &t = c->ft;
+  hipFree(t.slots);
+  hipFree(t.slot_of);
+  hipFree(t.birth);
+  hipFree(t.tseq);
+  hipFree(t.stack);
+  hipFree(t.ctl);
+  Workspace &w = c->ws;
+  void *ptrs[] = {w.miss, w.miss_sorted, w.defer, w.mkey, w.mhash, w.first,
+                  w.rank, w.rep, w.assign, w.scratch, w.cub_tmp, w.ekey,
+                  w.ekey2, w.eidx, w.eidx2, w.d_frames, w.d_len, w.d_in,
+                  w.d_out, w.d_now, c->crc_tab, c->macw};
+  for (void *p : ptrs) hipFree(p);
+  if (w.h_frames) hipHostFree(w.h_frames);
+  if (c->ev0) hipEventDestroy(c->ev0);
+  if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+}  // namespace vp
+
+using namespace vp;
+
+extern "C" {
+
+const char *vp_version(void) { return "vigpath 0.1 gfx950"; }
+
+int vp_nat_create(const vp_nat_config *cfg, int gpu, vp_ctx **out) {
+  if (!cfg || !out) return VP_EINVAL;
+  // nat_config.c / map.c:73: power-of-two capacity, known devices
+  if (!is_pow2(cfg->max_flows) || cfg->n_devices == 0 ||
+      cfg->n_devices > VP_MAX_DEVICES || cfg->wan_device >= cfg->n_devices ||
+      cfg->max_flows > (1u << 30))
+    return VP_EINVAL;
+  vp_ctx *c = new vp_ctx();
+  c->kind = KIND_NAT;
+  c->nat = *cfg;
+  int rc = ctx_common(c, gpu);
+  if (!rc) rc = table_alloc(c, cfg->max_flows);
+  if (!rc) {
+    std::vector<uint32_t> tab;
+    build_flowid_tables(tab);
+    rc = dalloc(&c->crc_tab, tab.size());
+    if (!rc && hipMemcpy(c->crc_tab, tab.data(), tab.size() * 4,
+                         hipMemcpyHostToDevice) != hipSuccess)
+      rc = VP_EIO;
+  }
+  if (!rc) {
+    std::vector<uint32_t> mw(3 * VP_MAX_DEVICES, 0);
+    for (int d = 0; d < cfg->n_devices; d++)
+      mac_words(cfg->endpoint_macs[d], cfg->device_macs[d], &mw[3 * d]);
+    memcpy(c->wan_macw, &mw[3 * cfg->wan_device], sizeof c->wan_macw);
+    rc = dalloc(&c->macw, mw.size());
+    if (!rc && hipMemcpy(c->macw, mw.data(), mw.size() * 4,
+                         hipMemcpyHostToDevice) != hipSuccess)
+      rc = VP_EIO;
+  }
+  if (rc) {
+    free_all(c);
+    return rc;
+  }
+  *out = c;
+  return 0;
+}
+
+int vp_bridge_create(const vp_bridge_config *cfg, int gpu, vp_ctx **out) {
+  (void)cfg;
+  (void)gpu;
+  (void)out;
+  return VP_ENOTSUP;
+}
+
+int vp_lb_create(const vp_lb_config *cfg, int gpu, vp_ctx **out) {
+  (void)cfg;
+  (void)gpu;
+  (void)out;
+  return VP_ENOTSUP;
+}
+
+void vp_destroy(vp_ctx *ctx) { free_all(ctx); }
+
+int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
+  if (!c || !b) return VP_EINVAL;
+  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  hipStream_t user = (hipStream_t)stream;
+  hipEvent_t dep = nullptr;
+  if (user && user != c->stream) {  // order after the caller's stream
+    VP_HIP(hipEventCreateWithFlags(&dep, hipEventDisableTiming));
+    VP_HIP(hipEventRecord(dep, user));
+    VP_HIP(hipStreamWaitEvent(c->stream, dep, 0));
+  }
+  int rc = VP_ENOTSUP;
+  switch (c->kind) {
+    case KIND_NAT:
+      rc = nat_process_device(c, b);
+      break;
+    default:
+      break;
+  }
+  if (dep) {
+    hipEventRecord(dep, c->stream);
+    hipStreamWaitEvent(user, dep, 0);
+    hipEventDestroy(dep);
+  }
+  return rc;
+}
+
+static int stage_meta(vp_ctx *c, uint32_t n) {
+  Workspace &w = c->ws;
+  if (n <= w.d_meta_n) return 0;
+  hipFree(w.d_len);
+  hipFree(w.d_in);
+  hipFree(w.d_out);
+  hipFree(w.d_now);
+  int rc;
+  if ((rc = dalloc(&w.d_len, n)) || (rc = dalloc(&w.d_in, n)) ||
+      (rc = dalloc(&w.d_out, n)) || (rc = dalloc(&w.d_now, n))) {
+    w.d_meta_n = 0;
+    return rc;
+  }
+  w.d_meta_n = n;
+  return 0;
+}
+
+static int stage_frames(vp_ctx *c, size_t bytes) {
+  Workspace &w = c->ws;
+  if (bytes > w.d_frames_bytes) {
+    hipFree(w.d_frames);
+    w.d_frames = nullptr;
+    w.d_frames_bytes = 0;
+    VP_HIP(hipMalloc((void **)&w.d_frames, bytes));
+    w.d_frames_bytes = bytes;
+  }
+  if (bytes > w.h_frames_bytes) {
+    if (w.h_frames) hipHostFree(w.h_frames);
+    w.h_frames = nullptr;
+    w.h_frames_bytes = 0;
+    VP_HIP(hipHostMalloc((void **)&w.h_frames, bytes, hipHostMallocDefault));
+    w.h_frames_bytes = bytes;
+  }
+  return 0;
+}
+
+static int run_staged(vp_ctx *c, uint32_t n, uint32_t slot, const uint16_t *in_dev,
+                      const uint16_t *len, const int64_t *now, uint16_t *out_dev) {
+  Workspace &w = c->ws;
+  VP_HIP(hipMemcpyAsync(w.d_frames, w.h_frames, (size_t)n * slot,
+                        hipMemcpyHostToDevice, c->stream));
+  VP_HIP(hipMemcpyAsync(w.d_len, len, 2ull * n, hipMemcpyHostToDevice, c->stream));
+  VP_HIP(hipMemcpyAsync(w.d_in, in_dev, 2ull * n, hipMemcpyHostToDevice, c->stream));
+  VP_HIP(hipMemcpyAsync(w.d_now, now, 8ull * n, hipMemcpyHostToDevice, c->stream));
+  vp_dev_batch b{};
+  b.frames = w.d_frames;
+  b.slot = slot;
+  b.n = n;
+  b.len = w.d_len;
+  b.in_dev = w.d_in;
+  b.now = w.d_now;
+  b.out_dev = w.d_out;
+  int rc = vp_process_device(c, &b, nullptr);
+  if (rc) return rc;
+  VP_HIP(hipMemcpyAsync(w.h_frames, w.d_frames, (size_t)n * slot,
+                        hipMemcpyDeviceToHost, c->stream));
+  VP_HIP(hipMemcpyAsync(out_dev, w.d_out, 2ull * n, hipMemcpyDeviceToHost, c->stream));
+  VP_HIP(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int vp_process_host(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
+                    uint8_t *frames, uint32_t slot, const uint16_t *len,
+                    const int64_t *now, uint16_t *out_dev) {
+  if (!c || (n && (!in_dev || !frames || !len || !now || !out_dev)))
+    return VP_EINVAL;
+  if (n == 0) return 0;
+  if (slot < 64 || (slot & 15)) return VP_EINVAL;
+  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  int rc = stage_meta(c, n);
+  if (!rc) rc = stage_frames(c, (size_t)n * slot);
+  if (rc) return rc;
+  memcpy(c->ws.h_frames, frames, (size_t)n * slot);
+  rc = run_staged(c, n, slot, in_dev, len, now, out_dev);
+  if (rc) return rc;
+  memcpy(frames, c->ws.h_frames, (size_t)n * slot);
+  return 0;
+}
+
+int vp_process_batch(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
+                     uint8_t *const *frames, const uint16_t *len,
+                     const int64_t *now, uint16_t *out_dev) {
+  if (!c || (n && (!in_dev || !frames || !len || !now || !out_dev)))
+    return VP_EINVAL;
+  if (n == 0) return 0;
+  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  uint32_t maxlen = 64;
+  for (uint32_t i = 0; i < n; i++) maxlen = std::max<uint32_t>(maxlen, len[i]);
+  const uint32_t slot = (maxlen + 15) & ~15u;
+  int rc = stage_meta(c, n);
+  if (!rc) rc = stage_frames(c, (size_t)n * slot);
+  if (rc) return rc;
+  uint8_t *h = c->ws.h_frames;
+  for (uint32_t i = 0; i < n; i++) {  // gather mbuf data into slots
+    memcpy(h + (size_t)i * slot, frames[i], len[i]);
+    memset(h + (size_t)i * slot + len[i], 0, slot - len[i]);
+  }
+  rc = run_staged(c, n, slot, in_dev, len, now, out_dev);
+  if (rc) return rc;
+  for (uint32_t i = 0; i < n; i++)  // scatter back in place
+    memcpy(frames[i], h + (size_t)i * slot, len[i]);
+  return 0;
+}
+
+int vp_nat_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *keys) {
+  if (!c || c->kind != KIND_NAT || !alloc || !ts || !keys) return VP_EINVAL;
+  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  return nat_dump(c, alloc, ts, keys);
+}
+
+int64_t vp_live_count(vp_ctx *c) {
+  if (!c) return VP_EINVAL;
+  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  Ctl h{};
+  if (hipMemcpy(&h, c->ft.ctl, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)
+    return VP_EIO;
+  return h.n_live;
+}
+
+int vp_last_kernel_ms(vp_ctx *c, float *ms, int *launches) {
+  if (!c || !ms || !launches) return VP_EINVAL;
+  *ms = c->last_ms;
+  *launches = c->last_launches;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,146 @@
+"""NF instances on the GPU: the batch form of the reference operator
+`int nf_process(uint16_t device, uint8_t *buffer, uint16_t len, vigor_time_t
+now)` (nf.h:13), driven the way nf.c's loop drives it (nf.c:150-176).
+
+`process_device` takes torch tensors already in HBM; `process_host` takes
+numpy arrays and stages them through pinned memory (hipMemcpyAsync);
+`process` is the per-packet nf_process equivalent (one-packet batch).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import (BridgeConfigC, DevBatchC, LbConfigC, NatConfigC, _check, lib)
+
+
+def _dptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class NfBase:
+    kind = "?"
+
+    def __init__(self):
+        self.h = C.c_void_p()
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().vp_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --------------------------------------------------------- device --
+    def process_device(self, frames, lens, in_dev, out, slot: int, now=None,
+                       now0: int = 0, now_step: int = 0, stream=None):
+        """frames: uint8 CUDA tensor of n*slot bytes (mutated in place);
+        lens/in_dev/out: int16/uint16-sized CUDA tensors of n; now: int64
+        CUDA tensor of n, or None for now0 + i*now_step."""
+        n = lens.numel()
+        assert frames.numel() == n * slot and frames.is_cuda
+        b = DevBatchC(frames=frames.data_ptr(), slot=slot, n=n,
+                      len=lens.data_ptr(), in_dev=in_dev.data_ptr(),
+                      now=now.data_ptr() if now is not None else None,
+                      now0=now0, now_step=now_step, out_dev=out.data_ptr())
+        s = C.c_void_p(stream.cuda_stream) if stream is not None else None
+        _check(lib().vp_process_device(self.h, C.byref(b), s),
+               "vp_process_device")
+
+    def last_kernel_ms(self):
+        ms, k = C.c_float(), C.c_int()
+        _check(lib().vp_last_kernel_ms(self.h, C.byref(ms), C.byref(k)),
+               "vp_last_kernel_ms")
+        return ms.value, k.value
+
+    def live_count(self) -> int:
+        v = lib().vp_live_count(self.h)
+        if v < 0:
+            _check(int(v), "vp_live_count")
+        return int(v)
+
+    # ----------------------------------------------------------- host --
+    def process_host(self, frames: np.ndarray, lens, in_dev, now, slot: int):
+        """Contiguous host batch; frames (u8, n*slot) rewritten in place.
+        Returns out_dev (u16)."""
+        n = int(lens.shape[0])
+        assert frames.dtype == np.uint8 and frames.flags.c_contiguous
+        assert frames.size == n * slot
+        lens = np.ascontiguousarray(lens, np.uint16)
+        in_dev = np.ascontiguousarray(in_dev, np.uint16)
+        now = np.ascontiguousarray(now, np.int64)
+        out = np.zeros(n, np.uint16)
+        P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
+        _check(lib().vp_process_host(self.h, n, P(in_dev), P(frames), slot,
+                                     P(lens), P(now), P(out)),
+               "vp_process_host")
+        return out
+
+    def process_mbufs(self, bufs, in_dev, now):
+        """Per-frame host buffers (bytearray each, mbuf-like), rewritten in
+        place. Returns out_dev."""
+        n = len(bufs)
+        ptrs = (C.c_void_p * n)()
+        arrs = []
+        lens = np.zeros(n, np.uint16)
+        for i, b in enumerate(bufs):
+            a = (C.c_uint8 * len(b)).from_buffer(b)
+            arrs.append(a)
+            ptrs[i] = C.cast(a, C.c_void_p)
+            lens[i] = len(b)
+        in_dev = np.ascontiguousarray(in_dev, np.uint16)
+        now = np.ascontiguousarray(now, np.int64)
+        out = np.zeros(n, np.uint16)
+        P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
+        _check(lib().vp_process_batch(self.h, n, P(in_dev), ptrs, P(lens),
+                                      P(now), P(out)), "vp_process_batch")
+        return out
+
+    def process(self, device: int, buffer: bytearray, now: int) -> int:
+        """nf_process for one packet (nf.h:13)."""
+        return int(self.process_mbufs([buffer], [device], [now])[0])
+
+
+class Nat(NfBase):
+    kind = "nat"
+
+    def __init__(self, cfg: NatConfigC, gpu: int = 0):
+        super().__init__()
+        self.cfg = cfg
+        _check(lib().vp_nat_create(C.byref(cfg), gpu, C.byref(self.h)),
+               "vp_nat_create")
+
+    def dump(self):
+        n = self.cfg.max_flows
+        alloc = np.zeros(n, np.uint8)
+        ts = np.zeros(n, np.int64)
+        keys = np.zeros(n * 16, np.uint8)
+        P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
+        _check(lib().vp_nat_dump(self.h, P(alloc), P(ts), P(keys)),
+               "vp_nat_dump")
+        return alloc, ts, keys.reshape(n, 16)
+
+
+class Bridge(NfBase):
+    kind = "bridge"
+
+    def __init__(self, cfg: BridgeConfigC, gpu: int = 0):
+        super().__init__()
+        self.cfg = cfg
+        _check(lib().vp_bridge_create(C.byref(cfg), gpu, C.byref(self.h)),
+               "vp_bridge_create")
+
+
+class Lb(NfBase):
+    kind = "lb"
+
+    def __init__(self, cfg: LbConfigC, gpu: int = 0):
+        super().__init__()
+        self.cfg = cfg
+        _check(lib().vp_lb_create(C.byref(cfg), gpu, C.byref(self.h)),
+               "vp_lb_create")
