@@ -1,0 +1,59 @@
+"""Diagnostic: where does nat_classify's time go? Runs the steady-state
+config-2 step on the product build and on ablation builds
+(vigor_amd/abl/libvigpath_<X>.so, `make -C vigor_amd/csrc ablate`) in one
+process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24), and
+prints kernel time per variant. Ablated builds compute wrong results and are
+never used for anything else."""
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import vigor_amd  # noqa: E402
+from vigor_amd import traces as T  # noqa: E402
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    B, NF = 1 << 24, 1 << 20
+    dev = torch.device("cuda:0")
+    variants = {"full": None}
+    for v in ("NOSTORE", "FULLSTORE", "NOPROBE", "NT"):
+        p = os.path.join(ROOT, "vigor_amd", "abl", "libvigpath_%s.so" % v)
+        if os.path.exists(p):
+            variants[v] = p
+    bank = bench.FlowBank(NF, 0, dev)
+    lens = torch.full((B,), 60, dtype=torch.int16, device=dev)
+    ind = torch.zeros(B, dtype=torch.int16, device=dev)
+    out = torch.zeros(B, dtype=torch.int16, device=dev)
+    buf = torch.empty(B * 64, dtype=torch.uint8, device=dev)
+    nfs = {}
+    for name, path in variants.items():
+        cfg = vigor_amd.nat_config_from_args(
+            bench.NAT_ARGS + ["--max-flows", str(NF)], 2, bench.DEV_MACS)
+        nat = vigor_amd.Nat(cfg, 0, libpath=path)
+        bank.fill(buf, 0)
+        nat.process_device(buf, lens, ind, out, 64, now0=T.NOW0, now_step=1)
+        nfs[name] = nat
+    res = {k: [] for k in nfs}
+    start = B
+    for r in range(rounds):
+        for name, nat in nfs.items():
+            bank.fill(buf, start)
+            torch.cuda.synchronize()
+            nat.process_device(buf, lens, ind, out, 64, now0=T.NOW0 + start,
+                               now_step=1)
+            res[name].append(nat.last_kernel_ms()[0])
+        start += B
+    for name, v in res.items():
+        med = statistics.median(v)
+        print("%-11s median %.3f ms  min %.3f ms  -> %.2f Gpps" %
+              (name, med, min(v), B / med / 1e6))
+
+
+if __name__ == "__main__":
+    main()

@@ -73,17 +73,18 @@ EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_destroy",
            "vp_process_device", "vp_process_batch", "vp_process_host",
            "vp_nat_dump", "vp_live_count", "vp_last_kernel_ms", "vp_version"]
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    """Load libvigpath.so; raises if it has not been built."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError(f"{LIB_PATH} missing: run __graft_entry__.build()")
-    L = C.CDLL(LIB_PATH)
+def lib(path: str | None = None):
+    """Load libvigpath.so (or, for diagnostics, another build of the same
+    ABI); raises if it has not been built."""
+    path = path or LIB_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} missing: run __graft_entry__.build()")
+    L = C.CDLL(path)
     L.vp_version.restype = C.c_char_p
     for name in ("vp_nat_create", "vp_bridge_create", "vp_lb_create"):
         getattr(L, name).restype = C.c_int
@@ -113,7 +114,7 @@ def lib():
     L.vp_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float),
                                     C.POINTER(C.c_int)]
     L.vp_last_kernel_ms.restype = C.c_int
-    _lib = L
+    _libs[path] = L
     return L
 
 

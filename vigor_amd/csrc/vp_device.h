@@ -215,15 +215,13 @@ inline void build_position_table(uint32_t *tab, int pos, int msg_len) {
 }
 
 // ------------------------------------------------------------- flow slot --
-// One open-addressing slot of the device flow table, 32 B (one half of a
-// 64-byte memory request). The key is stored in the slot so a hit costs one
-// random line. ts is the libVig dchain timestamp of the flow index stored
-// here (double-chain.c:16-19 keeps it per index; the GPU keeps it per slot).
+// One open-addressing slot of a device table, 32 B (half of a 64-byte memory
+// request): the key is stored in the slot so a hit costs one random line.
 struct __align__(32) FlowSlot {
-  uint32_t k[4];  // 16 key bytes, reference struct layout, padding zero
+  uint32_t k[4];   // 16 key bytes, reference struct layout, padding zero
   uint32_t hash;
   uint32_t index;  // kEmpty / kTomb / dchain index
-  uint64_t ts;     // vigor_time_t, >= 0
+  uint32_t pad[2];
 };
 
 __device__ inline bool key_eq(const uint32_t a[4], const uint32_t b[4]) {

@@ -8,7 +8,7 @@
 #include <cstring>
 #include <vector>
 
-#include "vp_internal.h"
+#include "vp_table.h"
 
 namespace vp {
 
@@ -32,58 +32,47 @@ static int dalloc(T **p, size_t count) {
   return e == hipSuccess ? 0 : hip_fail(e, "hipMalloc", __FILE__, __LINE__);
 }
 
+__global__ void iota_k(uint32_t *v, uint32_t n) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += gridDim.x * blockDim.x)
+    v[i] = i;
+}
+
+static void ws_release(Workspace &w) {
+  void *ptrs[] = {w.miss,  w.miss_sorted, w.defer, w.mkey, w.mhash,
+                  w.first, w.rank,        w.rep,   w.assign, w.scratch,
+                  w.log,   w.iota,        w.skey,  w.sval};
+  for (void *p : ptrs) hipFree(p);
+  w.miss = w.miss_sorted = w.defer = w.mkey = w.mhash = w.first = w.rank =
+      w.rep = w.assign = w.scratch = w.log = w.iota = w.skey = w.sval = nullptr;
+  w.cap_n = 0;
+}
+
+// Per-batch scratch sized for the largest batch seen so far.
 int ws_reserve(vp_ctx *c, uint32_t n) {
   Workspace &w = c->ws;
   if (n <= w.cap_n) return 0;
-  uint32_t cap = std::max<uint32_t>(n, 1024);
-  hipFree(w.miss);
-  hipFree(w.miss_sorted);
-  hipFree(w.defer);
-  hipFree(w.mkey);
-  hipFree(w.mhash);
-  hipFree(w.first);
-  hipFree(w.rank);
-  hipFree(w.rep);
-  hipFree(w.assign);
-  hipFree(w.scratch);
-  int rc = 0;
-  uint64_t ss = 1;
-  while (ss < 2ull * cap) ss <<= 1;
-  if ((rc = dalloc(&w.miss, cap)) || (rc = dalloc(&w.miss_sorted, cap)) ||
-      (rc = dalloc(&w.defer, cap)) || (rc = dalloc(&w.mkey, 4ull * cap)) ||
-      (rc = dalloc(&w.mhash, cap)) || (rc = dalloc(&w.first, cap)) ||
-      (rc = dalloc(&w.rank, cap)) || (rc = dalloc(&w.rep, cap)) ||
-      (rc = dalloc(&w.assign, cap)) || (rc = dalloc(&w.scratch, ss))) {
-    w.cap_n = 0;
-    return rc;
-  }
+  VP_HIP(hipStreamSynchronize(c->stream));
+  ws_release(w);
+  const uint32_t cap = std::max<uint32_t>(n, 1024);
+  const uint64_t ss = next_pow2(2ull * cap);
+  VP_TRY(dalloc(&w.miss, cap));
+  VP_TRY(dalloc(&w.miss_sorted, cap));
+  VP_TRY(dalloc(&w.defer, cap));
+  VP_TRY(dalloc(&w.mkey, 4ull * cap));
+  VP_TRY(dalloc(&w.mhash, cap));
+  VP_TRY(dalloc(&w.first, cap));
+  VP_TRY(dalloc(&w.rank, cap));
+  VP_TRY(dalloc(&w.rep, cap));
+  VP_TRY(dalloc(&w.assign, cap));
+  VP_TRY(dalloc(&w.scratch, ss));
+  VP_TRY(dalloc(&w.log, cap));
+  VP_TRY(dalloc(&w.iota, cap));
+  VP_TRY(dalloc(&w.skey, cap));
+  VP_TRY(dalloc(&w.sval, cap));
+  iota_k<<<grid_for(cap), 256, 0, c->stream>>>(w.iota, cap);
+  VP_HIP(hipGetLastError());
   w.cap_n = cap;
-  return 0;
-}
-
-static int table_alloc(vp_ctx *c, uint32_t cap) {
-  FlowTable &t = c->ft;
-  // >= 2x the index range: load factor <= 1/2 (+ tombstones <= 1/4, rebuild)
-  uint64_t ns = 1024;
-  while (ns < 2ull * cap) ns <<= 1;
-  t.tmask = (uint32_t)(ns - 1);
-  t.cap = cap;
-  int rc;
-  if ((rc = dalloc(&t.slots, ns)) || (rc = dalloc(&t.slot_of, cap)) ||
-      (rc = dalloc(&t.birth, cap)) || (rc = dalloc(&t.tseq, cap)) ||
-      (rc = dalloc(&t.stack, cap)) || (rc = dalloc(&t.ctl, 1)))
-    return rc;
-  VP_HIP(hipMemset(t.slots, 0xFF, sizeof(FlowSlot) * ns));
-  VP_HIP(hipMemset(t.slot_of, 0xFF, sizeof(uint32_t) * (size_t)cap));
-  VP_HIP(hipMemset(t.birth, 0, sizeof(uint64_t) * (size_t)cap));
-  VP_HIP(hipMemset(t.tseq, 0, sizeof(uint64_t) * (size_t)cap));
-  VP_HIP(hipMemset(t.ctl, 0, sizeof(Ctl)));
-  Workspace &w = c->ws;
-  w.exp_cap = cap;
-  if ((rc = dalloc(&w.ekey, cap)) || (rc = dalloc(&w.ekey2, cap)) ||
-      (rc = dalloc(&w.eidx, cap)) || (rc = dalloc(&w.eidx2, cap)))
-    return rc;
-  t.ts_floor = ~0ull;
   return 0;
 }
 
@@ -107,20 +96,13 @@ static int ctx_common(vp_ctx *c, int gpu) {
 
 static void free_all(vp_ctx *c) {
   if (!c) return;
-  if (c->gpu >= 0) hipSetDevice(c->gpu);
+  hipSetDevice(c->gpu);
   if (c->stream) hipStreamSynchronize(c->stream);
-  FlowTable &t = c->ft;
-  hipFree(t.slots);
-  hipFree(t.slot_of);
-  hipFree(t.birth);
-  hipFree(t.tseq);
-  hipFree(t.stack);
-  hipFree(t.ctl);
+  tbl_free(c->ft);
   Workspace &w = c->ws;
-  void *ptrs[] = {w.miss, w.miss_sorted, w.defer, w.mkey, w.mhash, w.first,
-                  w.rank, w.rep, w.assign, w.scratch, w.cub_tmp, w.ekey,
-                  w.ekey2, w.eidx, w.eidx2, w.d_frames, w.d_len, w.d_in,
-                  w.d_out, w.d_now, c->crc_tab, c->macw};
+  ws_release(w);
+  void *ptrs[] = {w.cub_tmp, w.d_frames, w.d_len,    w.d_in,
+                  w.d_out,   w.d_now,    c->crc_tab, c->macw};
   for (void *p : ptrs) hipFree(p);
   if (w.h_frames) hipHostFree(w.h_frames);
   if (c->ev0) hipEventDestroy(c->ev0);
@@ -129,44 +111,82 @@ static void free_all(vp_ctx *c) {
   delete c;
 }
 
+static int upload(uint32_t **dst, const std::vector<uint32_t> &v) {
+  VP_TRY(dalloc(dst, v.size()));
+  VP_HIP(hipMemcpy(*dst, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+  return 0;
+}
+
+static int nat_init(vp_ctx *c, const vp_nat_config *cfg) {
+  c->kind = KIND_NAT;
+  c->nat = *cfg;
+  VP_TRY(tbl_alloc(c, c->ft, cfg->max_flows));
+  std::vector<uint32_t> tab;
+  build_flowid_tables(tab);
+  VP_TRY(upload(&c->crc_tab, tab));
+  std::vector<uint32_t> mw(3 * VP_MAX_DEVICES, 0);
+  for (int d = 0; d < cfg->n_devices; d++)
+    mac_words(cfg->endpoint_macs[d], cfg->device_macs[d], &mw[3 * d]);
+  memcpy(c->wan_macw, &mw[3 * cfg->wan_device], sizeof c->wan_macw);
+  VP_TRY(upload(&c->macw, mw));
+  return 0;
+}
+
+static int stage_meta(vp_ctx *c, uint32_t n) {
+  Workspace &w = c->ws;
+  if (n <= w.d_meta_n) return 0;
+  hipFree(w.d_len);
+  hipFree(w.d_in);
+  hipFree(w.d_out);
+  hipFree(w.d_now);
+  w.d_len = w.d_in = w.d_out = nullptr;
+  w.d_now = nullptr;
+  w.d_meta_n = 0;
+  VP_TRY(dalloc(&w.d_len, n));
+  VP_TRY(dalloc(&w.d_in, n));
+  VP_TRY(dalloc(&w.d_out, n));
+  VP_TRY(dalloc(&w.d_now, n));
+  w.d_meta_n = n;
+  return 0;
+}
+
+static int stage_frames(vp_ctx *c, size_t bytes) {
+  Workspace &w = c->ws;
+  if (bytes > w.d_frames_bytes) {
+    hipFree(w.d_frames);
+    w.d_frames = nullptr;
+    w.d_frames_bytes = 0;
+    VP_HIP(hipMalloc((void **)&w.d_frames, bytes));
+    w.d_frames_bytes = bytes;
+  }
+  if (bytes > w.h_frames_bytes) {
+    if (w.h_frames) hipHostFree(w.h_frames);
+    w.h_frames = nullptr;
+    w.h_frames_bytes = 0;
+    VP_HIP(hipHostMalloc((void **)&w.h_frames, bytes, hipHostMallocDefault));
+    w.h_frames_bytes = bytes;
+  }
+  return 0;
+}
+
 }  // namespace vp
 
 using namespace vp;
 
 extern "C" {
 
-const char *vp_version(void) { return "vigpath 0.1 gfx950"; }
+const char *vp_version(void) { return "vigpath 0.2 gfx950"; }
 
 int vp_nat_create(const vp_nat_config *cfg, int gpu, vp_ctx **out) {
   if (!cfg || !out) return VP_EINVAL;
-  // nat_config.c / map.c:73: power-of-two capacity, known devices
+  // map.c:73 (CAPACITY_POW2): power-of-two capacity; nat_config.c: devices
   if (!is_pow2(cfg->max_flows) || cfg->n_devices == 0 ||
       cfg->n_devices > VP_MAX_DEVICES || cfg->wan_device >= cfg->n_devices ||
       cfg->max_flows > (1u << 30))
     return VP_EINVAL;
   vp_ctx *c = new vp_ctx();
-  c->kind = KIND_NAT;
-  c->nat = *cfg;
   int rc = ctx_common(c, gpu);
-  if (!rc) rc = table_alloc(c, cfg->max_flows);
-  if (!rc) {
-    std::vector<uint32_t> tab;
-    build_flowid_tables(tab);
-    rc = dalloc(&c->crc_tab, tab.size());
-    if (!rc && hipMemcpy(c->crc_tab, tab.data(), tab.size() * 4,
-                         hipMemcpyHostToDevice) != hipSuccess)
-      rc = VP_EIO;
-  }
-  if (!rc) {
-    std::vector<uint32_t> mw(3 * VP_MAX_DEVICES, 0);
-    for (int d = 0; d < cfg->n_devices; d++)
-      mac_words(cfg->endpoint_macs[d], cfg->device_macs[d], &mw[3 * d]);
-    memcpy(c->wan_macw, &mw[3 * cfg->wan_device], sizeof c->wan_macw);
-    rc = dalloc(&c->macw, mw.size());
-    if (!rc && hipMemcpy(c->macw, mw.data(), mw.size() * 4,
-                         hipMemcpyHostToDevice) != hipSuccess)
-      rc = VP_EIO;
-  }
+  if (!rc) rc = nat_init(c, cfg);
   if (rc) {
     free_all(c);
     return rc;
@@ -217,42 +237,6 @@ int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
   return rc;
 }
 
-static int stage_meta(vp_ctx *c, uint32_t n) {
-  Workspace &w = c->ws;
-  if (n <= w.d_meta_n) return 0;
-  hipFree(w.d_len);
-  hipFree(w.d_in);
-  hipFree(w.d_out);
-  hipFree(w.d_now);
-  int rc;
-  if ((rc = dalloc(&w.d_len, n)) || (rc = dalloc(&w.d_in, n)) ||
-      (rc = dalloc(&w.d_out, n)) || (rc = dalloc(&w.d_now, n))) {
-    w.d_meta_n = 0;
-    return rc;
-  }
-  w.d_meta_n = n;
-  return 0;
-}
-
-static int stage_frames(vp_ctx *c, size_t bytes) {
-  Workspace &w = c->ws;
-  if (bytes > w.d_frames_bytes) {
-    hipFree(w.d_frames);
-    w.d_frames = nullptr;
-    w.d_frames_bytes = 0;
-    VP_HIP(hipMalloc((void **)&w.d_frames, bytes));
-    w.d_frames_bytes = bytes;
-  }
-  if (bytes > w.h_frames_bytes) {
-    if (w.h_frames) hipHostFree(w.h_frames);
-    w.h_frames = nullptr;
-    w.h_frames_bytes = 0;
-    VP_HIP(hipHostMalloc((void **)&w.h_frames, bytes, hipHostMallocDefault));
-    w.h_frames_bytes = bytes;
-  }
-  return 0;
-}
-
 static int run_staged(vp_ctx *c, uint32_t n, uint32_t slot, const uint16_t *in_dev,
                       const uint16_t *len, const int64_t *now, uint16_t *out_dev) {
   Workspace &w = c->ws;
@@ -269,11 +253,11 @@ static int run_staged(vp_ctx *c, uint32_t n, uint32_t slot, const uint16_t *in_d
   b.in_dev = w.d_in;
   b.now = w.d_now;
   b.out_dev = w.d_out;
-  int rc = vp_process_device(c, &b, nullptr);
-  if (rc) return rc;
+  VP_TRY(vp_process_device(c, &b, nullptr));
   VP_HIP(hipMemcpyAsync(w.h_frames, w.d_frames, (size_t)n * slot,
                         hipMemcpyDeviceToHost, c->stream));
-  VP_HIP(hipMemcpyAsync(out_dev, w.d_out, 2ull * n, hipMemcpyDeviceToHost, c->stream));
+  VP_HIP(hipMemcpyAsync(out_dev, w.d_out, 2ull * n, hipMemcpyDeviceToHost,
+                        c->stream));
   VP_HIP(hipStreamSynchronize(c->stream));
   return 0;
 }
@@ -286,12 +270,10 @@ int vp_process_host(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
   if (n == 0) return 0;
   if (slot < 64 || (slot & 15)) return VP_EINVAL;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
-  int rc = stage_meta(c, n);
-  if (!rc) rc = stage_frames(c, (size_t)n * slot);
-  if (rc) return rc;
+  VP_TRY(stage_meta(c, n));
+  VP_TRY(stage_frames(c, (size_t)n * slot));
   memcpy(c->ws.h_frames, frames, (size_t)n * slot);
-  rc = run_staged(c, n, slot, in_dev, len, now, out_dev);
-  if (rc) return rc;
+  VP_TRY(run_staged(c, n, slot, in_dev, len, now, out_dev));
   memcpy(frames, c->ws.h_frames, (size_t)n * slot);
   return 0;
 }
@@ -306,16 +288,14 @@ int vp_process_batch(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
   uint32_t maxlen = 64;
   for (uint32_t i = 0; i < n; i++) maxlen = std::max<uint32_t>(maxlen, len[i]);
   const uint32_t slot = (maxlen + 15) & ~15u;
-  int rc = stage_meta(c, n);
-  if (!rc) rc = stage_frames(c, (size_t)n * slot);
-  if (rc) return rc;
+  VP_TRY(stage_meta(c, n));
+  VP_TRY(stage_frames(c, (size_t)n * slot));
   uint8_t *h = c->ws.h_frames;
-  for (uint32_t i = 0; i < n; i++) {  // gather mbuf data into slots
+  for (uint32_t i = 0; i < n; i++) {  // gather the mbuf data into slots
     memcpy(h + (size_t)i * slot, frames[i], len[i]);
     memset(h + (size_t)i * slot + len[i], 0, slot - len[i]);
   }
-  rc = run_staged(c, n, slot, in_dev, len, now, out_dev);
-  if (rc) return rc;
+  VP_TRY(run_staged(c, n, slot, in_dev, len, now, out_dev));
   for (uint32_t i = 0; i < n; i++)  // scatter back in place
     memcpy(frames[i], h + (size_t)i * slot, len[i]);
   return 0;

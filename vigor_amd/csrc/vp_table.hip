@@ -1,0 +1,451 @@
+// Device table kernels + host orchestration (see vp_table.h).
+//
+// Reference semantics (paths relative to the reference repository):
+//   map_put / find_empty     libvig/verified/map-impl-pow2.c:1110-1217,2156-2222
+//   dchain alloc / free      double-chain-impl.c:1197-1415, 1839-2078
+//   dchain expire            double-chain.c:772-826 (strict ts < cutoff)
+//   expire_items_single_map  expirator.c:110-218
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+
+#include "vp_table.h"
+
+namespace vp {
+
+uint32_t grid_for(uint64_t n, uint32_t block, uint32_t max_blocks) {
+  uint64_t g = (n + block - 1) / block;
+  if (g == 0) g = 1;
+  return (uint32_t)(g < max_blocks ? g : max_blocks);
+}
+
+uint32_t next_pow2(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return (uint32_t)p;
+}
+
+int cub_reserve(vp_ctx *c, size_t bytes) {
+  Workspace &w = c->ws;
+  if (bytes <= w.cub_bytes) return 0;
+  if (w.cub_tmp) VP_HIP(hipFree(w.cub_tmp));
+  w.cub_tmp = nullptr;
+  w.cub_bytes = 0;
+  VP_HIP(hipMalloc(&w.cub_tmp, bytes));
+  w.cub_bytes = bytes;
+  return 0;
+}
+
+int read_ctl(vp_ctx *c, FlowTable &t) {
+  VP_HIP(hipMemcpyAsync(&t.h_ctl, t.ctl, sizeof(Ctl), hipMemcpyDeviceToHost,
+                        c->stream));
+  VP_HIP(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+TableDev tbl_dev(const FlowTable &t) {
+  return TableDev{t.slots, t.tmask, t.cap, t.slot_of, t.ts,
+                  t.tseq,  t.birth, t.stack, t.ctl};
+}
+
+template <class T>
+static int dalloc(T **p, size_t count) {
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc((void **)p, sizeof(T) * count);
+  return e == hipSuccess ? 0 : hip_fail(e, "hipMalloc", __FILE__, __LINE__);
+}
+
+int tbl_alloc(vp_ctx *c, FlowTable &t, uint32_t cap) {
+  (void)c;
+  // >= 2x the index range: load factor <= 1/2 (+ tombstones <= 1/4)
+  uint64_t ns = 1024;
+  while (ns < 2ull * cap) ns <<= 1;
+  t.tmask = (uint32_t)(ns - 1);
+  t.cap = cap;
+  VP_TRY(dalloc(&t.slots, ns));
+  VP_TRY(dalloc(&t.slot_of, cap));
+  VP_TRY(dalloc(&t.ts, cap));
+  VP_TRY(dalloc(&t.tseq, cap));
+  VP_TRY(dalloc(&t.birth, cap));
+  VP_TRY(dalloc(&t.stack, cap));
+  VP_TRY(dalloc(&t.ctl, 1));
+  VP_TRY(dalloc(&t.ekey, cap));
+  VP_TRY(dalloc(&t.ekey2, cap));
+  VP_TRY(dalloc(&t.eidx, cap));
+  VP_TRY(dalloc(&t.eidx2, cap));
+  VP_HIP(hipMemset(t.slots, 0xFF, sizeof(FlowSlot) * ns));
+  VP_HIP(hipMemset(t.slot_of, 0xFF, sizeof(uint32_t) * (size_t)cap));
+  VP_HIP(hipMemset(t.ts, 0, sizeof(uint64_t) * (size_t)cap));
+  VP_HIP(hipMemset(t.tseq, 0, sizeof(uint64_t) * (size_t)cap));
+  VP_HIP(hipMemset(t.birth, 0, sizeof(uint64_t) * (size_t)cap));
+  VP_HIP(hipMemset(t.ctl, 0, sizeof(Ctl)));
+  t.ts_floor = ~0ull;
+  return 0;
+}
+
+void tbl_free(FlowTable &t) {
+  void *ptrs[] = {t.slots, t.slot_of, t.ts,   t.tseq,  t.birth, t.stack,
+                  t.ctl,   t.ekey,    t.ekey2, t.eidx, t.eidx2};
+  for (void *p : ptrs) hipFree(p);
+  t = FlowTable{};
+}
+
+// ------------------------------------------------------------ new keys --
+
+struct NkArgs {
+  TableDev t;
+  const uint32_t *pos;
+  uint32_t n;
+  uint32_t *mkey, *mhash, *first, *rank, *rep, *assign, *scratch;
+  uint32_t smask;
+  uint64_t seq_base;
+};
+
+// In-batch de-duplication: one scratch slot per distinct key holding the
+// smallest miss ordinal (= earliest packet) with that key.
+__global__ void nk_dedup(NkArgs m) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m.n;
+       j += gridDim.x * blockDim.x) {
+    const uint32_t *kj = m.mkey + 4 * (size_t)j;
+    uint32_t s = m.mhash[j] & m.smask;
+    for (;;) {
+      uint32_t old = atomicCAS(&m.scratch[s], kEmpty, j);
+      if (old == kEmpty) break;
+      const uint32_t *ko = m.mkey + 4 * (size_t)old;
+      if (m.mhash[old] == m.mhash[j] && key_eq(ko, kj)) {
+        atomicMin(&m.scratch[s], j);
+        break;
+      }
+      s = (s + 1) & m.smask;
+    }
+    m.rep[j] = s;
+  }
+}
+
+__global__ void nk_first(NkArgs m) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m.n;
+       j += gridDim.x * blockDim.x)
+    m.first[j] = m.scratch[m.rep[j]] == j ? 1u : 0u;
+}
+
+// dchain_allocate_new_index for each first sighting in packet order: rank r
+// takes the r-th free-list entry (stack top first, then never-used indices),
+// then map_put of the key.
+__global__ void nk_alloc(NkArgs m) {
+  const TableDev &t = m.t;
+  const uint32_t stack_top = t.ctl->stack_top;
+  const uint32_t fresh = t.ctl->fresh_next;
+  const uint32_t free_total = stack_top + (t.cap - fresh);
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m.n;
+       j += gridDim.x * blockDim.x) {
+    if (!m.first[j]) continue;
+    const uint32_t r = m.rank[j];
+    if (r >= free_total) {  // table full
+      m.assign[j] = kNone;
+      continue;
+    }
+    const uint32_t idx =
+        r < stack_top ? t.stack[stack_top - 1 - r] : fresh + (r - stack_top);
+    const uint32_t h = m.mhash[j];
+    uint32_t s = h & t.tmask;
+    for (;;) {
+      const uint32_t cur = __hip_atomic_load(&t.slots[s].index, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == kEmpty || cur == kTomb) {
+        if (atomicCAS(&t.slots[s].index, cur, idx) == cur) {
+          if (cur == kTomb) atomicAdd(&t.ctl->tomb_reused, 1u);
+          break;
+        }
+        continue;  // lost the race for this slot; look at it again
+      }
+      s = (s + 1) & t.tmask;
+    }
+    FlowSlot &fs = t.slots[s];
+    const uint32_t *k = m.mkey + 4 * (size_t)j;
+    fs.k[0] = k[0];
+    fs.k[1] = k[1];
+    fs.k[2] = k[2];
+    fs.k[3] = k[3];
+    fs.hash = h;
+    t.slot_of[idx] = s;
+    t.birth[idx] = m.seq_base + m.pos[j];
+    m.assign[j] = idx;
+  }
+}
+
+__global__ void nk_commit(NkArgs m) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Ctl *c = m.t.ctl;
+  const uint32_t K = m.rank[m.n - 1] + m.first[m.n - 1];
+  const uint32_t free_total = c->stack_top + (m.t.cap - c->fresh_next);
+  const uint32_t used = K < free_total ? K : free_total;
+  if (used <= c->stack_top) {
+    c->stack_top -= used;
+  } else {
+    c->fresh_next += used - c->stack_top;
+    c->stack_top = 0;
+  }
+  c->n_live += used;
+  c->n_tomb -= c->tomb_reused;
+  c->tomb_reused = 0;
+  c->new_count = used;
+}
+
+int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
+                 uint32_t *n_new) {
+  Workspace &w = c->ws;
+  NkArgs m{};
+  m.t = tbl_dev(t);
+  m.pos = nk.pos;
+  m.n = nk.n;
+  m.mkey = w.mkey;
+  m.mhash = w.mhash;
+  m.first = w.first;
+  m.rank = w.rank;
+  m.rep = w.rep;
+  m.assign = w.assign;
+  m.scratch = w.scratch;
+  m.seq_base = seq_base;
+  const uint32_t ssize = next_pow2((uint64_t)nk.n * 2);
+  m.smask = ssize - 1;
+  size_t need = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, need, w.first, w.rank, (int)nk.n,
+                                   c->stream);
+  VP_TRY(cub_reserve(c, need));
+  VP_HIP(hipMemsetAsync(w.scratch, 0xFF, sizeof(uint32_t) * (size_t)ssize,
+                        c->stream));
+  const uint32_t g = grid_for(nk.n);
+  nk_dedup<<<g, 256, 0, c->stream>>>(m);
+  nk_first<<<g, 256, 0, c->stream>>>(m);
+  VP_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub_tmp, w.cub_bytes, w.first,
+                                          w.rank, (int)nk.n, c->stream));
+  nk_alloc<<<g, 256, 0, c->stream>>>(m);
+  nk_commit<<<1, 64, 0, c->stream>>>(m);
+  VP_HIP(hipGetLastError());
+  if (n_new) {
+    VP_TRY(read_ctl(c, t));
+    *n_new = t.h_ctl.new_count;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------- touch log --
+
+__global__ void touch_runs(const uint32_t *skey, const uint32_t *sval,
+                           uint32_t n, uint32_t none, uint32_t p0, NowSpec now,
+                           uint64_t seq_base, uint64_t *ts, uint64_t *tseq) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += gridDim.x * blockDim.x) {
+    const uint32_t k = skey[j];
+    if (k >= none) continue;
+    if (j + 1 < n && skey[j + 1] == k) continue;  // not the last toucher
+    const uint32_t p = p0 + sval[j];
+    ts[k] = (uint64_t)now.at(p);
+    tseq[k] = seq_base + p;
+  }
+}
+
+int tbl_touch_reduce(vp_ctx *c, FlowTable &t, const uint32_t *log, uint32_t p0,
+                     uint32_t p1, const NowSpec &now, uint64_t seq_base) {
+  Workspace &w = c->ws;
+  const uint32_t n = p1 - p0;
+  if (n == 0) return 0;
+  // log entries are < cap (a power of two) or kNone; sort on the bits that
+  // separate them, kNone sorting last (it has all those bits set)
+  int bits = 1;
+  while ((1ull << bits) <= t.cap) bits++;
+  size_t need = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, need, log + p0, w.skey, w.iota,
+                                     w.sval, (int)n, 0, bits, c->stream);
+  VP_TRY(cub_reserve(c, need));
+  VP_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, w.cub_bytes, log + p0,
+                                            w.skey, w.iota, w.sval, (int)n, 0,
+                                            bits, c->stream));
+  const uint32_t none = (uint32_t)((1ull << bits) - 1);
+  touch_runs<<<grid_for(n), 256, 0, c->stream>>>(w.skey, w.sval, n, none, p0,
+                                                 now, seq_base, t.ts, t.tseq);
+  VP_HIP(hipGetLastError());
+  return 0;
+}
+
+// ---------------------------------------------------------------- expiry --
+
+__global__ void tbl_min_ts(TableDev t) {
+  unsigned long long best = ~0ull;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.cap;
+       i += gridDim.x * blockDim.x)
+    if (t.slot_of[i] != kNone && t.ts[i] < best) best = t.ts[i];
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long v = __shfl_xor(best, o);
+    best = v < best ? v : best;
+  }
+  if (__lane_id() == 0 && best != ~0ull)
+    atomicMin((unsigned long long *)&t.ctl->min_ts, best);
+}
+
+int tbl_exact_floor(vp_ctx *c, FlowTable &t) {
+  const uint64_t all = ~0ull;
+  VP_HIP(hipMemcpyAsync(&t.ctl->min_ts, &all, 8, hipMemcpyHostToDevice,
+                        c->stream));
+  tbl_min_ts<<<grid_for(t.cap), 256, 0, c->stream>>>(tbl_dev(t));
+  VP_HIP(hipGetLastError());
+  VP_TRY(read_ctl(c, t));
+  t.ts_floor = t.h_ctl.min_ts;
+  return 0;
+}
+
+// Every allocated index with ts < cutoff: the set expire_items_single_map
+// frees (LRU order is (ts, last-touch) order, so the loop stops exactly at
+// the first stamp >= cutoff).
+__global__ void exp_collect(TableDev t, int64_t cutoff, uint64_t *ekey,
+                            uint32_t *eidx) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.cap;
+       i += gridDim.x * blockDim.x) {
+    const bool take = t.slot_of[i] != kNone && (int64_t)t.ts[i] < cutoff;
+    const uint32_t k = wave_append(&t.ctl->exp_count, take);
+    if (take) {
+      eidx[k] = i;
+      ekey[k] = t.tseq[i];
+    }
+  }
+}
+
+__global__ void exp_gather_ts(const uint32_t *eidx, uint32_t n, const uint64_t *ts,
+                              uint64_t *ekey) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += gridDim.x * blockDim.x)
+    ekey[j] = ts[eidx[j]];
+}
+
+// Free in LRU order: the oldest is pushed first, so the youngest expired
+// index ends on top (double-chain-impl.c:1968-1981); erase the keys.
+__global__ void exp_apply(TableDev t, const uint32_t *eidx, uint32_t n) {
+  const uint32_t top = t.ctl->stack_top;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += gridDim.x * blockDim.x) {
+    const uint32_t idx = eidx[j];
+    t.stack[top + j] = idx;
+    t.slots[t.slot_of[idx]].index = kTomb;
+    t.slot_of[idx] = kNone;
+  }
+}
+
+__global__ void exp_commit(Ctl *ctl, uint32_t n) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    ctl->stack_top += n;
+    ctl->n_live -= n;
+    ctl->n_tomb += n;
+  }
+}
+
+// Rebuild (tombstone purge): copy live slots out, clear, re-insert.
+__global__ void rb_collect(TableDev t, FlowSlot *out) {
+  const uint32_t ns = t.tmask + 1;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < ns;
+       s += gridDim.x * blockDim.x) {
+    const bool live = t.slots[s].index < kTomb;
+    const uint32_t k = wave_append(&t.ctl->exp_count, live);
+    if (live) out[k] = t.slots[s];
+  }
+}
+__global__ void rb_insert(TableDev t, const FlowSlot *in, uint32_t n) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += gridDim.x * blockDim.x) {
+    const FlowSlot v = in[j];
+    uint32_t s = v.hash & t.tmask;
+    while (atomicCAS(&t.slots[s].index, kEmpty, v.index) != kEmpty)
+      s = (s + 1) & t.tmask;
+    FlowSlot &d = t.slots[s];
+    d.k[0] = v.k[0];
+    d.k[1] = v.k[1];
+    d.k[2] = v.k[2];
+    d.k[3] = v.k[3];
+    d.hash = v.hash;
+    t.slot_of[v.index] = s;
+  }
+}
+
+static int tbl_rebuild(vp_ctx *c, FlowTable &t) {
+  const uint32_t ns = t.tmask + 1;
+  FlowSlot *tmp = nullptr;
+  VP_HIP(hipMalloc((void **)&tmp, sizeof(FlowSlot) * (size_t)t.cap));
+  VP_HIP(hipMemsetAsync(&t.ctl->exp_count, 0, 4, c->stream));
+  rb_collect<<<grid_for(ns), 256, 0, c->stream>>>(tbl_dev(t), tmp);
+  VP_TRY(read_ctl(c, t));
+  const uint32_t live = t.h_ctl.exp_count;
+  VP_HIP(hipMemsetAsync(t.slots, 0xFF, sizeof(FlowSlot) * (size_t)ns, c->stream));
+  if (live)
+    rb_insert<<<grid_for(live), 256, 0, c->stream>>>(tbl_dev(t), tmp, live);
+  VP_HIP(hipMemsetAsync(&t.ctl->n_tomb, 0, 4, c->stream));
+  VP_HIP(hipMemsetAsync(&t.ctl->exp_count, 0, 4, c->stream));
+  VP_HIP(hipStreamSynchronize(c->stream));
+  VP_HIP(hipFree(tmp));
+  return 0;
+}
+
+int tbl_expire(vp_ctx *c, FlowTable &t, int64_t cutoff, uint32_t *n_out) {
+  VP_HIP(hipMemsetAsync(&t.ctl->exp_count, 0, 4, c->stream));
+  exp_collect<<<grid_for(t.cap), 256, 0, c->stream>>>(tbl_dev(t), cutoff, t.ekey,
+                                                      t.eidx);
+  VP_HIP(hipGetLastError());
+  VP_TRY(read_ctl(c, t));
+  const uint32_t k = t.h_ctl.exp_count;
+  if (n_out) *n_out = k;
+  if (k == 0) return 0;
+  size_t need = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, need, t.ekey, t.ekey2, t.eidx,
+                                     t.eidx2, (int)k, 0, 64, c->stream);
+  VP_TRY(cub_reserve(c, need));
+  // 1) by last-touch sequence, 2) stable by timestamp
+  VP_HIP(hipcub::DeviceRadixSort::SortPairs(c->ws.cub_tmp, c->ws.cub_bytes,
+                                            t.ekey, t.ekey2, t.eidx, t.eidx2,
+                                            (int)k, 0, 64, c->stream));
+  exp_gather_ts<<<grid_for(k), 256, 0, c->stream>>>(t.eidx2, k, t.ts, t.ekey);
+  VP_HIP(hipcub::DeviceRadixSort::SortPairs(c->ws.cub_tmp, c->ws.cub_bytes,
+                                            t.ekey, t.ekey2, t.eidx2, t.eidx,
+                                            (int)k, 0, 64, c->stream));
+  exp_apply<<<grid_for(k), 256, 0, c->stream>>>(tbl_dev(t), t.eidx, k);
+  exp_commit<<<1, 64, 0, c->stream>>>(t.ctl, k);
+  VP_HIP(hipGetLastError());
+  VP_TRY(read_ctl(c, t));
+  if ((uint64_t)t.h_ctl.n_tomb + t.h_ctl.n_live > (uint64_t)(t.tmask + 1) * 3 / 4)
+    return tbl_rebuild(c, t);
+  return 0;
+}
+
+// ------------------------------------------------------------------ dump --
+
+__global__ void dump_k(TableDev t, uint8_t *alloc, int64_t *ts, uint32_t *keys) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.cap;
+       i += gridDim.x * blockDim.x) {
+    const uint32_t s = t.slot_of[i];
+    alloc[i] = s != kNone;
+    ts[i] = s != kNone ? (int64_t)t.ts[i] : 0;
+    for (int w = 0; w < 4; w++) keys[4 * i + w] = s != kNone ? t.slots[s].k[w] : 0;
+  }
+}
+
+int tbl_dump(vp_ctx *c, FlowTable &t, uint8_t *alloc, int64_t *ts,
+             uint32_t *keys) {
+  const uint32_t cap = t.cap;
+  uint8_t *d_alloc = nullptr;
+  int64_t *d_ts = nullptr;
+  uint32_t *d_keys = nullptr;
+  VP_TRY(dalloc(&d_alloc, cap));
+  VP_TRY(dalloc(&d_ts, cap));
+  VP_TRY(dalloc(&d_keys, 4ull * cap));
+  dump_k<<<grid_for(cap), 256, 0, c->stream>>>(tbl_dev(t), d_alloc, d_ts, d_keys);
+  VP_HIP(hipMemcpyAsync(alloc, d_alloc, cap, hipMemcpyDeviceToHost, c->stream));
+  VP_HIP(hipMemcpyAsync(ts, d_ts, 8ull * cap, hipMemcpyDeviceToHost, c->stream));
+  VP_HIP(hipMemcpyAsync(keys, d_keys, 16ull * cap, hipMemcpyDeviceToHost,
+                        c->stream));
+  VP_HIP(hipStreamSynchronize(c->stream));
+  hipFree(d_alloc);
+  hipFree(d_ts);
+  hipFree(d_keys);
+  return 0;
+}
+
+}  // namespace vp

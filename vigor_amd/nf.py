@@ -22,12 +22,13 @@ def _dptr(t):
 class NfBase:
     kind = "?"
 
-    def __init__(self):
+    def __init__(self, libpath=None):
         self.h = C.c_void_p()
+        self.L = lib(libpath)
 
     def close(self):
         if getattr(self, "h", None) and self.h.value:
-            lib().vp_destroy(self.h)
+            self.L.vp_destroy(self.h)
             self.h = C.c_void_p()
 
     def __del__(self):
@@ -49,17 +50,17 @@ class NfBase:
                       now=now.data_ptr() if now is not None else None,
                       now0=now0, now_step=now_step, out_dev=out.data_ptr())
         s = C.c_void_p(stream.cuda_stream) if stream is not None else None
-        _check(lib().vp_process_device(self.h, C.byref(b), s),
+        _check(self.L.vp_process_device(self.h, C.byref(b), s),
                "vp_process_device")
 
     def last_kernel_ms(self):
         ms, k = C.c_float(), C.c_int()
-        _check(lib().vp_last_kernel_ms(self.h, C.byref(ms), C.byref(k)),
+        _check(self.L.vp_last_kernel_ms(self.h, C.byref(ms), C.byref(k)),
                "vp_last_kernel_ms")
         return ms.value, k.value
 
     def live_count(self) -> int:
-        v = lib().vp_live_count(self.h)
+        v = self.L.vp_live_count(self.h)
         if v < 0:
             _check(int(v), "vp_live_count")
         return int(v)
@@ -76,7 +77,7 @@ class NfBase:
         now = np.ascontiguousarray(now, np.int64)
         out = np.zeros(n, np.uint16)
         P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
-        _check(lib().vp_process_host(self.h, n, P(in_dev), P(frames), slot,
+        _check(self.L.vp_process_host(self.h, n, P(in_dev), P(frames), slot,
                                      P(lens), P(now), P(out)),
                "vp_process_host")
         return out
@@ -97,7 +98,7 @@ class NfBase:
         now = np.ascontiguousarray(now, np.int64)
         out = np.zeros(n, np.uint16)
         P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
-        _check(lib().vp_process_batch(self.h, n, P(in_dev), ptrs, P(lens),
+        _check(self.L.vp_process_batch(self.h, n, P(in_dev), ptrs, P(lens),
                                       P(now), P(out)), "vp_process_batch")
         return out
 
@@ -109,10 +110,10 @@ class NfBase:
 class Nat(NfBase):
     kind = "nat"
 
-    def __init__(self, cfg: NatConfigC, gpu: int = 0):
-        super().__init__()
+    def __init__(self, cfg: NatConfigC, gpu: int = 0, libpath=None):
+        super().__init__(libpath)
         self.cfg = cfg
-        _check(lib().vp_nat_create(C.byref(cfg), gpu, C.byref(self.h)),
+        _check(self.L.vp_nat_create(C.byref(cfg), gpu, C.byref(self.h)),
                "vp_nat_create")
 
     def dump(self):
@@ -121,7 +122,7 @@ class Nat(NfBase):
         ts = np.zeros(n, np.int64)
         keys = np.zeros(n * 16, np.uint8)
         P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
-        _check(lib().vp_nat_dump(self.h, P(alloc), P(ts), P(keys)),
+        _check(self.L.vp_nat_dump(self.h, P(alloc), P(ts), P(keys)),
                "vp_nat_dump")
         return alloc, ts, keys.reshape(n, 16)
 
@@ -129,18 +130,18 @@ class Nat(NfBase):
 class Bridge(NfBase):
     kind = "bridge"
 
-    def __init__(self, cfg: BridgeConfigC, gpu: int = 0):
-        super().__init__()
+    def __init__(self, cfg: BridgeConfigC, gpu: int = 0, libpath=None):
+        super().__init__(libpath)
         self.cfg = cfg
-        _check(lib().vp_bridge_create(C.byref(cfg), gpu, C.byref(self.h)),
+        _check(self.L.vp_bridge_create(C.byref(cfg), gpu, C.byref(self.h)),
                "vp_bridge_create")
 
 
 class Lb(NfBase):
     kind = "lb"
 
-    def __init__(self, cfg: LbConfigC, gpu: int = 0):
-        super().__init__()
+    def __init__(self, cfg: LbConfigC, gpu: int = 0, libpath=None):
+        super().__init__(libpath)
         self.cfg = cfg
-        _check(lib().vp_lb_create(C.byref(cfg), gpu, C.byref(self.h)),
+        _check(self.L.vp_lb_create(C.byref(cfg), gpu, C.byref(self.h)),
                "vp_lb_create")
