@@ -7,6 +7,7 @@ never used for anything else."""
 import os
 import statistics
 import sys
+import time
 
 import torch
 
@@ -21,18 +22,21 @@ def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     B, NF = 1 << 24, 1 << 20
     dev = torch.device("cuda:0")
-    variants = {"full": None}
-    for v in ("NOSTORE", "FULLSTORE", "NOPROBE", "NT"):
+    variants = {"full": (None, {}), "perlane": (None, {"VIGPATH_COALESCED": "0"})}
+    for v in ("NOPROBE", "NOINLINE", "NT", "NOFRAME"):
         p = os.path.join(ROOT, "vigor_amd", "abl", "libvigpath_%s.so" % v)
-        if os.path.exists(p):
-            variants[v] = p
+        if os.path.exists(p):  # NOFRAME lives in the per-lane kernel
+            variants[v] = (p, {"VIGPATH_COALESCED": "0"} if v == "NOFRAME"
+                           else {})
     bank = bench.FlowBank(NF, 0, dev)
     lens = torch.full((B,), 60, dtype=torch.int16, device=dev)
     ind = torch.zeros(B, dtype=torch.int16, device=dev)
     out = torch.zeros(B, dtype=torch.int16, device=dev)
     buf = torch.empty(B * 64, dtype=torch.uint8, device=dev)
     nfs = {}
-    for name, path in variants.items():
+    for name, (path, env) in variants.items():
+        os.environ.pop("VIGPATH_COALESCED", None)
+        os.environ.update(env)
         cfg = vigor_amd.nat_config_from_args(
             bench.NAT_ARGS + ["--max-flows", str(NF)], 2, bench.DEV_MACS)
         nat = vigor_amd.Nat(cfg, 0, libpath=path)
@@ -40,19 +44,26 @@ def main():
         nat.process_device(buf, lens, ind, out, 64, now0=T.NOW0, now_step=1)
         nfs[name] = nat
     res = {k: [] for k in nfs}
+    step_ms = {k: [] for k in nfs}
     start = B
     for r in range(rounds):
         for name, nat in nfs.items():
             bank.fill(buf, start)
             torch.cuda.synchronize()
+            t0 = time.perf_counter()
             nat.process_device(buf, lens, ind, out, 64, now0=T.NOW0 + start,
                                now_step=1)
+            torch.cuda.synchronize()
+            nat.step_ms = (time.perf_counter() - t0) * 1e3
             res[name].append(nat.last_kernel_ms()[0])
+            step_ms[name].append(nat.step_ms)
         start += B
     for name, v in res.items():
         med = statistics.median(v)
-        print("%-11s median %.3f ms  min %.3f ms  -> %.2f Gpps" %
-              (name, med, min(v), B / med / 1e6))
+        sm = statistics.median(step_ms[name])
+        print("%-11s kernel median %.3f ms min %.3f ms -> %.2f Gpps | step "
+              "%.3f ms -> %.2f Gpps" % (name, med, min(v), B / med / 1e6, sm,
+                                        B / sm / 1e6))
 
 
 if __name__ == "__main__":

@@ -134,6 +134,28 @@ __device__ inline void set_macs(const GFrame &f, const uint32_t mw[3]) {
   for (int k = 0; k < 3; k++) f.w32(4 * k, mw[k]);
 }
 
+// Frame-stream loads/stores (64 B per packet, read once, written once).
+// VP_ABL_NT builds mark them non-temporal so the stream does not displace the
+// flow table from the caches (tools/ablate.py measures both).
+__device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
+#ifdef VP_ABL_NT
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void st_stream(uint4 *p, uint4 v) {
+#ifdef VP_ABL_NT
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  v4u x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<v4u *>(p));
+#else
+  *p = v;
+#endif
+}
+
 // ------------------------------------------------------------ fast frames --
 // The 64-byte slot held in 16 registers (LE words). Only compile-time word
 // indices are used so nothing spills to scratch.

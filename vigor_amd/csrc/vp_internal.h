@@ -73,6 +73,8 @@ struct Workspace {
   uint32_t *log = nullptr;   // touch log, one entry per packet
   uint32_t *iota = nullptr;  // 0..cap_n-1
   uint32_t *skey = nullptr, *sval = nullptr;
+  uint32_t *hist = nullptr, *hoff = nullptr;  // touch-reduce (chunk x span)
+  uint64_t hist_cap = 0;
   void *cub_tmp = nullptr;
   size_t cub_bytes = 0;
   // host staging for the host-batch entry points
@@ -101,5 +103,6 @@ struct vp_ctx {
   uint32_t *crc_tab = nullptr;  // CRC position tables (LDS-staged)
   uint32_t *macw = nullptr;     // per device: d_addr|s_addr header words
   uint32_t wan_macw[3] = {0, 0, 0};
+  bool coalesced_io = true;  // LDS-staged 64 B frame I/O (VIGPATH_COALESCED=0 off)
   vp::Workspace ws;
 };

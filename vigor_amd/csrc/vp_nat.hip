@@ -85,7 +85,12 @@ __device__ __forceinline__ void macs_for(const NatArgs &a, uint32_t dst,
 
 // Generic (byte-addressed) phase A for frames outside the register fast path
 // (IP options, long frames, odd headers). Same decisions as nat_classify.
-__device__ void nat_generic_a(const NatArgs &a, const uint32_t *T, uint32_t p,
+#ifdef VP_ABL_NOINLINE
+#define VP_GENERIC_FN __device__ __noinline__
+#else
+#define VP_GENERIC_FN __device__  // inlined: measured faster (tools/ablate.py)
+#endif
+VP_GENERIC_FN void nat_generic_a(const NatArgs &a, const uint32_t *T, uint32_t p,
                               uint32_t in, uint32_t len) {
   GFrame f{a.frames + (size_t)p * a.slot, a.slot};
   L34 h = parse_l34(f, len);
@@ -108,6 +113,7 @@ __device__ void nat_generic_a(const NatArgs &a, const uint32_t *T, uint32_t p,
     const uint32_t s = a.t.slot_of[idx];
     if (s == kNone) {
       a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
+      a.log[p] = kNone;  // phase C writes the real entry
       return;
     }
     const FlowSlot &fs = a.t.slots[s];
@@ -126,6 +132,7 @@ __device__ void nat_generic_a(const NatArgs &a, const uint32_t *T, uint32_t p,
                                    key);
     if (idx == kNone) {
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
+      a.log[p] = kNone;  // phase B writes the real entry
       return;
     }
     a.log[p] = idx;
@@ -140,124 +147,195 @@ __device__ void nat_generic_a(const NatArgs &a, const uint32_t *T, uint32_t p,
   a.out[p] = (uint16_t)dst;
 }
 
-// Phase A. One packet per lane, grid-stride; a 64-byte slot is four 16-byte
-// loads per lane, processed in registers.
+// Phase A for one packet whose 64-byte slot is in registers. Returns true
+// when `f` was rewritten and must be stored back.
+__device__ __forceinline__ bool nat_fast(const NatArgs &a, const uint32_t *T,
+                                         uint32_t p, RFrame &f) {
+  const uint32_t in = a.in_dev[p];
+  const uint32_t len = a.len[p];
+  const uint32_t et = f.w[3] & 0xFFFF;
+  const uint32_t ihl = (f.w[3] >> 16) & 0x0F;
+  const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
+  if (!(et == 0x0008 && ihl == 5 && tl <= 50)) {
+    nat_generic_a(a, T, p, in, len);  // writes global memory itself
+    return false;
+  }
+  // nf_then_get_rte_ipv4_header / nf_then_get_tcpudp_header with IHL = 5
+  const uint16_t unread = (uint16_t)(len - 14);
+  const uint32_t proto = f.w[5] >> 24;
+  const bool ok = (unread >= 20) & (unread >= tl) &
+                  ((proto == 6) | (proto == 17)) & ((uint32_t)(len - 34) >= 4u);
+  if (!ok) {
+    a.out[p] = (uint16_t)in;
+    a.log[p] = kNone;
+    return false;
+  }
+  const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
+  const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
+  uint32_t dst;
+  uint32_t mw[3];
+  if (in == a.wan) {
+    // flow_manager_get_external (nat_flowmanager.c:78-94)
+    const int idx = (int)dp - (int)a.start_port;
+    if (idx < 0 || idx >= (int)a.t.cap) {
+      a.out[p] = (uint16_t)in;
+      a.log[p] = kNone;
+      return false;
+    }
+    const uint32_t s = a.t.slot_of[idx];
+    if (s == kNone) {  // maybe allocated earlier in this segment: phase C
+      a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
+      a.log[p] = kNone;  // phase C writes the real entry
+      return false;
+    }
+    const uint4 k = *reinterpret_cast<const uint4 *>(a.t.slots + s);
+    a.log[p] = (uint32_t)idx;  // rejuvenated before the anti-spoof check
+    if ((k.z != sip) | ((k.x >> 16) != sp) | (((k.w >> 16) & 0xFF) != proto)) {
+      a.out[p] = (uint16_t)in;  // nat_main.c:55-60
+      return false;
+    }
+    f.set32at2(30, k.y);        // dst_addr = flow.src_ip
+    f.set16(36, k.x & 0xFFFF);  // dst_port = flow.src_port
+    dst = k.w & 0xFFFF;         // flow.internal_device
+    macs_for(a, dst, mw);
+  } else {
+    // flow_manager_get_internal (nat_flowmanager.c:67-76)
+    const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
+    const uint32_t hh = flowid_hash(T, sp, dp, sip, dip, in, proto);
+#ifdef VP_ABL_NOPROBE  // diagnostic builds only (tools/ablate.py)
+    asm volatile("" ::"v"(key[0]), "v"(key[1]), "v"(key[2]), "v"(key[3]));
+    const uint32_t idx = hh & (a.t.cap - 1);
+#else
+    const uint32_t idx = tbl_probe(a.t, hh, key);
+#endif
+    if (idx == kNone) {  // new flow, or not yet visible: phase B
+      a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
+      a.log[p] = kNone;  // phase B writes the real entry
+      return false;
+    }
+    a.log[p] = idx;
+    f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
+    f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
+    dst = a.wan;
+    mw[0] = a.wan_macw0;
+    mw[1] = a.wan_macw1;
+    mw[2] = a.wan_macw2;
+  }
+  fast_checksums(f, proto, tl);
+  f.w[0] = mw[0];
+  f.w[1] = mw[1];
+  f.w[2] = mw[2];
+  a.out[p] = (uint16_t)dst;
+  return true;
+}
+
+__device__ __forceinline__ void load_crc_tables(uint32_t *T, const uint32_t *g) {
+  for (uint32_t i = threadIdx.x; i < 15 * 256; i += blockDim.x) T[i] = g[i];
+  __syncthreads();
+}
+
+// Phase A, any slot size: one packet per lane, grid-stride, the first 64
+// bytes of the slot as four 16-byte loads per lane.
 __global__ __launch_bounds__(256) void nat_classify(NatArgs a) {
   __shared__ uint32_t T[15 * 256];
-  for (uint32_t i = threadIdx.x; i < 15 * 256; i += blockDim.x)
-    T[i] = a.crc_tab[i];
-  __syncthreads();
-
+  load_crc_tables(T, a.crc_tab);
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t p = a.p0 + blockIdx.x * blockDim.x + threadIdx.x; p < a.p1;
        p += stride) {
-    const uint32_t in = a.in_dev[p];
-    const uint32_t len = a.len[p];
+#ifdef VP_ABL_NOFRAME  // diagnostic: synthesise the bench trace's frame
+    uint4 *fp = reinterpret_cast<uint4 *>(a.frames + (size_t)(p & 63) * a.slot);
+#else
     uint4 *fp = reinterpret_cast<uint4 *>(a.frames + (size_t)p * a.slot);
+#endif
     RFrame f;
+    const uint4 c0 = ld_stream(fp), c1 = ld_stream(fp + 1), c2 = ld_stream(fp + 2),
+                c3 = ld_stream(fp + 3);
+    f.w[0] = c0.x; f.w[1] = c0.y; f.w[2] = c0.z; f.w[3] = c0.w;
+    f.w[4] = c1.x; f.w[5] = c1.y; f.w[6] = c1.z; f.w[7] = c1.w;
+    f.w[8] = c2.x; f.w[9] = c2.y; f.w[10] = c2.z; f.w[11] = c2.w;
+    f.w[12] = c3.x; f.w[13] = c3.y; f.w[14] = c3.z; f.w[15] = c3.w;
+#ifdef VP_ABL_NOFRAME
     {
-#ifdef VP_ABL_NT
-      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-      const v4u *vp4 = reinterpret_cast<const v4u *>(fp);
-      v4u n0 = __builtin_nontemporal_load(vp4), n1 = __builtin_nontemporal_load(vp4 + 1),
-          n2 = __builtin_nontemporal_load(vp4 + 2), n3 = __builtin_nontemporal_load(vp4 + 3);
-      uint4 c0 = make_uint4(n0.x, n0.y, n0.z, n0.w), c1 = make_uint4(n1.x, n1.y, n1.z, n1.w),
-            c2 = make_uint4(n2.x, n2.y, n2.z, n2.w), c3 = make_uint4(n3.x, n3.y, n3.z, n3.w);
+      const uint32_t fl = p & (a.t.cap - 1), v = fl >> 16;
+      f.set16(34, bswap16((uint16_t)(fl & 0xFFFF)));
+      f.set32at2(26, 10u | (((v >> 8) & 0xFF) << 16) | ((v & 0xFF) << 24));
+    }
+    asm volatile("" ::"v"(nat_fast(a, T, p, f) ? f.w[6] ^ f.w[10] : 0u));
 #else
-      uint4 c0 = fp[0], c1 = fp[1], c2 = fp[2], c3 = fp[3];
+    if (nat_fast(a, T, p, f)) {
+      st_stream(fp, make_uint4(f.w[0], f.w[1], f.w[2], f.w[3]));
+      st_stream(fp + 1, make_uint4(f.w[4], f.w[5], f.w[6], f.w[7]));
+      st_stream(fp + 2, make_uint4(f.w[8], f.w[9], f.w[10], f.w[11]));
+      if ((f.w[5] >> 24) == 6)
+        st_stream(fp + 3, make_uint4(f.w[12], f.w[13], f.w[14], f.w[15]));
+    }
 #endif
-      f.w[0] = c0.x; f.w[1] = c0.y; f.w[2] = c0.z; f.w[3] = c0.w;
-      f.w[4] = c1.x; f.w[5] = c1.y; f.w[6] = c1.z; f.w[7] = c1.w;
-      f.w[8] = c2.x; f.w[9] = c2.y; f.w[10] = c2.z; f.w[11] = c2.w;
-      f.w[12] = c3.x; f.w[13] = c3.y; f.w[14] = c3.z; f.w[15] = c3.w;
+  }
+}
+
+// LDS image of one wave's 64 frames (64 x 64 B): 16-byte chunk c (packet
+// c/4, part c%4) lives at c ^ ((c >> 4) & 3), so both the lane-contiguous
+// global<->LDS copies and each lane's 4 reads of its own frame are
+// bank-conflict-free ds_*_b128 accesses.
+__device__ __forceinline__ uint32_t chunk_swz(uint32_t c) {
+  return c ^ ((c >> 4) & 3u);
+}
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Phase A for 64-byte slots: every global load/store instruction moves 1 KiB
+// contiguous (lane l <-> bytes 16l..16l+15 of a 1 KiB piece), staged through
+// LDS; each wave owns 64 consecutive packets per step.
+__global__ __launch_bounds__(256) void nat_classify64(NatArgs a, uint32_t n_all) {
+  __shared__ uint32_t T[15 * 256];
+  __shared__ uint4 stage[4][256];
+  load_crc_tables(T, a.crc_tab);
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint4 *S = stage[wv];
+  const uint32_t first = a.p0 & ~63u;
+  const uint32_t tiles = (a.p1 - first + 63) / 64;
+  const uint32_t nwaves = gridDim.x * 4;
+  for (uint32_t tile = blockIdx.x * 4 + wv; tile < tiles; tile += nwaves) {
+    const uint32_t tb = first + tile * 64;
+    uint4 *g = reinterpret_cast<uint4 *>(a.frames + (size_t)tb * 64);
+    // packets of the tile that exist in the batch
+    const uint32_t avail = n_all - tb < 64 ? n_all - tb : 64;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+      const uint32_t c = 64 * j + lane;
+      if ((c >> 2) < avail) S[chunk_swz(c)] = g[c];
     }
-    const uint32_t et = f.w[3] & 0xFFFF;
-    const uint32_t ihl = (f.w[3] >> 16) & 0x0F;
-    const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
-    if (!(et == 0x0008 && ihl == 5 && tl <= 50)) {
-      nat_generic_a(a, T, p, in, len);
-      continue;
+    wave_lds_sync();
+    const uint32_t p = tb + lane;
+    const bool mine = p >= a.p0 && p < a.p1;
+    RFrame f;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint4 v = S[chunk_swz(4 * lane + k)];
+      f.w[4 * k] = v.x;
+      f.w[4 * k + 1] = v.y;
+      f.w[4 * k + 2] = v.z;
+      f.w[4 * k + 3] = v.w;
     }
-    // nf_then_get_rte_ipv4_header / nf_then_get_tcpudp_header with IHL = 5
-    const uint16_t unread = (uint16_t)(len - 14);
-    const uint32_t proto = f.w[5] >> 24;
-    const bool ok = (unread >= 20) & (unread >= tl) &
-                    ((proto == 6) | (proto == 17)) &
-                    ((uint32_t)(len - 34) >= 4u);
-    if (!ok) {
-      a.out[p] = (uint16_t)in;
-      a.log[p] = kNone;
-      continue;
+    bool mod = false;
+    if (mine) mod = nat_fast(a, T, p, f);
+    if (mod) {
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++)
+        S[chunk_swz(4 * lane + k)] =
+            make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
     }
-    const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
-    const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
-    uint32_t dst;
-    uint32_t mw[3];
-    if (in == a.wan) {
-      // flow_manager_get_external (nat_flowmanager.c:78-94)
-      const int idx = (int)dp - (int)a.start_port;
-      if (idx < 0 || idx >= (int)a.t.cap) {
-        a.out[p] = (uint16_t)in;
-        a.log[p] = kNone;
-        continue;
-      }
-      const uint32_t s = a.t.slot_of[idx];
-      if (s == kNone) {  // maybe allocated earlier in this segment: phase C
-        a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
-        continue;
-      }
-      const uint4 k = *reinterpret_cast<const uint4 *>(a.t.slots + s);
-      a.log[p] = (uint32_t)idx;  // rejuvenated before the anti-spoof check
-      if ((k.z != sip) | ((k.x >> 16) != sp) | (((k.w >> 16) & 0xFF) != proto)) {
-        a.out[p] = (uint16_t)in;  // nat_main.c:55-60
-        continue;
-      }
-      f.set32at2(30, k.y);        // dst_addr = flow.src_ip
-      f.set16(36, k.x & 0xFFFF);  // dst_port = flow.src_port
-      dst = k.w & 0xFFFF;         // flow.internal_device
-      macs_for(a, dst, mw);
-    } else {
-      // flow_manager_get_internal (nat_flowmanager.c:67-76)
-      const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
-      const uint32_t hh = flowid_hash(T, sp, dp, sip, dip, in, proto);
-#ifdef VP_ABL_NOPROBE  // diagnostic builds only (tools/ablate.py)
-      asm volatile("" ::"v"(key[0]), "v"(key[1]), "v"(key[2]), "v"(key[3]));
-      const uint32_t idx = hh & (a.t.cap - 1);
-#else
-      const uint32_t idx = tbl_probe(a.t, hh, key);
-#endif
-      if (idx == kNone) {  // new flow, or not yet visible: phase B
-        a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
-        continue;
-      }
-      a.log[p] = idx;
-      f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
-      f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
-      dst = a.wan;
-      mw[0] = a.wan_macw0;
-      mw[1] = a.wan_macw1;
-      mw[2] = a.wan_macw2;
+    const uint64_t modmask = __ballot(mod);
+    wave_lds_sync();
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+      const uint32_t c = 64 * j + lane;
+      if ((modmask >> (c >> 2)) & 1ull) g[c] = S[chunk_swz(c)];
     }
-    fast_checksums(f, proto, tl);
-    f.w[0] = mw[0];
-    f.w[1] = mw[1];
-    f.w[2] = mw[2];
-#ifdef VP_ABL_NOSTORE
-    asm volatile("" ::"v"(f.w[0] ^ f.w[1] ^ f.w[2] ^ f.w[3] ^ f.w[4] ^ f.w[5] ^
-                          f.w[6] ^ f.w[7] ^ f.w[8] ^ f.w[9] ^ f.w[10] ^
-                          f.w[11] ^ f.w[12]));
-#elif defined(VP_ABL_FULLSTORE)
-    fp[0] = make_uint4(f.w[0], f.w[1], f.w[2], f.w[3]);
-    fp[1] = make_uint4(f.w[4], f.w[5], f.w[6], f.w[7]);
-    fp[2] = make_uint4(f.w[8], f.w[9], f.w[10], f.w[11]);
-    fp[3] = make_uint4(f.w[12], f.w[13], f.w[14], f.w[15]);
-#else
-    fp[0] = make_uint4(f.w[0], f.w[1], f.w[2], f.w[3]);
-    fp[1] = make_uint4(f.w[4], f.w[5], f.w[6], f.w[7]);
-    fp[2] = make_uint4(f.w[8], f.w[9], f.w[10], f.w[11]);
-    if (proto == 6) fp[3] = make_uint4(f.w[12], f.w[13], f.w[14], f.w[15]);
-#endif
-    a.out[p] = (uint16_t)dst;
+    wave_lds_sync();  // the next tile overwrites S
   }
 }
 
@@ -388,9 +466,17 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
 
   VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 8, c->stream));  // + defer
   VP_HIP(hipEventRecord(c->ev0, c->stream));
-  nat_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
+  if (b->slot == 64 && c->coalesced_io) {
+    const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
+    nat_classify64<<<grid_for((uint64_t)tiles * 64), 256, 0, c->stream>>>(a, b->n);
+  } else {
+    nat_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
+  }
   VP_HIP(hipGetLastError());
   VP_HIP(hipEventRecord(c->ev1, c->stream));
+  // Optimistic: fold phase A's touches right away (queued packets logged
+  // kNone); if B/C run, the fold is redone over the completed log.
+  VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, c->seq));
   VP_TRY(read_ctl(c, t));
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
@@ -419,8 +505,8 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     nat_defer_finish<<<grid_for(ndefer), 256, 0, c->stream>>>(a, w.defer, ndefer);
     VP_HIP(hipGetLastError());
   }
-  VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, c->seq));
-  if (nmiss) {
+  if (nmiss || ndefer) {
+    VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, c->seq));
     VP_TRY(read_ctl(c, t));
   }
   return 0;

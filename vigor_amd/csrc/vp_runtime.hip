@@ -87,6 +87,8 @@ static void mac_words(const uint8_t d[6], const uint8_t s[6], uint32_t w[3]) {
 
 static int ctx_common(vp_ctx *c, int gpu) {
   c->gpu = gpu;
+  const char *co = getenv("VIGPATH_COALESCED");
+  c->coalesced_io = !co || atoi(co) != 0;  // default on (tools/ablate.py)
   VP_HIP(hipSetDevice(gpu));
   VP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   VP_HIP(hipEventCreate(&c->ev0));
@@ -101,7 +103,7 @@ static void free_all(vp_ctx *c) {
   tbl_free(c->ft);
   Workspace &w = c->ws;
   ws_release(w);
-  void *ptrs[] = {w.cub_tmp, w.d_frames, w.d_len,    w.d_in,
+  void *ptrs[] = {w.hist, w.hoff, w.cub_tmp, w.d_frames, w.d_len,    w.d_in,
                   w.d_out,   w.d_now,    c->crc_tab, c->macw};
   for (void *p : ptrs) hipFree(p);
   if (w.h_frames) hipHostFree(w.h_frames);

@@ -233,17 +233,102 @@ int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
 
 // ---------------------------------------------------------- touch log --
 
-__global__ void touch_runs(const uint32_t *skey, const uint32_t *sval,
-                           uint32_t n, uint32_t none, uint32_t p0, NowSpec now,
-                           uint64_t seq_base, uint64_t *ts, uint64_t *tseq) {
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
-       j += gridDim.x * blockDim.x) {
-    const uint32_t k = skey[j];
-    if (k >= none) continue;
-    if (j + 1 < n && skey[j + 1] == k) continue;  // not the last toucher
-    const uint32_t p = p0 + sval[j];
-    ts[k] = (uint64_t)now.at(p);
-    tseq[k] = seq_base + p;
+// The index space is cut into chunks of 2^kChunkBits indices (one LDS tile of
+// last-toucher positions per chunk). Pass 1 counts each log span's touches
+// per chunk, an exclusive scan turns the counts into (chunk, span) offsets,
+// pass 2 scatters (index-in-chunk, position) pairs into chunk order, pass 3
+// keeps the largest position per index with LDS atomics and writes ts/tseq.
+// About 24 B of streaming traffic per packet, no global atomics.
+constexpr uint32_t kChunkBits = 12;
+constexpr uint32_t kSpan = 16384;  // log entries per pass-1/2 block
+
+__global__ __launch_bounds__(256) void touch_count(const uint32_t *log,
+                                                   uint32_t n, uint32_t nchunks,
+                                                   uint32_t nspans,
+                                                   uint32_t *hist) {
+  extern __shared__ uint32_t cnt[];
+  for (uint32_t b = threadIdx.x; b < nchunks; b += blockDim.x) cnt[b] = 0;
+  __syncthreads();
+  const uint32_t s0 = blockIdx.x * kSpan, s1 = min(n, s0 + kSpan);
+  // 4 independent loads in flight per thread
+  for (uint32_t j = s0 + threadIdx.x; j < s1; j += 4 * blockDim.x) {
+    uint32_t k[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t jj = j + u * blockDim.x;
+      k[u] = jj < s1 ? log[jj] : kNone;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (k[u] != kNone) atomicAdd(&cnt[k[u] >> kChunkBits], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nchunks; b += blockDim.x)
+    hist[(size_t)b * nspans + blockIdx.x] = cnt[b];
+}
+
+__global__ __launch_bounds__(256) void touch_scatter(const uint32_t *log,
+                                                     uint32_t n, uint32_t nchunks,
+                                                     uint32_t nspans,
+                                                     const uint32_t *off,
+                                                     uint2 *out) {
+  extern __shared__ uint32_t pos[];
+  for (uint32_t b = threadIdx.x; b < nchunks; b += blockDim.x)
+    pos[b] = off[(size_t)b * nspans + blockIdx.x];
+  __syncthreads();
+  const uint32_t s0 = blockIdx.x * kSpan, s1 = min(n, s0 + kSpan);
+  for (uint32_t j = s0 + threadIdx.x; j < s1; j += 4 * blockDim.x) {
+    uint32_t k[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t jj = j + u * blockDim.x;
+      k[u] = jj < s1 ? log[jj] : kNone;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      if (k[u] == kNone) continue;
+      const uint32_t at = atomicAdd(&pos[k[u] >> kChunkBits], 1u);
+      out[at] = make_uint2(k[u] & ((1u << kChunkBits) - 1), j + u * blockDim.x);
+    }
+  }
+}
+
+__global__ void touch_total(const uint32_t *hist, const uint32_t *off,
+                            uint32_t nh, uint32_t *total) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *total = off[nh - 1] + hist[nh - 1];
+}
+
+__global__ __launch_bounds__(1024) void touch_reduce_k2(
+    const uint2 *in, const uint32_t *off, uint32_t nspans, uint32_t nchunks,
+    const uint32_t *total, uint32_t cap, uint32_t p0, NowSpec now,
+    uint64_t seq_base, uint64_t *ts, uint64_t *tseq) {
+  __shared__ uint32_t last[1u << kChunkBits];  // 1 + last position, 0 = none
+  const uint32_t ch = blockIdx.x;
+  for (uint32_t i = threadIdx.x; i < (1u << kChunkBits); i += blockDim.x)
+    last[i] = 0;
+  __syncthreads();
+  const uint32_t a = off[(size_t)ch * nspans];
+  const uint32_t b = ch + 1 < nchunks ? off[(size_t)(ch + 1) * nspans] : *total;
+  for (uint32_t j = a + threadIdx.x; j < b; j += 4 * blockDim.x) {
+    uint2 e[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t jj = j + u * blockDim.x;
+      e[u] = jj < b ? in[jj] : make_uint2(0, 0xFFFFFFFFu);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (e[u].y != 0xFFFFFFFFu) atomicMax(&last[e[u].x], e[u].y + 1);
+  }
+  __syncthreads();
+  const uint32_t base = ch << kChunkBits;
+  for (uint32_t i = threadIdx.x; i < (1u << kChunkBits) && base + i < cap;
+       i += blockDim.x) {
+    const uint32_t l = last[i];
+    if (!l) continue;
+    const uint32_t p = p0 + l - 1;
+    ts[base + i] = (uint64_t)now.at(p);
+    tseq[base + i] = seq_base + p;
   }
 }
 
@@ -252,20 +337,36 @@ int tbl_touch_reduce(vp_ctx *c, FlowTable &t, const uint32_t *log, uint32_t p0,
   Workspace &w = c->ws;
   const uint32_t n = p1 - p0;
   if (n == 0) return 0;
-  // log entries are < cap (a power of two) or kNone; sort on the bits that
-  // separate them, kNone sorting last (it has all those bits set)
-  int bits = 1;
-  while ((1ull << bits) <= t.cap) bits++;
+  const uint32_t nchunks = (t.cap + (1u << kChunkBits) - 1) >> kChunkBits;
+  const uint32_t nspans = (n + kSpan - 1) / kSpan;
+  const uint64_t nh = (uint64_t)nchunks * nspans;
+  if (nh > w.hist_cap) {
+    VP_HIP(hipStreamSynchronize(c->stream));
+    hipFree(w.hist);
+    hipFree(w.hoff);
+    w.hist = w.hoff = nullptr;
+    w.hist_cap = 0;
+    VP_TRY(dalloc(&w.hist, nh));
+    VP_TRY(dalloc(&w.hoff, nh));
+    w.hist_cap = nh;
+  }
+  uint32_t *hist = w.hist, *off = w.hoff;
+  uint2 *pairs = reinterpret_cast<uint2 *>(w.mkey);  // 4 words per packet
+  const size_t lds = sizeof(uint32_t) * nchunks;
+  if (lds > 64 * 1024) return VP_ENOTSUP;
+  touch_count<<<nspans, 256, lds, c->stream>>>(log + p0, n, nchunks, nspans, hist);
   size_t need = 0;
-  hipcub::DeviceRadixSort::SortPairs(nullptr, need, log + p0, w.skey, w.iota,
-                                     w.sval, (int)n, 0, bits, c->stream);
+  hipcub::DeviceScan::ExclusiveSum(nullptr, need, hist, off, (int)nh, c->stream);
   VP_TRY(cub_reserve(c, need));
-  VP_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, w.cub_bytes, log + p0,
-                                            w.skey, w.iota, w.sval, (int)n, 0,
-                                            bits, c->stream));
-  const uint32_t none = (uint32_t)((1ull << bits) - 1);
-  touch_runs<<<grid_for(n), 256, 0, c->stream>>>(w.skey, w.sval, n, none, p0,
-                                                 now, seq_base, t.ts, t.tseq);
+  VP_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub_tmp, w.cub_bytes, hist, off,
+                                          (int)nh, c->stream));
+  touch_scatter<<<nspans, 256, lds, c->stream>>>(log + p0, n, nchunks, nspans, off,
+                                                 pairs);
+  // total = off[last] + hist[last]; computed on device by the reducer
+  touch_total<<<1, 64, 0, c->stream>>>(hist, off, (uint32_t)nh, &t.ctl->aux_count);
+  touch_reduce_k2<<<nchunks, 1024, 0, c->stream>>>(pairs, off, nspans, nchunks,
+                                                  &t.ctl->aux_count, t.cap, p0,
+                                                  now, seq_base, t.ts, t.tseq);
   VP_HIP(hipGetLastError());
   return 0;
 }
