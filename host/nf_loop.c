@@ -1,0 +1,123 @@
+/*
+ * Host-side C driver restating the reference's nf.c worker loop over a trace
+ * file instead of DPDK rx/tx queues (reference nf.c:143-216):
+ *
+ *   per packet:  packet_state_total_length -> dst = nf_process(port, data,
+ *                len, now) -> dst == in ? drop : dst == FLOOD_FRAME ? flood
+ *                : tx                                      (nf.c:150-176)
+ *
+ * It links against the nf.h surface only (nf_config_init / nf_init /
+ * nf_process), so the same source links against the reference NF objects or
+ * against our libvignat_nf.so. With --batch B it instead hands B packets at
+ * a time to vp_process_batch (the batched form, nf.c:178-215).
+ *
+ * usage: nf_loop <trace.in> <trace.out> [--batch B] -- <NF options>
+ * trace.in:  "VPTR" u32 n u32 slot, u16 in_dev[n], u16 len[n], i64 now[n],
+ *            u8 frames[n*slot]
+ * trace.out: "VPTO" u32 n u32 slot, u16 out_dev[n], u8 frames[n*slot]
+ */
+#include <stdbool.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/vigpath.h"
+
+typedef int64_t vigor_time_t;
+bool nf_init(void);
+int nf_process(uint16_t device, uint8_t *buffer, uint16_t packet_length,
+               vigor_time_t now);
+void nf_config_init(int argc, char **argv);
+void nf_config_print(void);
+#define FLOOD_FRAME ((uint16_t)-1)
+
+static void *xread(FILE *f, size_t bytes) {
+  void *p = malloc(bytes ? bytes : 1);
+  if (!p || fread(p, 1, bytes, f) != bytes) {
+    fprintf(stderr, "short trace\n");
+    exit(2);
+  }
+  return p;
+}
+
+int main(int argc, char **argv) {
+  if (argc < 3) {
+    fprintf(stderr, "usage: %s in out [--batch B] -- NF options\n", argv[0]);
+    return 2;
+  }
+  uint32_t batch = 0;
+  int nf_argc = 1;
+  char **nf_argv = argv + 2; /* argv[2] stands in for the program name */
+  for (int i = 3; i < argc; i++) {
+    if (!strcmp(argv[i], "--batch") && i + 1 < argc) {
+      batch = (uint32_t)atoi(argv[++i]);
+    } else if (!strcmp(argv[i], "--")) {
+      nf_argv = argv + i;
+      nf_argc = argc - i;
+      break;
+    }
+  }
+  FILE *f = fopen(argv[1], "rb");
+  if (!f) {
+    perror(argv[1]);
+    return 2;
+  }
+  char magic[4];
+  uint32_t n, slot;
+  if (fread(magic, 1, 4, f) != 4 || memcmp(magic, "VPTR", 4) ||
+      fread(&n, 4, 1, f) != 1 || fread(&slot, 4, 1, f) != 1) {
+    fprintf(stderr, "bad trace header\n");
+    return 2;
+  }
+  uint16_t *in_dev = xread(f, 2ull * n);
+  uint16_t *len = xread(f, 2ull * n);
+  int64_t *now = xread(f, 8ull * n);
+  uint8_t *frames = xread(f, (size_t)n * slot);
+  fclose(f);
+
+  nf_config_init(nf_argc, nf_argv); /* nf.c:230 */
+  if (!nf_init()) {                 /* nf.c:144-146 */
+    fprintf(stderr, "Error initializing NF\n");
+    return 1;
+  }
+  uint16_t *out = calloc(n ? n : 1, 2);
+  uint64_t drops = 0, floods = 0, tx = 0;
+  if (batch == 0) {
+    for (uint32_t i = 0; i < n; i++) /* nf.c:150-176 */
+      out[i] = (uint16_t)nf_process(in_dev[i], frames + (size_t)i * slot, len[i],
+                                    now[i]);
+  } else {
+    extern vp_ctx *vp_nf_context(void);
+    uint8_t **ptrs = malloc(sizeof(uint8_t *) * batch);
+    for (uint32_t a = 0; a < n; a += batch) {
+      uint32_t m = n - a < batch ? n - a : batch;
+      for (uint32_t i = 0; i < m; i++) ptrs[i] = frames + (size_t)(a + i) * slot;
+      if (vp_process_batch(vp_nf_context(), m, in_dev + a, ptrs, len + a,
+                           now + a, out + a) != VP_OK) {
+        fprintf(stderr, "vp_process_batch failed\n");
+        return 1;
+      }
+    }
+    free(ptrs);
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    if (out[i] == in_dev[i]) drops++;
+    else if (out[i] == FLOOD_FRAME) floods++;
+    else tx++;
+  }
+  FILE *o = fopen(argv[2], "wb");
+  if (!o) {
+    perror(argv[2]);
+    return 2;
+  }
+  fwrite("VPTO", 1, 4, o);
+  fwrite(&n, 4, 1, o);
+  fwrite(&slot, 4, 1, o);
+  fwrite(out, 2, n, o);
+  fwrite(frames, 1, (size_t)n * slot, o);
+  fclose(o);
+  printf("packets %u tx %llu drop %llu flood %llu\n", n, (unsigned long long)tx,
+         (unsigned long long)drops, (unsigned long long)floods);
+  return 0;
+}

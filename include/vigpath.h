@@ -156,6 +156,11 @@ int vp_last_kernel_ms(vp_ctx *ctx, float *ms, int *launches);
 /* Build identification (e.g. "vigpath gfx950"). */
 const char *vp_version(void);
 
+/* Exported by the nf.h shim libraries (libvig*_nf.so), not libvigpath.so:
+ * the context nf_init() created, so a batching caller can pass it to
+ * vp_process_batch / vp_process_device. NULL before nf_init(). */
+vp_ctx *vp_nf_context(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,6 +1,8 @@
-"""CPU-side checks of the drop-in boundary: the C-ABI library loads and
-exports every symbol include/vigpath.h declares; host config parsing follows
-the reference's option semantics. No compute calls (no GPU here)."""
+"""CPU-side checks of the drop-in boundary: the C-ABI library and the nf.h
+shims load and export every symbol include/vigpath.h (and the reference's
+nf.h, nf.h:8-18) declares; config parsing follows the reference's option
+semantics. No compute calls (no GPU here)."""
+import ctypes as C
 import os
 import re
 import subprocess
@@ -11,23 +13,26 @@ import vigor_amd
 from vigor_amd import config as cfgmod
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SHIMS = {"nat": os.path.join(ROOT, "vigor_amd", "libvignat_nf.so")}
+NF_H = ["nf_init", "nf_process", "nf_config_init", "nf_config_usage",
+        "nf_config_print", "config"]
 
 
 def declared(header):
     txt = open(os.path.join(ROOT, "include", header)).read()
-    return sorted(set(re.findall(r"^[\w\s\*]*?\b(vp_\w+|nf_\w+)\s*\(", txt,
-                                 re.M)))
+    return sorted(set(re.findall(r"^[\w\s\*]*?\b(vp_\w+)\s*\(", txt, re.M)))
 
 
 def exported(lib):
     out = subprocess.run(["nm", "-D", "--defined-only", lib], check=True,
                          capture_output=True, text=True).stdout
-    return {l.split()[-1] for l in out.splitlines() if " T " in l}
+    return {l.split()[-1] for l in out.splitlines()
+            if len(l.split()) == 3 and l.split()[1] in "TBD"}
 
 
 def test_library_exports_every_declared_symbol():
     syms = exported(vigor_amd.LIB_PATH)
-    want = [s for s in declared("vigpath.h") if s.startswith("vp_")]
+    want = [s for s in declared("vigpath.h") if s != "vp_nf_context"]
     assert want, "no declarations parsed"
     missing = [s for s in want if s not in syms]
     assert not missing, missing
@@ -35,12 +40,49 @@ def test_library_exports_every_declared_symbol():
     vigor_amd.lib()  # loads (resolves every ctypes binding)
 
 
+@pytest.mark.parametrize("nf", sorted(SHIMS))
+def test_shim_exports_nf_h_surface(nf):
+    syms = exported(SHIMS[nf])
+    missing = [s for s in NF_H + ["vp_nf_context"] if s not in syms]
+    assert not missing, missing
+
+
+class RteEther(C.Structure):
+    _fields_ = [("b", C.c_uint8 * 6)]
+
+
+class NatNfConfig(C.Structure):
+    """vignat/nat_config.h:5-31 as the shim defines it."""
+    _fields_ = [("lan_main_device", C.c_uint16), ("wan_device", C.c_uint16),
+                ("external_addr", C.c_uint32),
+                ("device_macs", C.POINTER(RteEther)),
+                ("endpoint_macs", C.POINTER(RteEther)),
+                ("start_port", C.c_uint16), ("expiration_time", C.c_uint32),
+                ("max_flows", C.c_uint32)]
+
+
+def test_shim_nf_config_init_parses_like_reference():
+    os.environ["VIGPATH_NB_DEVICES"] = "2"
+    L = C.CDLL(SHIMS["nat"])
+    args = [b"nf", b"--wan", b"1", b"--expire", b"10", b"--starting-port",
+            b"5", b"--max-flows", b"65536", b"--extip", b"192.168.4.2",
+            b"--eth-dest", b"1,01:23:45:67:89:01"]
+    argv = (C.c_char_p * (len(args) + 1))(*args, None)
+    L.nf_config_init(len(args), argv)
+    cfg = NatNfConfig.in_dll(L, "config")
+    assert (cfg.wan_device, cfg.start_port, cfg.max_flows) == (1, 5, 65536)
+    assert cfg.expiration_time == 10
+    assert cfg.external_addr == 0xC0A80402  # host order (nf-parse.h:25-28)
+    assert bytes(cfg.endpoint_macs[1].b) == bytes.fromhex("012345678901")
+    assert bytes(cfg.device_macs[1].b) == bytes.fromhex("020000000001")
+
+
 def test_nat_config_parse_semantics():
     c = cfgmod.nat_config_from_args(
         ["--wan", "1", "--expire", "10", "--extip", "192.168.4.2",
          "--max-flows", "65536", "--starting-port", "7",
          "--eth-dest", "1,01:23:45:67:89:01"], 2, [b"\x02" * 6, b"\x12" * 6])
-    assert c.external_addr == 0xC0A80402  # host order (nf-parse.h:25-28)
+    assert c.external_addr == 0xC0A80402
     assert (c.wan_device, c.start_port, c.max_flows) == (1, 7, 65536)
     assert bytes(c.endpoint_macs[1]) == bytes.fromhex("012345678901")
     with pytest.raises(ValueError):

@@ -237,14 +237,15 @@ inline void build_position_table(uint32_t *tab, int pos, int msg_len) {
 }
 
 // ------------------------------------------------------------- flow slot --
-// One open-addressing slot of a device table, 32 B (half of a 64-byte memory
-// request): the key is stored in the slot so a hit costs one random line.
-struct __align__(32) FlowSlot {
-  uint32_t k[4];   // 16 key bytes, reference struct layout, padding zero
-  uint32_t hash;
-  uint32_t index;  // kEmpty / kTomb / dchain index
-  uint32_t pad[2];
+// One 64-byte bucket of a device table (one aligned memory request): three
+// entries, each a 16-byte key (reference struct layout, padding zero) and
+// its dchain index (kEmpty / kTomb / index).
+struct __align__(64) Bucket {
+  uint32_t k[3][4];
+  uint32_t idx[3];
+  uint32_t pad;
 };
+constexpr uint32_t kBucketEntries = 3;
 
 __device__ inline bool key_eq(const uint32_t a[4], const uint32_t b[4]) {
   return ((a[0] ^ b[0]) | (a[1] ^ b[1]) | (a[2] ^ b[2]) | (a[3] ^ b[3])) == 0;

@@ -38,18 +38,23 @@ struct Ctl {
   uint64_t min_ts;
   uint32_t new_count;
   uint32_t aux_count;
+  uint32_t max_disp;  // longest insert probe (buckets) since last check
+  uint32_t pad;
 };
 
 // One device table (see vp_table.h).
 struct FlowTable {
-  FlowSlot *slots = nullptr;
-  uint32_t tmask = 0;
+  Bucket *bk = nullptr;
+  uint32_t bmask = 0;  // buckets - 1
   uint32_t cap = 0;
+  uint32_t mix = 0;    // home-bucket mode (vp_table.h home_bucket)
   uint32_t *slot_of = nullptr;
+  uint32_t *hash_of = nullptr;
   uint64_t *ts = nullptr;
   uint64_t *tseq = nullptr;
   uint64_t *birth = nullptr;
   uint32_t *stack = nullptr;
+  uint32_t *lastg = nullptr;  // touch-reduce partial maxima (small tables)
   Ctl *ctl = nullptr;
   Ctl h_ctl{};                     // last copy read back
   uint64_t ts_floor = UINT64_MAX;  // lower bound of min ts over live indices

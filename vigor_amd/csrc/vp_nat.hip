@@ -116,8 +116,8 @@ VP_GENERIC_FN void nat_generic_a(const NatArgs &a, const uint32_t *T, uint32_t p
       a.log[p] = kNone;  // phase C writes the real entry
       return;
     }
-    const FlowSlot &fs = a.t.slots[s];
-    const uint32_t k0 = fs.k[0], k1 = fs.k[1], k2 = fs.k[2], k3 = fs.k[3];
+    const uint4 fk = tbl_key_of(a.t, (uint32_t)idx);
+    const uint32_t k0 = fk.x, k1 = fk.y, k2 = fk.z, k3 = fk.w;
     a.log[p] = (uint32_t)idx;  // rejuvenated before the anti-spoof check
     if ((k2 != sip) | ((k0 >> 16) != sp) | (((k3 >> 16) & 0xFF) != proto)) {
       a.out[p] = (uint16_t)in;
@@ -188,7 +188,7 @@ __device__ __forceinline__ bool nat_fast(const NatArgs &a, const uint32_t *T,
       a.log[p] = kNone;  // phase C writes the real entry
       return false;
     }
-    const uint4 k = *reinterpret_cast<const uint4 *>(a.t.slots + s);
+    const uint4 k = reinterpret_cast<const uint4 *>(a.t.bk + (s >> 2))[s & 3];
     a.log[p] = (uint32_t)idx;  // rejuvenated before the anti-spoof check
     if ((k.z != sip) | ((k.x >> 16) != sp) | (((k.w >> 16) & 0xFF) != proto)) {
       a.out[p] = (uint16_t)in;  // nat_main.c:55-60
@@ -408,8 +408,8 @@ __global__ void nat_defer_finish(NatArgs a, const uint32_t *list, uint32_t n) {
       a.log[p] = kNone;
       continue;
     }
-    const FlowSlot &fs = a.t.slots[a.t.slot_of[idx]];
-    const uint32_t k0 = fs.k[0], k1 = fs.k[1], k2 = fs.k[2], k3 = fs.k[3];
+    const uint4 fk = tbl_key_of(a.t, idx);
+    const uint32_t k0 = fk.x, k1 = fk.y, k2 = fk.z, k3 = fk.w;
     a.log[p] = idx;
     if ((k2 != sip) | ((k0 >> 16) != sp) | (((k3 >> 16) & 0xFF) != proto)) {
       a.out[p] = (uint16_t)in;

@@ -7,19 +7,21 @@
 // order indices are handed out, and which indices expire when (SURVEY.md §0
 // fact 3), so the device keeps an equivalent, batch-friendly form:
 //
-//   slots[]    open-addressed table, 32 B slot = key(16) | hash | index
-//              (tombstones on erase, rebuilt when they pile up)
-//   slot_of[]  index -> slot                    (kNone = index not allocated)
-//   ts[]       index -> dchain timestamp         (exact, see touch log below)
+//   buckets[]  open addressing over 64-byte buckets of 3 entries
+//              (key 16 B + index 4 B each; one aligned 64 B line per probe
+//              step); entries are scanned bucket by bucket, entry by entry;
+//              erase leaves a tombstone, rebuilt when they pile up
+//   slot_of[]  index -> entry (bucket * 4 + e)   (kNone = not allocated)
+//   hash_of[]  index -> key hash (only for rebuilds)
+//   ts[]       index -> dchain timestamp         (exact, see touch log)
 //   tseq[]     index -> global packet seq of the last touch (LRU tie-break)
 //   birth[]    index -> global packet seq of its allocation
-//   stack[]    freed indices, LIFO (dchain free list front); the rest of the
+//   stack[]    freed indices, LIFO (dchain free-list front); the rest of the
 //              free list is the never-used range [fresh_next, cap)
 //
 // Rejuvenation is recorded as a touch log (one u32 index per packet) and
-// folded into ts/tseq after each segment by a stable radix sort: the last
-// entry of each index's run is its last toucher in packet order. No
-// per-packet atomics on shared timestamps.
+// folded into ts/tseq after each segment (last toucher in packet order
+// wins); no per-packet atomics on shared timestamps.
 #pragma once
 
 #include "vp_device.h"
@@ -28,9 +30,10 @@
 namespace vp {
 
 struct TableDev {
-  FlowSlot *slots;
-  uint32_t tmask, cap;
+  Bucket *bk;
+  uint32_t bmask, cap, mix;
   uint32_t *slot_of;
+  uint32_t *hash_of;
   uint64_t *ts;
   uint64_t *tseq;
   uint64_t *birth;
@@ -46,22 +49,50 @@ struct NowSpec {
   }
 };
 
+// Home bucket of a key hash. Mode 0 masks the CRC like the reference
+// (hash & (cap-1), map-impl-pow2.c:15-27): CRC32C is GF(2)-linear, so keys
+// that differ in a few low bits (sequential ports/addresses, the benchmark's
+// flows) land on a structured, well-spread set of buckets, which the memory
+// system serves faster than random lines. For some key sets the masked bits
+// lose rank and buckets cluster; the table detects long insert probes and
+// rebuilds in mode 1 (multiplicative spread). Only the key -> index mapping
+// is observable, so either layout gives identical results.
+__host__ __device__ __forceinline__ uint32_t home_bucket(uint32_t h,
+                                                         uint32_t bmask,
+                                                         uint32_t mix) {
+  return mix ? (uint32_t)(((uint64_t)(h * 0x9E3779B1u) * (bmask + 1ull)) >> 32)
+             : (h & bmask);
+}
+
 // map_get (find_key, map-impl-pow2.c:629-732) on the device table. Returns
 // the index or kNone.
 __device__ __forceinline__ uint32_t tbl_probe(const TableDev &t, uint32_t h,
                                               const uint32_t key[4]) {
-  uint32_t s = h & t.tmask;
-  for (uint32_t i = 0; i <= t.tmask; i++) {
-    const uint4 *sp4 = reinterpret_cast<const uint4 *>(t.slots + s);
-    const uint4 k = sp4[0];
-    const uint4 m = sp4[1];
-    if (m.y == kEmpty) return kNone;
-    if (m.y != kTomb && m.x == h && k.x == key[0] && k.y == key[1] &&
-        k.z == key[2] && k.w == key[3])
-      return m.y;
-    s = (s + 1) & t.tmask;
+  uint32_t b = home_bucket(h, t.bmask, t.mix);
+  for (uint32_t i = 0; i <= t.bmask; i++) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(t.bk + b);
+    const uint4 k0 = q[0], k1 = q[1], k2 = q[2], ix = q[3];
+    if (ix.x == kEmpty) return kNone;
+    if (ix.x != kTomb && k0.x == key[0] && k0.y == key[1] && k0.z == key[2] &&
+        k0.w == key[3])
+      return ix.x;
+    if (ix.y == kEmpty) return kNone;
+    if (ix.y != kTomb && k1.x == key[0] && k1.y == key[1] && k1.z == key[2] &&
+        k1.w == key[3])
+      return ix.y;
+    if (ix.z == kEmpty) return kNone;
+    if (ix.z != kTomb && k2.x == key[0] && k2.y == key[1] && k2.z == key[2] &&
+        k2.w == key[3])
+      return ix.z;
+    b = (b + 1) & t.bmask;
   }
   return kNone;
+}
+
+// Key words of an allocated index's entry.
+__device__ __forceinline__ uint4 tbl_key_of(const TableDev &t, uint32_t idx) {
+  const uint32_t e = t.slot_of[idx];
+  return reinterpret_cast<const uint4 *>(t.bk + (e >> 2))[e & 3];
 }
 
 // dchain_is_index_allocated as seen by the packet with global sequence q
@@ -74,10 +105,10 @@ __device__ __forceinline__ bool tbl_allocated_before(const TableDev &t,
 // ------------------------------------------------------------ host API --
 
 // New-key pipeline input: `n` misses with keys/hashes already in
-// ws.mkey/ws.mhash and positions (ascending) in ws.miss_sorted.
+// ws.mkey/ws.mhash and positions (ascending) in `pos`.
 struct NewKeys {
   uint32_t n;
-  const uint32_t *pos;  // packet positions, ascending
+  const uint32_t *pos;
 };
 
 int tbl_alloc(vp_ctx *c, FlowTable &t, uint32_t cap);
@@ -86,7 +117,7 @@ TableDev tbl_dev(const FlowTable &t);
 
 // Dedup the misses by key (earliest packet wins), rank first sightings in
 // packet order, hand out dchain indices (free-list order) and insert the
-// keys. Afterwards ws.assign[j0] holds the index for first-sighting j0 (or
+// keys. Afterwards ws.assign[j0] holds the index for first sighting j0 (or
 // kNone when the table was full) and scratch[rep[j]] = j0 for every j.
 int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
                  uint32_t *n_new);
@@ -101,7 +132,6 @@ int tbl_exact_floor(vp_ctx *c, FlowTable &t);
 
 // expire_items_single_map for cutoff: free every allocated index with
 // ts < cutoff in LRU order (ts, then tseq) onto the stack, erase its key.
-// *n_out = how many expired.
 int tbl_expire(vp_ctx *c, FlowTable &t, int64_t cutoff, uint32_t *n_out);
 
 // Per index: alloc flag, ts, key words.

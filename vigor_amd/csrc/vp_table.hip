@@ -46,8 +46,8 @@ int read_ctl(vp_ctx *c, FlowTable &t) {
 }
 
 TableDev tbl_dev(const FlowTable &t) {
-  return TableDev{t.slots, t.tmask, t.cap, t.slot_of, t.ts,
-                  t.tseq,  t.birth, t.stack, t.ctl};
+  return TableDev{t.bk, t.bmask, t.cap,   t.mix,   t.slot_of, t.hash_of,
+                  t.ts, t.tseq,  t.birth, t.stack, t.ctl};
 }
 
 template <class T>
@@ -57,25 +57,33 @@ static int dalloc(T **p, size_t count) {
   return e == hipSuccess ? 0 : hip_fail(e, "hipMalloc", __FILE__, __LINE__);
 }
 
+static int tbl_rebuild(vp_ctx *c, FlowTable &t);
+
+static uint64_t tbl_entries(const FlowTable &t) {
+  return (uint64_t)(t.bmask + 1) * kBucketEntries;
+}
+
 int tbl_alloc(vp_ctx *c, FlowTable &t, uint32_t cap) {
   (void)c;
-  // >= 2x the index range: load factor <= 1/2 (+ tombstones <= 1/4)
-  uint64_t ns = 1024;
-  while (ns < 2ull * cap) ns <<= 1;
-  t.tmask = (uint32_t)(ns - 1);
+  // load factor <= ~0.7 of the entries; tombstones purged at 0.85
+  uint64_t nb = 64;
+  while (nb * kBucketEntries * 7 < 10ull * cap) nb <<= 1;
+  t.bmask = (uint32_t)(nb - 1);
   t.cap = cap;
-  VP_TRY(dalloc(&t.slots, ns));
+  VP_TRY(dalloc(&t.bk, nb));
   VP_TRY(dalloc(&t.slot_of, cap));
+  VP_TRY(dalloc(&t.hash_of, cap));
   VP_TRY(dalloc(&t.ts, cap));
   VP_TRY(dalloc(&t.tseq, cap));
   VP_TRY(dalloc(&t.birth, cap));
   VP_TRY(dalloc(&t.stack, cap));
+  VP_TRY(dalloc(&t.lastg, cap));
   VP_TRY(dalloc(&t.ctl, 1));
   VP_TRY(dalloc(&t.ekey, cap));
   VP_TRY(dalloc(&t.ekey2, cap));
   VP_TRY(dalloc(&t.eidx, cap));
   VP_TRY(dalloc(&t.eidx2, cap));
-  VP_HIP(hipMemset(t.slots, 0xFF, sizeof(FlowSlot) * ns));
+  VP_HIP(hipMemset(t.bk, 0xFF, sizeof(Bucket) * nb));
   VP_HIP(hipMemset(t.slot_of, 0xFF, sizeof(uint32_t) * (size_t)cap));
   VP_HIP(hipMemset(t.ts, 0, sizeof(uint64_t) * (size_t)cap));
   VP_HIP(hipMemset(t.tseq, 0, sizeof(uint64_t) * (size_t)cap));
@@ -86,10 +94,41 @@ int tbl_alloc(vp_ctx *c, FlowTable &t, uint32_t cap) {
 }
 
 void tbl_free(FlowTable &t) {
-  void *ptrs[] = {t.slots, t.slot_of, t.ts,   t.tseq,  t.birth, t.stack,
-                  t.ctl,   t.ekey,    t.ekey2, t.eidx, t.eidx2};
+  void *ptrs[] = {t.bk,    t.slot_of, t.hash_of, t.ts,    t.tseq,
+                  t.birth, t.stack,   t.lastg,   t.ctl,   t.ekey,
+                  t.ekey2, t.eidx,    t.eidx2};
   for (void *p : ptrs) hipFree(p);
   t = FlowTable{};
+}
+
+// Claim the first empty-or-erased entry on key hash h's probe path (the
+// map_put position; the key is known to be absent) and store key + index.
+// Returns the entry id. Concurrent claimers race on the index word only.
+__device__ uint32_t tbl_insert(const TableDev &t, uint32_t h, const uint32_t *k,
+                               uint32_t idx, bool *reused_tomb) {
+  uint32_t b = home_bucket(h, t.bmask, t.mix);
+  for (uint32_t d = 0;; d++) {
+    if (d == 8) atomicMax(&t.ctl->max_disp, d);  // clustering signal
+    for (uint32_t e = 0; e < kBucketEntries; e++) {
+      uint32_t *w = &t.bk[b].idx[e];
+      uint32_t cur = __hip_atomic_load(w, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+      while (cur == kEmpty || cur == kTomb) {
+        const uint32_t old = atomicCAS(w, cur, idx);
+        if (old == cur) {
+          uint32_t *kk = t.bk[b].k[e];
+          kk[0] = k[0];
+          kk[1] = k[1];
+          kk[2] = k[2];
+          kk[3] = k[3];
+          *reused_tomb = cur == kTomb;
+          return (b << 2) | e;
+        }
+        cur = old;  // lost the race; look at this entry again
+      }
+    }
+    b = (b + 1) & t.bmask;
+  }
 }
 
 // ------------------------------------------------------------ new keys --
@@ -109,7 +148,7 @@ __global__ void nk_dedup(NkArgs m) {
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m.n;
        j += gridDim.x * blockDim.x) {
     const uint32_t *kj = m.mkey + 4 * (size_t)j;
-    uint32_t s = m.mhash[j] & m.smask;
+    uint32_t s = home_bucket(m.mhash[j], m.smask, 1);
     for (;;) {
       uint32_t old = atomicCAS(&m.scratch[s], kEmpty, j);
       if (old == kEmpty) break;
@@ -148,28 +187,11 @@ __global__ void nk_alloc(NkArgs m) {
     }
     const uint32_t idx =
         r < stack_top ? t.stack[stack_top - 1 - r] : fresh + (r - stack_top);
-    const uint32_t h = m.mhash[j];
-    uint32_t s = h & t.tmask;
-    for (;;) {
-      const uint32_t cur = __hip_atomic_load(&t.slots[s].index, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-      if (cur == kEmpty || cur == kTomb) {
-        if (atomicCAS(&t.slots[s].index, cur, idx) == cur) {
-          if (cur == kTomb) atomicAdd(&t.ctl->tomb_reused, 1u);
-          break;
-        }
-        continue;  // lost the race for this slot; look at it again
-      }
-      s = (s + 1) & t.tmask;
-    }
-    FlowSlot &fs = t.slots[s];
-    const uint32_t *k = m.mkey + 4 * (size_t)j;
-    fs.k[0] = k[0];
-    fs.k[1] = k[1];
-    fs.k[2] = k[2];
-    fs.k[3] = k[3];
-    fs.hash = h;
-    t.slot_of[idx] = s;
+    bool tomb = false;
+    const uint32_t e = tbl_insert(t, m.mhash[j], m.mkey + 4 * (size_t)j, idx, &tomb);
+    if (tomb) atomicAdd(&t.ctl->tomb_reused, 1u);
+    t.slot_of[idx] = e;
+    t.hash_of[idx] = m.mhash[j];
     t.birth[idx] = m.seq_base + m.pos[j];
     m.assign[j] = idx;
   }
@@ -224,15 +246,17 @@ int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
   nk_alloc<<<g, 256, 0, c->stream>>>(m);
   nk_commit<<<1, 64, 0, c->stream>>>(m);
   VP_HIP(hipGetLastError());
-  if (n_new) {
-    VP_TRY(read_ctl(c, t));
-    *n_new = t.h_ctl.new_count;
+  VP_TRY(read_ctl(c, t));
+  if (n_new) *n_new = t.h_ctl.new_count;
+  if (t.h_ctl.max_disp && !t.mix) {  // masked layout clusters for these keys
+    t.mix = 1;
+    VP_HIP(hipMemsetAsync(&t.ctl->max_disp, 0, 4, c->stream));
+    VP_TRY(tbl_rebuild(c, t));
   }
   return 0;
 }
 
 // ---------------------------------------------------------- touch log --
-
 // The index space is cut into chunks of 2^kChunkBits indices (one LDS tile of
 // last-toucher positions per chunk). Pass 1 counts each log span's touches
 // per chunk, an exclusive scan turns the counts into (chunk, span) offsets,
@@ -242,6 +266,26 @@ int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
 constexpr uint32_t kChunkBits = 12;
 constexpr uint32_t kSpan = 16384;  // log entries per pass-1/2 block
 
+// Lanes holding chunk `ch` (valid `v`) that share the first valid lane's
+// chunk are served by one LDS atomic (traffic with locality would otherwise
+// serialise a wave on one counter); the rest add individually. Returns this
+// lane's reserved position.
+__device__ __forceinline__ uint32_t chunk_reserve(uint32_t *ctr, uint32_t ch,
+                                                  bool v) {
+  const uint64_t vm = __ballot(v);
+  if (!vm) return 0;
+  const uint32_t lead = __shfl(ch, __ffsll((unsigned long long)vm) - 1);
+  const bool grp = v && ch == lead;
+  const uint64_t same = __ballot(grp);
+  const uint32_t first = __ffsll((unsigned long long)same) - 1;
+  uint32_t base = 0;
+  if (grp && __lane_id() == first)
+    base = atomicAdd(&ctr[ch], (uint32_t)__popcll(same));
+  base = __shfl(base, first);
+  if (grp) return base + (uint32_t)__popcll(same & ((1ull << __lane_id()) - 1ull));
+  return v ? atomicAdd(&ctr[ch], 1u) : 0;
+}
+
 __global__ __launch_bounds__(256) void touch_count(const uint32_t *log,
                                                    uint32_t n, uint32_t nchunks,
                                                    uint32_t nspans,
@@ -250,17 +294,16 @@ __global__ __launch_bounds__(256) void touch_count(const uint32_t *log,
   for (uint32_t b = threadIdx.x; b < nchunks; b += blockDim.x) cnt[b] = 0;
   __syncthreads();
   const uint32_t s0 = blockIdx.x * kSpan, s1 = min(n, s0 + kSpan);
-  // 4 independent loads in flight per thread
   for (uint32_t j = s0 + threadIdx.x; j < s1; j += 4 * blockDim.x) {
     uint32_t k[4];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < 4; u++) {  // 4 independent loads in flight
       const uint32_t jj = j + u * blockDim.x;
       k[u] = jj < s1 ? log[jj] : kNone;
     }
 #pragma unroll
     for (int u = 0; u < 4; u++)
-      if (k[u] != kNone) atomicAdd(&cnt[k[u] >> kChunkBits], 1u);
+      chunk_reserve(cnt, k[u] >> kChunkBits, k[u] != kNone);
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nchunks; b += blockDim.x)
@@ -286,9 +329,10 @@ __global__ __launch_bounds__(256) void touch_scatter(const uint32_t *log,
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      if (k[u] == kNone) continue;
-      const uint32_t at = atomicAdd(&pos[k[u] >> kChunkBits], 1u);
-      out[at] = make_uint2(k[u] & ((1u << kChunkBits) - 1), j + u * blockDim.x);
+      const bool v = k[u] != kNone;
+      const uint32_t at = chunk_reserve(pos, k[u] >> kChunkBits, v);
+      if (v)
+        out[at] = make_uint2(k[u] & ((1u << kChunkBits) - 1), j + u * blockDim.x);
     }
   }
 }
@@ -298,17 +342,24 @@ __global__ void touch_total(const uint32_t *hist, const uint32_t *off,
   if (threadIdx.x == 0 && blockIdx.x == 0) *total = off[nh - 1] + hist[nh - 1];
 }
 
+// One block per (chunk, part). With one part per chunk the block owns its
+// indices and writes ts/tseq; with several (small tables: too few chunks to
+// fill the chip) the parts combine their maxima in `lastg` and
+// touch_finalize writes ts/tseq.
 __global__ __launch_bounds__(1024) void touch_reduce_k2(
     const uint2 *in, const uint32_t *off, uint32_t nspans, uint32_t nchunks,
-    const uint32_t *total, uint32_t cap, uint32_t p0, NowSpec now,
-    uint64_t seq_base, uint64_t *ts, uint64_t *tseq) {
+    uint32_t split, const uint32_t *total, uint32_t cap, uint32_t p0,
+    NowSpec now, uint64_t seq_base, uint64_t *ts, uint64_t *tseq,
+    uint32_t *lastg) {
   __shared__ uint32_t last[1u << kChunkBits];  // 1 + last position, 0 = none
-  const uint32_t ch = blockIdx.x;
+  const uint32_t ch = blockIdx.x / split, part = blockIdx.x % split;
   for (uint32_t i = threadIdx.x; i < (1u << kChunkBits); i += blockDim.x)
     last[i] = 0;
   __syncthreads();
-  const uint32_t a = off[(size_t)ch * nspans];
-  const uint32_t b = ch + 1 < nchunks ? off[(size_t)(ch + 1) * nspans] : *total;
+  const uint32_t ca = off[(size_t)ch * nspans];
+  const uint32_t cb = ch + 1 < nchunks ? off[(size_t)(ch + 1) * nspans] : *total;
+  const uint32_t per = (cb - ca + split - 1) / split;
+  const uint32_t a = min(cb, ca + part * per), b = min(cb, a + per);
   for (uint32_t j = a + threadIdx.x; j < b; j += 4 * blockDim.x) {
     uint2 e[4];
 #pragma unroll
@@ -326,9 +377,26 @@ __global__ __launch_bounds__(1024) void touch_reduce_k2(
        i += blockDim.x) {
     const uint32_t l = last[i];
     if (!l) continue;
+    if (split > 1) {
+      atomicMax(&lastg[base + i], l);
+      continue;
+    }
     const uint32_t p = p0 + l - 1;
     ts[base + i] = (uint64_t)now.at(p);
     tseq[base + i] = seq_base + p;
+  }
+}
+
+__global__ void touch_finalize(const uint32_t *lastg, uint32_t cap, uint32_t p0,
+                               NowSpec now, uint64_t seq_base, uint64_t *ts,
+                               uint64_t *tseq) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap;
+       i += gridDim.x * blockDim.x) {
+    const uint32_t l = lastg[i];
+    if (!l) continue;
+    const uint32_t p = p0 + l - 1;
+    ts[i] = (uint64_t)now.at(p);
+    tseq[i] = seq_base + p;
   }
 }
 
@@ -362,11 +430,17 @@ int tbl_touch_reduce(vp_ctx *c, FlowTable &t, const uint32_t *log, uint32_t p0,
                                           (int)nh, c->stream));
   touch_scatter<<<nspans, 256, lds, c->stream>>>(log + p0, n, nchunks, nspans, off,
                                                  pairs);
-  // total = off[last] + hist[last]; computed on device by the reducer
   touch_total<<<1, 64, 0, c->stream>>>(hist, off, (uint32_t)nh, &t.ctl->aux_count);
-  touch_reduce_k2<<<nchunks, 1024, 0, c->stream>>>(pairs, off, nspans, nchunks,
-                                                  &t.ctl->aux_count, t.cap, p0,
-                                                  now, seq_base, t.ts, t.tseq);
+  // enough blocks to cover the chip, splitting chunks when there are few
+  const uint32_t split = std::max<uint32_t>(1, 512 / nchunks);
+  if (split > 1)
+    VP_HIP(hipMemsetAsync(t.lastg, 0, sizeof(uint32_t) * (size_t)t.cap, c->stream));
+  touch_reduce_k2<<<nchunks * split, 1024, 0, c->stream>>>(
+      pairs, off, nspans, nchunks, split, &t.ctl->aux_count, t.cap, p0, now,
+      seq_base, t.ts, t.tseq, t.lastg);
+  if (split > 1)
+    touch_finalize<<<grid_for(t.cap), 256, 0, c->stream>>>(t.lastg, t.cap, p0, now,
+                                                           seq_base, t.ts, t.tseq);
   VP_HIP(hipGetLastError());
   return 0;
 }
@@ -427,8 +501,9 @@ __global__ void exp_apply(TableDev t, const uint32_t *eidx, uint32_t n) {
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
        j += gridDim.x * blockDim.x) {
     const uint32_t idx = eidx[j];
+    const uint32_t e = t.slot_of[idx];
     t.stack[top + j] = idx;
-    t.slots[t.slot_of[idx]].index = kTomb;
+    t.bk[e >> 2].idx[e & 3] = kTomb;
     t.slot_of[idx] = kNone;
   }
 }
@@ -441,48 +516,34 @@ __global__ void exp_commit(Ctl *ctl, uint32_t n) {
   }
 }
 
-// Rebuild (tombstone purge): copy live slots out, clear, re-insert.
-__global__ void rb_collect(TableDev t, FlowSlot *out) {
-  const uint32_t ns = t.tmask + 1;
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < ns;
-       s += gridDim.x * blockDim.x) {
-    const bool live = t.slots[s].index < kTomb;
-    const uint32_t k = wave_append(&t.ctl->exp_count, live);
-    if (live) out[k] = t.slots[s];
+// Rebuild (tombstone purge): keys of live indices out, clear, re-insert.
+__global__ void rb_collect(TableDev t, uint32_t *keys) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.cap;
+       i += gridDim.x * blockDim.x) {
+    if (t.slot_of[i] == kNone) continue;
+    const uint4 k = tbl_key_of(t, i);
+    reinterpret_cast<uint4 *>(keys)[i] = k;
   }
 }
-__global__ void rb_insert(TableDev t, const FlowSlot *in, uint32_t n) {
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
-       j += gridDim.x * blockDim.x) {
-    const FlowSlot v = in[j];
-    uint32_t s = v.hash & t.tmask;
-    while (atomicCAS(&t.slots[s].index, kEmpty, v.index) != kEmpty)
-      s = (s + 1) & t.tmask;
-    FlowSlot &d = t.slots[s];
-    d.k[0] = v.k[0];
-    d.k[1] = v.k[1];
-    d.k[2] = v.k[2];
-    d.k[3] = v.k[3];
-    d.hash = v.hash;
-    t.slot_of[v.index] = s;
+__global__ void rb_insert(TableDev t, const uint32_t *keys) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.cap;
+       i += gridDim.x * blockDim.x) {
+    if (t.slot_of[i] == kNone) continue;
+    bool tomb = false;
+    t.slot_of[i] = tbl_insert(t, t.hash_of[i], keys + 4 * (size_t)i, i, &tomb);
   }
 }
 
 static int tbl_rebuild(vp_ctx *c, FlowTable &t) {
-  const uint32_t ns = t.tmask + 1;
-  FlowSlot *tmp = nullptr;
-  VP_HIP(hipMalloc((void **)&tmp, sizeof(FlowSlot) * (size_t)t.cap));
-  VP_HIP(hipMemsetAsync(&t.ctl->exp_count, 0, 4, c->stream));
-  rb_collect<<<grid_for(ns), 256, 0, c->stream>>>(tbl_dev(t), tmp);
-  VP_TRY(read_ctl(c, t));
-  const uint32_t live = t.h_ctl.exp_count;
-  VP_HIP(hipMemsetAsync(t.slots, 0xFF, sizeof(FlowSlot) * (size_t)ns, c->stream));
-  if (live)
-    rb_insert<<<grid_for(live), 256, 0, c->stream>>>(tbl_dev(t), tmp, live);
+  uint32_t *keys = nullptr;
+  VP_TRY(dalloc(&keys, 4ull * t.cap));
+  rb_collect<<<grid_for(t.cap), 256, 0, c->stream>>>(tbl_dev(t), keys);
+  VP_HIP(hipMemsetAsync(t.bk, 0xFF, sizeof(Bucket) * ((size_t)t.bmask + 1),
+                        c->stream));
+  rb_insert<<<grid_for(t.cap), 256, 0, c->stream>>>(tbl_dev(t), keys);
   VP_HIP(hipMemsetAsync(&t.ctl->n_tomb, 0, 4, c->stream));
-  VP_HIP(hipMemsetAsync(&t.ctl->exp_count, 0, 4, c->stream));
   VP_HIP(hipStreamSynchronize(c->stream));
-  VP_HIP(hipFree(tmp));
+  VP_HIP(hipFree(keys));
   return 0;
 }
 
@@ -511,7 +572,7 @@ int tbl_expire(vp_ctx *c, FlowTable &t, int64_t cutoff, uint32_t *n_out) {
   exp_commit<<<1, 64, 0, c->stream>>>(t.ctl, k);
   VP_HIP(hipGetLastError());
   VP_TRY(read_ctl(c, t));
-  if ((uint64_t)t.h_ctl.n_tomb + t.h_ctl.n_live > (uint64_t)(t.tmask + 1) * 3 / 4)
+  if ((uint64_t)t.h_ctl.n_tomb + t.h_ctl.n_live > tbl_entries(t) * 85 / 100)
     return tbl_rebuild(c, t);
   return 0;
 }
@@ -521,10 +582,11 @@ int tbl_expire(vp_ctx *c, FlowTable &t, int64_t cutoff, uint32_t *n_out) {
 __global__ void dump_k(TableDev t, uint8_t *alloc, int64_t *ts, uint32_t *keys) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.cap;
        i += gridDim.x * blockDim.x) {
-    const uint32_t s = t.slot_of[i];
-    alloc[i] = s != kNone;
-    ts[i] = s != kNone ? (int64_t)t.ts[i] : 0;
-    for (int w = 0; w < 4; w++) keys[4 * i + w] = s != kNone ? t.slots[s].k[w] : 0;
+    const bool live = t.slot_of[i] != kNone;
+    alloc[i] = live;
+    ts[i] = live ? (int64_t)t.ts[i] : 0;
+    const uint4 k = live ? tbl_key_of(t, i) : make_uint4(0, 0, 0, 0);
+    reinterpret_cast<uint4 *>(keys)[i] = k;
   }
 }
 
