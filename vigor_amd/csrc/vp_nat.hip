@@ -437,7 +437,7 @@ static inline int64_t nat_cutoff(const vp_ctx *c, int64_t t) {
 
 static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
                        uint32_t p0, uint32_t p1, float *ms, int *launches,
-                       bool *allocated) {
+                       uint32_t *allocated) {
   FlowTable &t = c->ft;
   Workspace &w = c->ws;
   NatArgs a{};
@@ -499,7 +499,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     nat_miss_finish<<<grid_for(nmiss), 256, 0, c->stream>>>(
         a, w.miss_sorted, nmiss, w.scratch, w.rep, w.assign);
     VP_HIP(hipGetLastError());
-    *allocated = true;
+    *allocated |= 1u;
   }
   if (ndefer) {
     nat_defer_finish<<<grid_for(ndefer), 256, 0, c->stream>>>(a, w.defer, ndefer);
@@ -512,77 +512,10 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   return 0;
 }
 
-// Whole batch: cut where an expiry may happen. No flow can expire at packet
-// p while cutoff(t_p) <= min(live stamps), and live stamps within a segment
-// starting at a are >= min(ts_floor, t_a) (rejuvenation only raises stamps,
-// new flows are stamped >= t_a).
+// Whole batch: segments without expiry (run_batch, vp_table.hip).
 int nat_process_device(vp_ctx *c, const vp_dev_batch *b) {
-  const uint32_t n = b->n;
-  c->last_ms = 0.f;
-  c->last_launches = 0;
-  if (n == 0) return 0;
-  if (b->slot < 64 || (b->slot & 15) || !b->frames || !b->len || !b->in_dev ||
-      !b->out_dev)
-    return VP_EINVAL;
-  extern int ws_reserve(vp_ctx *, uint32_t);
-  VP_TRY(ws_reserve(c, n));
-
-  std::vector<int64_t> h_now;
-  int64_t t_first, t_last;
-  if (b->now) {
-    h_now.resize(n);
-    VP_HIP(hipMemcpyAsync(h_now.data(), b->now, sizeof(int64_t) * (size_t)n,
-                          hipMemcpyDeviceToHost, c->stream));
-    VP_HIP(hipStreamSynchronize(c->stream));
-    for (uint32_t i = 1; i < n; i++)
-      if (h_now[i] < h_now[i - 1]) return VP_ENOTSUP;
-    t_first = h_now[0];
-    t_last = h_now[n - 1];
-  } else {
-    if (b->now_step < 0) return VP_ENOTSUP;
-    t_first = b->now0;
-    t_last = b->now0 + (int64_t)(n - 1) * b->now_step;
-  }
-  if (t_first < 0 || t_first < c->last_now) return VP_ENOTSUP;
-  const NowSpec now{b->now, b->now0, b->now_step};
-  auto at = [&](uint32_t p) { return b->now ? h_now[p] : now.at(p); };
-
-  float ms = 0.f;
-  int launches = 0;
-  FlowTable &t = c->ft;
-  uint32_t a0 = 0;
-  while (a0 < n) {
-    const int64_t ta = at(a0);
-    uint64_t lim = std::min<uint64_t>(t.ts_floor, (uint64_t)ta);
-    auto safe = [&](uint32_t p) { return nat_cutoff(c, at(p)) <= (int64_t)lim; };
-    if (!safe(a0)) {
-      VP_TRY(tbl_exact_floor(c, t));
-      if (t.ts_floor != ~0ull && (int64_t)t.ts_floor < nat_cutoff(c, ta)) {
-        VP_TRY(tbl_expire(c, t, nat_cutoff(c, ta), nullptr));
-        VP_TRY(tbl_exact_floor(c, t));
-      }
-      lim = std::min<uint64_t>(t.ts_floor, (uint64_t)ta);
-    }
-    uint32_t b1 = n;
-    if (!safe(n - 1)) {  // first unsafe packet (cutoff is monotone in time)
-      uint32_t lo = a0 + 1, hi = n - 1;
-      while (lo < hi) {
-        const uint32_t mid = lo + (hi - lo) / 2;
-        if (safe(mid)) lo = mid + 1; else hi = mid;
-      }
-      b1 = lo;
-    }
-    bool allocated = false;
-    VP_TRY(nat_segment(c, b, now, a0, b1, &ms, &launches, &allocated));
-    if (allocated) t.ts_floor = std::min<uint64_t>(t.ts_floor, (uint64_t)ta);
-    a0 = b1;
-  }
-  VP_HIP(hipStreamSynchronize(c->stream));
-  c->seq += n;
-  c->last_now = t_last;
-  c->last_ms = ms;
-  c->last_launches = launches;
-  return 0;
+  ExpiringTable tabs[1] = {{&c->ft, nat_cutoff}};
+  return run_batch(c, b, tabs, 1, nat_segment);
 }
 
 int nat_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *keys) {

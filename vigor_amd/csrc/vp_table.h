@@ -140,6 +140,23 @@ int tbl_dump(vp_ctx *c, FlowTable &t, uint8_t *alloc, int64_t *ts,
 
 int read_ctl(vp_ctx *c, FlowTable &t);
 
+// ---------------------------------------------------------- batch driver --
+// A table whose entries expire, and the cutoff for a packet at time t (the
+// NF's own arithmetic, e.g. vignat's u32 wrap).
+struct ExpiringTable {
+  FlowTable *t;
+  int64_t (*cutoff)(const vp_ctx *c, int64_t t);
+};
+// Process packets [p0, p1) of `b` with no expiry inside; set bit i of
+// *allocated when table i got new indices.
+using SegmentFn = int (*)(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
+                          uint32_t p0, uint32_t p1, float *kernel_ms,
+                          int *launches, uint32_t *allocated);
+// Validates the batch, then cuts it where any table may expire an entry and
+// runs the exact expiries between segments (see vp_nat.hip header).
+int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
+              SegmentFn seg);
+
 uint32_t grid_for(uint64_t n, uint32_t block = 256, uint32_t max_blocks = 2048);
 uint32_t next_pow2(uint64_t v);
 int cub_reserve(vp_ctx *c, size_t bytes);

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <vector>
 
 #include "vp_table.h"
 
@@ -574,6 +575,91 @@ int tbl_expire(vp_ctx *c, FlowTable &t, int64_t cutoff, uint32_t *n_out) {
   VP_TRY(read_ctl(c, t));
   if ((uint64_t)t.h_ctl.n_tomb + t.h_ctl.n_live > tbl_entries(t) * 85 / 100)
     return tbl_rebuild(c, t);
+  return 0;
+}
+
+// ---------------------------------------------------------- batch driver --
+
+int ws_reserve(vp_ctx *c, uint32_t n);
+
+// No entry of a table can expire at packet p while cutoff(t_p) <= min(live
+// stamps); inside a segment starting at packet a the live stamps are
+// >= min(ts_floor, t_a) (rejuvenation only raises stamps, new entries are
+// stamped >= t_a). The batch is cut at the first packet where that fails for
+// some table; there the exact expiry of that packet's nf_process runs.
+int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
+              SegmentFn seg) {
+  const uint32_t n = b->n;
+  c->last_ms = 0.f;
+  c->last_launches = 0;
+  if (n == 0) return 0;
+  if (b->slot < 64 || (b->slot & 15) || !b->frames || !b->len || !b->in_dev ||
+      !b->out_dev)
+    return VP_EINVAL;
+  VP_TRY(ws_reserve(c, n));
+
+  std::vector<int64_t> h_now;
+  int64_t t_first, t_last;
+  if (b->now) {
+    h_now.resize(n);
+    VP_HIP(hipMemcpyAsync(h_now.data(), b->now, sizeof(int64_t) * (size_t)n,
+                          hipMemcpyDeviceToHost, c->stream));
+    VP_HIP(hipStreamSynchronize(c->stream));
+    for (uint32_t i = 1; i < n; i++)
+      if (h_now[i] < h_now[i - 1]) return VP_ENOTSUP;
+    t_first = h_now[0];
+    t_last = h_now[n - 1];
+  } else {
+    if (b->now_step < 0) return VP_ENOTSUP;
+    t_first = b->now0;
+    t_last = b->now0 + (int64_t)(n - 1) * b->now_step;
+  }
+  if (t_first < 0 || t_first < c->last_now) return VP_ENOTSUP;
+  const NowSpec now{b->now, b->now0, b->now_step};
+  auto at = [&](uint32_t p) { return b->now ? h_now[p] : now.at(p); };
+
+  float ms = 0.f;
+  int launches = 0;
+  uint32_t a0 = 0;
+  while (a0 < n) {
+    const int64_t ta = at(a0);
+    auto lim = [&](int i) { return std::min<uint64_t>(tabs[i].t->ts_floor, (uint64_t)ta); };
+    auto safe = [&](uint32_t p) {
+      for (int i = 0; i < ntabs; i++)
+        if (tabs[i].cutoff(c, at(p)) > (int64_t)lim(i)) return false;
+      return true;
+    };
+    for (int i = 0; i < ntabs; i++) {  // expiries due at packet a0, in order
+      FlowTable &t = *tabs[i].t;
+      const int64_t cut = tabs[i].cutoff(c, ta);
+      if (cut <= (int64_t)lim(i)) continue;
+      VP_TRY(tbl_exact_floor(c, t));
+      if (t.ts_floor != ~0ull && (int64_t)t.ts_floor < cut) {
+        VP_TRY(tbl_expire(c, t, cut, nullptr));
+        VP_TRY(tbl_exact_floor(c, t));
+      }
+    }
+    uint32_t b1 = n;
+    if (!safe(n - 1)) {  // first unsafe packet (cutoffs are monotone in time)
+      uint32_t lo = a0 + 1, hi = n - 1;
+      while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if (safe(mid)) lo = mid + 1; else hi = mid;
+      }
+      b1 = lo;
+    }
+    uint32_t allocated = 0;
+    VP_TRY(seg(c, b, now, a0, b1, &ms, &launches, &allocated));
+    for (int i = 0; i < ntabs; i++)
+      if (allocated & (1u << i))
+        tabs[i].t->ts_floor = std::min<uint64_t>(tabs[i].t->ts_floor, (uint64_t)ta);
+    a0 = b1;
+  }
+  VP_HIP(hipStreamSynchronize(c->stream));
+  c->seq += n;
+  c->last_now = t_last;
+  c->last_ms = ms;
+  c->last_launches = launches;
   return 0;
 }
 
