@@ -145,6 +145,11 @@ int vp_process_host(vp_ctx *ctx, uint32_t n, const uint16_t *in_dev,
  * bytes, vignat/flow.h:3-10 layout, padding zero). */
 int vp_nat_dump(vp_ctx *ctx, uint8_t *alloc, int64_t *ts, uint8_t *keys);
 
+/* vigbridge dynamic table by index i < dyn_capacity: alloc[i], ts[i],
+ * macs[6*i] (dyn_keys), port[i] (dyn_vals DynamicValue.device). */
+int vp_bridge_dump(vp_ctx *ctx, uint8_t *alloc, int64_t *ts, uint8_t *macs,
+                   uint16_t *port);
+
 /* Number of live flows / learned MACs / flows+backends. */
 int64_t vp_live_count(vp_ctx *ctx);
 

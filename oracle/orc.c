@@ -455,6 +455,29 @@ void orc_nat_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *keys) {
   free(fre);
 }
 
+/* Dynamic table by index: dchain allocated?, ts, dyn_keys[i], dyn_vals[i]. */
+void orc_bridge_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *macs,
+                     uint16_t *port) {
+  struct bridge_state *s = &nf->u.br;
+  int n = (int)s->cfg.dyn_capacity;
+  int *order = malloc(sizeof(int) * (size_t)n);
+  int *fre = malloc(sizeof(int) * (size_t)n);
+  int na, nfree;
+  lv_dchain_dump(s->dyn_heap, n, order, &na, fre, &nfree, ts);
+  for (int i = 0; i < n; i++) {
+    alloc[i] = (uint8_t)lv_dchain_is_index_allocated(s->dyn_heap, i);
+    void *k;
+    lv_vector_borrow(s->dyn_keys, i, &k);
+    memcpy(macs + (size_t)6 * i, k, 6);
+    lv_vector_return(s->dyn_keys, i, k);
+    lv_vector_borrow(s->dyn_vals, i, &k);
+    port[i] = ((struct DynamicValue *)k)->device;
+    lv_vector_return(s->dyn_vals, i, k);
+  }
+  free(order);
+  free(fre);
+}
+
 /* ---- vigbridge ---- */
 orc_nf *orc_bridge_create(const orc_bridge_cfg *cfg) {
   orc_nf *nf = calloc(1, sizeof *nf);

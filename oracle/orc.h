@@ -97,5 +97,7 @@ uint32_t orc_nat_flow_count(orc_nf *nf);
 /* Writes, for index i < max_flows: alloc[i] = allocated?, ts[i] timestamp,
  * key[i] = the 16-byte FlowId stored at that index. */
 void orc_nat_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *keys);
+void orc_bridge_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *macs,
+                     uint16_t *port);
 
 #endif

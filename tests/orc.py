@@ -88,6 +88,7 @@ def lib(ref: bool = False):
     L.orc_nat_flow_count.restype = C.c_uint32
     L.orc_nat_flow_count.argtypes = [C.c_void_p]
     L.orc_nat_dump.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.orc_bridge_dump.argtypes = [C.c_void_p] * 5
     L.orc_test_dchain.restype = C.c_int
     L.orc_test_dchain.argtypes = [C.c_int, C.c_uint32] + [C.c_void_p] * 9
     L.orc_test_map.restype = C.c_int
@@ -179,6 +180,15 @@ class Oracle:
         keys = np.zeros(max_flows * 16, np.uint8)
         self.L.orc_nat_dump(self.h, _ptr(alloc), _ptr(ts), _ptr(keys))
         return alloc, ts, keys.reshape(max_flows, 16)
+
+    def bridge_dump(self, cap):
+        alloc = np.zeros(cap, np.uint8)
+        ts = np.zeros(cap, np.int64)
+        macs = np.zeros(cap * 6, np.uint8)
+        port = np.zeros(cap, np.uint16)
+        self.L.orc_bridge_dump(self.h, _ptr(alloc), _ptr(ts), _ptr(macs),
+                               _ptr(port))
+        return alloc, ts, macs.reshape(cap, 6), port
 
 
 def digest(frames, slot, lens, out_dev, ref=False) -> int:

@@ -5,10 +5,9 @@ vigor_amd); the oracle (oracle/liborc.so) is only the checker.
 """
 import numpy as np
 import pytest
-import torch
-
 import orc
 import vigor_amd
+from gpuh import check_batches, run_gpu
 from tracegen import edge_nat_trace, mixed_nat_trace
 from vigor_amd import traces as T
 
@@ -34,45 +33,6 @@ def make_pair(max_flows=65536, expire_us=60_000_000, start_port=0, wan=1,
                        max_flows=max_flows, device_macs=DEV_MACS[:n_dev],
                        endpoint_macs=END_MACS[:n_dev], n_devices=n_dev)
     return gpu, orc.Oracle("nat", ocfg)
-
-
-def run_gpu(nat, frames, lens, in_dev, now, slot, affine=None):
-    d = torch.device("cuda:0")
-    f = torch.from_numpy(frames.copy()).to(d)
-    l_ = torch.from_numpy(lens.astype(np.uint16).view(np.int16)).to(d)
-    i_ = torch.from_numpy(in_dev.astype(np.uint16).view(np.int16)).to(d)
-    o = torch.zeros(lens.shape[0], dtype=torch.int16, device=d)
-    if affine is None:
-        nt = torch.from_numpy(now.astype(np.int64)).to(d)
-        nat.process_device(f, l_, i_, o, slot, now=nt)
-    else:
-        nat.process_device(f, l_, i_, o, slot, now0=affine[0],
-                           now_step=affine[1])
-    torch.cuda.synchronize()
-    return f.cpu().numpy(), o.cpu().numpy().view(np.uint16)
-
-
-def check_batches(nat, oracle, frames, lens, in_dev, now, slot, cuts,
-                  affine=False):
-    """Feed the trace as consecutive batches split at `cuts`; compare every
-    batch's outputs with the oracle run over the same packets."""
-    exp = frames.copy()
-    exp_out = oracle.run(exp, lens, in_dev, now, slot)
-    bounds = [0] + sorted(set(cuts)) + [lens.shape[0]]
-    for a, b in zip(bounds[:-1], bounds[1:]):
-        if a == b:
-            continue
-        fr = frames[a * slot:b * slot]
-        aff = (int(now[a]), int(now[a + 1] - now[a]) if b - a > 1 else 1) \
-            if affine else None
-        got, out = run_gpu(nat, fr, lens[a:b], in_dev[a:b], now[a:b], slot,
-                           aff)
-        bad = np.nonzero(out != exp_out[a:b])[0]
-        assert bad.size == 0, "out port mismatch at packets %s" % (bad[:10] + a)
-        gf = got.reshape(b - a, slot)
-        ef = exp[a * slot:b * slot].reshape(b - a, slot)
-        badf = np.nonzero((gf != ef).any(axis=1))[0]
-        assert badf.size == 0, "frame mismatch at packets %s" % (badf[:10] + a)
 
 
 def check_state(nat, oracle, max_flows):

@@ -271,9 +271,14 @@ def test_bridge_trace_matches_reference(seed, cap, expire_us):
                             n_devices=3)
         o = orc.Oracle("bridge", cfg, ref=ref, statics=statics)
         f = fr.copy()
-        res.append((o.run(f, ln, dv, now, 64), f))
+        res.append((o.run(f, ln, dv, now, 64), f, o.bridge_dump(cap)))
     np.testing.assert_array_equal(res[0][0], res[1][0])
     np.testing.assert_array_equal(res[0][1], res[1][1])
+    (a0, t0, m0, p0), (a1, t1, m1, p1) = res[0][2], res[1][2]
+    np.testing.assert_array_equal(a0, a1)
+    np.testing.assert_array_equal(t0[a0 == 1], t1[a1 == 1])
+    np.testing.assert_array_equal(m0, m1)
+    np.testing.assert_array_equal(p0, p1)
 
 
 def lb_cfg(flow_cap=1024, bcap=32, height=97, fexp=60_000_000, bexp=3_600_000):

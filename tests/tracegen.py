@@ -76,3 +76,29 @@ def edge_nat_trace(rng, n, n_flows, slot=128, long_frames=False):
                 f[l4 + 2:l4 + 4] = (k >> 8, k & 0xFF)
         lens[i] = flen
     return frames.reshape(-1), lens, in_dev
+
+
+def mixed_bridge_trace(rng, n, n_stations, n_dev=3, slot=64):
+    """vigbridge stress: stations 02:00:00:00:kk:kk on random ports (MAC
+    moves), dst from the same pool (known, unknown, the frame's own src) or
+    broadcast/never-learned, short frames, monotone time with ties."""
+    src = rng.integers(0, n_stations, n)
+    dst = rng.integers(0, n_stations + n_stations // 4, n)  # some never seen
+    same = rng.random(n) < 0.05
+    dst[same] = src[same]
+    frames = np.zeros((n, slot), np.uint8)
+    frames[:, 0:4] = [0x02, 0, 0, 0]
+    frames[:, 4] = (dst >> 8) & 0xFF
+    frames[:, 5] = dst & 0xFF
+    frames[:, 6:10] = [0x02, 0, 0, 0]
+    frames[:, 10] = (src >> 8) & 0xFF
+    frames[:, 11] = src & 0xFF
+    bc = rng.random(n) < 0.03
+    frames[bc, 0:6] = 0xFF
+    frames[:, 12:14] = [0x08, 0x00]
+    frames[:, 14:] = rng.integers(0, 256, (n, slot - 14), dtype=np.uint8)
+    lens = rng.integers(60, slot + 1, n).astype(np.uint16)
+    lens[rng.random(n) < 0.02] = rng.integers(0, 14)  # runts: no length check
+    in_dev = rng.integers(0, n_dev, n).astype(np.uint16)
+    now = T.NOW0 + np.cumsum(rng.integers(0, 3, n))
+    return frames.reshape(-1), lens, in_dev, now.astype(np.int64)

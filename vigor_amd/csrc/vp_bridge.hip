@@ -1,0 +1,337 @@
+// vigbridge on MI355X: MAC learning + forwarding lookup over a packet batch.
+//
+// Reference behaviour (paths relative to the reference repository):
+//   nf_process                 vigbridge/bridge_main.c:311-329
+//   expiry                     bridge_expire_entries, bridge_main.c:29-36
+//                              (u32 wrap of expiration_time * 1000 as vignat)
+//   learn src -> in port       bridge_put_update_entry, bridge_main.c:63-89
+//                              (a known MAC is only rejuvenated; its port is
+//                              not updated)
+//   lookup {dst, in} static,   bridge_get_device, bridge_main.c:38-61
+//   then dst dynamic; miss -> FLOOD_FRAME; -2 -> drop (return in port)
+//   rte_ether_addr_hash        libvig/verified/ether.c:61-90 (6 CRC steps)
+//   static table               read_static_ft_from_file, bridge_main.c:130-230
+//
+// Same segment scheme as vignat (vp_nat.hip header):
+//   phase A  hash + probe src and dst; a known src is logged for
+//            rejuvenation, an unknown one queued; a dst known at segment
+//            start (or in the static table) is forwarded at once, an unknown
+//            one flooded provisionally and queued;
+//   phase B  queued src MACs are de-duplicated (earliest packet wins) and
+//            given dchain indices in packet order; the first sighting's in
+//            port becomes the entry's port;
+//   phase C  (only when B allocated something) queued dst MACs are looked up
+//            again: a MAC learned by a packet at or before this one (the
+//            packet's own src counts: learn precedes lookup) forwards there.
+//
+// Dynamic table entry: key words {mac[0..3], mac[4..5], port, 0}. Only words
+// 0-1 identify the MAC; word 2 carries the DynamicValue (dyn_vals vector in
+// the reference) so one bucket read resolves a lookup.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstring>
+#include <vector>
+
+#include "vp_table.h"
+
+namespace vp {
+
+// rte_ether_addr_hash: crc32c_u32 of each byte in turn, so the non-zero byte
+// positions of the 24-byte CRC message are 0, 4, 8, 12, 16, 20.
+constexpr int kEthTabs = 6;
+// StaticKey hash (generated; nested struct field hashed by its own hash):
+// crc(crc(0, ether_hash(addr)), device), an 8-byte message with non-zero
+// bytes 0-3 (the MAC hash) and 4-5 (the u16 device).
+constexpr int kStatTabs = 6;
+constexpr int kBridgeTabs = kEthTabs + kStatTabs;
+
+__device__ __forceinline__ uint32_t eth_hash(const uint32_t *T, uint32_t m0,
+                                             uint32_t m1) {
+  return T[0 * 256 + (m0 & 0xFF)] ^ T[1 * 256 + ((m0 >> 8) & 0xFF)] ^
+         T[2 * 256 + ((m0 >> 16) & 0xFF)] ^ T[3 * 256 + (m0 >> 24)] ^
+         T[4 * 256 + (m1 & 0xFF)] ^ T[5 * 256 + ((m1 >> 8) & 0xFF)];
+}
+__device__ __forceinline__ uint32_t static_hash(const uint32_t *T, uint32_t eh,
+                                                uint32_t dev) {
+  const uint32_t *S = T + kEthTabs * 256;
+  return S[0 * 256 + (eh & 0xFF)] ^ S[1 * 256 + ((eh >> 8) & 0xFF)] ^
+         S[2 * 256 + ((eh >> 16) & 0xFF)] ^ S[3 * 256 + (eh >> 24)] ^
+         S[4 * 256 + (dev & 0xFF)] ^ S[5 * 256 + ((dev >> 8) & 0xFF)];
+}
+
+// map_get on the dynamic table keyed by words 0-1; *port = entry word 2.
+__device__ __forceinline__ uint32_t mac_probe(const TableDev &t, uint32_t h,
+                                              uint32_t m0, uint32_t m1,
+                                              uint32_t *port) {
+  uint32_t b = home_bucket(h, t.bmask, t.mix);
+  for (uint32_t i = 0; i <= t.bmask; i++) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(t.bk + b);
+    const uint4 k0 = q[0], k1 = q[1], k2 = q[2], ix = q[3];
+    if (ix.x == kEmpty) return kNone;
+    if (ix.x != kTomb && k0.x == m0 && k0.y == m1) {
+      *port = k0.z;
+      return ix.x;
+    }
+    if (ix.y == kEmpty) return kNone;
+    if (ix.y != kTomb && k1.x == m0 && k1.y == m1) {
+      *port = k1.z;
+      return ix.y;
+    }
+    if (ix.z == kEmpty) return kNone;
+    if (ix.z != kTomb && k2.x == m0 && k2.y == m1) {
+      *port = k2.z;
+      return ix.z;
+    }
+    b = (b + 1) & t.bmask;
+  }
+  return kNone;
+}
+
+struct BridgeArgs {
+  const uint8_t *frames;
+  const uint16_t *in_dev;
+  uint16_t *out;
+  uint32_t *log;
+  uint64_t seq_base;
+  uint32_t slot, p0, p1;
+  TableDev t;
+  TableDev st;  // static table: bk/bmask/mix only; idx = rule number
+  const int32_t *st_val;
+  uint32_t n_static;
+  const uint32_t *crc_tab;
+  uint32_t *miss;
+  uint32_t *defer;
+};
+
+// nf_process's return value for a forwarding decision (bridge_main.c:322-328).
+__device__ __forceinline__ uint16_t resolve(int32_t fwd, uint32_t in) {
+  if (fwd == -1) return VP_FLOOD_FRAME;
+  if (fwd == -2) return (uint16_t)in;
+  return (uint16_t)fwd;
+}
+
+// Ethernet header words: dst = {w0, w1 & 0xFFFF}, src = {w1 >> 16 | w2 << 16,
+// w2 >> 16} (bridge_main.c:312 borrows 14 bytes with no length check).
+__device__ __forceinline__ uint4 eth_words(const BridgeArgs &a, uint32_t p) {
+  return *reinterpret_cast<const uint4 *>(a.frames + (size_t)p * a.slot);
+}
+
+__global__ __launch_bounds__(256) void bridge_classify(BridgeArgs a) {
+  __shared__ uint32_t T[kBridgeTabs * 256];
+  for (uint32_t i = threadIdx.x; i < kBridgeTabs * 256; i += blockDim.x)
+    T[i] = a.crc_tab[i];
+  __syncthreads();
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t p = a.p0 + blockIdx.x * blockDim.x + threadIdx.x; p < a.p1;
+       p += stride) {
+    const uint4 h = eth_words(a, p);
+    const uint32_t in = a.in_dev[p];
+    const uint32_t d0 = h.x, d1 = h.y & 0xFFFF;
+    const uint32_t s0 = (h.y >> 16) | (h.z << 16), s1 = h.z >> 16;
+    // bridge_put_update_entry
+    uint32_t unused;
+    const uint32_t si = mac_probe(a.t, eth_hash(T, s0, s1), s0, s1, &unused);
+    a.log[p] = si;  // kNone: phase B writes the real entry
+    if (si == kNone) a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
+    // bridge_get_device
+    const uint32_t dh = eth_hash(T, d0, d1);
+    if (a.n_static) {
+      const uint32_t key[4] = {d0, d1 | (in << 16), 0, 0};
+      const uint32_t k = tbl_probe(a.st, static_hash(T, dh, in), key);
+      if (k != kNone) {
+        a.out[p] = resolve(a.st_val[k], in);
+        continue;
+      }
+    }
+    uint32_t port = 0;
+    const uint32_t di = mac_probe(a.t, dh, d0, d1, &port);
+    if (di != kNone) {
+      a.out[p] = (uint16_t)port;
+    } else {  // flooded unless learned earlier in this segment (phase C)
+      a.out[p] = VP_FLOOD_FRAME;
+      a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
+    }
+  }
+}
+
+// Keys + hashes of the queued src MACs (packet order).
+__global__ void bridge_miss_keys(BridgeArgs a, const uint32_t *list, uint32_t n,
+                                 uint32_t *mkey, uint32_t *mhash) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += gridDim.x * blockDim.x) {
+    const uint4 h = eth_words(a, list[j]);
+    const uint32_t s0 = (h.y >> 16) | (h.z << 16), s1 = h.z >> 16;
+    uint32_t *k = mkey + 4 * (size_t)j;
+    k[0] = s0;
+    k[1] = s1;
+    k[2] = 0;
+    k[3] = 0;
+    mhash[j] = eth_hash(a.crc_tab, s0, s1);
+  }
+}
+
+// Touch log for every queued src; the first sighting stores its in port as
+// the entry's DynamicValue (bridge_main.c:80-84).
+__global__ void bridge_learn_finish(BridgeArgs a, const uint32_t *list,
+                                    uint32_t n, const uint32_t *scratch,
+                                    const uint32_t *rep, const uint32_t *assign) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += gridDim.x * blockDim.x) {
+    const uint32_t p = list[j];
+    const uint32_t j0 = scratch[rep[j]];
+    const uint32_t idx = assign[j0];
+    a.log[p] = idx;  // kNone: table full, nothing learned (bridge_main.c:73-76)
+    if (j0 == j && idx != kNone) {
+      const uint32_t e = a.t.slot_of[idx];
+      a.t.bk[e >> 2].k[e & 3][2] = a.in_dev[p];
+    }
+  }
+}
+
+__global__ void bridge_defer_finish(BridgeArgs a, const uint32_t *list,
+                                    uint32_t n) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += gridDim.x * blockDim.x) {
+    const uint32_t p = list[j];
+    const uint4 h = eth_words(a, p);
+    const uint32_t d0 = h.x, d1 = h.y & 0xFFFF;
+    uint32_t port = 0;
+    const uint32_t di = mac_probe(a.t, eth_hash(a.crc_tab, d0, d1), d0, d1, &port);
+    // learned by packet q' <= p: the packet's own src is learned first
+    if (di != kNone && tbl_allocated_before(a.t, di, a.seq_base + p + 1))
+      a.out[p] = (uint16_t)port;
+  }
+}
+
+// =============================================================== host ==
+
+static inline int64_t bridge_cutoff(const vp_ctx *c, int64_t t) {
+  const uint32_t e = c->brg.expiration_time * 1000u;  // u32, as vignat
+  return (int64_t)((uint64_t)t - e);
+}
+
+static int bridge_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
+                          uint32_t p0, uint32_t p1, float *ms, int *launches,
+                          uint32_t *allocated) {
+  FlowTable &t = c->ft;
+  Workspace &w = c->ws;
+  BridgeArgs a{};
+  a.frames = b->frames;
+  a.in_dev = b->in_dev;
+  a.out = b->out_dev;
+  a.log = w.log;
+  a.seq_base = c->seq;
+  a.slot = b->slot;
+  a.p0 = p0;
+  a.p1 = p1;
+  a.t = tbl_dev(t);
+  a.st = TableDev{};
+  a.st.bk = c->st_bk;
+  a.st.bmask = c->st_bmask;
+  a.st.mix = 1;
+  a.st_val = c->st_val;
+  a.n_static = c->n_static;
+  a.crc_tab = c->crc_tab;
+  a.miss = w.miss;
+  a.defer = w.defer;
+
+  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 8, c->stream));  // + defer
+  VP_HIP(hipEventRecord(c->ev0, c->stream));
+  bridge_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
+  VP_HIP(hipGetLastError());
+  VP_HIP(hipEventRecord(c->ev1, c->stream));
+  VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, c->seq));
+  VP_TRY(read_ctl(c, t));
+  float kms = 0.f;
+  VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
+  *ms += kms;
+  *launches += 1;
+  const uint32_t nmiss = t.h_ctl.miss_count, ndefer = t.h_ctl.defer_count;
+  if (!nmiss) return 0;  // nothing learned: provisional floods stand
+
+  size_t need = 0;
+  hipcub::DeviceRadixSort::SortKeys(nullptr, need, w.miss, w.miss_sorted,
+                                    (int)nmiss, 0, 32, c->stream);
+  VP_TRY(cub_reserve(c, need));
+  VP_HIP(hipcub::DeviceRadixSort::SortKeys(w.cub_tmp, w.cub_bytes, w.miss,
+                                           w.miss_sorted, (int)nmiss, 0, 32,
+                                           c->stream));
+  bridge_miss_keys<<<grid_for(nmiss), 256, 0, c->stream>>>(a, w.miss_sorted, nmiss,
+                                                           w.mkey, w.mhash);
+  VP_HIP(hipGetLastError());
+  VP_TRY(tbl_new_keys(c, t, NewKeys{nmiss, w.miss_sorted}, c->seq, nullptr));
+  a.t = tbl_dev(t);  // a rebuild may have changed the layout
+  bridge_learn_finish<<<grid_for(nmiss), 256, 0, c->stream>>>(
+      a, w.miss_sorted, nmiss, w.scratch, w.rep, w.assign);
+  VP_HIP(hipGetLastError());
+  if (ndefer) {
+    bridge_defer_finish<<<grid_for(ndefer), 256, 0, c->stream>>>(a, w.defer, ndefer);
+    VP_HIP(hipGetLastError());
+  }
+  *allocated |= 1u;
+  VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, c->seq));
+  VP_TRY(read_ctl(c, t));
+  return 0;
+}
+
+int bridge_process_device(vp_ctx *c, const vp_dev_batch *b) {
+  ExpiringTable tabs[1] = {{&c->ft, bridge_cutoff}};
+  return run_batch(c, b, tabs, 1, bridge_segment);
+}
+
+void build_bridge_tables(std::vector<uint32_t> &tab) {
+  tab.assign(kBridgeTabs * 256, 0);
+  for (int j = 0; j < kEthTabs; j++)
+    build_position_table(&tab[j * 256], 4 * j, 24);
+  for (int j = 0; j < kStatTabs; j++)
+    build_position_table(&tab[(kEthTabs + j) * 256], j, 8);
+}
+
+// Static table (read_static_ft_from_file): rule k keyed {mac, (u16)from},
+// value `to`. Built on the host into the device bucket layout. A repeated key
+// keeps the first rule: the reference's map_put appends the duplicate
+// further along the same probe path, so map_get finds the first.
+int bridge_static_build(const vp_bridge_config *cfg, std::vector<Bucket> &bk,
+                        uint32_t *bmask) {
+  uint32_t nb = 64;
+  while ((uint64_t)nb * kBucketEntries < 2ull * cfg->n_static) nb <<= 1;
+  bk.assign(nb, Bucket{});
+  for (auto &x : bk)
+    for (uint32_t e = 0; e < kBucketEntries; e++) x.idx[e] = kEmpty;
+  *bmask = nb - 1;
+  std::vector<uint32_t> tab;
+  build_bridge_tables(tab);
+  const uint32_t *E = tab.data(), *S = tab.data() + kEthTabs * 256;
+  for (uint32_t r = 0; r < cfg->n_static; r++) {
+    const vp_bridge_rule &R = cfg->static_rules[r];
+    const uint32_t m0 = R.mac[0] | (R.mac[1] << 8) | (R.mac[2] << 16) |
+                        ((uint32_t)R.mac[3] << 24);
+    const uint32_t m1 = R.mac[4] | (R.mac[5] << 8);
+    const uint32_t dev = (uint16_t)R.device_from;
+    const uint32_t key[4] = {m0, m1 | (dev << 16), 0, 0};
+    uint32_t eh = 0;
+    for (int j = 0; j < 6; j++) eh ^= E[j * 256 + R.mac[j]];
+    const uint32_t h = S[0 * 256 + (eh & 0xFF)] ^ S[1 * 256 + ((eh >> 8) & 0xFF)] ^
+                       S[2 * 256 + ((eh >> 16) & 0xFF)] ^ S[3 * 256 + (eh >> 24)] ^
+                       S[4 * 256 + (dev & 0xFF)] ^ S[5 * 256 + (dev >> 8)];
+    uint32_t b = home_bucket(h, *bmask, 1);
+    bool placed = false;
+    while (!placed) {
+      for (uint32_t e = 0; e < kBucketEntries && !placed; e++) {
+        Bucket &x = bk[b];
+        if (x.idx[e] == kEmpty) {
+          memcpy(x.k[e], key, 16);
+          x.idx[e] = r;
+          placed = true;
+        } else if (!memcmp(x.k[e], key, 16)) {
+          placed = true;  // duplicate: the first rule stays visible
+        }
+      }
+      b = (b + 1) & *bmask;
+    }
+  }
+  return 0;
+}
+
+}  // namespace vp

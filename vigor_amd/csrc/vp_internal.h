@@ -104,7 +104,12 @@ struct vp_ctx {
   uint64_t seq = 0;       // packets processed so far (global packet order)
   int64_t last_now = -1;  // time of the last packet processed
   vp_nat_config nat{};
+  vp_bridge_config brg{};  // static_rules not kept (built into st_*)
   vp::FlowTable ft;       // vignat flows / vigbridge dyn MACs / viglb flows
+  vp::Bucket *st_bk = nullptr;  // vigbridge static table (rule number = idx)
+  uint32_t st_bmask = 0;
+  int32_t *st_val = nullptr;    // rule -> device_to
+  uint32_t n_static = 0;
   uint32_t *crc_tab = nullptr;  // CRC position tables (LDS-staged)
   uint32_t *macw = nullptr;     // per device: d_addr|s_addr header words
   uint32_t wan_macw[3] = {0, 0, 0};

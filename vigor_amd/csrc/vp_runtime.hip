@@ -22,6 +22,10 @@ int hip_fail(hipError_t e, const char *what, const char *file, int line) {
 int nat_process_device(vp_ctx *c, const vp_dev_batch *b);
 int nat_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *keys);
 void build_flowid_tables(std::vector<uint32_t> &tab);
+int bridge_process_device(vp_ctx *c, const vp_dev_batch *b);
+void build_bridge_tables(std::vector<uint32_t> &tab);
+int bridge_static_build(const vp_bridge_config *cfg, std::vector<Bucket> &bk,
+                        uint32_t *bmask);
 
 static bool is_pow2(uint32_t v) { return v && !(v & (v - 1)); }
 
@@ -104,7 +108,8 @@ static void free_all(vp_ctx *c) {
   Workspace &w = c->ws;
   ws_release(w);
   void *ptrs[] = {w.hist, w.hoff, w.cub_tmp, w.d_frames, w.d_len,    w.d_in,
-                  w.d_out,   w.d_now,    c->crc_tab, c->macw};
+                  w.d_out,   w.d_now,    c->crc_tab, c->macw,
+                  c->st_bk,  c->st_val};
   for (void *p : ptrs) hipFree(p);
   if (w.h_frames) hipHostFree(w.h_frames);
   if (c->ev0) hipEventDestroy(c->ev0);
@@ -131,6 +136,28 @@ static int nat_init(vp_ctx *c, const vp_nat_config *cfg) {
     mac_words(cfg->endpoint_macs[d], cfg->device_macs[d], &mw[3 * d]);
   memcpy(c->wan_macw, &mw[3 * cfg->wan_device], sizeof c->wan_macw);
   VP_TRY(upload(&c->macw, mw));
+  return 0;
+}
+
+static int bridge_init(vp_ctx *c, const vp_bridge_config *cfg) {
+  c->kind = KIND_BRIDGE;
+  c->brg = *cfg;
+  c->brg.static_rules = nullptr;
+  VP_TRY(tbl_alloc(c, c->ft, cfg->dyn_capacity));
+  std::vector<uint32_t> tab;
+  build_bridge_tables(tab);
+  VP_TRY(upload(&c->crc_tab, tab));
+  std::vector<Bucket> bk;
+  VP_TRY(bridge_static_build(cfg, bk, &c->st_bmask));
+  VP_TRY(dalloc(&c->st_bk, bk.size()));
+  VP_HIP(hipMemcpy(c->st_bk, bk.data(), bk.size() * sizeof(Bucket),
+                   hipMemcpyHostToDevice));
+  std::vector<int32_t> val(cfg->n_static + 1, 0);
+  for (uint32_t r = 0; r < cfg->n_static; r++)
+    val[r] = cfg->static_rules[r].device_to;
+  VP_TRY(dalloc(&c->st_val, val.size()));
+  VP_HIP(hipMemcpy(c->st_val, val.data(), val.size() * 4, hipMemcpyHostToDevice));
+  c->n_static = cfg->n_static;
   return 0;
 }
 
@@ -198,10 +225,21 @@ int vp_nat_create(const vp_nat_config *cfg, int gpu, vp_ctx **out) {
 }
 
 int vp_bridge_create(const vp_bridge_config *cfg, int gpu, vp_ctx **out) {
-  (void)cfg;
-  (void)gpu;
-  (void)out;
-  return VP_ENOTSUP;
+  if (!cfg || !out || (cfg->n_static && !cfg->static_rules)) return VP_EINVAL;
+  // map.c:73 (CAPACITY_POW2); bridge_main.c:150-154: the static map (8192
+  // entries, bridge_main.c:293) must stay at most half full
+  if (!is_pow2(cfg->dyn_capacity) || cfg->dyn_capacity > (1u << 30) ||
+      2ull * cfg->n_static >= 8192)
+    return VP_EINVAL;
+  vp_ctx *c = new vp_ctx();
+  int rc = ctx_common(c, gpu);
+  if (!rc) rc = bridge_init(c, cfg);
+  if (rc) {
+    free_all(c);
+    return rc;
+  }
+  *out = c;
+  return 0;
 }
 
 int vp_lb_create(const vp_lb_config *cfg, int gpu, vp_ctx **out) {
@@ -227,6 +265,9 @@ int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
   switch (c->kind) {
     case KIND_NAT:
       rc = nat_process_device(c, b);
+      break;
+    case KIND_BRIDGE:
+      rc = bridge_process_device(c, b);
       break;
     default:
       break;
@@ -307,6 +348,22 @@ int vp_nat_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *keys) {
   if (!c || c->kind != KIND_NAT || !alloc || !ts || !keys) return VP_EINVAL;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
   return nat_dump(c, alloc, ts, keys);
+}
+
+int vp_bridge_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *macs,
+                   uint16_t *port) {
+  if (!c || c->kind != KIND_BRIDGE || !alloc || !ts || !macs || !port)
+    return VP_EINVAL;
+  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  std::vector<uint32_t> keys(4ull * c->ft.cap);
+  VP_TRY(tbl_dump(c, c->ft, alloc, ts, keys.data()));
+  for (uint32_t i = 0; i < c->ft.cap; i++) {
+    const uint32_t *k = &keys[4ull * i];
+    memcpy(macs + 6ull * i, k, 4);
+    memcpy(macs + 6ull * i + 4, k + 1, 2);
+    port[i] = (uint16_t)k[2];
+  }
+  return 0;
 }
 
 int64_t vp_live_count(vp_ctx *c) {

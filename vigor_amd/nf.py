@@ -136,6 +136,18 @@ class Bridge(NfBase):
         _check(self.L.vp_bridge_create(C.byref(cfg), gpu, C.byref(self.h)),
                "vp_bridge_create")
 
+    def dump(self):
+        """Dynamic table by index: alloc, ts, MAC (6 B), learned port."""
+        n = self.cfg.dyn_capacity
+        alloc = np.zeros(n, np.uint8)
+        ts = np.zeros(n, np.int64)
+        macs = np.zeros(n * 6, np.uint8)
+        port = np.zeros(n, np.uint16)
+        P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
+        _check(self.L.vp_bridge_dump(self.h, P(alloc), P(ts), P(macs), P(port)),
+               "vp_bridge_dump")
+        return alloc, ts, macs.reshape(n, 6), port
+
 
 class Lb(NfBase):
     kind = "lb"
