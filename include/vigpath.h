@@ -150,6 +150,15 @@ int vp_nat_dump(vp_ctx *ctx, uint8_t *alloc, int64_t *ts, uint8_t *keys);
 int vp_bridge_dump(vp_ctx *ctx, uint8_t *alloc, int64_t *ts, uint8_t *macs,
                    uint16_t *port);
 
+/* viglb state. Flows i < flow_capacity: f_alloc[i], f_ts[i], f_keys[16*i]
+ * (LoadBalancedFlow bytes, lb_flow.h:6-12, padding zero), f_backend[i]
+ * (flow_id_to_backend_id). Backends b < backend_capacity: b_alloc[b],
+ * b_ts[b], and backends[b] (lb_backend.h:7-11) as b_ip[b], b_mac[6*b],
+ * b_nic[b]. */
+int vp_lb_dump(vp_ctx *ctx, uint8_t *f_alloc, int64_t *f_ts, uint8_t *f_keys,
+               uint32_t *f_backend, uint8_t *b_alloc, int64_t *b_ts,
+               uint32_t *b_ip, uint8_t *b_mac, uint16_t *b_nic);
+
 /* Number of live flows / learned MACs / flows+backends. */
 int64_t vp_live_count(vp_ctx *ctx);
 

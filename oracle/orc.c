@@ -478,6 +478,51 @@ void orc_bridge_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *macs,
   free(fre);
 }
 
+/* viglb state by index. Flows i < flow_capacity: allocated?, ts, LbFlow
+ * bytes (16, padding zero), flow_id_to_backend_id. Backends b <
+ * backend_capacity: allocated?, ts, backends[b] as {ip, mac, nic}. */
+void orc_lb_dump(orc_nf *nf, uint8_t *f_alloc, int64_t *f_ts, uint8_t *f_keys,
+                 uint32_t *f_backend, uint8_t *b_alloc, int64_t *b_ts,
+                 uint32_t *b_ip, uint8_t *b_mac, uint16_t *b_nic) {
+  struct lb_state *s = &nf->u.lb;
+  int nf_ = (int)s->cfg.flow_capacity, nb = (int)s->cfg.backend_capacity;
+  int n = nf_ > nb ? nf_ : nb;
+  int *order = malloc(sizeof(int) * (size_t)n);
+  int *fre = malloc(sizeof(int) * (size_t)n);
+  int na, nfree;
+  lv_dchain_dump(s->flow_chain, nf_, order, &na, fre, &nfree, f_ts);
+  for (int i = 0; i < nf_; i++) {
+    f_alloc[i] = (uint8_t)lv_dchain_is_index_allocated(s->flow_chain, i);
+    void *k;
+    lv_vector_borrow(s->flow_heap, i, &k);
+    struct LbFlow *fl = k;
+    uint8_t *o = f_keys + (size_t)16 * i;
+    memset(o, 0, 16);
+    memcpy(o, &fl->src_ip, 4);
+    memcpy(o + 4, &fl->dst_ip, 4);
+    memcpy(o + 8, &fl->src_port, 2);
+    memcpy(o + 10, &fl->dst_port, 2);
+    o[12] = fl->protocol;
+    lv_vector_return(s->flow_heap, i, k);
+    lv_vector_borrow(s->flow_id_to_backend_id, i, &k);
+    f_backend[i] = *(uint32_t *)k;
+    lv_vector_return(s->flow_id_to_backend_id, i, k);
+  }
+  lv_dchain_dump(s->active_backends, nb, order, &na, fre, &nfree, b_ts);
+  for (int i = 0; i < nb; i++) {
+    b_alloc[i] = (uint8_t)lv_dchain_is_index_allocated(s->active_backends, i);
+    void *k;
+    lv_vector_borrow(s->backends, i, &k);
+    struct LbBackend *b = k;
+    b_ip[i] = b->ip;
+    memcpy(b_mac + (size_t)6 * i, b->mac.b, 6);
+    b_nic[i] = b->nic;
+    lv_vector_return(s->backends, i, k);
+  }
+  free(order);
+  free(fre);
+}
+
 /* ---- vigbridge ---- */
 orc_nf *orc_bridge_create(const orc_bridge_cfg *cfg) {
   orc_nf *nf = calloc(1, sizeof *nf);

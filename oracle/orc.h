@@ -99,5 +99,8 @@ uint32_t orc_nat_flow_count(orc_nf *nf);
 void orc_nat_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *keys);
 void orc_bridge_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *macs,
                      uint16_t *port);
+void orc_lb_dump(orc_nf *nf, uint8_t *f_alloc, int64_t *f_ts, uint8_t *f_keys,
+                 uint32_t *f_backend, uint8_t *b_alloc, int64_t *b_ts,
+                 uint32_t *b_ip, uint8_t *b_mac, uint16_t *b_nic);
 
 #endif

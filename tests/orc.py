@@ -89,6 +89,7 @@ def lib(ref: bool = False):
     L.orc_nat_flow_count.argtypes = [C.c_void_p]
     L.orc_nat_dump.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.orc_bridge_dump.argtypes = [C.c_void_p] * 5
+    L.orc_lb_dump.argtypes = [C.c_void_p] * 10
     L.orc_test_dchain.restype = C.c_int
     L.orc_test_dchain.argtypes = [C.c_int, C.c_uint32] + [C.c_void_p] * 9
     L.orc_test_map.restype = C.c_int
@@ -189,6 +190,23 @@ class Oracle:
         self.L.orc_bridge_dump(self.h, _ptr(alloc), _ptr(ts), _ptr(macs),
                                _ptr(port))
         return alloc, ts, macs.reshape(cap, 6), port
+
+    def lb_dump(self, flow_cap, backend_cap):
+        """(flow alloc, ts, keys[16], backend id), (backend alloc, ts, ip,
+        mac[6], nic)."""
+        fa = np.zeros(flow_cap, np.uint8)
+        ft = np.zeros(flow_cap, np.int64)
+        fk = np.zeros(flow_cap * 16, np.uint8)
+        fb = np.zeros(flow_cap, np.uint32)
+        ba = np.zeros(backend_cap, np.uint8)
+        bt = np.zeros(backend_cap, np.int64)
+        bi = np.zeros(backend_cap, np.uint32)
+        bm = np.zeros(backend_cap * 6, np.uint8)
+        bn = np.zeros(backend_cap, np.uint16)
+        self.L.orc_lb_dump(self.h, *[_ptr(x) for x in
+                                     (fa, ft, fk, fb, ba, bt, bi, bm, bn)])
+        return ((fa, ft, fk.reshape(flow_cap, 16), fb),
+                (ba, bt, bi, bm.reshape(backend_cap, 6), bn))
 
 
 def digest(frames, slot, lens, out_dev, ref=False) -> int:

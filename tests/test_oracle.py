@@ -310,6 +310,11 @@ def test_lb_trace_matches_reference(seed, fexp, bexp):
     for ref in (False, True):
         o = orc.Oracle("lb", lb_cfg(fexp=fexp, bexp=bexp), ref=ref)
         f = fr.copy()
-        res.append((o.run(f, ln, dv, now, 64), f))
+        res.append((o.run(f, ln, dv, now, 64), f, o.lb_dump(1024, 32)))
     np.testing.assert_array_equal(res[0][0], res[1][0])
     np.testing.assert_array_equal(res[0][1], res[1][1])
+    for x, y in zip(res[0][2], res[1][2]):  # flows, then backends
+        live = x[0] == 1
+        np.testing.assert_array_equal(x[0], y[0])
+        for a, b in zip(x[1:], y[1:]):
+            np.testing.assert_array_equal(a[live], b[live])

@@ -102,3 +102,40 @@ def mixed_bridge_trace(rng, n, n_stations, n_dev=3, slot=64):
     in_dev = rng.integers(0, n_dev, n).astype(np.uint16)
     now = T.NOW0 + np.cumsum(rng.integers(0, 3, n))
     return frames.reshape(-1), lens, in_dev, now.astype(np.int64)
+
+
+def mixed_lb_trace(rng, n, n_flows, n_backends, hb_frac=0.05, quiet=None,
+                   wan=2, slot=64, bad_frac=0.03):
+    """viglb stress: WAN traffic over n_flows (uniform) with heartbeats from
+    n_backends IPs on ports 0/1 mixed in; no heartbeats inside the packet
+    window `quiet` (so backends can all expire), malformed frames, monotone
+    time with ties."""
+    fl = rng.integers(0, n_flows, n)
+    sip = T.ip4(11, 0, 0, 0) + fl
+    dip = T.ip4(10, 9, 8, 7) + (fl % 3)
+    sp = 2000 + fl % 11
+    dp = np.full(n, 80)
+    proto = np.where(fl % 4 == 0, 6, 17)
+    hb = rng.random(n) < hb_frac
+    if quiet is not None:
+        hb[quiet[0]:quiet[1]] = False
+    be = rng.integers(0, n_backends, n)
+    sip = np.where(hb, T.ip4(192, 168, 0, 0) + be, sip)
+    frames = np.zeros((n, slot), np.uint8)
+    lens = np.zeros(n, np.uint16)
+    for p_ in (6, 17):
+        m = proto == p_
+        f, ln = T.udp_frames(sip[m], dip[m], sp[m], dp[m], slot=slot, proto=p_)
+        frames[m] = f.reshape(-1, slot)
+        lens[m] = ln
+    frames[:, 6:8] = [0x02, 0xBE]
+    frames[:, 8] = (be >> 8) & 0xFF
+    frames[:, 9] = be & 0xFF
+    frames[:, 10:12] = rng.integers(0, 256, (n, 2), dtype=np.uint8)
+    in_dev = np.where(hb, be & 1, wan).astype(np.uint16)
+    bad = rng.random(n)
+    frames[bad < bad_frac / 3, 12] = 0x86
+    frames[(bad >= bad_frac / 3) & (bad < 2 * bad_frac / 3), 23] = 1
+    frames[(bad >= 2 * bad_frac / 3) & (bad < bad_frac), 17] = 250
+    now = T.NOW0 + np.cumsum(rng.integers(0, 3, n))
+    return frames.reshape(-1), lens, in_dev, now.astype(np.int64)

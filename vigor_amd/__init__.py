@@ -71,7 +71,7 @@ class DevBatchC(C.Structure):
 # every symbol include/vigpath.h declares
 EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_destroy",
            "vp_process_device", "vp_process_batch", "vp_process_host",
-           "vp_nat_dump", "vp_bridge_dump", "vp_live_count", "vp_last_kernel_ms", "vp_version"]
+           "vp_nat_dump", "vp_bridge_dump", "vp_lb_dump", "vp_live_count", "vp_last_kernel_ms", "vp_version"]
 
 _libs = {}
 
@@ -111,6 +111,8 @@ def lib(path: str | None = None):
     L.vp_nat_dump.restype = C.c_int
     L.vp_bridge_dump.argtypes = [C.c_void_p] * 5
     L.vp_bridge_dump.restype = C.c_int
+    L.vp_lb_dump.argtypes = [C.c_void_p] * 10
+    L.vp_lb_dump.restype = C.c_int
     L.vp_live_count.argtypes = [C.c_void_p]
     L.vp_live_count.restype = C.c_int64
     L.vp_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float),

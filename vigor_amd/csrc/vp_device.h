@@ -180,6 +180,73 @@ struct RFrame {
   }
 };
 
+// LDS image of one wave's 64 frames (64 x 64 B): 16-byte chunk c (packet
+// c/4, part c%4) lives at c ^ ((c >> 4) & 3), so both the lane-contiguous
+// global<->LDS copies and each lane's 4 reads of its own frame are
+// bank-conflict-free ds_*_b128 accesses.
+__device__ __forceinline__ uint32_t chunk_swz(uint32_t c) {
+  return c ^ ((c >> 4) & 3u);
+}
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Packets [p0, p1) of a batch of n_all 64-byte slots, in tiles of 64
+// consecutive packets per wave (256-thread blocks, 4 waves): every global
+// load/store instruction moves 1 KiB contiguous (lane l <-> bytes
+// 16l..16l+15 of a 1 KiB piece), staged through the wave's LDS tile S
+// (256 x uint4). fn(p, RFrame&) handles one packet and returns true when the
+// frame was modified and must be written back.
+template <class Fn>
+__device__ __forceinline__ void frames64_tiles(uint8_t *frames, uint32_t p0,
+                                               uint32_t p1, uint32_t n_all,
+                                               uint4 *S, Fn fn) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t first = p0 & ~63u;
+  const uint32_t tiles = (p1 - first + 63) / 64;
+  const uint32_t nwaves = gridDim.x * 4;
+  for (uint32_t tile = blockIdx.x * 4 + wv; tile < tiles; tile += nwaves) {
+    const uint32_t tb = first + tile * 64;
+    uint4 *g = reinterpret_cast<uint4 *>(frames + (size_t)tb * 64);
+    const uint32_t avail = n_all - tb < 64 ? n_all - tb : 64;  // in the batch
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+      const uint32_t c = 64 * j + lane;
+      if ((c >> 2) < avail) S[chunk_swz(c)] = g[c];
+    }
+    wave_lds_sync();
+    const uint32_t p = tb + lane;
+    const bool mine = p >= p0 && p < p1;
+    RFrame f;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint4 v = S[chunk_swz(4 * lane + k)];
+      f.w[4 * k] = v.x;
+      f.w[4 * k + 1] = v.y;
+      f.w[4 * k + 2] = v.z;
+      f.w[4 * k + 3] = v.w;
+    }
+    bool mod = false;
+    if (mine) mod = fn(p, f);
+    if (mod) {
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++)
+        S[chunk_swz(4 * lane + k)] =
+            make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
+    }
+    const uint64_t modmask = __ballot(mod);
+    wave_lds_sync();
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+      const uint32_t c = 64 * j + lane;
+      if ((modmask >> (c >> 2)) & 1ull) g[c] = S[chunk_swz(c)];
+    }
+    wave_lds_sync();  // the next tile overwrites S
+  }
+}
+
 // Checksums of a 64-byte IHL=5 frame with total_length <= 50 (so every byte
 // the L4 sum covers lies in the slot). Same arithmetic as set_checksums.
 __device__ inline void fast_checksums(RFrame &f, uint32_t proto, uint32_t tl) {

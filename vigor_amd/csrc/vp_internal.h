@@ -76,6 +76,10 @@ struct Workspace {
   uint32_t *assign = nullptr;
   uint32_t *scratch = nullptr;
   uint32_t *log = nullptr;   // touch log, one entry per packet
+  uint32_t *log2 = nullptr;  // second table's touch log (viglb backends)
+  uint32_t *defer_sorted = nullptr;
+  uint32_t *aux = nullptr, *aux_sorted = nullptr;  // third queue (viglb)
+  uint32_t *rlist = nullptr;  // re-classification input (viglb rounds)
   uint32_t *iota = nullptr;  // 0..cap_n-1
   uint32_t *skey = nullptr, *sval = nullptr;
   uint32_t *hist = nullptr, *hoff = nullptr;  // touch-reduce (chunk x span)
@@ -106,6 +110,11 @@ struct vp_ctx {
   vp_nat_config nat{};
   vp_bridge_config brg{};  // static_rules not kept (built into st_*)
   vp::FlowTable ft;       // vignat flows / vigbridge dyn MACs / viglb flows
+  vp::FlowTable ft2;      // viglb backends (ip_to_backend_id + dchain)
+  vp_lb_config lb{};
+  uint4 *be_rec = nullptr;  // viglb backends[]: {ip, mac0-3, mac4-5|nic<<16, 0}
+  uint32_t *cht = nullptr;  // viglb CHT, cht[bucket * backend_capacity + prio]
+  uint32_t *dmacw = nullptr;  // per device: {s_addr[0..1] << 16, s_addr[2..5]}
   vp::Bucket *st_bk = nullptr;  // vigbridge static table (rule number = idx)
   uint32_t st_bmask = 0;
   int32_t *st_val = nullptr;    // rule -> device_to

@@ -273,70 +273,14 @@ __global__ __launch_bounds__(256) void nat_classify(NatArgs a) {
   }
 }
 
-// LDS image of one wave's 64 frames (64 x 64 B): 16-byte chunk c (packet
-// c/4, part c%4) lives at c ^ ((c >> 4) & 3), so both the lane-contiguous
-// global<->LDS copies and each lane's 4 reads of its own frame are
-// bank-conflict-free ds_*_b128 accesses.
-__device__ __forceinline__ uint32_t chunk_swz(uint32_t c) {
-  return c ^ ((c >> 4) & 3u);
-}
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Phase A for 64-byte slots: every global load/store instruction moves 1 KiB
-// contiguous (lane l <-> bytes 16l..16l+15 of a 1 KiB piece), staged through
-// LDS; each wave owns 64 consecutive packets per step.
+// Phase A for 64-byte slots: LDS-staged 1 KiB-contiguous frame I/O
+// (frames64_tiles, vp_device.h); each wave owns 64 consecutive packets.
 __global__ __launch_bounds__(256) void nat_classify64(NatArgs a, uint32_t n_all) {
   __shared__ uint32_t T[15 * 256];
   __shared__ uint4 stage[4][256];
   load_crc_tables(T, a.crc_tab);
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint4 *S = stage[wv];
-  const uint32_t first = a.p0 & ~63u;
-  const uint32_t tiles = (a.p1 - first + 63) / 64;
-  const uint32_t nwaves = gridDim.x * 4;
-  for (uint32_t tile = blockIdx.x * 4 + wv; tile < tiles; tile += nwaves) {
-    const uint32_t tb = first + tile * 64;
-    uint4 *g = reinterpret_cast<uint4 *>(a.frames + (size_t)tb * 64);
-    // packets of the tile that exist in the batch
-    const uint32_t avail = n_all - tb < 64 ? n_all - tb : 64;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
-      const uint32_t c = 64 * j + lane;
-      if ((c >> 2) < avail) S[chunk_swz(c)] = g[c];
-    }
-    wave_lds_sync();
-    const uint32_t p = tb + lane;
-    const bool mine = p >= a.p0 && p < a.p1;
-    RFrame f;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-      const uint4 v = S[chunk_swz(4 * lane + k)];
-      f.w[4 * k] = v.x;
-      f.w[4 * k + 1] = v.y;
-      f.w[4 * k + 2] = v.z;
-      f.w[4 * k + 3] = v.w;
-    }
-    bool mod = false;
-    if (mine) mod = nat_fast(a, T, p, f);
-    if (mod) {
-#pragma unroll
-      for (uint32_t k = 0; k < 4; k++)
-        S[chunk_swz(4 * lane + k)] =
-            make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
-    }
-    const uint64_t modmask = __ballot(mod);
-    wave_lds_sync();
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
-      const uint32_t c = 64 * j + lane;
-      if ((modmask >> (c >> 2)) & 1ull) g[c] = S[chunk_swz(c)];
-    }
-    wave_lds_sync();  // the next tile overwrites S
-  }
+  frames64_tiles(a.frames, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
+                 [&](uint32_t p, RFrame &f) { return nat_fast(a, T, p, f); });
 }
 
 // ------------------------------------------------------------- phase B --

@@ -26,6 +26,12 @@ int bridge_process_device(vp_ctx *c, const vp_dev_batch *b);
 void build_bridge_tables(std::vector<uint32_t> &tab);
 int bridge_static_build(const vp_bridge_config *cfg, std::vector<Bucket> &bk,
                         uint32_t *bmask);
+int lb_process_device(vp_ctx *c, const vp_dev_batch *b);
+void build_lb_tables(std::vector<uint32_t> &tab);
+void lb_fill_cht(uint32_t height, uint32_t bcap, std::vector<uint32_t> &cht);
+int lb_dump(vp_ctx *c, uint8_t *f_alloc, int64_t *f_ts, uint8_t *f_keys,
+            uint32_t *f_backend, uint8_t *b_alloc, int64_t *b_ts, uint32_t *b_ip,
+            uint8_t *b_mac, uint16_t *b_nic);
 
 static bool is_pow2(uint32_t v) { return v && !(v & (v - 1)); }
 
@@ -45,10 +51,12 @@ __global__ void iota_k(uint32_t *v, uint32_t n) {
 static void ws_release(Workspace &w) {
   void *ptrs[] = {w.miss,  w.miss_sorted, w.defer, w.mkey, w.mhash,
                   w.first, w.rank,        w.rep,   w.assign, w.scratch,
-                  w.log,   w.iota,        w.skey,  w.sval};
+                  w.log,   w.iota,        w.skey,  w.sval,
+                  w.log2,  w.defer_sorted, w.aux,  w.aux_sorted, w.rlist};
   for (void *p : ptrs) hipFree(p);
   w.miss = w.miss_sorted = w.defer = w.mkey = w.mhash = w.first = w.rank =
       w.rep = w.assign = w.scratch = w.log = w.iota = w.skey = w.sval = nullptr;
+  w.log2 = w.defer_sorted = w.aux = w.aux_sorted = w.rlist = nullptr;
   w.cap_n = 0;
 }
 
@@ -71,6 +79,13 @@ int ws_reserve(vp_ctx *c, uint32_t n) {
   VP_TRY(dalloc(&w.assign, cap));
   VP_TRY(dalloc(&w.scratch, ss));
   VP_TRY(dalloc(&w.log, cap));
+  if (c->kind == KIND_LB) {  // second table + round queues
+    VP_TRY(dalloc(&w.log2, cap));
+    VP_TRY(dalloc(&w.defer_sorted, cap));
+    VP_TRY(dalloc(&w.aux, cap));
+    VP_TRY(dalloc(&w.aux_sorted, cap));
+    VP_TRY(dalloc(&w.rlist, cap));
+  }
   VP_TRY(dalloc(&w.iota, cap));
   VP_TRY(dalloc(&w.skey, cap));
   VP_TRY(dalloc(&w.sval, cap));
@@ -105,11 +120,12 @@ static void free_all(vp_ctx *c) {
   hipSetDevice(c->gpu);
   if (c->stream) hipStreamSynchronize(c->stream);
   tbl_free(c->ft);
+  tbl_free(c->ft2);
   Workspace &w = c->ws;
   ws_release(w);
   void *ptrs[] = {w.hist, w.hoff, w.cub_tmp, w.d_frames, w.d_len,    w.d_in,
                   w.d_out,   w.d_now,    c->crc_tab, c->macw,
-                  c->st_bk,  c->st_val};
+                  c->st_bk,  c->st_val,  c->be_rec,   c->cht,   c->dmacw};
   for (void *p : ptrs) hipFree(p);
   if (w.h_frames) hipHostFree(w.h_frames);
   if (c->ev0) hipEventDestroy(c->ev0);
@@ -159,6 +175,36 @@ static int bridge_init(vp_ctx *c, const vp_bridge_config *cfg) {
   VP_HIP(hipMemcpy(c->st_val, val.data(), val.size() * 4, hipMemcpyHostToDevice));
   c->n_static = cfg->n_static;
   return 0;
+}
+
+static int lb_init(vp_ctx *c, const vp_lb_config *cfg) {
+  c->kind = KIND_LB;
+  c->lb = *cfg;
+  VP_TRY(tbl_alloc(c, c->ft, cfg->flow_capacity));
+  VP_TRY(tbl_alloc(c, c->ft2, cfg->backend_capacity));
+  std::vector<uint32_t> tab;
+  build_lb_tables(tab);
+  VP_TRY(upload(&c->crc_tab, tab));
+  std::vector<uint32_t> cht;
+  lb_fill_cht(cfg->cht_height, cfg->backend_capacity, cht);
+  VP_TRY(upload(&c->cht, cht));
+  VP_TRY(dalloc(&c->be_rec, cfg->backend_capacity));
+  VP_HIP(hipMemset(c->be_rec, 0, sizeof(uint4) * cfg->backend_capacity));
+  std::vector<uint32_t> dm(2 * VP_MAX_DEVICES, 0);
+  for (int d = 0; d < cfg->n_devices; d++) {
+    const uint8_t *m = cfg->device_macs[d];
+    dm[2 * d] = ((uint32_t)m[0] | ((uint32_t)m[1] << 8)) << 16;
+    dm[2 * d + 1] = m[2] | (m[3] << 8) | (m[4] << 16) | ((uint32_t)m[5] << 24);
+  }
+  VP_TRY(upload(&c->dmacw, dm));
+  return 0;
+}
+
+static bool is_prime(uint32_t v) {
+  if (v < 2) return false;
+  for (uint32_t d = 2; (uint64_t)d * d <= v; d++)
+    if (v % d == 0) return false;
+  return true;
 }
 
 static int stage_meta(vp_ctx *c, uint32_t n) {
@@ -243,10 +289,23 @@ int vp_bridge_create(const vp_bridge_config *cfg, int gpu, vp_ctx **out) {
 }
 
 int vp_lb_create(const vp_lb_config *cfg, int gpu, vp_ctx **out) {
-  (void)cfg;
-  (void)gpu;
-  (void)out;
-  return VP_ENOTSUP;
+  if (!cfg || !out) return VP_EINVAL;
+  // map.c:73 (CAPACITY_POW2) for both maps; cht_fill_cht's precondition
+  // (cht.c:546-553): prime height < MAX_CHT_HEIGHT, 0 < backends < height
+  if (!is_pow2(cfg->flow_capacity) || cfg->flow_capacity > (1u << 30) ||
+      !is_pow2(cfg->backend_capacity) || cfg->backend_capacity >= cfg->cht_height ||
+      cfg->cht_height >= 40000 || !is_prime(cfg->cht_height) ||
+      cfg->n_devices == 0 || cfg->n_devices > VP_MAX_DEVICES)
+    return VP_EINVAL;
+  vp_ctx *c = new vp_ctx();
+  int rc = ctx_common(c, gpu);
+  if (!rc) rc = lb_init(c, cfg);
+  if (rc) {
+    free_all(c);
+    return rc;
+  }
+  *out = c;
+  return 0;
 }
 
 void vp_destroy(vp_ctx *ctx) { free_all(ctx); }
@@ -268,6 +327,9 @@ int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
       break;
     case KIND_BRIDGE:
       rc = bridge_process_device(c, b);
+      break;
+    case KIND_LB:
+      rc = lb_process_device(c, b);
       break;
     default:
       break;
@@ -372,7 +434,24 @@ int64_t vp_live_count(vp_ctx *c) {
   Ctl h{};
   if (hipMemcpy(&h, c->ft.ctl, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)
     return VP_EIO;
-  return h.n_live;
+  int64_t live = h.n_live;
+  if (c->kind == KIND_LB) {
+    if (hipMemcpy(&h, c->ft2.ctl, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)
+      return VP_EIO;
+    live += h.n_live;
+  }
+  return live;
+}
+
+int vp_lb_dump(vp_ctx *c, uint8_t *f_alloc, int64_t *f_ts, uint8_t *f_keys,
+               uint32_t *f_backend, uint8_t *b_alloc, int64_t *b_ts,
+               uint32_t *b_ip, uint8_t *b_mac, uint16_t *b_nic) {
+  if (!c || c->kind != KIND_LB || !f_alloc || !f_ts || !f_keys || !f_backend ||
+      !b_alloc || !b_ts || !b_ip || !b_mac || !b_nic)
+    return VP_EINVAL;
+  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  return lb_dump(c, f_alloc, f_ts, f_keys, f_backend, b_alloc, b_ts, b_ip, b_mac,
+                 b_nic);
 }
 
 int vp_last_kernel_ms(vp_ctx *c, float *ms, int *launches) {

@@ -134,6 +134,9 @@ int tbl_exact_floor(vp_ctx *c, FlowTable &t);
 // ts < cutoff in LRU order (ts, then tseq) onto the stack, erase its key.
 int tbl_expire(vp_ctx *c, FlowTable &t, int64_t cutoff, uint32_t *n_out);
 
+// Purge tombstones (rebuild) once live + erased entries pass 85 %.
+int tbl_check_tombs(vp_ctx *c, FlowTable &t);
+
 // Per index: alloc flag, ts, key words.
 int tbl_dump(vp_ctx *c, FlowTable &t, uint8_t *alloc, int64_t *ts,
              uint32_t *keys);

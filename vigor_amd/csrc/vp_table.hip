@@ -572,6 +572,10 @@ int tbl_expire(vp_ctx *c, FlowTable &t, int64_t cutoff, uint32_t *n_out) {
   exp_apply<<<grid_for(k), 256, 0, c->stream>>>(tbl_dev(t), t.eidx, k);
   exp_commit<<<1, 64, 0, c->stream>>>(t.ctl, k);
   VP_HIP(hipGetLastError());
+  return tbl_check_tombs(c, t);
+}
+
+int tbl_check_tombs(vp_ctx *c, FlowTable &t) {
   VP_TRY(read_ctl(c, t));
   if ((uint64_t)t.h_ctl.n_tomb + t.h_ctl.n_live > tbl_entries(t) * 85 / 100)
     return tbl_rebuild(c, t);

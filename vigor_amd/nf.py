@@ -157,3 +157,18 @@ class Lb(NfBase):
         self.cfg = cfg
         _check(self.L.vp_lb_create(C.byref(cfg), gpu, C.byref(self.h)),
                "vp_lb_create")
+
+    def dump(self):
+        """(flow alloc, ts, keys[16], backend id), (backend alloc, ts, ip,
+        mac[6], nic) by index."""
+        nf_, nb = self.cfg.flow_capacity, self.cfg.backend_capacity
+        fa, ft = np.zeros(nf_, np.uint8), np.zeros(nf_, np.int64)
+        fk, fb = np.zeros(nf_ * 16, np.uint8), np.zeros(nf_, np.uint32)
+        ba, bt = np.zeros(nb, np.uint8), np.zeros(nb, np.int64)
+        bi, bm = np.zeros(nb, np.uint32), np.zeros(nb * 6, np.uint8)
+        bn = np.zeros(nb, np.uint16)
+        _check(self.L.vp_lb_dump(self.h, *[C.c_void_p(x.ctypes.data) for x in
+                                           (fa, ft, fk, fb, ba, bt, bi, bm, bn)]),
+               "vp_lb_dump")
+        return ((fa, ft, fk.reshape(nf_, 16), fb),
+                (ba, bt, bi, bm.reshape(nb, 6), bn))
