@@ -9,6 +9,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -71,6 +72,8 @@ int tbl_alloc(vp_ctx *c, FlowTable &t, uint32_t cap) {
   while (nb * kBucketEntries * 7 < 10ull * cap) nb <<= 1;
   t.bmask = (uint32_t)(nb - 1);
   t.cap = cap;
+  const char *mix = getenv("VIGPATH_MIX");  // diagnostics: start in mode 1
+  t.mix = mix && atoi(mix) ? 1 : 0;
   VP_TRY(dalloc(&t.bk, nb));
   VP_TRY(dalloc(&t.slot_of, cap));
   VP_TRY(dalloc(&t.hash_of, cap));
