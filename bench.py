@@ -44,6 +44,7 @@ METRIC = "Mpackets/s device-resident, 64B vignat @1M flows; %HBM roofline"
 ALG_BYTES = 92          # 64 frame + 4 len/port + 16 key + 4 tag + 4 value
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SLOT = 64
+TRAFFIC_PROFILE = "r01_bench_traffic.json"  # rocprofv3 --pmc passes
 DEV_MACS = [T.mac("02:00:00:00:00:00"), T.mac("02:00:00:00:00:01")]
 NAT_ARGS = ["--expire", "60000000", "--starting-port", "0", "--wan", "1",
             "--extip", "192.168.4.2", "--eth-dest", "0,90:e2:ba:55:12:20",
@@ -178,6 +179,12 @@ def main():
     per_launch_s = kernel_s / max(1, launches)
     pkts_per_launch = B * args.steps / max(1, launches)
     achieved = ALG_BYTES * pkts_per_launch / per_launch_s / 1e9
+    traffic = None  # PMC bytes of the same kernel (profiles/, per launch)
+    tpath = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE)
+    if os.path.exists(tpath) and B == 1 << 24 and args.flows == 1 << 20:
+        with open(tpath) as fh:
+            tb = json.load(fh)["traffic_bytes_per_launch"]
+        traffic = round(tb * pkts_per_launch / (1 << 24) / per_launch_s / 1e9, 1)
     if rank == 0:
         cpu = None
         if not args.no_cpu and world == 1:
@@ -204,8 +211,12 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None,
-                         "kernel": "nat_classify",
+                         "traffic": traffic,
+                         "traffic_source": "profiles/%s: (2 x FETCH_SIZE + "
+                                           "WRITE_SIZE) per launch / this "
+                                           "run's kernel time" % TRAFFIC_PROFILE
+                                           if traffic else None,
+                         "kernel": "nat_classify64",
                          "kernel_ms_per_launch": round(per_launch_s * 1e3, 4),
                          "alg_bytes_per_packet": ALG_BYTES,
                          "kernel_mpps": round(pkts_per_launch / per_launch_s
