@@ -16,13 +16,14 @@
 //   phase A  hash + probe src and dst; a known src is logged for
 //            rejuvenation, an unknown one queued; a dst known at segment
 //            start (or in the static table) is forwarded at once, an unknown
-//            one flooded provisionally and queued;
+//            one flooded provisionally;
 //   phase B  queued src MACs are de-duplicated (earliest packet wins) and
 //            given dchain indices in packet order; the first sighting's in
 //            port becomes the entry's port;
-//   phase C  (only when B allocated something) queued dst MACs are looked up
-//            again: a MAC learned by a packet at or before this one (the
-//            packet's own src counts: learn precedes lookup) forwards there.
+//   phase C  (only when B learned something) provisionally flooded frames are
+//            looked up again: a MAC learned by a packet at or before this one
+//            (the packet's own src counts: learn precedes lookup) forwards
+//            there.
 //
 // Dynamic table entry: key words {mac[0..3], mac[4..5], port, 0}. Only words
 // 0-1 identify the MAC; word 2 carries the DynamicValue (dyn_vals vector in
@@ -146,12 +147,9 @@ __global__ __launch_bounds__(256) void bridge_classify(BridgeArgs a) {
     }
     uint32_t port = 0;
     const uint32_t di = mac_probe(a.t, dh, d0, d1, &port);
-    if (di != kNone) {
-      a.out[p] = (uint16_t)port;
-    } else {  // flooded unless learned earlier in this segment (phase C)
-      a.out[p] = VP_FLOOD_FRAME;
-      a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
-    }
+    // unknown: flooded unless learned earlier in this segment (phase C
+    // re-examines flooded frames only when phase B learned something)
+    a.out[p] = di != kNone ? (uint16_t)port : VP_FLOOD_FRAME;
   }
 }
 
@@ -189,16 +187,23 @@ __global__ void bridge_learn_finish(BridgeArgs a, const uint32_t *list,
   }
 }
 
-__global__ void bridge_defer_finish(BridgeArgs a, const uint32_t *list,
-                                    uint32_t n) {
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
-       j += gridDim.x * blockDim.x) {
-    const uint32_t p = list[j];
+// Phase C over the segment's flooded frames: a static rule (e.g. one that
+// floods explicitly) still wins; otherwise a MAC learned by a packet q' <= p
+// (the packet's own src is learned before its dst is looked up) forwards.
+__global__ void bridge_defer_finish(BridgeArgs a) {
+  for (uint32_t p = a.p0 + blockIdx.x * blockDim.x + threadIdx.x; p < a.p1;
+       p += gridDim.x * blockDim.x) {
+    if (a.out[p] != VP_FLOOD_FRAME) continue;
     const uint4 h = eth_words(a, p);
     const uint32_t d0 = h.x, d1 = h.y & 0xFFFF;
+    const uint32_t dh = eth_hash(a.crc_tab, d0, d1);
+    if (a.n_static) {
+      const uint32_t in = a.in_dev[p];
+      const uint32_t key[4] = {d0, d1 | (in << 16), 0, 0};
+      if (tbl_probe(a.st, static_hash(a.crc_tab, dh, in), key) != kNone) continue;
+    }
     uint32_t port = 0;
-    const uint32_t di = mac_probe(a.t, eth_hash(a.crc_tab, d0, d1), d0, d1, &port);
-    // learned by packet q' <= p: the packet's own src is learned first
+    const uint32_t di = mac_probe(a.t, dh, d0, d1, &port);
     if (di != kNone && tbl_allocated_before(a.t, di, a.seq_base + p + 1))
       a.out[p] = (uint16_t)port;
   }
@@ -247,7 +252,7 @@ static int bridge_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
   *ms += kms;
   *launches += 1;
-  const uint32_t nmiss = t.h_ctl.miss_count, ndefer = t.h_ctl.defer_count;
+  const uint32_t nmiss = t.h_ctl.miss_count;
   if (!nmiss) return 0;  // nothing learned: provisional floods stand
 
   size_t need = 0;
@@ -265,10 +270,8 @@ static int bridge_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   bridge_learn_finish<<<grid_for(nmiss), 256, 0, c->stream>>>(
       a, w.miss_sorted, nmiss, w.scratch, w.rep, w.assign);
   VP_HIP(hipGetLastError());
-  if (ndefer) {
-    bridge_defer_finish<<<grid_for(ndefer), 256, 0, c->stream>>>(a, w.defer, ndefer);
-    VP_HIP(hipGetLastError());
-  }
+  bridge_defer_finish<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
+  VP_HIP(hipGetLastError());
   *allocated |= 1u;
   VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, c->seq));
   VP_TRY(read_ctl(c, t));
