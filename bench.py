@@ -11,9 +11,13 @@ Every timed step reads its own pre-generated batch, so no input restore sits
 inside the timed region. A warm-up pass allocates all 1M flows first (its
 rate is reported as new_flow_mpps).
 
-N > 1 (torch.distributed, one rank per GPU): each rank runs its own NF
-replica over its own flows (weak scaling, no data-path collective;
-DESIGN.md §6). value = all ranks' packets / max-over-ranks time.
+N > 1 (torch.distributed, one rank per GPU; BASELINE configs[4]): ONE vignat
+over all GPUs with 16M flows; every global batch is N x B packets and rank r
+ingests its contiguous slice r (B packets, weak scaling). The ranks keep a
+replicated dictionary; new flows are all-gathered over RCCL so every rank
+allocates identically; results equal one nf.c over the concatenated batch
+(tests/test_shard_gpu.py). value = all ranks' packets /
+max-over-ranks time.
 
 Also reported:
   roofline      algorithmic HBM-read bytes per packet (92 B)
@@ -107,7 +111,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1 << 24)
-    ap.add_argument("--flows", type=int, default=1 << 20)
+    ap.add_argument("--flows", type=int, default=None,
+                    help="default: 1M (config 2) on one GPU, 16M (config 5) "
+                         "over N > 1 GPUs")
     ap.add_argument("--cpu-sample", type=int, default=1 << 24)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -115,6 +121,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.flows is None:
+        args.flows = 1 << 20 if world == 1 else 1 << 24
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
@@ -123,33 +131,39 @@ def main():
     cfg = vigor_amd.nat_config_from_args(
         NAT_ARGS + ["--max-flows", str(args.flows)], 2, DEV_MACS)
     nat = vigor_amd.Nat(cfg, gpu=local)
-    bank = FlowBank(args.flows, rank * args.flows, dev)
+    if world > 1:  # one vignat over all ranks (RCCL)
+        from vigor_amd import shard
+        shard.attach_rccl(nat, rank, world)
+    bank = FlowBank(args.flows, 0, dev)
     B = args.batch
     lens = torch.full((B,), 60, dtype=torch.int16, device=dev)
     in_dev = torch.zeros(B, dtype=torch.int16, device=dev)
     out = torch.zeros(B, dtype=torch.int16, device=dev)
 
-    def step(frames, start):
-        nat.process_device(frames, lens, in_dev, out, SLOT,
-                           now0=T.NOW0 + start, now_step=1)
+    def gstart(k):  # global position of this rank's slice of global batch k
+        return (k * world + rank) * B
 
-    # warm-up: first pass allocates every flow
+    def step(frames, k):
+        nat.process_device(frames, lens, in_dev, out, SLOT,
+                           now0=T.NOW0 + gstart(k), now_step=1)
+
+    # warm-up: the first global batch allocates every flow
     wbuf = torch.empty(B * SLOT, dtype=torch.uint8, device=dev)
     new_flow_mpps = None
     for w in range(args.warmup):
-        bank.fill(wbuf, w * B)
+        bank.fill(wbuf, gstart(w))
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        step(wbuf, w * B)
+        step(wbuf, w)
         torch.cuda.synchronize()
         if w == 0:
-            new_flow_mpps = B / (time.perf_counter() - t0) / 1e6
-    assert nat.live_count() == min(args.flows, B * max(1, args.warmup))
+            new_flow_mpps = B * world / (time.perf_counter() - t0) / 1e6
+    assert nat.live_count() == min(args.flows, B * world * max(1, args.warmup))
     del wbuf
     bufs = []
     for k in range(args.steps):
         b = torch.empty(B * SLOT, dtype=torch.uint8, device=dev)
-        bank.fill(b, (args.warmup + k) * B)
+        bank.fill(b, gstart(args.warmup + k))
         bufs.append(b)
     torch.cuda.synchronize()
 
@@ -159,7 +173,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(bufs[k], (args.warmup + k) * B)
+        step(bufs[k], args.warmup + k)
         kms.append(nat.last_kernel_ms())
     torch.cuda.synchronize()
     if world > 1:
@@ -181,10 +195,21 @@ def main():
     achieved = ALG_BYTES * pkts_per_launch / per_launch_s / 1e9
     traffic = None  # PMC bytes of the same kernel (profiles/, per launch)
     tpath = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE)
-    if os.path.exists(tpath) and B == 1 << 24 and args.flows == 1 << 20:
+    if (os.path.exists(tpath) and B == 1 << 24 and args.flows == 1 << 20
+            and world == 1):
         with open(tpath) as fh:
             tb = json.load(fh)["traffic_bytes_per_launch"]
         traffic = round(tb * pkts_per_launch / (1 << 24) / per_launch_s / 1e9, 1)
+    if world == 1 and args.flows == 1 << 20:
+        workload = ("vignat 64B, 1M flows, 1xMI355X (parse+hash+map-probe "
+                    "kernel, checksum rewrite)")
+    elif world > 1:
+        workload = ("vignat 64B, %d flows, %dxMI355X: one NF over all GPUs, "
+                    "each ingesting a contiguous 1/%d of every global batch "
+                    "(replicated dictionary, new flows all-gathered over "
+                    "RCCL)" % (args.flows, world, world))
+    else:
+        workload = "vignat 64B, %d flows, 1xMI355X" % args.flows
     if rank == 0:
         cpu = None
         if not args.no_cpu and world == 1:
@@ -200,13 +225,11 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "u8", "data": "synthetic",
-            "config": {"workload": "vignat 64B, 1M flows, 1xMI355X "
-                                   "(parse+hash+map-probe kernel, checksum "
-                                   "rewrite)" if args.flows == 1 << 20 else
-                                   "vignat 64B, %d flows" % args.flows,
-                       "flows_per_gpu": args.flows, "batch_packets": B,
+            "config": {"workload": workload, "flows": args.flows,
+                       "batch_packets_per_gpu": B,
+                       "global_batch_packets": B * world,
                        "frame_bytes": 60, "slot_bytes": SLOT,
-                       "parallelism": "replicas%d" % world if world > 1
+                       "parallelism": "shard%d" % world if world > 1
                        else "single"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",

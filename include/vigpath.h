@@ -29,6 +29,7 @@
 #ifndef VIGPATH_H
 #define VIGPATH_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -137,6 +138,38 @@ int vp_process_batch(vp_ctx *ctx, uint32_t n, const uint16_t *in_dev,
 int vp_process_host(vp_ctx *ctx, uint32_t n, const uint16_t *in_dev,
                     uint8_t *frames, uint32_t slot, const uint16_t *len,
                     const int64_t *now, uint16_t *out_dev);
+
+/* -------------------------------------------------------- multi-GPU -- *
+ * One vignat instance over N GPUs (one process and one context per GPU),
+ * identical to a single nf.c processing the concatenation of the ranks'
+ * slices (rank 0's packets first) of every global batch. Every rank keeps a
+ * replica of the flow dictionary and allocator; new flows are all-gathered
+ * and allocated identically everywhere; timestamps are per-rank partial
+ * maxima merged (all-reduce MAX) only where an expiry may happen. After an
+ * attach, vp_process_device is a collective: every rank calls it once per
+ * global batch with its own slice (n may be 0), in the same order. See
+ * DESIGN.md §6. */
+
+/* RCCL over xGMI: rank 0 creates the id, the host distributes it. */
+#define VP_COMM_ID_BYTES 128
+int vp_comm_unique_id(uint8_t id[VP_COMM_ID_BYTES]);
+int vp_attach_rccl(vp_ctx *ctx, const uint8_t id[VP_COMM_ID_BYTES], int nranks,
+                   int rank);
+
+/* Host-memory collectives supplied by the caller (e.g. torch.distributed /
+ * gloo, or several ranks sharing one GPU). Return 0 on success. */
+typedef struct vp_comm_ops {
+  void *user;
+  /* every rank contributes `bytes`; recv receives nranks * bytes, rank order */
+  int (*allgather)(void *user, const void *send, void *recv, size_t bytes);
+  /* element-wise maximum over ranks of `count` u64 values (all < 2^63) */
+  int (*allreduce_max_u64)(void *user, uint64_t *buf, size_t count);
+} vp_comm_ops;
+int vp_attach_comm(vp_ctx *ctx, const vp_comm_ops *ops, int nranks, int rank);
+
+/* Collective: merge the ranks' timestamps so vp_nat_dump is exact on every
+ * rank (the dictionary and allocator are identical everywhere already). */
+int vp_sync_state(vp_ctx *ctx);
 
 /* ------------------------------------------------------- observability -- */
 

@@ -1,0 +1,150 @@
+"""Multi-GPU vignat parity: N ranks (processes) act as ONE vignat over the
+concatenation of their slices of every global batch (rank 0 first), and the
+result must equal the oracle over the whole trace — out ports, frames, and
+the merged table state. The ranks share the box's one GPU and talk through
+the host-callback transport (gloo); the 8-GPU bench uses RCCL, same library
+code above the transport."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import orc
+from tracegen import mixed_nat_trace
+from vigor_amd import traces as T
+
+pytestmark = pytest.mark.gpu
+
+DEV_MACS = [T.mac("02:03:04:05:06:07"), T.mac("12:13:14:15:16:17")]
+END_MACS = [T.mac("01:23:45:67:89:00"), T.mac("01:23:45:67:89:01")]
+
+
+def _trace(spec):
+    kind = spec["kind"]
+    if kind == "rr":
+        return T.nat_lan_trace(spec["n"], spec["flows"])
+    rng = np.random.default_rng(spec["seed"])
+    fr, ln, dv, now = mixed_nat_trace(rng, spec["n"], spec["flows"],
+                                      max_idx=spec["max_flows"])
+    if spec.get("ties"):
+        now = T.NOW0 + (np.arange(spec["n"]) // 7).astype(np.int64) * 1_000_000
+    return fr, ln, dv, now
+
+
+def _slices(spec, a, b, world):
+    """Per-rank sizes of global batch [a, b)."""
+    n = b - a
+    if spec.get("uneven"):
+        cut = sorted(np.random.default_rng(a).integers(0, n + 1, world - 1))
+        cut = [0] + list(cut) + [n]
+        return [int(cut[r + 1] - cut[r]) for r in range(world)]
+    base, extra = divmod(n, world)
+    return [base + (1 if r < extra else 0) for r in range(world)]
+
+
+def _worker(rank, world, port, spec, outdir):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import vigor_amd
+    from gpuh import run_gpu
+    from vigor_amd import shard
+    args = ["--wan", "1", "--expire", str(spec["expire_us"]),
+            "--starting-port", "0", "--max-flows", str(spec["max_flows"]),
+            "--extip", "192.168.4.2", "--eth-dest",
+            "0," + END_MACS[0].hex(":"), "--eth-dest", "1," + END_MACS[1].hex(":")]
+    cfg = vigor_amd.nat_config_from_args(args, 2, DEV_MACS)
+    nat = vigor_amd.Nat(cfg, gpu=0)
+    shard.attach_torch(nat, rank, world)
+    fr, ln, dv, now = _trace(spec)
+    n = ln.shape[0]
+    bounds = [0] + spec["cuts"] + [n]
+    outs, frames, pos = [], [], []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        sizes = _slices(spec, a, b, world)
+        s = a + sum(sizes[:rank])
+        e = s + sizes[rank]
+        got, out = run_gpu(nat, fr[s * 64:e * 64], ln[s:e], dv[s:e], now[s:e],
+                           64, affine=(int(now[s]), 1) if spec.get("affine")
+                           and e > s else None)
+        outs.append(out)
+        frames.append(got)
+        pos.append(np.arange(s, e))
+    nat.sync_state()
+    res = dict(out=np.concatenate(outs), frames=np.concatenate(frames),
+               pos=np.concatenate(pos))
+    if rank == 0:
+        a_, t_, k_ = nat.dump()
+        res.update(alloc=a_, ts=t_, keys=k_, live=np.array([nat.live_count()]))
+    np.savez(os.path.join(outdir, "r%d.npz" % rank), **res)
+    torch.cuda.synchronize()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run_sharded(spec, world):
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        port = _free_port()
+        ps = [ctx.Process(target=_worker, args=(r, world, port, spec, d))
+              for r in range(world)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(timeout=300)
+        codes = [p.exitcode for p in ps]
+        assert codes == [0] * world, codes
+        return [dict(np.load(os.path.join(d, "r%d.npz" % r)))
+                for r in range(world)]
+
+
+@pytest.mark.parametrize("world,spec", [
+    (2, dict(kind="rr", n=40_000, flows=1000, max_flows=65536,
+             expire_us=60_000_000, cuts=[1000, 20_000], affine=True)),
+    (3, dict(kind="mixed", seed=1, n=5000, flows=100, max_flows=64,
+             expire_us=1, cuts=[1, 2, 500, 4000], uneven=True)),
+    (2, dict(kind="mixed", seed=2, n=5000, flows=40, max_flows=16,
+             expire_us=60_000_000, cuts=[2500], uneven=True)),
+    (4, dict(kind="mixed", seed=3, n=6000, flows=300, max_flows=256,
+             expire_us=5, cuts=[1000, 1001, 3000])),
+    (2, dict(kind="mixed", seed=7, n=6000, flows=300, max_flows=512,
+             expire_us=4_295_000, cuts=[1234, 3000], ties=True)),
+])
+def test_sharded_nat_equals_single_nf(world, spec):
+    res = run_sharded(spec, world)
+    fr, ln, dv, now = _trace(spec)
+    cfg = orc.nat_cfg(wan=1, start_port=0, ext_ip=T.ip4(192, 168, 4, 2),
+                      expire_us=spec["expire_us"], max_flows=spec["max_flows"],
+                      device_macs=DEV_MACS, endpoint_macs=END_MACS)
+    o = orc.Oracle("nat", cfg)
+    exp = fr.copy()
+    exp_out = o.run(exp, ln, dv, now, 64)
+    n = ln.shape[0]
+    got_out = np.zeros(n, np.uint16)
+    got_fr = np.zeros((n, 64), np.uint8)
+    seen = np.zeros(n, bool)
+    for r in res:
+        got_out[r["pos"]] = r["out"]
+        got_fr[r["pos"]] = r["frames"].reshape(-1, 64)
+        seen[r["pos"]] = True
+    assert seen.all()
+    bad = np.nonzero(got_out != exp_out)[0]
+    assert bad.size == 0, "out mismatch at %s" % bad[:10]
+    badf = np.nonzero((got_fr != exp.reshape(n, 64)).any(axis=1))[0]
+    assert badf.size == 0, "frame mismatch at %s" % badf[:10]
+    oa, ots, ok = o.nat_dump(spec["max_flows"])
+    np.testing.assert_array_equal(res[0]["alloc"], oa)
+    np.testing.assert_array_equal(res[0]["ts"][oa == 1], ots[oa == 1])
+    np.testing.assert_array_equal(res[0]["keys"][oa == 1], ok[oa == 1])

@@ -61,6 +61,17 @@ class LbConfigC(C.Structure):
                 ("device_macs", MacTable)]
 
 
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                           C.c_size_t)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t)
+
+
+class CommOpsC(C.Structure):
+    """vp_comm_ops: host-memory collectives supplied by the caller."""
+    _fields_ = [("user", C.c_void_p), ("allgather", ALLGATHER_FN),
+                ("allreduce_max_u64", ALLREDUCE_FN)]
+
+
 class DevBatchC(C.Structure):
     _fields_ = [("frames", C.c_void_p), ("slot", C.c_uint32), ("n", C.c_uint32),
                 ("len", C.c_void_p), ("in_dev", C.c_void_p),
@@ -71,7 +82,8 @@ class DevBatchC(C.Structure):
 # every symbol include/vigpath.h declares
 EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_destroy",
            "vp_process_device", "vp_process_batch", "vp_process_host",
-           "vp_nat_dump", "vp_bridge_dump", "vp_lb_dump", "vp_live_count", "vp_last_kernel_ms", "vp_version"]
+           "vp_nat_dump", "vp_bridge_dump", "vp_lb_dump", "vp_comm_unique_id",
+           "vp_attach_rccl", "vp_attach_comm", "vp_sync_state", "vp_live_count", "vp_last_kernel_ms", "vp_version"]
 
 _libs = {}
 
@@ -113,6 +125,15 @@ def lib(path: str | None = None):
     L.vp_bridge_dump.restype = C.c_int
     L.vp_lb_dump.argtypes = [C.c_void_p] * 10
     L.vp_lb_dump.restype = C.c_int
+    L.vp_comm_unique_id.argtypes = [C.c_void_p]
+    L.vp_comm_unique_id.restype = C.c_int
+    L.vp_attach_rccl.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+    L.vp_attach_rccl.restype = C.c_int
+    L.vp_attach_comm.argtypes = [C.c_void_p, C.POINTER(CommOpsC), C.c_int,
+                                 C.c_int]
+    L.vp_attach_comm.restype = C.c_int
+    L.vp_sync_state.argtypes = [C.c_void_p]
+    L.vp_sync_state.restype = C.c_int
     L.vp_live_count.argtypes = [C.c_void_p]
     L.vp_live_count.restype = C.c_int64
     L.vp_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float),

@@ -1,0 +1,24 @@
+// Collectives between the ranks of one multi-GPU NF instance.
+// Two transports: RCCL on device buffers (one GPU per rank, xGMI), and
+// caller-supplied host-memory callbacks (vp_comm_ops; e.g. gloo, or several
+// ranks sharing one GPU in tests). All calls are collective and ordered on
+// the context's stream.
+#pragma once
+
+#include "vp_internal.h"
+
+namespace vp {
+
+struct Comm {
+  int n = 1, r = 0;
+  virtual ~Comm() {}
+  // every rank contributes `bytes`; recv gets n * bytes in rank order
+  virtual int allgather_host(vp_ctx *c, const void *send, void *recv,
+                             size_t bytes) = 0;
+  virtual int allgather_dev(vp_ctx *c, const void *send, void *recv,
+                            size_t bytes) = 0;
+  // in place, element-wise max over ranks (values < 2^63)
+  virtual int allreduce_max_u64_dev(vp_ctx *c, uint64_t *buf, size_t count) = 0;
+};
+
+}  // namespace vp

@@ -1,0 +1,160 @@
+// Comm transports (vp_comm.h) and the multi-GPU C-ABI entry points.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "vp_comm.h"
+
+namespace vp {
+
+static int nccl_fail(ncclResult_t e, const char *what) {
+  if (getenv("VIGPATH_DEBUG"))
+    fprintf(stderr, "vigpath: %s failed: %s\n", what, ncclGetErrorString(e));
+  return VP_EIO;
+}
+#define VP_NCCL(call)                                  \
+  do {                                                 \
+    ncclResult_t e_ = (call);                          \
+    if (e_ != ncclSuccess) return nccl_fail(e_, #call); \
+  } while (0)
+
+// RCCL on device buffers; host variants stage through a device buffer.
+struct RcclComm : Comm {
+  ncclComm_t comm = nullptr;
+  void *stage = nullptr;
+  size_t stage_bytes = 0;
+  ~RcclComm() override {
+    if (comm) ncclCommDestroy(comm);
+    if (stage) hipFree(stage);
+  }
+  int reserve(size_t bytes) {
+    if (bytes <= stage_bytes) return 0;
+    if (stage) hipFree(stage);
+    stage = nullptr;
+    stage_bytes = 0;
+    VP_HIP(hipMalloc(&stage, bytes));
+    stage_bytes = bytes;
+    return 0;
+  }
+  int allgather_host(vp_ctx *c, const void *send, void *recv, size_t bytes) override {
+    VP_TRY(reserve(bytes * (n + 1)));
+    uint8_t *s = static_cast<uint8_t *>(stage);
+    VP_HIP(hipMemcpyAsync(s, send, bytes, hipMemcpyHostToDevice, c->stream));
+    VP_NCCL(ncclAllGather(s, s + bytes, bytes, ncclUint8, comm, c->stream));
+    VP_HIP(hipMemcpyAsync(recv, s + bytes, bytes * n, hipMemcpyDeviceToHost,
+                          c->stream));
+    VP_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+  }
+  int allgather_dev(vp_ctx *c, const void *send, void *recv, size_t bytes) override {
+    VP_NCCL(ncclAllGather(send, recv, bytes, ncclUint8, comm, c->stream));
+    return 0;
+  }
+  int allreduce_max_u64_dev(vp_ctx *c, uint64_t *buf, size_t count) override {
+    VP_NCCL(ncclAllReduce(buf, buf, count, ncclUint64, ncclMax, comm, c->stream));
+    return 0;
+  }
+};
+
+// Caller-supplied host-memory collectives; device variants stage through
+// host memory.
+struct HostComm : Comm {
+  vp_comm_ops ops{};
+  std::vector<uint8_t> hs, hr;
+  int allgather_host(vp_ctx *c, const void *send, void *recv, size_t bytes) override {
+    (void)c;
+    return ops.allgather(ops.user, send, recv, bytes) ? VP_EIO : 0;
+  }
+  int allgather_dev(vp_ctx *c, const void *send, void *recv, size_t bytes) override {
+    hs.resize(bytes ? bytes : 1);
+    hr.resize(bytes * n ? bytes * n : 1);
+    VP_HIP(hipMemcpyAsync(hs.data(), send, bytes, hipMemcpyDeviceToHost, c->stream));
+    VP_HIP(hipStreamSynchronize(c->stream));
+    if (ops.allgather(ops.user, hs.data(), hr.data(), bytes)) return VP_EIO;
+    VP_HIP(hipMemcpyAsync(recv, hr.data(), bytes * n, hipMemcpyHostToDevice,
+                          c->stream));
+    VP_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+  }
+  int allreduce_max_u64_dev(vp_ctx *c, uint64_t *buf, size_t count) override {
+    hs.resize(count * 8 ? count * 8 : 1);
+    VP_HIP(hipMemcpyAsync(hs.data(), buf, count * 8, hipMemcpyDeviceToHost,
+                          c->stream));
+    VP_HIP(hipStreamSynchronize(c->stream));
+    if (ops.allreduce_max_u64(ops.user, reinterpret_cast<uint64_t *>(hs.data()),
+                              count))
+      return VP_EIO;
+    VP_HIP(hipMemcpyAsync(buf, hs.data(), count * 8, hipMemcpyHostToDevice,
+                          c->stream));
+    VP_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+  }
+};
+
+int sync_tables(vp_ctx *c);
+
+}  // namespace vp
+
+using namespace vp;
+
+extern "C" {
+
+int vp_comm_unique_id(uint8_t id[VP_COMM_ID_BYTES]) {
+  if (!id) return VP_EINVAL;
+  ncclUniqueId u;
+  VP_NCCL(ncclGetUniqueId(&u));
+  memcpy(id, u.internal, VP_COMM_ID_BYTES);
+  return 0;
+}
+
+static int attach_check(vp_ctx *c, int nranks, int rank) {
+  if (!c || nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks ||
+      c->comm)
+    return VP_EINVAL;
+  if (c->kind != KIND_NAT) return VP_ENOTSUP;  // vignat only
+  return 0;
+}
+
+int vp_attach_rccl(vp_ctx *c, const uint8_t id[VP_COMM_ID_BYTES], int nranks,
+                   int rank) {
+  VP_TRY(attach_check(c, nranks, rank));
+  if (!id) return VP_EINVAL;
+  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  ncclUniqueId u;
+  memcpy(u.internal, id, VP_COMM_ID_BYTES);
+  RcclComm *m = new RcclComm();
+  m->n = nranks;
+  m->r = rank;
+  ncclResult_t e = ncclCommInitRank(&m->comm, nranks, u, rank);
+  if (e != ncclSuccess) {
+    m->comm = nullptr;
+    delete m;
+    return nccl_fail(e, "ncclCommInitRank");
+  }
+  c->comm = m;
+  return 0;
+}
+
+int vp_attach_comm(vp_ctx *c, const vp_comm_ops *ops, int nranks, int rank) {
+  VP_TRY(attach_check(c, nranks, rank));
+  if (!ops || !ops->allgather || !ops->allreduce_max_u64) return VP_EINVAL;
+  HostComm *m = new HostComm();
+  m->n = nranks;
+  m->r = rank;
+  m->ops = *ops;
+  c->comm = m;
+  return 0;
+}
+
+int vp_sync_state(vp_ctx *c) {
+  if (!c) return VP_EINVAL;
+  if (!c->comm) return 0;
+  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  return sync_tables(c);
+}
+
+}  // extern "C"

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../include/vigpath.h"
 #include "vp_device.h"
 
@@ -22,6 +24,9 @@
 namespace vp {
 
 int hip_fail(hipError_t e, const char *what, const char *file, int line);
+
+struct Comm;  // vp_comm.hip: collectives between the ranks of one NF
+constexpr int kMaxRanks = 64;
 
 enum Kind { KIND_NAT = 1, KIND_BRIDGE = 2, KIND_LB = 3 };
 
@@ -80,6 +85,10 @@ struct Workspace {
   uint32_t *defer_sorted = nullptr;
   uint32_t *aux = nullptr, *aux_sorted = nullptr;  // third queue (viglb)
   uint32_t *rlist = nullptr;  // re-classification input (viglb rounds)
+  // multi-GPU: new-flow records exchanged between ranks, union positions/times
+  void *sbuf = nullptr, *rbuf = nullptr;
+  size_t sbuf_bytes = 0, rbuf_bytes = 0;
+  int64_t *unow = nullptr;
   uint32_t *iota = nullptr;  // 0..cap_n-1
   uint32_t *skey = nullptr, *sval = nullptr;
   uint32_t *hist = nullptr, *hoff = nullptr;  // touch-reduce (chunk x span)
@@ -124,4 +133,10 @@ struct vp_ctx {
   uint32_t wan_macw[3] = {0, 0, 0};
   bool coalesced_io = true;  // LDS-staged 64 B frame I/O (VIGPATH_COALESCED=0 off)
   vp::Workspace ws;
+  // multi-GPU (vp_attach_*): this rank's collectives, and during a batch the
+  // global position of local packet 0 and the per-rank slice sizes
+  vp::Comm *comm = nullptr;
+  uint32_t off = 0;
+  std::vector<uint32_t> rank_n;    // slice sizes of the current batch
+  std::vector<uint32_t> rank_cnt;  // new keys per rank of the current segment
 };

@@ -391,7 +391,8 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.out = b->out_dev;
   a.log = w.log;
   a.now = now;
-  a.seq_base = c->seq;
+  const uint64_t seq0 = c->seq + c->off;  // global sequence of local packet 0
+  a.seq_base = seq0;
   a.slot = b->slot;
   a.p0 = p0;
   a.p1 = p1;
@@ -410,17 +411,19 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
 
   VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 8, c->stream));  // + defer
   VP_HIP(hipEventRecord(c->ev0, c->stream));
-  if (b->slot == 64 && c->coalesced_io) {
-    const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
-    nat_classify64<<<grid_for((uint64_t)tiles * 64), 256, 0, c->stream>>>(a, b->n);
-  } else {
-    nat_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
+  if (p1 > p0) {
+    if (b->slot == 64 && c->coalesced_io) {
+      const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
+      nat_classify64<<<grid_for((uint64_t)tiles * 64), 256, 0, c->stream>>>(a, b->n);
+    } else {
+      nat_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
+    }
+    VP_HIP(hipGetLastError());
   }
-  VP_HIP(hipGetLastError());
   VP_HIP(hipEventRecord(c->ev1, c->stream));
   // Optimistic: fold phase A's touches right away (queued packets logged
   // kNone); if B/C run, the fold is redone over the completed log.
-  VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, c->seq));
+  VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
   VP_TRY(read_ctl(c, t));
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
@@ -428,6 +431,8 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   *launches += 1;
   const uint32_t nmiss = t.h_ctl.miss_count, ndefer = t.h_ctl.defer_count;
 
+  uint32_t union_n = nmiss, union_off = 0;  // this rank's misses in the union
+  if (c->comm) VP_TRY(union_sizes(c, nmiss, &union_n, &union_off));
   if (nmiss) {
     size_t need = 0;
     hipcub::DeviceRadixSort::SortKeys(nullptr, need, w.miss, w.miss_sorted,
@@ -439,20 +444,30 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     nat_miss_keys<<<grid_for(nmiss), 256, 0, c->stream>>>(a, w.miss_sorted, nmiss,
                                                           w.mkey, w.mhash);
     VP_HIP(hipGetLastError());
-    VP_TRY(tbl_new_keys(c, t, NewKeys{nmiss, w.miss_sorted}, c->seq, nullptr));
-    nat_miss_finish<<<grid_for(nmiss), 256, 0, c->stream>>>(
-        a, w.miss_sorted, nmiss, w.scratch, w.rep, w.assign);
-    VP_HIP(hipGetLastError());
+  }
+  if (union_n) {
+    if (c->comm) {  // every rank allocates the union in global packet order
+      VP_TRY(union_exchange(c, nmiss, now));
+      VP_TRY(tbl_new_keys(c, t, NewKeys{union_n, w.skey}, c->seq, nullptr));
+      union_stamp<<<grid_for(union_n), 256, 0, c->stream>>>(
+          w.first, w.assign, w.skey, w.unow, union_n, c->seq, t.ts, t.tseq);
+      VP_HIP(hipGetLastError());
+    } else {
+      VP_TRY(tbl_new_keys(c, t, NewKeys{nmiss, w.miss_sorted}, c->seq, nullptr));
+    }
+    if (nmiss) {
+      nat_miss_finish<<<grid_for(nmiss), 256, 0, c->stream>>>(
+          a, w.miss_sorted, nmiss, w.scratch, w.rep + union_off, w.assign);
+      VP_HIP(hipGetLastError());
+    }
     *allocated |= 1u;
   }
   if (ndefer) {
     nat_defer_finish<<<grid_for(ndefer), 256, 0, c->stream>>>(a, w.defer, ndefer);
     VP_HIP(hipGetLastError());
   }
-  if (nmiss || ndefer) {
-    VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, c->seq));
-    VP_TRY(read_ctl(c, t));
-  }
+  if (nmiss || ndefer) VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
+  if (union_n || ndefer) VP_TRY(read_ctl(c, t));
   return 0;
 }
 

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <vector>
 
+#include "vp_comm.h"
 #include "vp_table.h"
 
 namespace vp {
@@ -52,11 +53,13 @@ static void ws_release(Workspace &w) {
   void *ptrs[] = {w.miss,  w.miss_sorted, w.defer, w.mkey, w.mhash,
                   w.first, w.rank,        w.rep,   w.assign, w.scratch,
                   w.log,   w.iota,        w.skey,  w.sval,
-                  w.log2,  w.defer_sorted, w.aux,  w.aux_sorted, w.rlist};
+                  w.log2,  w.defer_sorted, w.aux,  w.aux_sorted, w.rlist,
+                  w.unow};
   for (void *p : ptrs) hipFree(p);
   w.miss = w.miss_sorted = w.defer = w.mkey = w.mhash = w.first = w.rank =
       w.rep = w.assign = w.scratch = w.log = w.iota = w.skey = w.sval = nullptr;
   w.log2 = w.defer_sorted = w.aux = w.aux_sorted = w.rlist = nullptr;
+  w.unow = nullptr;
   w.cap_n = 0;
 }
 
@@ -79,6 +82,7 @@ int ws_reserve(vp_ctx *c, uint32_t n) {
   VP_TRY(dalloc(&w.assign, cap));
   VP_TRY(dalloc(&w.scratch, ss));
   VP_TRY(dalloc(&w.log, cap));
+  if (c->comm) VP_TRY(dalloc(&w.unow, cap));  // multi-GPU union times
   if (c->kind == KIND_LB) {  // second table + round queues
     VP_TRY(dalloc(&w.log2, cap));
     VP_TRY(dalloc(&w.defer_sorted, cap));
@@ -125,9 +129,11 @@ static void free_all(vp_ctx *c) {
   ws_release(w);
   void *ptrs[] = {w.hist, w.hoff, w.cub_tmp, w.d_frames, w.d_len,    w.d_in,
                   w.d_out,   w.d_now,    c->crc_tab, c->macw,
-                  c->st_bk,  c->st_val,  c->be_rec,   c->cht,   c->dmacw};
+                  c->st_bk,  c->st_val,  c->be_rec,   c->cht,   c->dmacw,
+                  w.sbuf,    w.rbuf};
   for (void *p : ptrs) hipFree(p);
   if (w.h_frames) hipHostFree(w.h_frames);
+  delete c->comm;
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->stream) hipStreamDestroy(c->stream);

@@ -160,6 +160,18 @@ using SegmentFn = int (*)(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
 int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
               SegmentFn seg);
 
+// ------------------------------------------------- multi-GPU new keys --
+// (run_batch_sharded, vp_table.hip) Gather every rank's count of local new
+// keys: the union size and this rank's offset in it.
+int union_sizes(vp_ctx *c, uint32_t nl, uint32_t *total, uint32_t *mine_off);
+// Local new keys (ws.mkey/ws.mhash [0, nl), sorted local positions in
+// ws.miss_sorted) -> the union on every rank, in global packet order:
+// ws.mkey/ws.mhash, global positions ws.skey, times ws.unow.
+int union_exchange(vp_ctx *c, uint32_t nl, const NowSpec &now);
+__global__ void union_stamp(const uint32_t *first, const uint32_t *assign,
+                            const uint32_t *upos, const int64_t *unow, uint32_t n,
+                            uint64_t seq, uint64_t *ts, uint64_t *tseq);
+
 uint32_t grid_for(uint64_t n, uint32_t block = 256, uint32_t max_blocks = 2048);
 uint32_t next_pow2(uint64_t v);
 int cub_reserve(vp_ctx *c, size_t bytes);

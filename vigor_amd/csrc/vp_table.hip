@@ -13,6 +13,7 @@
 #include <cstring>
 #include <vector>
 
+#include "vp_comm.h"
 #include "vp_table.h"
 
 namespace vp {
@@ -594,8 +595,13 @@ int ws_reserve(vp_ctx *c, uint32_t n);
 // >= min(ts_floor, t_a) (rejuvenation only raises stamps, new entries are
 // stamped >= t_a). The batch is cut at the first packet where that fails for
 // some table; there the exact expiry of that packet's nf_process runs.
+static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
+                             ExpiringTable *tabs, int ntabs, SegmentFn seg);
+
 int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
               SegmentFn seg) {
+  if (c->comm) return run_batch_sharded(c, b, tabs, ntabs, seg);
+  c->off = 0;
   const uint32_t n = b->n;
   c->last_ms = 0.f;
   c->last_launches = 0;
@@ -665,6 +671,271 @@ int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
   VP_HIP(hipStreamSynchronize(c->stream));
   c->seq += n;
   c->last_now = t_last;
+  c->last_ms = ms;
+  c->last_launches = launches;
+  return 0;
+}
+
+// ------------------------------------------------------ multi-GPU batch --
+// Every rank holds the same dictionary and allocator (new keys are
+// all-gathered, vp_nat.hip) and partial stamps: ts_r[i] / tseq_r[i] describe
+// rank r's own last touch of i (or its allocation), so the true stamp is the
+// maximum over ranks. Because ts_r <= ts, max_r(floor_r) is still a lower
+// bound of the live minimum and the no-expiry test of run_batch stays exact.
+// Where an expiry may happen the stamps are merged (all-reduce MAX of ts and
+// tseq) and the single-GPU expiry then runs identically on every rank.
+
+static int sync_ts(vp_ctx *c, FlowTable &t) {
+  VP_TRY(c->comm->allreduce_max_u64_dev(c, t.ts, t.cap));
+  VP_TRY(c->comm->allreduce_max_u64_dev(c, t.tseq, t.cap));
+  return 0;
+}
+
+int sync_tables(vp_ctx *c) {
+  VP_TRY(sync_ts(c, c->ft));
+  if (c->kind == KIND_LB) VP_TRY(sync_ts(c, c->ft2));
+  VP_HIP(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+struct RankInfo {
+  int64_t bad, n, t_first, t_last;
+  uint64_t floor[2];
+};
+
+// New keys of a segment, exchanged so that every rank allocates the same
+// union in global packet order (ranks' slices are consecutive, each sorted).
+struct NewRec {
+  uint32_t k[4];
+  uint32_t hash, gp;
+  int64_t now;
+};
+struct RankSlices {
+  uint32_t n, maxn;
+  uint32_t cnt[kMaxRanks], pre[kMaxRanks];
+};
+
+int union_sizes(vp_ctx *c, uint32_t nl, uint32_t *total, uint32_t *mine_off) {
+  Comm &m = *c->comm;
+  c->rank_cnt.assign(m.n, 0);
+  VP_TRY(m.allgather_host(c, &nl, c->rank_cnt.data(), sizeof nl));
+  uint32_t t = 0;
+  *mine_off = 0;
+  for (int r = 0; r < m.n; r++) {
+    if (r == m.r) *mine_off = t;
+    t += c->rank_cnt[r];
+  }
+  *total = t;
+  return 0;
+}
+
+__global__ void rec_pack(const uint32_t *mkey, const uint32_t *mhash,
+                         const uint32_t *pos, uint32_t n, uint32_t off, NowSpec now,
+                         NewRec *out) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += gridDim.x * blockDim.x) {
+    NewRec r;
+    for (int k = 0; k < 4; k++) r.k[k] = mkey[4 * (size_t)j + k];
+    r.hash = mhash[j];
+    r.gp = off + pos[j];
+    r.now = now.at(pos[j]);
+    out[j] = r;
+  }
+}
+
+__global__ void rec_unpack(const NewRec *in, RankSlices rs, uint32_t *mkey,
+                           uint32_t *mhash, uint32_t *upos, int64_t *unow) {
+  const uint64_t total = (uint64_t)rs.n * rs.maxn;
+  for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < total;
+       x += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = (uint32_t)(x / rs.maxn), j = (uint32_t)(x % rs.maxn);
+    if (j >= rs.cnt[r]) continue;
+    const NewRec v = in[x];
+    const uint32_t u = rs.pre[r] + j;
+    for (int k = 0; k < 4; k++) mkey[4 * (size_t)u + k] = v.k[k];
+    mhash[u] = v.hash;
+    upos[u] = v.gp;
+    unow[u] = v.now;
+  }
+}
+
+static int grow(void **p, size_t *have, size_t bytes) {
+  if (bytes <= *have) return 0;
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  VP_HIP(hipMalloc(p, bytes));
+  *have = bytes;
+  return 0;
+}
+
+int union_exchange(vp_ctx *c, uint32_t nl, const NowSpec &now) {
+  Comm &m = *c->comm;
+  Workspace &w = c->ws;
+  RankSlices rs{};
+  rs.n = (uint32_t)m.n;
+  uint32_t pre = 0;
+  for (int r = 0; r < m.n; r++) {
+    rs.cnt[r] = c->rank_cnt[r];
+    rs.pre[r] = pre;
+    pre += c->rank_cnt[r];
+    rs.maxn = std::max(rs.maxn, c->rank_cnt[r]);
+  }
+  const size_t bytes = sizeof(NewRec) * (size_t)rs.maxn;
+  VP_HIP(hipStreamSynchronize(c->stream));  // buffers may be reallocated
+  VP_TRY(grow(&w.sbuf, &w.sbuf_bytes, bytes));
+  VP_TRY(grow(&w.rbuf, &w.rbuf_bytes, bytes * m.n));
+  if (nl)
+    rec_pack<<<grid_for(nl), 256, 0, c->stream>>>(w.mkey, w.mhash, w.miss_sorted,
+                                                  nl, c->off, now,
+                                                  static_cast<NewRec *>(w.sbuf));
+  VP_HIP(hipGetLastError());
+  VP_TRY(m.allgather_dev(c, w.sbuf, w.rbuf, bytes));
+  rec_unpack<<<grid_for((uint64_t)rs.n * rs.maxn), 256, 0, c->stream>>>(
+      static_cast<const NewRec *>(w.rbuf), rs, w.mkey, w.mhash, w.skey, w.unow);
+  VP_HIP(hipGetLastError());
+  return 0;
+}
+
+// Allocation stamps on every rank (the allocating packet's rank would also
+// log it): ts = its time, tseq = its global sequence.
+__global__ void union_stamp(const uint32_t *first, const uint32_t *assign,
+                            const uint32_t *upos, const int64_t *unow, uint32_t n,
+                            uint64_t seq, uint64_t *ts, uint64_t *tseq) {
+  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < n;
+       u += gridDim.x * blockDim.x) {
+    if (!first[u] || assign[u] == kNone) continue;
+    ts[assign[u]] = (uint64_t)unow[u];
+    tseq[assign[u]] = seq + upos[u];
+  }
+}
+
+static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
+                             ExpiringTable *tabs, int ntabs, SegmentFn seg) {
+  Comm &m = *c->comm;
+  const uint32_t n = b->n;
+  c->last_ms = 0.f;
+  c->last_launches = 0;
+  // 1. every rank's slice size, time range and floors (one small gather);
+  //    errors are decided from the gathered data so all ranks agree
+  RankInfo me{};
+  me.n = n;
+  if (n && (b->slot < 64 || (b->slot & 15) || !b->frames || !b->len ||
+            !b->in_dev || !b->out_dev))
+    me.bad = 1;
+  std::vector<int64_t> h_now;
+  if (!me.bad && n) {
+    if (b->now) {
+      h_now.resize(n);
+      VP_HIP(hipMemcpyAsync(h_now.data(), b->now, sizeof(int64_t) * (size_t)n,
+                            hipMemcpyDeviceToHost, c->stream));
+      VP_HIP(hipStreamSynchronize(c->stream));
+      for (uint32_t i = 1; i < n; i++)
+        if (h_now[i] < h_now[i - 1]) me.bad = 2;
+      me.t_first = h_now[0];
+      me.t_last = h_now[n - 1];
+    } else {
+      if (b->now_step < 0) me.bad = 2;
+      me.t_first = b->now0;
+      me.t_last = b->now0 + (int64_t)(n - 1) * b->now_step;
+    }
+  }
+  for (int i = 0; i < ntabs; i++) me.floor[i] = tabs[i].t->ts_floor;
+  std::vector<RankInfo> all(m.n);
+  VP_TRY(m.allgather_host(c, &me, all.data(), sizeof me));
+  int bad = 0;
+  uint64_t G = 0;
+  uint32_t off = 0;
+  int64_t prev = c->last_now, t_first_g = 0, t_last_g = 0;
+  bool seen = false;
+  c->rank_n.assign(m.n, 0);
+  for (int r = 0; r < m.n; r++) {
+    bad |= (int)all[r].bad;
+    c->rank_n[r] = (uint32_t)all[r].n;
+    if (r < m.r) off += (uint32_t)all[r].n;
+    if (all[r].n) {  // global order: rank 0's packets first
+      if (all[r].t_first < 0 || all[r].t_first < prev) bad |= 2;
+      if (!seen) t_first_g = all[r].t_first;
+      seen = true;
+      prev = t_last_g = all[r].t_last;
+    }
+    G += (uint64_t)all[r].n;
+  }
+  if (bad & 1) return VP_EINVAL;
+  if (bad & 2) return VP_ENOTSUP;
+  if (G == 0) return 0;
+  if (G > 0xFFFFFFF0ull) return VP_EINVAL;
+  c->off = off;
+  VP_TRY(ws_reserve(c, (uint32_t)G));  // the union of new keys can reach G
+  uint64_t F[2] = {0, 0};
+  for (int i = 0; i < ntabs; i++)
+    for (int r = 0; r < m.n; r++) F[i] = std::max(F[i], all[r].floor[i]);
+
+  const NowSpec now{b->now, b->now0, b->now_step};
+  auto at = [&](uint32_t p) { return b->now ? h_now[p] : now.at(p); };
+  float ms = 0.f;
+  int launches = 0;
+  uint64_t A = 0;
+  int64_t tA = t_first_g;
+  while (A < G) {
+    // 2. expiries due at global packet A (identical decisions everywhere)
+    for (int i = 0; i < ntabs; i++) {
+      FlowTable &t = *tabs[i].t;
+      const int64_t cut = tabs[i].cutoff(c, tA);
+      if (cut <= (int64_t)std::min<uint64_t>(F[i], (uint64_t)tA)) continue;
+      VP_TRY(sync_ts(c, t));
+      VP_TRY(tbl_exact_floor(c, t));
+      if (t.ts_floor != ~0ull && (int64_t)t.ts_floor < cut) {
+        VP_TRY(tbl_expire(c, t, cut, nullptr));
+        VP_TRY(tbl_exact_floor(c, t));
+      }
+      F[i] = t.ts_floor;
+    }
+    auto safe_t = [&](int64_t tp) {
+      for (int i = 0; i < ntabs; i++)
+        if (tabs[i].cutoff(c, tp) > (int64_t)std::min<uint64_t>(F[i], (uint64_t)tA))
+          return false;
+      return true;
+    };
+    // 3. the next cut: the first unsafe packet over all ranks
+    uint64_t B1 = G;
+    int64_t tB1 = 0;
+    if (!safe_t(t_last_g)) {
+      int64_t mine[2] = {(int64_t)G, 0};
+      const uint64_t lo_g = std::max<uint64_t>(A + 1, off), hi_g = (uint64_t)off + n;
+      if (lo_g < hi_g && !safe_t(at(n - 1))) {
+        uint32_t lo = (uint32_t)(lo_g - off), hi = n - 1;
+        while (lo < hi) {
+          const uint32_t mid = lo + (hi - lo) / 2;
+          if (safe_t(at(mid))) lo = mid + 1; else hi = mid;
+        }
+        mine[0] = (int64_t)off + lo;
+        mine[1] = at(lo);
+      }
+      std::vector<int64_t> cuts(2 * (size_t)m.n);
+      VP_TRY(m.allgather_host(c, mine, cuts.data(), sizeof mine));
+      for (int r = 0; r < m.n; r++)
+        if ((uint64_t)cuts[2 * r] < B1) {
+          B1 = (uint64_t)cuts[2 * r];
+          tB1 = cuts[2 * r + 1];
+        }
+    }
+    // 4. this rank's part of [A, B1); collectives inside run on every rank
+    const uint32_t lp0 = (uint32_t)(std::min<uint64_t>(std::max<uint64_t>(A, off), off + (uint64_t)n) - off);
+    const uint32_t lp1 = (uint32_t)(std::min<uint64_t>(std::max<uint64_t>(B1, off), off + (uint64_t)n) - off);
+    uint32_t allocated = 0;
+    VP_TRY(seg(c, b, now, lp0, lp1, &ms, &launches, &allocated));
+    for (int i = 0; i < ntabs; i++)
+      if (allocated & (1u << i)) {
+        F[i] = std::min<uint64_t>(F[i], (uint64_t)tA);
+        tabs[i].t->ts_floor = std::min<uint64_t>(tabs[i].t->ts_floor, (uint64_t)tA);
+      }
+    A = B1;
+    tA = tB1;
+  }
+  VP_HIP(hipStreamSynchronize(c->stream));
+  c->seq += G;
+  c->last_now = t_last_g;
   c->last_ms = ms;
   c->last_launches = launches;
   return 0;

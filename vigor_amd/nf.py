@@ -53,6 +53,10 @@ class NfBase:
         _check(self.L.vp_process_device(self.h, C.byref(b), s),
                "vp_process_device")
 
+    def sync_state(self):
+        """Multi-GPU: merge the ranks' timestamps (collective)."""
+        _check(self.L.vp_sync_state(self.h), "vp_sync_state")
+
     def last_kernel_ms(self):
         ms, k = C.c_float(), C.c_int()
         _check(self.L.vp_last_kernel_ms(self.h, C.byref(ms), C.byref(k)),
