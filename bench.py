@@ -123,17 +123,29 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.flows is None:
         args.flows = 1 << 20 if world == 1 else 1 << 24
+    # VIGPATH_COMM=host: every rank on GPU 0 with gloo host collectives (a
+    # rehearsal of the N > 1 path on a one-GPU box); default RCCL
+    host_comm = os.environ.get("VIGPATH_COMM", "rccl") == "host"
+    if host_comm:
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if host_comm:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl",
+                                    device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
     cfg = vigor_amd.nat_config_from_args(
         NAT_ARGS + ["--max-flows", str(args.flows)], 2, DEV_MACS)
     nat = vigor_amd.Nat(cfg, gpu=local)
-    if world > 1:  # one vignat over all ranks (RCCL)
+    if world > 1:  # one vignat over all ranks
         from vigor_amd import shard
-        shard.attach_rccl(nat, rank, world)
+        if host_comm:
+            shard.attach_torch(nat, rank, world)
+        else:
+            shard.attach_rccl(nat, rank, world)
     bank = FlowBank(args.flows, 0, dev)
     B = args.batch
     lens = torch.full((B,), 60, dtype=torch.int16, device=dev)
@@ -180,7 +192,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=dev)
+        t = torch.tensor([elapsed], device="cpu" if host_comm else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     # every packet hit (steady state) and went out on the WAN port

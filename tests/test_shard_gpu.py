@@ -110,6 +110,33 @@ def run_sharded(spec, world):
                 for r in range(world)]
 
 
+def test_rccl_transport_single_rank():
+    """The RCCL transport in-process (one rank: every collective is a copy on
+    the context's stream) through the multi-GPU batch driver."""
+    import vigor_amd
+    from gpuh import check_batches
+    from vigor_amd import shard
+    args = ["--wan", "1", "--expire", "5", "--starting-port", "0",
+            "--max-flows", "256", "--extip", "192.168.4.2", "--eth-dest",
+            "0," + END_MACS[0].hex(":"), "--eth-dest", "1," + END_MACS[1].hex(":")]
+    nat = vigor_amd.Nat(vigor_amd.nat_config_from_args(args, 2, DEV_MACS), gpu=0)
+    import ctypes as C
+    uid = (C.c_uint8 * 128).from_buffer_copy(shard.rccl_unique_id())
+    assert nat.L.vp_attach_rccl(nat.h, uid, 1, 0) == 0
+    rng = np.random.default_rng(3)
+    fr, ln, dv, now = mixed_nat_trace(rng, 6000, 300, max_idx=256)
+    cfg = orc.nat_cfg(wan=1, start_port=0, ext_ip=T.ip4(192, 168, 4, 2),
+                      expire_us=5, max_flows=256, device_macs=DEV_MACS,
+                      endpoint_macs=END_MACS)
+    o = orc.Oracle("nat", cfg)
+    check_batches(nat, o, fr, ln, dv, now, 64, [1000, 1001, 3000])
+    nat.sync_state()
+    oa, ots, ok = o.nat_dump(256)
+    ga, gts, gk = nat.dump()
+    np.testing.assert_array_equal(ga, oa)
+    np.testing.assert_array_equal(gts[oa == 1], ots[oa == 1])
+
+
 @pytest.mark.parametrize("world,spec", [
     (2, dict(kind="rr", n=40_000, flows=1000, max_flows=65536,
              expire_us=60_000_000, cuts=[1000, 20_000], affine=True)),
