@@ -155,3 +155,25 @@ def test_rejects_bad_config():
     cfg = vigor_amd.nat_config_from_args(args, 2, DEV_MACS[:2])
     with pytest.raises(vigor_amd.VigpathError):
         vigor_amd.Nat(cfg)  # map_allocate rejects a non power of two
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_pipeline_chunks(pinned, monkeypatch):
+    """vp_process_host in several double-buffered chunks (copy stream beside
+    the compute stream), pageable and page-locked frames."""
+    import torch
+    monkeypatch.setenv("VIGPATH_HOST_CHUNK", "700")
+    rng = np.random.default_rng(17)
+    fr, ln, dv, now = mixed_nat_trace(rng, 5000, 200, max_idx=256)
+    nat, o = make_pair(max_flows=256, expire_us=3)
+    exp = fr.copy()
+    exp_out = o.run(exp, ln, dv, now, 64)
+    if pinned:
+        t = torch.from_numpy(fr.copy()).pin_memory()
+        got = t.numpy()
+    else:
+        got = fr.copy()
+    out = nat.process_host(got, ln, dv, now, 64)
+    np.testing.assert_array_equal(out, exp_out)
+    np.testing.assert_array_equal(got, exp)
+    check_state(nat, o, 256)

@@ -103,6 +103,13 @@ struct Workspace {
   uint16_t *d_len = nullptr, *d_in = nullptr, *d_out = nullptr;
   int64_t *d_now = nullptr;
   uint32_t d_meta_n = 0;
+  // pipelined host batches (vp_process_host): copy stream, per-buffer
+  // events, pinned staging of the small per-packet arrays
+  hipStream_t cstream = nullptr;
+  hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr},
+             ev_out[2] = {nullptr, nullptr};
+  uint8_t *h_meta = nullptr;
+  size_t h_meta_bytes = 0;
 };
 
 }  // namespace vp

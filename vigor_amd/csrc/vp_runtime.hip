@@ -133,6 +133,13 @@ static void free_all(vp_ctx *c) {
                   w.sbuf,    w.rbuf};
   for (void *p : ptrs) hipFree(p);
   if (w.h_frames) hipHostFree(w.h_frames);
+  if (w.h_meta) hipHostFree(w.h_meta);
+  for (int i = 0; i < 2; i++) {
+    if (w.ev_in[i]) hipEventDestroy(w.ev_in[i]);
+    if (w.ev_done[i]) hipEventDestroy(w.ev_done[i]);
+    if (w.ev_out[i]) hipEventDestroy(w.ev_out[i]);
+  }
+  if (w.cstream) hipStreamDestroy(w.cstream);
   delete c->comm;
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
@@ -247,6 +254,126 @@ static int stage_frames(vp_ctx *c, size_t bytes) {
     VP_HIP(hipHostMalloc((void **)&w.h_frames, bytes, hipHostMallocDefault));
     w.h_frames_bytes = bytes;
   }
+  return 0;
+}
+
+// Page-locked (hipHostMalloc'd or hipHostRegister'ed, e.g. a DPDK hugepage
+// pool) host memory can be DMA'd directly.
+static bool is_pinned(const void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// Host batch in chunks of `ch` packets, double-buffered in HBM: a copy
+// stream moves chunk k+1 in and chunk k-1 out while chunk k is processed
+// (chunks are processed in order, so results equal one call on the batch).
+// Pinned frames are DMA'd in place; pageable ones through pinned staging.
+// The small per-packet arrays always go through pinned staging.
+static int host_pipeline(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
+                         uint8_t *frames, uint32_t slot, const uint16_t *len,
+                         const int64_t *now, uint16_t *out_dev) {
+  Workspace &w = c->ws;
+  const char *env = getenv("VIGPATH_HOST_CHUNK");
+  uint32_t ch = env ? (uint32_t)atoi(env) : (1u << 20);
+  if (ch == 0) ch = 1u << 20;
+  ch = std::min(ch, n);
+  const uint32_t K = (n + ch - 1) / ch;
+  const bool pinned = is_pinned(frames);
+  VP_TRY(stage_meta(c, 2 * ch));
+  {  // device frames (2 chunks); pinned staging only for pageable frames
+    const size_t bytes = 2ull * ch * slot;
+    if (bytes > w.d_frames_bytes) {
+      hipFree(w.d_frames);
+      w.d_frames = nullptr;
+      w.d_frames_bytes = 0;
+      VP_HIP(hipMalloc((void **)&w.d_frames, bytes));
+      w.d_frames_bytes = bytes;
+    }
+    if (!pinned && bytes > w.h_frames_bytes) {
+      if (w.h_frames) hipHostFree(w.h_frames);
+      w.h_frames = nullptr;
+      w.h_frames_bytes = 0;
+      VP_HIP(hipHostMalloc((void **)&w.h_frames, bytes, hipHostMallocDefault));
+      w.h_frames_bytes = bytes;
+    }
+  }
+  const size_t meta = 14ull * ch;  // len 2 + in 2 + now 8 + out 2 per packet
+  if (2 * meta > w.h_meta_bytes) {
+    if (w.h_meta) hipHostFree(w.h_meta);
+    w.h_meta = nullptr;
+    w.h_meta_bytes = 0;
+    VP_HIP(hipHostMalloc((void **)&w.h_meta, 2 * meta, hipHostMallocDefault));
+    w.h_meta_bytes = 2 * meta;
+  }
+  if (!w.cstream) {
+    VP_HIP(hipStreamCreateWithFlags(&w.cstream, hipStreamNonBlocking));
+    for (int i = 0; i < 2; i++) {
+      VP_HIP(hipEventCreateWithFlags(&w.ev_in[i], hipEventDisableTiming));
+      VP_HIP(hipEventCreateWithFlags(&w.ev_done[i], hipEventDisableTiming));
+      VP_HIP(hipEventCreateWithFlags(&w.ev_out[i], hipEventDisableTiming));
+    }
+  }
+  auto cnt = [&](uint32_t k) { return std::min(ch, n - k * ch); };
+  auto hm = [&](uint32_t k) { return w.h_meta + (k & 1) * meta; };
+  auto dfr = [&](uint32_t k) { return w.d_frames + (size_t)(k & 1) * ch * slot; };
+  auto hfr = [&](uint32_t k) {
+    return pinned ? frames + (size_t)k * ch * slot
+                  : w.h_frames + (size_t)(k & 1) * ch * slot;
+  };
+  // chunk k's results back to the caller (after its D2H completed)
+  auto retire = [&](uint32_t k) -> int {
+    VP_HIP(hipEventSynchronize(w.ev_out[k & 1]));
+    const uint32_t m = cnt(k);
+    if (!pinned) memcpy(frames + (size_t)k * ch * slot, hfr(k), (size_t)m * slot);
+    memcpy(out_dev + (size_t)k * ch, hm(k) + 12ull * ch, 2ull * m);
+    return 0;
+  };
+  auto issue_in = [&](uint32_t k) -> int {
+    const uint32_t m = cnt(k), o = k * ch, i = k & 1;
+    if (k >= 2) VP_TRY(retire(k - 2));  // frees buffer set k & 1
+    uint8_t *h = hm(k);
+    memcpy(h, len + o, 2ull * m);
+    memcpy(h + 2ull * ch, in_dev + o, 2ull * m);
+    memcpy(h + 4ull * ch, now + o, 8ull * m);
+    if (!pinned) memcpy(hfr(k), frames + (size_t)o * slot, (size_t)m * slot);
+    VP_HIP(hipMemcpyAsync(dfr(k), hfr(k), (size_t)m * slot, hipMemcpyHostToDevice,
+                          w.cstream));
+    VP_HIP(hipMemcpyAsync(w.d_len + i * ch, h, 2ull * m, hipMemcpyHostToDevice,
+                          w.cstream));
+    VP_HIP(hipMemcpyAsync(w.d_in + i * ch, h + 2ull * ch, 2ull * m,
+                          hipMemcpyHostToDevice, w.cstream));
+    VP_HIP(hipMemcpyAsync(w.d_now + i * ch, h + 4ull * ch, 8ull * m,
+                          hipMemcpyHostToDevice, w.cstream));
+    VP_HIP(hipEventRecord(w.ev_in[i], w.cstream));
+    return 0;
+  };
+  VP_TRY(issue_in(0));
+  for (uint32_t k = 0; k < K; k++) {
+    const uint32_t i = k & 1, m = cnt(k);
+    if (k + 1 < K) VP_TRY(issue_in(k + 1));
+    VP_HIP(hipStreamWaitEvent(c->stream, w.ev_in[i], 0));
+    vp_dev_batch b{};
+    b.frames = dfr(k);
+    b.slot = slot;
+    b.n = m;
+    b.len = w.d_len + i * ch;
+    b.in_dev = w.d_in + i * ch;
+    b.now = w.d_now + i * ch;
+    b.out_dev = w.d_out + i * ch;
+    VP_TRY(vp_process_device(c, &b, nullptr));
+    VP_HIP(hipEventRecord(w.ev_done[i], c->stream));
+    VP_HIP(hipStreamWaitEvent(w.cstream, w.ev_done[i], 0));
+    VP_HIP(hipMemcpyAsync(hfr(k), dfr(k), (size_t)m * slot, hipMemcpyDeviceToHost,
+                          w.cstream));
+    VP_HIP(hipMemcpyAsync(hm(k) + 12ull * ch, w.d_out + i * ch, 2ull * m,
+                          hipMemcpyDeviceToHost, w.cstream));
+    VP_HIP(hipEventRecord(w.ev_out[i], w.cstream));
+  }
+  for (uint32_t k = K >= 2 ? K - 2 : 0; k < K; k++) VP_TRY(retire(k));
   return 0;
 }
 
@@ -381,12 +508,7 @@ int vp_process_host(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
   if (n == 0) return 0;
   if (slot < 64 || (slot & 15)) return VP_EINVAL;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
-  VP_TRY(stage_meta(c, n));
-  VP_TRY(stage_frames(c, (size_t)n * slot));
-  memcpy(c->ws.h_frames, frames, (size_t)n * slot);
-  VP_TRY(run_staged(c, n, slot, in_dev, len, now, out_dev));
-  memcpy(frames, c->ws.h_frames, (size_t)n * slot);
-  return 0;
+  return host_pipeline(c, n, in_dev, frames, slot, len, now, out_dev);
 }
 
 int vp_process_batch(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
