@@ -197,25 +197,58 @@ __device__ __forceinline__ void wave_lds_sync() {
 // consecutive packets per wave (256-thread blocks, 4 waves): every global
 // load/store instruction moves 1 KiB contiguous (lane l <-> bytes
 // 16l..16l+15 of a 1 KiB piece), staged through the wave's LDS tile S
-// (256 x uint4). fn(p, RFrame&) handles one packet and returns true when the
-// frame was modified and must be written back.
-template <class Fn>
-__device__ __forceinline__ void frames64_tiles(uint8_t *frames, uint32_t p0,
-                                               uint32_t p1, uint32_t n_all,
-                                               uint4 *S, Fn fn) {
+// (256 x uint4).
+//
+// Each packet is handled in two halves around the prefetch of the wave's
+// next tile (its four 1 KiB frame loads plus the lane's len / in_dev):
+//   pend = issue(p, f, in, len, mine)  parse, hash, issue any per-lane read;
+//                                      pend.row = the 64-byte table row
+//                                      (bucket) this packet needs, or kNone;
+//   mod  = finish(pend, row, p, f, in, len)
+//                                      consume the row, rewrite f, return
+//                                      true when f must be written back.
+// Rows are gathered cooperatively: four lanes fetch one row as 64 contiguous
+// bytes (one memory request per row instead of four 16-byte pieces per
+// lane) and the wave's LDS tile hands each lane its own row, the same
+// layout as the frames. The gather is issued before the prefetch: vector-
+// memory counters drain in issue order (MI355X_MICROARCH.md §Per-instruction
+// cycle constants), so rows can be consumed while the prefetch is still in
+// flight and the frame stream's HBM latency hides under the probes. The grid
+// is persistent (resident_grid()), each wave striding over tiles.
+template <class Issue, class Finish>
+__device__ __forceinline__ void frames64_tiles(uint8_t *frames,
+                                               const uint16_t *len,
+                                               const uint16_t *in_dev,
+                                               uint32_t p0, uint32_t p1,
+                                               uint32_t n_all, uint4 *S,
+                                               const uint4 *rows, Issue issue,
+                                               Finish finish) {
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t first = p0 & ~63u;
   const uint32_t tiles = (p1 - first + 63) / 64;
   const uint32_t nwaves = gridDim.x * 4;
-  for (uint32_t tile = blockIdx.x * 4 + wv; tile < tiles; tile += nwaves) {
+  uint4 r[4];
+  uint32_t m_in = 0, m_len = 0;
+  auto fetch = [&](uint32_t tile) {
     const uint32_t tb = first + tile * 64;
-    uint4 *g = reinterpret_cast<uint4 *>(frames + (size_t)tb * 64);
-    const uint32_t avail = n_all - tb < 64 ? n_all - tb : 64;  // in the batch
+    const uint4 *g = reinterpret_cast<const uint4 *>(frames + (size_t)tb * 64);
+    const uint32_t avail = n_all - tb < 64 ? n_all - tb : 64u;  // in the batch
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) {
       const uint32_t c = 64 * j + lane;
-      if ((c >> 2) < avail) S[chunk_swz(c)] = g[c];
+      r[j] = (c >> 2) < avail ? g[c] : make_uint4(0, 0, 0, 0);
     }
+    const uint32_t p = tb + lane;
+    m_in = p < n_all ? in_dev[p] : 0u;
+    m_len = p < n_all ? len[p] : 0u;
+  };
+  uint32_t tile = blockIdx.x * 4 + wv;
+  if (tile < tiles) fetch(tile);
+  for (; tile < tiles; tile += nwaves) {
+    const uint32_t tb = first + tile * 64;
+    uint4 *g = reinterpret_cast<uint4 *>(frames + (size_t)tb * 64);
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = r[j];
     wave_lds_sync();
     const uint32_t p = tb + lane;
     const bool mine = p >= p0 && p < p1;
@@ -228,8 +261,30 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames, uint32_t p0,
       f.w[4 * k + 2] = v.z;
       f.w[4 * k + 3] = v.w;
     }
+    const uint32_t in = m_in, ln = m_len;
+    auto pend = issue(p, f, in, ln, mine);
+    // piece j of lane L: part L % 4 of the row of packet 16 j + L / 4
+    uint4 q[4];
+    if (rows) {
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t row = __shfl(pend.row, 16 * j + (lane >> 2));
+        q[j] = row != kNone ? rows[4 * (size_t)row + (lane & 3)]
+                            : make_uint4(0, 0, 0, 0);
+      }
+    }
+    if (tile + nwaves < tiles) fetch(tile + nwaves);
+    uint4 row[4] = {};
+    if (rows) {  // S is free: f is in registers
+      wave_lds_sync();
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = q[j];
+      wave_lds_sync();
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) row[k] = S[chunk_swz(4 * lane + k)];
+    }
     bool mod = false;
-    if (mine) mod = fn(p, f);
+    if (mine) mod = finish(pend, row, p, f, in, ln);
     if (mod) {
 #pragma unroll
       for (uint32_t k = 0; k < 4; k++)

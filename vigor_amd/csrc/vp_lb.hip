@@ -240,9 +240,8 @@ VP_LB_GENERIC_FN void lb_generic_a(const LbArgs &a, const uint32_t *T,
 }
 
 __device__ __forceinline__ bool lb_fast(const LbArgs &a, const uint32_t *T,
-                                        uint32_t p, RFrame &f) {
-  const uint32_t in = a.in_dev[p];
-  const uint32_t len = a.len[p];
+                                        uint32_t p, RFrame &f, uint32_t in,
+                                        uint32_t len) {
   const uint32_t et = f.w[3] & 0xFFFF;
   const uint32_t ihl = (f.w[3] >> 16) & 0x0F;
   const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
@@ -276,8 +275,17 @@ __global__ __launch_bounds__(256) void lb_classify64(LbArgs a, uint32_t n_all) {
   __shared__ uint32_t T[kLbTabs * 256];
   __shared__ uint4 stage[4][256];
   lb_load_tables(T, a.crc_tab);
-  frames64_tiles(a.frames, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
-                 [&](uint32_t p, RFrame &f) { return lb_fast(a, T, p, f); });
+  struct NoPend {
+    uint32_t row;
+  };
+  frames64_tiles(
+      a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
+      nullptr,
+      [&](uint32_t, const RFrame &, uint32_t, uint32_t, bool) {
+        return NoPend{kNone};
+      },
+      [&](NoPend, const uint4 *, uint32_t p, RFrame &f, uint32_t in,
+          uint32_t len) { return lb_fast(a, T, p, f, in, len); });
 }
 
 __global__ __launch_bounds__(256) void lb_classify(LbArgs a) {
@@ -542,7 +550,8 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   if (b->slot == 64 && c->coalesced_io) {
     const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
-    lb_classify64<<<grid_for((uint64_t)tiles * 64), 256, 0, c->stream>>>(a, b->n);
+    lb_classify64<<<resident_grid((const void *)lb_classify64, (tiles + 3) / 4), 256,
+                    0, c->stream>>>(a, b->n);
   } else {
     lb_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
   }

@@ -147,18 +147,33 @@ VP_GENERIC_FN void nat_generic_a(const NatArgs &a, const uint32_t *T, uint32_t p
   a.out[p] = (uint16_t)dst;
 }
 
-// Phase A for one packet whose 64-byte slot is in registers. Returns true
-// when `f` was rewritten and must be stored back.
-__device__ __forceinline__ bool nat_fast(const NatArgs &a, const uint32_t *T,
-                                         uint32_t p, RFrame &f) {
-  const uint32_t in = a.in_dev[p];
-  const uint32_t len = a.len[p];
+// Phase A for one packet whose 64-byte slot is in registers, in two halves
+// (frames64_tiles): nat_issue parses the headers and issues the packet's
+// first dependent read — the home bucket of a LAN packet's FlowId, the
+// entry slot of a WAN packet's index — and nat_finish consumes it, rewrites
+// the frame and returns true when it must be stored back.
+enum : uint32_t { kPendDone = 0, kPendGeneric = 1, kPendLan = 2, kPendWan = 3 };
+struct NatPend {
+  uint32_t kind;
+  uint32_t row;  // LAN: home bucket, gathered by frames64_tiles; else kNone
+  uint32_t b;    // LAN: home bucket; WAN: flow index
+  uint32_t s;    // WAN: slot_of[index]
+};
+
+__device__ __forceinline__ NatPend nat_issue(const NatArgs &a, const uint32_t *T,
+                                             uint32_t p, const RFrame &f,
+                                             uint32_t in, uint32_t len,
+                                             bool mine) {
+  NatPend P;
+  P.kind = kPendDone;
+  P.row = kNone;
+  if (!mine) return P;
   const uint32_t et = f.w[3] & 0xFFFF;
   const uint32_t ihl = (f.w[3] >> 16) & 0x0F;
   const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
   if (!(et == 0x0008 && ihl == 5 && tl <= 50)) {
-    nat_generic_a(a, T, p, in, len);  // writes global memory itself
-    return false;
+    P.kind = kPendGeneric;  // byte-addressed path (nat_generic_a)
+    return P;
   }
   // nf_then_get_rte_ipv4_header / nf_then_get_tcpudp_header with IHL = 5
   const uint16_t unread = (uint16_t)(len - 14);
@@ -168,28 +183,58 @@ __device__ __forceinline__ bool nat_fast(const NatArgs &a, const uint32_t *T,
   if (!ok) {
     a.out[p] = (uint16_t)in;
     a.log[p] = kNone;
-    return false;
+    return P;
   }
   const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
-  const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
-  uint32_t dst;
-  uint32_t mw[3];
   if (in == a.wan) {
     // flow_manager_get_external (nat_flowmanager.c:78-94)
     const int idx = (int)dp - (int)a.start_port;
     if (idx < 0 || idx >= (int)a.t.cap) {
       a.out[p] = (uint16_t)in;
       a.log[p] = kNone;
-      return false;
+      return P;
     }
-    const uint32_t s = a.t.slot_of[idx];
+    P.kind = kPendWan;
+    P.b = (uint32_t)idx;
+    P.s = a.t.slot_of[idx];
+  } else {
+    // flow_manager_get_internal (nat_flowmanager.c:67-76): map_get's hash
+    const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
+    const uint32_t hh = flowid_hash(T, sp, dp, sip, dip, in, proto);
+    P.kind = kPendLan;
+    P.b = home_bucket(hh, a.t.bmask, a.t.mix);
+#ifndef VP_ABL_NOPROBE  // diagnostic builds skip the read (tools/ablate.py)
+    P.row = P.b;
+#endif
+  }
+  return P;
+}
+
+__device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
+                                           const NatPend &P, const uint4 *row,
+                                           uint32_t p, RFrame &f, uint32_t in,
+                                           uint32_t len) {
+  if (P.kind == kPendDone) return false;
+  if (P.kind == kPendGeneric) {
+    nat_generic_a(a, T, p, in, len);  // writes global memory itself
+    return false;
+  }
+  const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
+  const uint32_t proto = f.w[5] >> 24;
+  const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
+  const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
+  uint32_t dst;
+  uint32_t mw[3];
+  if (P.kind == kPendWan) {
+    const uint32_t idx = P.b;
+    const uint32_t s = P.s;
     if (s == kNone) {  // maybe allocated earlier in this segment: phase C
       a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
       a.log[p] = kNone;  // phase C writes the real entry
       return false;
     }
     const uint4 k = reinterpret_cast<const uint4 *>(a.t.bk + (s >> 2))[s & 3];
-    a.log[p] = (uint32_t)idx;  // rejuvenated before the anti-spoof check
+    a.log[p] = idx;  // rejuvenated before the anti-spoof check
     if ((k.z != sip) | ((k.x >> 16) != sp) | (((k.w >> 16) & 0xFF) != proto)) {
       a.out[p] = (uint16_t)in;  // nat_main.c:55-60
       return false;
@@ -199,14 +244,15 @@ __device__ __forceinline__ bool nat_fast(const NatArgs &a, const uint32_t *T,
     dst = k.w & 0xFFFF;         // flow.internal_device
     macs_for(a, dst, mw);
   } else {
-    // flow_manager_get_internal (nat_flowmanager.c:67-76)
     const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
-    const uint32_t hh = flowid_hash(T, sp, dp, sip, dip, in, proto);
 #ifdef VP_ABL_NOPROBE  // diagnostic builds only (tools/ablate.py)
     asm volatile("" ::"v"(key[0]), "v"(key[1]), "v"(key[2]), "v"(key[3]));
-    const uint32_t idx = hh & (a.t.cap - 1);
+    const uint32_t idx = P.b & (a.t.cap - 1);
 #else
-    const uint32_t idx = tbl_probe(a.t, hh, key);
+    bool done;
+    uint32_t idx = bucket_match(row[0], row[1], row[2], row[3], key, &done);
+    if (!done)  // the home bucket is full of other keys: rest of the path
+      idx = tbl_probe_from(a.t, (P.b + 1) & a.t.bmask, key, a.t.bmask);
 #endif
     if (idx == kNone) {  // new flow, or not yet visible: phase B
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
@@ -254,15 +300,28 @@ __global__ __launch_bounds__(256) void nat_classify(NatArgs a) {
     f.w[4] = c1.x; f.w[5] = c1.y; f.w[6] = c1.z; f.w[7] = c1.w;
     f.w[8] = c2.x; f.w[9] = c2.y; f.w[10] = c2.z; f.w[11] = c2.w;
     f.w[12] = c3.x; f.w[13] = c3.y; f.w[14] = c3.z; f.w[15] = c3.w;
+    const uint32_t in = a.in_dev[p], len = a.len[p];
 #ifdef VP_ABL_NOFRAME
     {
       const uint32_t fl = p & (a.t.cap - 1), v = fl >> 16;
       f.set16(34, bswap16((uint16_t)(fl & 0xFFFF)));
       f.set32at2(26, 10u | (((v >> 8) & 0xFF) << 16) | ((v & 0xFF) << 24));
     }
-    asm volatile("" ::"v"(nat_fast(a, T, p, f) ? f.w[6] ^ f.w[10] : 0u));
+    const NatPend P = nat_issue(a, T, p, f, in, len, true);
+    const uint4 row[4] = {};
+    asm volatile("" ::"v"(nat_finish(a, T, P, row, p, f, in, len)
+                              ? f.w[6] ^ f.w[10] : 0u));
 #else
-    if (nat_fast(a, T, p, f)) {
+    const NatPend P = nat_issue(a, T, p, f, in, len, true);
+    uint4 row[4] = {};
+    if (P.row != kNone) {
+      const uint4 *q = reinterpret_cast<const uint4 *>(a.t.bk + P.row);
+      row[0] = q[0];
+      row[1] = q[1];
+      row[2] = q[2];
+      row[3] = q[3];
+    }
+    if (nat_finish(a, T, P, row, p, f, in, len)) {
       st_stream(fp, make_uint4(f.w[0], f.w[1], f.w[2], f.w[3]));
       st_stream(fp + 1, make_uint4(f.w[4], f.w[5], f.w[6], f.w[7]));
       st_stream(fp + 2, make_uint4(f.w[8], f.w[9], f.w[10], f.w[11]));
@@ -275,12 +334,18 @@ __global__ __launch_bounds__(256) void nat_classify(NatArgs a) {
 
 // Phase A for 64-byte slots: LDS-staged 1 KiB-contiguous frame I/O
 // (frames64_tiles, vp_device.h); each wave owns 64 consecutive packets.
-__global__ __launch_bounds__(256) void nat_classify64(NatArgs a, uint32_t n_all) {
+__global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_all) {
   __shared__ uint32_t T[15 * 256];
   __shared__ uint4 stage[4][256];
   load_crc_tables(T, a.crc_tab);
-  frames64_tiles(a.frames, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
-                 [&](uint32_t p, RFrame &f) { return nat_fast(a, T, p, f); });
+  frames64_tiles(
+      a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
+      reinterpret_cast<const uint4 *>(a.t.bk),
+      [&](uint32_t p, const RFrame &f, uint32_t in, uint32_t len, bool mine) {
+        return nat_issue(a, T, p, f, in, len, mine);
+      },
+      [&](const NatPend &P, const uint4 *row, uint32_t p, RFrame &f, uint32_t in,
+          uint32_t len) { return nat_finish(a, T, P, row, p, f, in, len); });
 }
 
 // ------------------------------------------------------------- phase B --
@@ -414,7 +479,8 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   if (p1 > p0) {
     if (b->slot == 64 && c->coalesced_io) {
       const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
-      nat_classify64<<<grid_for((uint64_t)tiles * 64), 256, 0, c->stream>>>(a, b->n);
+      nat_classify64<<<resident_grid((const void *)nat_classify64, (tiles + 3) / 4),
+                       256, 0, c->stream>>>(a, b->n);
     } else {
       nat_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
     }

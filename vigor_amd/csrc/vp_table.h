@@ -64,29 +64,49 @@ __host__ __device__ __forceinline__ uint32_t home_bucket(uint32_t h,
              : (h & bmask);
 }
 
+// One bucket (key words k0-k2, entry indices ix) against `key`, entries in
+// order: the index on a match; kNone with *done on an empty entry (the probe
+// path ends there); kNone with !*done when the probe continues in the next
+// bucket.
+__device__ __forceinline__ uint32_t bucket_match(uint4 k0, uint4 k1, uint4 k2,
+                                                 uint4 ix, const uint32_t key[4],
+                                                 bool *done) {
+  *done = true;
+  if (ix.x == kEmpty) return kNone;
+  if (ix.x != kTomb && k0.x == key[0] && k0.y == key[1] && k0.z == key[2] &&
+      k0.w == key[3])
+    return ix.x;
+  if (ix.y == kEmpty) return kNone;
+  if (ix.y != kTomb && k1.x == key[0] && k1.y == key[1] && k1.z == key[2] &&
+      k1.w == key[3])
+    return ix.y;
+  if (ix.z == kEmpty) return kNone;
+  if (ix.z != kTomb && k2.x == key[0] && k2.y == key[1] && k2.z == key[2] &&
+      k2.w == key[3])
+    return ix.z;
+  *done = false;
+  return kNone;
+}
+
+// The rest of a probe path, from bucket b for at most `steps` buckets.
+__device__ __forceinline__ uint32_t tbl_probe_from(const TableDev &t, uint32_t b,
+                                                   const uint32_t key[4],
+                                                   uint32_t steps) {
+  for (uint32_t i = 0; i < steps; i++) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(t.bk + b);
+    bool done;
+    const uint32_t r = bucket_match(q[0], q[1], q[2], q[3], key, &done);
+    if (done) return r;
+    b = (b + 1) & t.bmask;
+  }
+  return kNone;
+}
+
 // map_get (find_key, map-impl-pow2.c:629-732) on the device table. Returns
 // the index or kNone.
 __device__ __forceinline__ uint32_t tbl_probe(const TableDev &t, uint32_t h,
                                               const uint32_t key[4]) {
-  uint32_t b = home_bucket(h, t.bmask, t.mix);
-  for (uint32_t i = 0; i <= t.bmask; i++) {
-    const uint4 *q = reinterpret_cast<const uint4 *>(t.bk + b);
-    const uint4 k0 = q[0], k1 = q[1], k2 = q[2], ix = q[3];
-    if (ix.x == kEmpty) return kNone;
-    if (ix.x != kTomb && k0.x == key[0] && k0.y == key[1] && k0.z == key[2] &&
-        k0.w == key[3])
-      return ix.x;
-    if (ix.y == kEmpty) return kNone;
-    if (ix.y != kTomb && k1.x == key[0] && k1.y == key[1] && k1.z == key[2] &&
-        k1.w == key[3])
-      return ix.y;
-    if (ix.z == kEmpty) return kNone;
-    if (ix.z != kTomb && k2.x == key[0] && k2.y == key[1] && k2.z == key[2] &&
-        k2.w == key[3])
-      return ix.z;
-    b = (b + 1) & t.bmask;
-  }
-  return kNone;
+  return tbl_probe_from(t, home_bucket(h, t.bmask, t.mix), key, t.bmask + 1);
 }
 
 // Key words of an allocated index's entry.
@@ -173,6 +193,12 @@ __global__ void union_stamp(const uint32_t *first, const uint32_t *assign,
                             uint64_t seq, uint64_t *ts, uint64_t *tseq);
 
 uint32_t grid_for(uint64_t n, uint32_t block = 256, uint32_t max_blocks = 2048);
+// Persistent grid for a grid-stride kernel of 256-thread blocks: as many
+// blocks as the device holds at once (occupancy of `kernel` x CUs; env
+// VIGPATH_BLOCKS_PER_CU overrides the per-CU count), at most work_blocks. A
+// larger grid leaves the blocks that do not fit to run after the first wave
+// of blocks, as a tail at lower occupancy.
+uint32_t resident_grid(const void *kernel, uint64_t work_blocks);
 uint32_t next_pow2(uint64_t v);
 int cub_reserve(vp_ctx *c, size_t bytes);
 

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "vp_comm.h"
@@ -22,6 +23,38 @@ uint32_t grid_for(uint64_t n, uint32_t block, uint32_t max_blocks) {
   uint64_t g = (n + block - 1) / block;
   if (g == 0) g = 1;
   return (uint32_t)(g < max_blocks ? g : max_blocks);
+}
+
+uint32_t resident_grid(const void *kernel, uint64_t work_blocks) {
+  struct Entry {
+    const void *kernel;
+    int dev;
+    uint32_t blocks;
+  };
+  static std::mutex mu;
+  static std::vector<Entry> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  uint32_t blocks = 0;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    for (const Entry &e : cache)
+      if (e.kernel == kernel && e.dev == dev) blocks = e.blocks;
+    if (!blocks) {
+      int cus = 0, per = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+              hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) !=
+              hipSuccess)
+        (void)hipGetLastError();
+      const char *env = getenv("VIGPATH_BLOCKS_PER_CU");
+      if (env && atoi(env) > 0) per = atoi(env);
+      blocks = (uint32_t)std::max(1, std::max(cus, 1) * std::max(per, 1));
+      cache.push_back(Entry{kernel, dev, blocks});
+    }
+  }
+  const uint64_t g = std::min<uint64_t>(work_blocks, blocks);
+  return (uint32_t)std::max<uint64_t>(g, 1);
 }
 
 uint32_t next_pow2(uint64_t v) {
