@@ -1,7 +1,7 @@
 /*
  * vigpath — MI355X-native implementation of Vigor's per-packet receive path
  * (parse -> CRC32C flow hash -> libVig map probe -> state update -> header
- * rewrite + IPv4/L4 checksum) for vignat, vigbridge and viglb.
+ * rewrite + IPv4/L4 checksum) for vignat, vigbridge, viglb and vigfw.
  *
  * C ABI only: plain pointers and sizes, no HIP or torch types. Two layers:
  *
@@ -93,12 +93,23 @@ typedef struct vp_lb_config {
   uint8_t device_macs[VP_MAX_DEVICES][6];
 } vp_lb_config;
 
+/* vigfw/fw_config.h:9-24 (+ device MACs, as for vignat). */
+typedef struct vp_fw_config {
+  uint16_t wan_device;
+  uint32_t expiration_time; /* microseconds */
+  uint32_t max_flows;       /* power of two (map.c:73, -DCAPACITY_POW2) */
+  uint16_t n_devices;       /* rte_eth_dev_count_avail() */
+  uint8_t device_macs[VP_MAX_DEVICES][6];
+  uint8_t endpoint_macs[VP_MAX_DEVICES][6];
+} vp_fw_config;
+
 /* Create an NF instance whose state lives in HBM of HIP device `gpu`.
  * Returns 0 and *out, or VP_EINVAL for a configuration the reference's
  * nf_init would reject (non power-of-two capacities, ...). */
 int vp_nat_create(const vp_nat_config *cfg, int gpu, vp_ctx **out);
 int vp_bridge_create(const vp_bridge_config *cfg, int gpu, vp_ctx **out);
 int vp_lb_create(const vp_lb_config *cfg, int gpu, vp_ctx **out);
+int vp_fw_create(const vp_fw_config *cfg, int gpu, vp_ctx **out);
 void vp_destroy(vp_ctx *ctx);
 
 /* ------------------------------------------------------------ batches -- */
@@ -191,6 +202,12 @@ int vp_bridge_dump(vp_ctx *ctx, uint8_t *alloc, int64_t *ts, uint8_t *macs,
 int vp_lb_dump(vp_ctx *ctx, uint8_t *f_alloc, int64_t *f_ts, uint8_t *f_keys,
                uint32_t *f_backend, uint8_t *b_alloc, int64_t *b_ts,
                uint32_t *b_ip, uint8_t *b_mac, uint16_t *b_nic);
+
+/* vigfw state by flow index i < max_flows: alloc[i], ts[i], key[16*i] (the
+ * FlowId bytes, vigfw/flow.h:3-9 layout, padding zero), int_dev[i] (the
+ * int_devices vector, fw_flowmanager.c:61-64; 0 where not allocated). */
+int vp_fw_dump(vp_ctx *ctx, uint8_t *alloc, int64_t *ts, uint8_t *keys,
+               uint32_t *int_dev);
 
 /* Number of live flows / learned MACs / flows+backends. */
 int64_t vp_live_count(vp_ctx *ctx);

@@ -11,6 +11,7 @@
  *   vignat/nat_main.c:14-109, nat_flowmanager.c:20-94
  *   vigbridge/bridge_main.c:29-128, 292-329
  *   viglb/lb_main.c:13-68, lb_balancer.c:22-237
+ *   vigfw/fw_main.c:21-80, fw_flowmanager.c:38-86
  *   codegen/main.ml:163-206, 328-401, 444-486 (generated _eq/_hash/_allocate)
  * libVig is reached only through orc_lv.h, so the same glue runs over the
  * restated libVig (liborc.so) or the reference's own (oracle/_ref).
@@ -64,6 +65,14 @@ struct FlowId {
   uint16_t internal_device;
   uint8_t protocol;
 };
+/* vigfw/flow.h:3-9 (13 bytes + padding) */
+struct FwFlowId {
+  uint16_t src_port;
+  uint16_t dst_port;
+  uint32_t src_ip;
+  uint32_t dst_ip;
+  uint8_t protocol;
+};
 /* rte_ether.h model :10-12 */
 struct EthAddr {
   uint8_t b[6];
@@ -113,6 +122,32 @@ static bool FlowId_eq(void *a, void *b) {
          x->internal_device == y->internal_device && x->protocol == y->protocol;
 }
 static void FlowId_allocate(void *k) { memset(k, 0, sizeof(struct FlowId)); }
+
+/* vigfw's generated FlowId_hash / _eq / _allocate (codegen/main.ml:163-206,
+ * 328-401, 444-486): five CRC steps in field order. */
+static unsigned FwFlowId_hash(void *k) {
+  struct FwFlowId *f = k;
+  unsigned h = 0;
+  h = orc_crc32c_u32(h, f->src_port);
+  h = orc_crc32c_u32(h, f->dst_port);
+  h = orc_crc32c_u32(h, f->src_ip);
+  h = orc_crc32c_u32(h, f->dst_ip);
+  h = orc_crc32c_u32(h, f->protocol);
+  return h;
+}
+static bool FwFlowId_eq(void *a, void *b) {
+  struct FwFlowId *x = a, *y = b;
+  return x->src_port == y->src_port && x->dst_port == y->dst_port &&
+         x->src_ip == y->src_ip && x->dst_ip == y->dst_ip &&
+         x->protocol == y->protocol;
+}
+static void FwFlowId_allocate(void *k) { memset(k, 0, sizeof(struct FwFlowId)); }
+
+uint32_t orc_fw_flowid_hash(uint16_t sp, uint16_t dp, uint32_t sip, uint32_t dip,
+                            uint8_t proto) {
+  struct FwFlowId f = {sp, dp, sip, dip, proto};
+  return FwFlowId_hash(&f);
+}
 
 uint32_t orc_flowid_hash(uint16_t sp, uint16_t dp, uint32_t sip, uint32_t dip,
                          uint16_t dev, uint8_t proto) {
@@ -309,12 +344,20 @@ static void set_macs(struct pkt *p, uint32_t eth, const uint8_t *src,
 }
 
 /* ---------------------------------------------------------------- NFs -- */
-enum nf_kind { NF_NAT = 1, NF_BRIDGE = 2, NF_LB = 3 };
+enum nf_kind { NF_NAT = 1, NF_BRIDGE = 2, NF_LB = 3, NF_FW = 4 };
 
 struct nat_state {
   orc_nat_cfg cfg;
   struct lv_map *fm;
   struct lv_vector *fv;
+  struct lv_dchain *heap;
+};
+/* vigfw/dataspec.ml:5-11: fm, fv, int_devices, heap */
+struct fw_state {
+  orc_fw_cfg cfg;
+  struct lv_map *fm;
+  struct lv_vector *fv;
+  struct lv_vector *int_devices;
   struct lv_dchain *heap;
 };
 struct bridge_state {
@@ -345,6 +388,7 @@ struct orc_nf {
     struct nat_state nat;
     struct bridge_state br;
     struct lb_state lb;
+    struct fw_state fw;
   } u;
 };
 
@@ -450,6 +494,104 @@ void orc_nat_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *keys) {
     void *k;
     lv_vector_borrow(s->fv, i, &k);
     memcpy(keys + (size_t)16 * i, k, 16);
+  }
+  free(order);
+  free(fre);
+}
+
+/* ---- vigfw ---- */
+orc_nf *orc_fw_create(const orc_fw_cfg *cfg) {
+  if (cfg->n_devices == 0 || cfg->n_devices > ORC_MAX_DEV) return NULL;
+  orc_nf *nf = calloc(1, sizeof *nf);
+  if (!nf) return NULL;
+  nf->kind = NF_FW;
+  struct fw_state *s = &nf->u.fw;
+  s->cfg = *cfg;
+  /* alloc_state(max_flows, fw_device): vigfw/dataspec.ml:5-11,
+   * loop_boilerplate_gen.ml:626-710 (containers in declaration order) */
+  if (!lv_map_allocate(FwFlowId_eq, FwFlowId_hash, cfg->max_flows, &s->fm) ||
+      !lv_vector_allocate(sizeof(struct FwFlowId), cfg->max_flows,
+                          FwFlowId_allocate, &s->fv) ||
+      !lv_vector_allocate(sizeof(uint32_t), cfg->max_flows, U32_init,
+                          &s->int_devices) ||
+      !lv_dchain_allocate((int)cfg->max_flows, &s->heap)) {
+    free(nf);
+    return NULL;
+  }
+  return nf;
+}
+
+/* vigfw/fw_main.c:21-80 with fw_flowmanager.c:38-86 inlined */
+static int fw_process(struct fw_state *s, uint16_t device, struct pkt *p,
+                      int64_t now) {
+  /* fw_flowmanager.c:66-73: FlowManager.expiration_time is a vigor_time_t,
+   * so the us -> ns product is 64-bit (no u32 wrap, unlike vignat). */
+  int64_t last_time =
+      (int64_t)((uint64_t)now - (uint64_t)((int64_t)s->cfg.expiration_time * 1000));
+  lv_expire_items_single_map(s->heap, s->fv, s->fm, last_time);
+
+  uint32_t eth = borrow(p, 14);
+  uint32_t ip, l4;
+  if (!get_ipv4(p, eth, &ip)) return device;
+  if (!get_tcpudp(p, ip, &l4)) return device;
+
+  uint16_t dst_device;
+  if (device == s->cfg.wan_device) {
+    /* reversed key for the reply flow (fw_main.c:46-53) */
+    struct FwFlowId id = {rd16(p, l4 + 2), rd16(p, l4), rd32(p, ip + 16),
+                          rd32(p, ip + 12), rd8(p, ip + 9)};
+    int index; /* flow_manager_get_refresh_flow (fw_flowmanager.c:75-86) */
+    if (!lv_map_get(s->fm, &id, &index)) return device;
+    uint32_t *int_dev;
+    lv_vector_borrow(s->int_devices, index, (void **)&int_dev);
+    uint32_t d = *int_dev;
+    lv_vector_return(s->int_devices, index, int_dev);
+    lv_dchain_rejuvenate_index(s->heap, index, now);
+    dst_device = (uint16_t)d;
+  } else {
+    struct FwFlowId id = {rd16(p, l4), rd16(p, l4 + 2), rd32(p, ip + 12),
+                          rd32(p, ip + 16), rd8(p, ip + 9)};
+    /* flow_manager_allocate_or_refresh_flow (fw_flowmanager.c:38-64) */
+    int index;
+    if (lv_map_get(s->fm, &id, &index)) {
+      lv_dchain_rejuvenate_index(s->heap, index, now);
+    } else if (lv_dchain_allocate_new_index(s->heap, &index, now)) {
+      struct FwFlowId *key;
+      lv_vector_borrow(s->fv, index, (void **)&key);
+      *key = id;
+      lv_map_put(s->fm, key, index);
+      lv_vector_return(s->fv, index, key);
+      uint32_t *int_dev;
+      lv_vector_borrow(s->int_devices, index, (void **)&int_dev);
+      *int_dev = device;
+      lv_vector_return(s->int_devices, index, int_dev);
+    } /* table full: the outgoing packet still goes out */
+    dst_device = s->cfg.wan_device;
+  }
+  const uint8_t *smac = dst_device < s->cfg.n_devices
+                            ? s->cfg.device_macs[dst_device] : zero_mac;
+  const uint8_t *dmac = dst_device < s->cfg.n_devices
+                            ? s->cfg.endpoint_macs[dst_device] : zero_mac;
+  set_macs(p, eth, smac, dmac);
+  return dst_device;
+}
+
+void orc_fw_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *keys,
+                 uint32_t *int_dev) {
+  struct fw_state *s = &nf->u.fw;
+  int n = (int)s->cfg.max_flows;
+  int *order = malloc(sizeof(int) * (size_t)n);
+  int *fre = malloc(sizeof(int) * (size_t)n);
+  int na, nfree;
+  lv_dchain_dump(s->heap, n, order, &na, fre, &nfree, ts);
+  for (int i = 0; i < n; i++) {
+    alloc[i] = (uint8_t)lv_dchain_is_index_allocated(s->heap, i);
+    void *k;
+    lv_vector_borrow(s->fv, i, &k);
+    memset(keys + (size_t)16 * i, 0, 16);
+    memcpy(keys + (size_t)16 * i, k, 13);
+    lv_vector_borrow(s->int_devices, i, &k);
+    int_dev[i] = alloc[i] ? *(uint32_t *)k : 0;
   }
   free(order);
   free(fre);
@@ -792,6 +934,12 @@ void orc_destroy(orc_nf *nf) {
       lv_dchain_free(nf->u.lb.active_backends);
       lv_vector_free(nf->u.lb.cht);
       break;
+    case NF_FW:
+      lv_map_free(nf->u.fw.fm);
+      lv_vector_free(nf->u.fw.fv);
+      lv_vector_free(nf->u.fw.int_devices);
+      lv_dchain_free(nf->u.fw.heap);
+      break;
   }
   free(nf);
 }
@@ -806,6 +954,8 @@ int orc_process(orc_nf *nf, uint16_t device, uint8_t *frame, uint16_t len,
       return bridge_process(&nf->u.br, device, &p, now);
     case NF_LB:
       return lb_process(&nf->u.lb, device, &p, now);
+    case NF_FW:
+      return fw_process(&nf->u.fw, device, &p, now);
   }
   return device;
 }

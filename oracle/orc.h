@@ -2,7 +2,7 @@
  * ORACLE — TEST INFRASTRUCTURE ONLY.
  *
  * CPU restatement of Vigor's per-packet path (nf.c dispatch -> nf_process of
- * vignat / vigbridge / viglb -> nf-util parse + DPDK 20.08 checksum -> libVig).
+ * vignat / vigbridge / viglb / vigfw -> nf-util parse + DPDK 20.08 checksum -> libVig).
  * Only tests/, bench.py's cpu_baseline leg and __graft_entry__.smoke() may
  * load it, and only as the checker (or the timed CPU baseline). The product
  * path (vigor_amd/, include/vigpath.h) never links, loads or calls it.
@@ -65,7 +65,18 @@ typedef struct {
   uint8_t device_macs[ORC_MAX_DEV][6];
 } orc_lb_cfg;
 
+/* vigfw/fw_config.h:9-24 */
+typedef struct {
+  uint16_t wan_device;
+  uint32_t expiration_time; /* microseconds (x1000 in 64 bits) */
+  uint32_t max_flows;       /* power of two */
+  uint16_t n_devices;
+  uint8_t device_macs[ORC_MAX_DEV][6];
+  uint8_t endpoint_macs[ORC_MAX_DEV][6];
+} orc_fw_cfg;
+
 orc_nf *orc_nat_create(const orc_nat_cfg *cfg);
+orc_nf *orc_fw_create(const orc_fw_cfg *cfg);
 orc_nf *orc_bridge_create(const orc_bridge_cfg *cfg);
 orc_nf *orc_lb_create(const orc_lb_cfg *cfg);
 void orc_destroy(orc_nf *nf);
@@ -90,6 +101,8 @@ uint32_t orc_crc32c_u32(uint32_t crc, uint32_t v);
 uint32_t orc_flowid_hash(uint16_t sp, uint16_t dp, uint32_t sip, uint32_t dip,
                          uint16_t dev, uint8_t proto);
 uint32_t orc_ether_hash(const uint8_t mac[6]);
+uint32_t orc_fw_flowid_hash(uint16_t sp, uint16_t dp, uint32_t sip, uint32_t dip,
+                            uint8_t proto);
 const char *orc_impl_name(void);
 
 /* Observable state for parity of state (not just outputs). */
@@ -97,6 +110,9 @@ uint32_t orc_nat_flow_count(orc_nf *nf);
 /* Writes, for index i < max_flows: alloc[i] = allocated?, ts[i] timestamp,
  * key[i] = the 16-byte FlowId stored at that index. */
 void orc_nat_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *keys);
+/* vigfw: alloc, ts, FlowId bytes (13 + zero padding), int_devices. */
+void orc_fw_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *keys,
+                 uint32_t *int_dev);
 void orc_bridge_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *macs,
                      uint16_t *port);
 void orc_lb_dump(orc_nf *nf, uint8_t *f_alloc, int64_t *f_ts, uint8_t *f_keys,

@@ -40,6 +40,13 @@ class LbCfg(C.Structure):
                 ("device_macs", (C.c_uint8 * 6) * MAX_DEV)]
 
 
+class FwCfg(C.Structure):
+    _fields_ = [("wan_device", C.c_uint16), ("expiration_time", C.c_uint32),
+                ("max_flows", C.c_uint32), ("n_devices", C.c_uint16),
+                ("device_macs", (C.c_uint8 * 6) * MAX_DEV),
+                ("endpoint_macs", (C.c_uint8 * 6) * MAX_DEV)]
+
+
 def _ptr(a):
     return C.c_void_p(a.ctypes.data) if a is not None else None
 
@@ -68,6 +75,12 @@ def lib(ref: bool = False):
     L.orc_bridge_create.argtypes = [C.POINTER(BridgeCfg)]
     L.orc_lb_create.restype = C.c_void_p
     L.orc_lb_create.argtypes = [C.POINTER(LbCfg)]
+    L.orc_fw_create.restype = C.c_void_p
+    L.orc_fw_create.argtypes = [C.POINTER(FwCfg)]
+    L.orc_fw_dump.argtypes = [C.c_void_p] * 5
+    L.orc_fw_flowid_hash.restype = C.c_uint32
+    L.orc_fw_flowid_hash.argtypes = [C.c_uint16, C.c_uint16, C.c_uint32,
+                                     C.c_uint32, C.c_uint8]
     L.orc_destroy.argtypes = [C.c_void_p]
     L.orc_process.restype = C.c_int
     L.orc_process.argtypes = [C.c_void_p, C.c_uint16, C.c_void_p, C.c_uint16,
@@ -118,8 +131,18 @@ def nat_cfg(wan=1, start_port=0, ext_ip=0, expire_us=60_000_000,
     return c
 
 
+def fw_cfg(wan=1, expire_us=60_000_000, max_flows=65536, device_macs=(),
+           endpoint_macs=(), n_devices=2):
+    c = FwCfg()
+    c.wan_device, c.expiration_time = wan, expire_us
+    c.max_flows, c.n_devices = max_flows, n_devices
+    _macs(c.device_macs, device_macs)
+    _macs(c.endpoint_macs, endpoint_macs)
+    return c
+
+
 class Oracle:
-    """One NF instance in the oracle. kind: 'nat' | 'bridge' | 'lb'."""
+    """One NF instance in the oracle. kind: 'nat' | 'bridge' | 'lb' | 'fw'."""
 
     def __init__(self, kind: str, cfg, ref: bool = False, statics=None):
         self.L = lib(ref)
@@ -140,6 +163,8 @@ class Oracle:
             self.h = self.L.orc_bridge_create(C.byref(cfg))
         elif kind == "lb":
             self.h = self.L.orc_lb_create(C.byref(cfg))
+        elif kind == "fw":
+            self.h = self.L.orc_fw_create(C.byref(cfg))
         else:
             raise ValueError(kind)
         if not self.h:
@@ -181,6 +206,14 @@ class Oracle:
         keys = np.zeros(max_flows * 16, np.uint8)
         self.L.orc_nat_dump(self.h, _ptr(alloc), _ptr(ts), _ptr(keys))
         return alloc, ts, keys.reshape(max_flows, 16)
+
+    def fw_dump(self, max_flows):
+        alloc = np.zeros(max_flows, np.uint8)
+        ts = np.zeros(max_flows, np.int64)
+        keys = np.zeros(max_flows * 16, np.uint8)
+        dev = np.zeros(max_flows, np.uint32)
+        self.L.orc_fw_dump(self.h, _ptr(alloc), _ptr(ts), _ptr(keys), _ptr(dev))
+        return alloc, ts, keys.reshape(max_flows, 16), dev
 
     def bridge_dump(self, cap):
         alloc = np.zeros(cap, np.uint8)

@@ -13,7 +13,8 @@ import vigor_amd
 from vigor_amd import config as cfgmod
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SHIMS = {"nat": os.path.join(ROOT, "vigor_amd", "libvignat_nf.so")}
+SHIMS = {nf: os.path.join(ROOT, "vigor_amd", "libvig%s_nf.so" % nf)
+         for nf in ("nat", "bridge", "lb", "fw")}
 NF_H = ["nf_init", "nf_process", "nf_config_init", "nf_config_usage",
         "nf_config_print", "config"]
 
@@ -91,3 +92,84 @@ def test_nat_config_parse_semantics():
         cfgmod.nat_config_from_args(["--wan", "5"], 2, [])
     with pytest.raises(ValueError):
         cfgmod.nat_config_from_args(["--max-flows", "12x"], 2, [])
+
+
+class FwNfConfig(C.Structure):
+    """vigfw/fw_config.h:9-24 as the shim defines it."""
+    _fields_ = [("wan_device", C.c_uint16),
+                ("device_macs", C.POINTER(RteEther)),
+                ("endpoint_macs", C.POINTER(RteEther)),
+                ("expiration_time", C.c_uint32), ("max_flows", C.c_uint32)]
+
+
+class LbNfConfig(C.Structure):
+    """viglb/lb_config.h:8-38 as the shim defines it."""
+    _fields_ = [("backend_count", C.c_uint16),
+                ("device_macs", C.POINTER(RteEther)),
+                ("flow_capacity", C.c_uint32),
+                ("flow_expiration_time", C.c_uint32),
+                ("backend_capacity", C.c_uint32), ("cht_height", C.c_uint32),
+                ("backend_expiration_time", C.c_uint32),
+                ("wan_device", C.c_uint16)]
+
+
+class BridgeNfConfig(C.Structure):
+    """vigbridge/bridge_config.h:8-18 as the shim defines it."""
+    _fields_ = [("expiration_time", C.c_uint32), ("dyn_capacity", C.c_uint32),
+                ("static_config_fname", C.c_char * 512)]
+
+
+def _init(lib, args):
+    args = [b"nf"] + [a.encode() for a in args]
+    argv = (C.c_char_p * (len(args) + 1))(*args, None)
+    lib.nf_config_init(len(args), argv)
+
+
+def test_fw_shim_parses_like_reference():
+    os.environ["VIGPATH_NB_DEVICES"] = "3"
+    L = C.CDLL(SHIMS["fw"])
+    _init(L, ["--wan", "2", "--expire", "99", "--max-flows", "1024",
+              "--eth-dest", "1,01:23:45:67:89:01"])
+    cfg = FwNfConfig.in_dll(L, "config")
+    assert (cfg.wan_device, cfg.expiration_time, cfg.max_flows) == (2, 99, 1024)
+    assert bytes(cfg.endpoint_macs[1].b) == bytes.fromhex("012345678901")
+    assert bytes(cfg.device_macs[2].b) == bytes.fromhex("020000000002")
+
+
+def test_lb_shim_parses_like_reference():
+    os.environ["VIGPATH_NB_DEVICES"] = "3"
+    L = C.CDLL(SHIMS["lb"])
+    _init(L, ["--flow-capacity", "1024", "--backend-capacity", "32",
+              "--cht-height", "97", "--flow-expiration", "10",
+              "--backend-expiration", "20", "--wan", "2"])
+    cfg = LbNfConfig.in_dll(L, "config")
+    assert (cfg.flow_capacity, cfg.backend_capacity, cfg.cht_height) == \
+        (1024, 32, 97)
+    assert (cfg.flow_expiration_time, cfg.backend_expiration_time,
+            cfg.wan_device) == (10, 20, 2)
+    assert bytes(cfg.device_macs[1].b) == bytes.fromhex("020000000001")
+
+
+def test_bridge_shim_parses_like_reference(tmp_path):
+    L = C.CDLL(SHIMS["bridge"])
+    _init(L, [])
+    cfg = BridgeNfConfig.in_dll(L, "config")
+    # DEFAULT_EXP_TIME / DEFAULT_CAPACITY (bridge_config.c:14-15)
+    assert (cfg.expiration_time, cfg.dyn_capacity) == (300000000, 128)
+    f = tmp_path / "static.cfg"
+    f.write_text("02:00:00:00:00:07 0 1\n")
+    _init(L, ["--expire", "5", "--capacity", "256", "--config", str(f)])
+    assert (cfg.expiration_time, cfg.dyn_capacity) == (5, 256)
+    assert cfg.static_config_fname == str(f).encode()
+
+
+def test_fw_config_parse_semantics():
+    c = cfgmod.fw_config_from_args(
+        ["--wan", "1", "--expire", "10", "--max-flows", "65536",
+         "--eth-dest", "0,01:23:45:67:89:00"], 2, [b"\x02" * 6, b"\x12" * 6])
+    assert (c.wan_device, c.expiration_time, c.max_flows) == (1, 10, 65536)
+    assert bytes(c.endpoint_macs[0]) == bytes.fromhex("012345678900")
+    for bad in (["--expire", "0"], ["--wan", "2"], ["--max-flows", "1k"],
+                ["--extip", "1.2.3.4"]):
+        with pytest.raises(ValueError):
+            cfgmod.fw_config_from_args(bad, 2, [])

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import orc
-from tracegen import mixed_nat_trace
+from tracegen import mixed_fw_trace, mixed_nat_trace
 from vigor_amd import traces as T
 
 pytestmark = pytest.mark.gpu
@@ -61,6 +61,37 @@ def test_nf_loop_matches_oracle(tmp_path, batch):
     np.testing.assert_array_equal(out, exp_out)
     # frames compared over each packet's valid bytes (the batched entry point
     # stages len bytes per mbuf)
+    f, e = frames.reshape(n, 64), exp.reshape(n, 64)
+    for i in range(n):
+        assert f[i, :ln[i]].tobytes() == e[i, :ln[i]].tobytes(), i
+
+
+@pytest.mark.parametrize("batch", [0, 700])
+def test_fw_loop_matches_oracle(tmp_path, batch):
+    """host/nf_loop_fw: nf.c's loop linked against libvigfw_nf.so."""
+    rng = np.random.default_rng(4)
+    n = 3000 if batch else 400
+    fr, ln, dv, now = mixed_fw_trace(rng, n, 150)
+    dev3 = DEV + [bytes.fromhex("020000000002")]
+    end3 = END + [T.mac("01:23:45:67:89:02")]
+    cfg = orc.fw_cfg(wan=1, expire_us=7, max_flows=256, device_macs=dev3,
+                     endpoint_macs=end3, n_devices=3)
+    exp = fr.copy()
+    exp_out = orc.Oracle("fw", cfg).run(exp, ln, dv, now, 64)
+    tin, tout = tmp_path / "t.in", tmp_path / "t.out"
+    write_trace(tin, fr, ln, dv, now, 64)
+    cmd = [LOOP + "_fw", str(tin), str(tout)]
+    if batch:
+        cmd += ["--batch", str(batch)]
+    args = ["--wan", "1", "--expire", "7", "--max-flows", "256",
+            "--eth-dest", "0,01:23:45:67:89:00", "--eth-dest",
+            "1,01:23:45:67:89:01", "--eth-dest", "2,01:23:45:67:89:02"]
+    env = dict(os.environ, VIGPATH_NB_DEVICES="3")
+    r = subprocess.run(cmd + ["--"] + args, capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    out, frames = read_out(tout, n, 64)
+    np.testing.assert_array_equal(out, exp_out)
     f, e = frames.reshape(n, 64), exp.reshape(n, 64)
     for i in range(n):
         assert f[i, :ln[i]].tobytes() == e[i, :ln[i]].tobytes(), i

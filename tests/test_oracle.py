@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 
 import orc
-from tracegen import mixed_nat_trace
+from tracegen import mixed_fw_trace, mixed_nat_trace
 from vigor_amd import traces as T
 
 HAVE_REF = os.path.isdir("/root/reference/libvig/verified")
@@ -318,3 +318,83 @@ def test_lb_trace_matches_reference(seed, fexp, bexp):
         np.testing.assert_array_equal(x[0], y[0])
         for a, b in zip(x[1:], y[1:]):
             np.testing.assert_array_equal(a[live], b[live])
+
+
+# ---------------------------------------------------------------- vigfw --
+
+@pytest.mark.parametrize("ref", IMPLS)
+def test_fw_flowid_hash_is_crc_chain(ref):
+    """vigfw's generated FlowId_hash: five crc32c_u32 steps in field order
+    (codegen/main.ml:328-401), checked against the chained u32 CRC."""
+    L = orc.lib(ref)
+    for sp, dp, sip, dip, pr in [(1, 2, 3, 4, 5), (0x3500, 0xE803, 0x0A000001,
+                                                   0x08080808, 17)]:
+        h = 0
+        for v in (sp, dp, sip, dip, pr):
+            h = L.orc_crc32c_u32(h, v)
+        assert L.orc_fw_flowid_hash(sp, dp, sip, dip, pr) == h
+
+
+def fw_oracle(ref, max_flows=64, expire_us=60_000_000, n_dev=3, wan=1):
+    cfg = orc.fw_cfg(wan=wan, expire_us=expire_us, max_flows=max_flows,
+                     device_macs=DEV3_MACS[:n_dev], endpoint_macs=END3_MACS[:n_dev],
+                     n_devices=n_dev)
+    return orc.Oracle("fw", cfg, ref=ref)
+
+
+DEV3_MACS = [T.mac("02:03:04:05:06:07"), T.mac("12:13:14:15:16:17"),
+             T.mac("22:23:24:25:26:27")]
+END3_MACS = [T.mac("01:23:45:67:89:00"), T.mac("01:23:45:67:89:01"),
+             T.mac("01:23:45:67:89:02")]
+
+
+@pytest.mark.parametrize("ref", IMPLS)
+def test_fw_semantics_kat(ref):
+    """fw_main.c:21-80 by hand: a LAN packet opens the flow and goes out on
+    the WAN with its MACs; the reply comes back to the LAN device that opened
+    it; an unknown reply is dropped; a non-TCP/UDP packet is dropped; the
+    header past the MACs is never touched."""
+    o = fw_oracle(ref)
+    f, _ = T.udp_frames(np.array([T.ip4(10, 0, 0, 5)]), np.array([T.ip4(8, 8, 8, 8)]),
+                        np.array([1234]), np.array([53]))
+    lan = bytearray(f.tobytes())
+    orig = bytes(lan)
+    assert o.process(2, lan, now=T.NOW0) == 1
+    assert bytes(lan[0:6]) == END3_MACS[1] and bytes(lan[6:12]) == DEV3_MACS[1]
+    assert bytes(lan[12:]) == orig[12:]
+    r, _ = T.udp_frames(np.array([T.ip4(8, 8, 8, 8)]), np.array([T.ip4(10, 0, 0, 5)]),
+                        np.array([53]), np.array([1234]))
+    rep = bytearray(r.tobytes())
+    assert o.process(1, rep, now=T.NOW0 + 1) == 2
+    assert bytes(rep[0:6]) == END3_MACS[2] and bytes(rep[6:12]) == DEV3_MACS[2]
+    u, _ = T.udp_frames(np.array([T.ip4(8, 8, 8, 8)]), np.array([T.ip4(10, 0, 0, 6)]),
+                        np.array([53]), np.array([1234]))
+    unk = bytearray(u.tobytes())
+    assert o.process(1, unk, now=T.NOW0 + 2) == 1 and bytes(unk) == u.tobytes()
+    icmp = bytearray(orig)
+    icmp[23] = 1
+    assert o.process(0, icmp, now=T.NOW0 + 3) == 0
+    alloc, ts, keys, dev = o.fw_dump(64)
+    assert alloc.sum() == 1 and dev[0] == 2 and ts[0] == T.NOW0 + 1
+
+
+@needs_ref
+@pytest.mark.parametrize("seed,max_flows,expire_us,n_flows",
+                         [(0, 64, 60_000_000, 40), (1, 64, 1, 100),
+                          (2, 16, 60_000_000, 40), (3, 256, 5, 300)])
+def test_fw_trace_matches_reference(seed, max_flows, expire_us, n_flows):
+    rng = np.random.default_rng(seed)
+    fr, ln, dv, now = mixed_fw_trace(rng, 5000, n_flows)
+    res = []
+    for ref in (False, True):
+        o = fw_oracle(ref, max_flows=max_flows, expire_us=expire_us)
+        f = fr.copy()
+        out = o.run(f, ln, dv, now, 64)
+        res.append((out, f, o.fw_dump(max_flows)))
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    (a0, t0, k0, d0), (a1, t1, k1, d1) = res[0][2], res[1][2]
+    np.testing.assert_array_equal(a0, a1)
+    np.testing.assert_array_equal(t0[a0 == 1], t1[a1 == 1])
+    np.testing.assert_array_equal(k0, k1)
+    np.testing.assert_array_equal(d0, d1)

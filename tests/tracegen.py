@@ -139,3 +139,42 @@ def mixed_lb_trace(rng, n, n_flows, n_backends, hb_frac=0.05, quiet=None,
     frames[(bad >= 2 * bad_frac / 3) & (bad < bad_frac), 17] = 250
     now = T.NOW0 + np.cumsum(rng.integers(0, 3, n))
     return frames.reshape(-1), lens, in_dev, now.astype(np.int64)
+
+
+def mixed_fw_trace(rng, n, n_flows, n_dev=3, wan=1, slot=64, reply_frac=0.35,
+                   unknown_frac=0.1):
+    """vigfw stress: LAN packets over n_flows from the non-WAN devices (the
+    same 5-tuple may arrive on different LAN devices), WAN replies (reversed
+    5-tuple) of pool flows (known, not yet seen, or expired) and of unknown
+    flows, malformed frames, TCP and UDP, monotone time with ties."""
+    fl = rng.integers(0, n_flows, n)
+    sip = T.ip4(10, 0, 0, 0) + fl
+    dip = T.ip4(8, 8, 0, 0) + (fl % 7)
+    sp = 1000 + fl % 13
+    dp = np.full(n, 53) + (fl % 3)
+    proto = np.where(fl % 5 == 0, 6, 17)
+    lan_devs = np.array([d for d in range(n_dev) if d != wan])
+    in_dev = lan_devs[rng.integers(0, lan_devs.size, n)].astype(np.uint16)
+    r = rng.random(n)
+    rep = r < reply_frac
+    unk = rep & (r < unknown_frac)
+    in_dev[rep] = wan
+    sip = np.where(unk, sip + 0x10000, sip)  # a flow no LAN packet opens
+    a_ip, b_ip = np.where(rep, dip, sip), np.where(rep, sip, dip)
+    a_p, b_p = np.where(rep, dp, sp), np.where(rep, sp, dp)
+    frames = np.zeros((n, slot), np.uint8)
+    lens = np.zeros(n, np.uint16)
+    for p_ in (6, 17):
+        m = proto == p_
+        f, ln = T.udp_frames(a_ip[m], b_ip[m], a_p[m], b_p[m], slot=slot,
+                             proto=p_)
+        frames[m] = f.reshape(-1, slot)
+        lens[m] = ln
+    bad = rng.random(n)
+    frames[bad < 0.02, 12] = 0x86
+    frames[(bad >= 0.02) & (bad < 0.04), 17] = 200
+    frames[(bad >= 0.04) & (bad < 0.05), 14] = 0x44
+    frames[(bad >= 0.05) & (bad < 0.06), 23] = 1
+    frames[(bad >= 0.06) & (bad < 0.08), 14] = 0x46  # IP options (generic path)
+    now = T.NOW0 + np.cumsum(rng.integers(0, 3, n))
+    return frames.reshape(-1), lens, in_dev, now.astype(np.int64)

@@ -1,4 +1,5 @@
-"""Side benchmarks for the other NFs on the path (BASELINE configs 3 and 4;
+"""Side benchmarks for the other NFs on the path (BASELINE configs 3 and 4,
+and vigfw, SURVEY.md §8(f);
 the headline line is bench.py's vignat). One JSON line per workload:
 device-resident Mpps over pre-generated batches, kernel time of the
 classification kernel, and the oracle's 1-core rate on a sample.
@@ -134,6 +135,40 @@ def bench_lb(args, dev):
                              "kind": "port"} if cpu else None}
 
 
+def bench_fw(args, dev):
+    """vigfw 64 B, 1M flows: warm-up opens every flow, then steady state with
+    every 4th packet the WAN reply of its flow (reversed-key lookup)."""
+    import orc
+    N = args.flows
+    macs = [bytes([2, 0, 0, 0, 0, d]) for d in range(2)]
+    argv = ["--max-flows", str(N), "--expire", "60000000", "--wan", "1",
+            "--eth-dest", "0,90:e2:ba:55:12:20", "--eth-dest", "1,90:e2:ba:55:12:21"]
+    cfg = vigor_amd.fw_config_from_args(argv, 2, macs)
+    fw = vigor_amd.Fw(cfg, gpu=0)
+    B = args.batch
+    gen = lambda s, r: T.fw_trace(B, N, start=s, reply_every=r)  # noqa
+    t0 = time.perf_counter()
+    warm = [to_dev(gen(w * B, 0), dev) for w in range(max(1, N // B))]
+    run(fw, warm, B, dev)
+    warm_s = time.perf_counter() - t0
+    base = len(warm) * B
+    batches = [to_dev(gen(base + k * B, 4), dev) for k in range(args.steps)]
+    mpps, kmpps, out = run(fw, batches, B, dev)
+    cpu = None
+    if not args.no_cpu:
+        ocfg = orc.fw_cfg(wan=1, expire_us=60_000_000, max_flows=N,
+                          device_macs=macs, n_devices=2)
+        cpu = cpu_rate("fw", ocfg, [T.fw_trace(N, N)],
+                       [T.fw_trace(1 << 21, N, start=N, reply_every=4)])
+    return {"workload": "vigfw 64B, %d flows, 1/4 WAN replies" % N,
+            "value": round(mpps, 1), "unit": "Mpps", "kernel_mpps": round(kmpps, 1),
+            "kernel": "fw_classify64", "batch_packets": B, "steps": args.steps,
+            "warm_s": round(warm_s, 2),
+            "dropped": int((out == 1).sum().item()) - (B - B // 4),
+            "cpu_baseline": {"value": round(cpu, 2), "unit": "Mpps", "cores": 1,
+                             "kind": "port"} if cpu else None}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1 << 22)
@@ -141,7 +176,7 @@ def main():
     ap.add_argument("--stations", type=int, default=1 << 20)
     ap.add_argument("--flows", type=int, default=1 << 20)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--only", default="bridge,flood,lb")
+    ap.add_argument("--only", default="bridge,flood,lb,fw")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     todo = args.only.split(",")
@@ -151,6 +186,8 @@ def main():
         print(json.dumps(bench_bridge(args, dev, True)), flush=True)
     if "lb" in todo:
         print(json.dumps(bench_lb(args, dev)), flush=True)
+    if "fw" in todo:
+        print(json.dumps(bench_fw(args, dev)), flush=True)
 
 
 if __name__ == "__main__":

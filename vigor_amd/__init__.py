@@ -61,6 +61,13 @@ class LbConfigC(C.Structure):
                 ("device_macs", MacTable)]
 
 
+class FwConfigC(C.Structure):
+    """vp_fw_config (vigfw/fw_config.h:9-24)."""
+    _fields_ = [("wan_device", C.c_uint16), ("expiration_time", C.c_uint32),
+                ("max_flows", C.c_uint32), ("n_devices", C.c_uint16),
+                ("device_macs", MacTable), ("endpoint_macs", MacTable)]
+
+
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                            C.c_size_t)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t)
@@ -80,10 +87,12 @@ class DevBatchC(C.Structure):
 
 
 # every symbol include/vigpath.h declares
-EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_destroy",
-           "vp_process_device", "vp_process_batch", "vp_process_host",
-           "vp_nat_dump", "vp_bridge_dump", "vp_lb_dump", "vp_comm_unique_id",
-           "vp_attach_rccl", "vp_attach_comm", "vp_sync_state", "vp_live_count", "vp_last_kernel_ms", "vp_version"]
+EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_fw_create",
+           "vp_destroy", "vp_process_device", "vp_process_batch",
+           "vp_process_host", "vp_nat_dump", "vp_bridge_dump", "vp_lb_dump",
+           "vp_fw_dump", "vp_comm_unique_id", "vp_attach_rccl",
+           "vp_attach_comm", "vp_sync_state", "vp_live_count",
+           "vp_last_kernel_ms", "vp_version"]
 
 _libs = {}
 
@@ -98,8 +107,13 @@ def lib(path: str | None = None):
         raise RuntimeError(f"{path} missing: run __graft_entry__.build()")
     L = C.CDLL(path)
     L.vp_version.restype = C.c_char_p
-    for name in ("vp_nat_create", "vp_bridge_create", "vp_lb_create"):
+    for name in ("vp_nat_create", "vp_bridge_create", "vp_lb_create",
+                 "vp_fw_create"):
         getattr(L, name).restype = C.c_int
+    L.vp_fw_create.argtypes = [C.POINTER(FwConfigC), C.c_int,
+                               C.POINTER(C.c_void_p)]
+    L.vp_fw_dump.argtypes = [C.c_void_p] * 5
+    L.vp_fw_dump.restype = C.c_int
     L.vp_nat_create.argtypes = [C.POINTER(NatConfigC), C.c_int,
                                 C.POINTER(C.c_void_p)]
     L.vp_bridge_create.argtypes = [C.POINTER(BridgeConfigC), C.c_int,
@@ -148,6 +162,6 @@ def _check(rc: int, what: str):
         raise VigpathError(rc, what)
 
 
-from .nf import Bridge, Lb, Nat, NfBase  # noqa: E402,F401
-from .config import (bridge_config_from_args, lb_config_from_args,  # noqa
-                     nat_config_from_args)
+from .nf import Bridge, Fw, Lb, Nat, NfBase  # noqa: E402,F401
+from .config import (bridge_config_from_args, fw_config_from_args,  # noqa
+                     lb_config_from_args, nat_config_from_args)

@@ -6,6 +6,8 @@ semantics (host side; the C shims in csrc/vp_nf_*.c do the same in C).
   vigbridge vigbridge/bridge_config.c:22-66 (--expire --capacity --config)
   viglb     viglb/lb_config.c:15-100     (--flow-expiration --flow-capacity
             --backend-capacity --cht-height --backend-expiration --wan)
+  vigfw     vigfw/fw_config.c:17-82      (--eth-dest --expire --max-flows
+            --wan)
 
 The reference calls exit(EXIT_FAILURE) on a bad option; here a ValueError is
 raised with the same message.
@@ -14,7 +16,7 @@ from __future__ import annotations
 
 import re
 
-from . import BridgeConfigC, BridgeRuleC, LbConfigC, NatConfigC
+from . import BridgeConfigC, BridgeRuleC, FwConfigC, LbConfigC, NatConfigC
 
 
 def _parse_int(s: str, name: str, nxt: str = "") -> tuple[int, str]:
@@ -172,4 +174,33 @@ def lb_config_from_args(argv, n_devices: int, device_macs) -> LbConfigC:
             raise ValueError("Unknown option.")
         if val == 0 and k != "wan":
             raise ValueError(f"{k} must be strictly positive.")
+    return c
+
+
+def fw_config_from_args(argv, n_devices: int, device_macs) -> FwConfigC:
+    c = FwConfigC()
+    c.n_devices = n_devices
+    for d, m in enumerate(device_macs):  # rte_eth_macaddr_get
+        c.device_macs[d][:] = list(m)
+    for k, v in _split(argv):
+        if k == "eth-dest":
+            dev, _ = _parse_int(v, "eth-dest device", ",")
+            if dev >= n_devices:
+                raise ValueError(f"eth-dest: device {dev} >= nb_devices "
+                                 f"({n_devices})")
+            c.endpoint_macs[dev][:] = list(_parse_mac(v[2:]))
+        elif k == "expire":
+            c.expiration_time = _parse_int(v, "exp-time")[0] & 0xFFFFFFFF
+            if c.expiration_time == 0:
+                raise ValueError("Expiration time must be strictly positive.")
+        elif k == "max-flows":
+            c.max_flows = _parse_int(v, "max-flows")[0] & 0xFFFFFFFF
+            if c.max_flows <= 0:
+                raise ValueError("Flow table size must be strictly positive.")
+        elif k == "wan":
+            c.wan_device = _parse_int(v, "wan-dev")[0] & 0xFFFF
+            if c.wan_device >= n_devices:
+                raise ValueError("WAN device does not exist.")
+        else:
+            raise ValueError("Unknown option.")
     return c

@@ -28,7 +28,7 @@ int hip_fail(hipError_t e, const char *what, const char *file, int line);
 struct Comm;  // vp_comm.hip: collectives between the ranks of one NF
 constexpr int kMaxRanks = 64;
 
-enum Kind { KIND_NAT = 1, KIND_BRIDGE = 2, KIND_LB = 3 };
+enum Kind { KIND_NAT = 1, KIND_BRIDGE = 2, KIND_LB = 3, KIND_FW = 4 };
 
 // Device control block of one table (dchain + map bookkeeping).
 struct Ctl {
@@ -125,9 +125,10 @@ struct vp_ctx {
   int64_t last_now = -1;  // time of the last packet processed
   vp_nat_config nat{};
   vp_bridge_config brg{};  // static_rules not kept (built into st_*)
-  vp::FlowTable ft;       // vignat flows / vigbridge dyn MACs / viglb flows
+  vp::FlowTable ft;       // vignat/vigfw flows / vigbridge dyn MACs / viglb flows
   vp::FlowTable ft2;      // viglb backends (ip_to_backend_id + dchain)
   vp_lb_config lb{};
+  vp_fw_config fw{};
   uint4 *be_rec = nullptr;  // viglb backends[]: {ip, mac0-3, mac4-5|nic<<16, 0}
   uint32_t *cht = nullptr;  // viglb CHT, cht[bucket * backend_capacity + prio]
   uint32_t *dmacw = nullptr;  // per device: {s_addr[0..1] << 16, s_addr[2..5]}

@@ -1,26 +1,18 @@
 /*
- * nf.h drop-in for vignat backed by the GPU path (libvignat_nf.so).
+ * nf.h drop-in for vigfw backed by the GPU path (libvigfw_nf.so).
  *
- * Exports exactly the operator surface the reference's nf.c links against
- * (nf.h:8-18): nf_init, nf_process, nf_config_init, nf_config_usage,
- * nf_config_print and `struct nf_config config`, with vignat's option names
- * and parse semantics (vignat/nat_config.c:17-106) and struct layout
- * (vignat/nat_config.h:5-31). nf_process runs one packet through the batch
- * C-ABI (vp_process_batch); a batching caller should call vp_process_batch
- * directly (include/vigpath.h).
- *
- * Device count, MACs and GPU selection: vp_nf_common.h.
+ * The nf.h operator surface (nf.h:8-18) with vigfw's option names and parse
+ * semantics (vigfw/fw_config.c:17-82), struct layout (vigfw/fw_config.h:9-24)
+ * and nf_init (fw_main.c:14-19). Device count, MACs and GPU selection:
+ * vp_nf_common.h.
  */
 #include "vp_nf_common.h"
 
-/* vignat/nat_config.h:5-31 */
+/* vigfw/fw_config.h:9-24 */
 struct nf_config {
-  uint16_t lan_main_device;
   uint16_t wan_device;
-  uint32_t external_addr;
   struct rte_ether_addr *device_macs;
   struct rte_ether_addr *endpoint_macs;
-  uint16_t start_port;
   uint32_t expiration_time;
   uint32_t max_flows;
 };
@@ -33,39 +25,23 @@ void nf_config_usage(void) {
          "\t--eth-dest <device>,<mac>: MAC address of the endpoint linked to "
          "a device.\n"
          "\t--expire <time>: flow expiration time (us).\n"
-         "\t--extip <ip>: external IP address.\n"
-         "\t--lan-dev <device>: set device to be the main LAN device (for "
-         "non-NAT).\n"
          "\t--max-flows <n>: flow table capacity.\n"
-         "\t--starting-port <n>: start of the port range for external ports.\n"
          "\t--wan <device>: set device to be the external one.\n");
 }
 
-/* nf_parse_ipv4addr (nf-parse.h:21-32) */
-static bool parse_ipv4(const char *s, uint32_t *out) {
-  uint8_t a, b, c, d;
-  if (sscanf(s, "%hhu.%hhu.%hhu.%hhu", &a, &b, &c, &d) != 4) return false;
-  *out = ((uint32_t)a << 24) | ((uint32_t)b << 16) | ((uint32_t)c << 8) | d;
-  return true;
-}
-
-/* vignat/nat_config.c:17-106 */
+/* vigfw/fw_config.c:17-82 */
 void nf_config_init(int argc, char **argv) {
   uint16_t nb = nb_devices();
   struct option long_options[] = {{"eth-dest", required_argument, NULL, 'm'},
                                   {"expire", required_argument, NULL, 't'},
-                                  {"extip", required_argument, NULL, 'i'},
-                                  {"lan-dev", required_argument, NULL, 'l'},
                                   {"max-flows", required_argument, NULL, 'f'},
-                                  {"starting-port", required_argument, NULL, 's'},
                                   {"wan", required_argument, NULL, 'w'},
                                   {NULL, 0, NULL, 0}};
   config.device_macs = calloc(nb, sizeof(struct rte_ether_addr));
   config.endpoint_macs = calloc(nb, sizeof(struct rte_ether_addr));
   for (uint16_t d = 0; d < nb; d++) device_mac(d, &config.device_macs[d]);
   int opt;
-  while ((opt = getopt_long(argc, argv, "m:e:t:i:l:f:p:s:w:", long_options,
-                            NULL)) != EOF) {
+  while ((opt = getopt_long(argc, argv, "m:t:f:w:", long_options, NULL)) != EOF) {
     unsigned device;
     switch (opt) {
       case 'm':
@@ -81,22 +57,10 @@ void nf_config_init(int argc, char **argv) {
         if (config.expiration_time == 0)
           PARSE_ERROR("Expiration time must be strictly positive.\n");
         break;
-      case 'i':
-        if (!parse_ipv4(optarg, &config.external_addr))
-          PARSE_ERROR("Invalid external IP address: %s\n", optarg);
-        break;
-      case 'l':
-        config.lan_main_device = (uint16_t)parse_int(optarg, "lan-dev", '\0');
-        if (config.lan_main_device >= nb)
-          PARSE_ERROR("Main LAN device does not exist.\n");
-        break;
       case 'f':
         config.max_flows = (uint32_t)parse_int(optarg, "max-flows", '\0');
         if (config.max_flows <= 0)
           PARSE_ERROR("Flow table size must be strictly positive.\n");
-        break;
-      case 's':
-        config.start_port = (uint16_t)parse_int(optarg, "start-port", '\0');
         break;
       case 'w':
         config.wan_device = (uint16_t)parse_int(optarg, "wan-dev", '\0');
@@ -109,38 +73,29 @@ void nf_config_init(int argc, char **argv) {
   optind = 1; /* reset getopt */
 }
 
+/* vigfw/fw_config.c:94-115 */
 void nf_config_print(void) {
   uint16_t nb = nb_devices();
-  printf("\n--- NAT Config ---\n\n");
-  printf("Main LAN device (only relevant for NOP): %" PRIu16 "\n",
-         config.lan_main_device);
+  printf("\n--- FW Config ---\n\n");
   printf("WAN device: %" PRIu16 "\n", config.wan_device);
-  uint32_t a = config.external_addr;
-  printf("External IP: %u.%u.%u.%u\n", a & 0xFF, (a >> 8) & 0xFF,
-         (a >> 16) & 0xFF, (a >> 24) & 0xFF); /* nf-util.c:95-111 */
   for (uint16_t d = 0; d < nb; d++) {
-    const uint8_t *m = config.device_macs[d].addr_bytes;
-    const uint8_t *e = config.endpoint_macs[d].addr_bytes;
-    printf("Device %" PRIu16 " own-mac: %02X:%02X:%02X:%02X:%02X:%02X, "
-           "end-mac: %02X:%02X:%02X:%02X:%02X:%02X\n",
-           d, m[0], m[1], m[2], m[3], m[4], m[5], e[0], e[1], e[2], e[3], e[4],
-           e[5]);
+    printf("Device %" PRIu16 " own-mac: ", d);
+    print_mac(config.device_macs[d].addr_bytes);
+    printf(", end-mac: ");
+    print_mac(config.endpoint_macs[d].addr_bytes);
+    printf("\n");
   }
-  printf("Starting port: %" PRIu16 "\n", config.start_port);
   printf("Expiration time: %" PRIu32 "us\n", config.expiration_time);
   printf("Max flows: %" PRIu32 "\n", config.max_flows);
   printf("\n--- --- ------ ---\n\n");
 }
 
-/* nat_main.c:14-20: allocate the flow manager; false on failure */
+/* fw_main.c:14-19: allocate the flow manager; false on failure */
 bool nf_init(void) {
-  vp_nat_config c;
+  vp_fw_config c;
   memset(&c, 0, sizeof c);
   uint16_t nb = nb_devices();
   c.wan_device = config.wan_device;
-  c.lan_main_device = config.lan_main_device;
-  c.start_port = config.start_port;
-  c.external_addr = config.external_addr;
   c.expiration_time = config.expiration_time;
   c.max_flows = config.max_flows;
   c.n_devices = nb;
@@ -151,10 +106,10 @@ bool nf_init(void) {
   }
   if (g_ctx) vp_destroy(g_ctx);
   g_ctx = NULL;
-  return vp_nat_create(&c, shim_gpu(), &g_ctx) == VP_OK;
+  return vp_fw_create(&c, shim_gpu(), &g_ctx) == VP_OK;
 }
 
-/* nat_main.c:22-109 for one packet */
+/* fw_main.c:21-80 for one packet */
 int nf_process(uint16_t device, uint8_t *buffer, uint16_t packet_length,
                vigor_time_t now) {
   return shim_process_one(device, buffer, packet_length, now);

@@ -30,6 +30,9 @@ int bridge_static_build(const vp_bridge_config *cfg, std::vector<Bucket> &bk,
 int lb_process_device(vp_ctx *c, const vp_dev_batch *b);
 void build_lb_tables(std::vector<uint32_t> &tab);
 void lb_fill_cht(uint32_t height, uint32_t bcap, std::vector<uint32_t> &cht);
+int fw_process_device(vp_ctx *c, const vp_dev_batch *b);
+void build_fw_tables(std::vector<uint32_t> &tab);
+int fw_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *keys, uint32_t *int_dev);
 int lb_dump(vp_ctx *c, uint8_t *f_alloc, int64_t *f_ts, uint8_t *f_keys,
             uint32_t *f_backend, uint8_t *b_alloc, int64_t *b_ts, uint32_t *b_ip,
             uint8_t *b_mac, uint16_t *b_nic);
@@ -210,6 +213,20 @@ static int lb_init(vp_ctx *c, const vp_lb_config *cfg) {
     dm[2 * d + 1] = m[2] | (m[3] << 8) | (m[4] << 16) | ((uint32_t)m[5] << 24);
   }
   VP_TRY(upload(&c->dmacw, dm));
+  return 0;
+}
+
+static int fw_init(vp_ctx *c, const vp_fw_config *cfg) {
+  c->kind = KIND_FW;
+  c->fw = *cfg;
+  VP_TRY(tbl_alloc(c, c->ft, cfg->max_flows));
+  std::vector<uint32_t> tab;
+  build_fw_tables(tab);
+  VP_TRY(upload(&c->crc_tab, tab));
+  std::vector<uint32_t> mw(3 * VP_MAX_DEVICES, 0);
+  for (int d = 0; d < cfg->n_devices; d++)
+    mac_words(cfg->endpoint_macs[d], cfg->device_macs[d], &mw[3 * d]);
+  VP_TRY(upload(&c->macw, mw));
   return 0;
 }
 
@@ -441,6 +458,24 @@ int vp_lb_create(const vp_lb_config *cfg, int gpu, vp_ctx **out) {
   return 0;
 }
 
+int vp_fw_create(const vp_fw_config *cfg, int gpu, vp_ctx **out) {
+  if (!cfg || !out) return VP_EINVAL;
+  // map.c:73 (CAPACITY_POW2); fw_config.c:39-75: devices, --wan < devices
+  if (!is_pow2(cfg->max_flows) || cfg->max_flows > (1u << 30) ||
+      cfg->n_devices == 0 || cfg->n_devices > VP_MAX_DEVICES ||
+      cfg->wan_device >= cfg->n_devices)
+    return VP_EINVAL;
+  vp_ctx *c = new vp_ctx();
+  int rc = ctx_common(c, gpu);
+  if (!rc) rc = fw_init(c, cfg);
+  if (rc) {
+    free_all(c);
+    return rc;
+  }
+  *out = c;
+  return 0;
+}
+
 void vp_destroy(vp_ctx *ctx) { free_all(ctx); }
 
 int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
@@ -463,6 +498,9 @@ int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
       break;
     case KIND_LB:
       rc = lb_process_device(c, b);
+      break;
+    case KIND_FW:
+      rc = fw_process_device(c, b);
       break;
     default:
       break;
@@ -554,6 +592,14 @@ int vp_bridge_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *macs,
     port[i] = (uint16_t)k[2];
   }
   return 0;
+}
+
+int vp_fw_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *keys,
+               uint32_t *int_dev) {
+  if (!c || c->kind != KIND_FW || !alloc || !ts || !keys || !int_dev)
+    return VP_EINVAL;
+  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  return fw_dump(c, alloc, ts, keys, int_dev);
 }
 
 int64_t vp_live_count(vp_ctx *c) {

@@ -67,35 +67,46 @@ __host__ __device__ __forceinline__ uint32_t home_bucket(uint32_t h,
 // One bucket (key words k0-k2, entry indices ix) against `key`, entries in
 // order: the index on a match; kNone with *done on an empty entry (the probe
 // path ends there); kNone with !*done when the probe continues in the next
-// bucket.
+// bucket. Word 3 is compared under M3: tables that keep a per-index value in
+// the key's padding bytes (viglb's backend, vigfw's internal device) match
+// on the protocol byte only.
+template <uint32_t M3 = 0xFFFFFFFFu>
 __device__ __forceinline__ uint32_t bucket_match(uint4 k0, uint4 k1, uint4 k2,
                                                  uint4 ix, const uint32_t key[4],
-                                                 bool *done) {
+                                                 bool *done, uint32_t *w3 = nullptr) {
   *done = true;
   if (ix.x == kEmpty) return kNone;
   if (ix.x != kTomb && k0.x == key[0] && k0.y == key[1] && k0.z == key[2] &&
-      k0.w == key[3])
+      ((k0.w ^ key[3]) & M3) == 0) {
+    if (w3) *w3 = k0.w;
     return ix.x;
+  }
   if (ix.y == kEmpty) return kNone;
   if (ix.y != kTomb && k1.x == key[0] && k1.y == key[1] && k1.z == key[2] &&
-      k1.w == key[3])
+      ((k1.w ^ key[3]) & M3) == 0) {
+    if (w3) *w3 = k1.w;
     return ix.y;
+  }
   if (ix.z == kEmpty) return kNone;
   if (ix.z != kTomb && k2.x == key[0] && k2.y == key[1] && k2.z == key[2] &&
-      k2.w == key[3])
+      ((k2.w ^ key[3]) & M3) == 0) {
+    if (w3) *w3 = k2.w;
     return ix.z;
+  }
   *done = false;
   return kNone;
 }
 
 // The rest of a probe path, from bucket b for at most `steps` buckets.
+template <uint32_t M3 = 0xFFFFFFFFu>
 __device__ __forceinline__ uint32_t tbl_probe_from(const TableDev &t, uint32_t b,
                                                    const uint32_t key[4],
-                                                   uint32_t steps) {
+                                                   uint32_t steps,
+                                                   uint32_t *w3 = nullptr) {
   for (uint32_t i = 0; i < steps; i++) {
     const uint4 *q = reinterpret_cast<const uint4 *>(t.bk + b);
     bool done;
-    const uint32_t r = bucket_match(q[0], q[1], q[2], q[3], key, &done);
+    const uint32_t r = bucket_match<M3>(q[0], q[1], q[2], q[3], key, &done, w3);
     if (done) return r;
     b = (b + 1) & t.bmask;
   }
@@ -104,9 +115,12 @@ __device__ __forceinline__ uint32_t tbl_probe_from(const TableDev &t, uint32_t b
 
 // map_get (find_key, map-impl-pow2.c:629-732) on the device table. Returns
 // the index or kNone.
+template <uint32_t M3 = 0xFFFFFFFFu>
 __device__ __forceinline__ uint32_t tbl_probe(const TableDev &t, uint32_t h,
-                                              const uint32_t key[4]) {
-  return tbl_probe_from(t, home_bucket(h, t.bmask, t.mix), key, t.bmask + 1);
+                                              const uint32_t key[4],
+                                              uint32_t *w3 = nullptr) {
+  return tbl_probe_from<M3>(t, home_bucket(h, t.bmask, t.mix), key, t.bmask + 1,
+                            w3);
 }
 
 // Key words of an allocated index's entry.

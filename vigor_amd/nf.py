@@ -12,7 +12,8 @@ import ctypes as C
 
 import numpy as np
 
-from . import (BridgeConfigC, DevBatchC, LbConfigC, NatConfigC, _check, lib)
+from . import (BridgeConfigC, DevBatchC, FwConfigC, LbConfigC, NatConfigC,
+               _check, lib)
 
 
 def _dptr(t):
@@ -176,3 +177,25 @@ class Lb(NfBase):
                "vp_lb_dump")
         return ((fa, ft, fk.reshape(nf_, 16), fb),
                 (ba, bt, bi, bm.reshape(nb, 6), bn))
+
+
+class Fw(NfBase):
+    kind = "fw"
+
+    def __init__(self, cfg: FwConfigC, gpu: int = 0, libpath=None):
+        super().__init__(libpath)
+        self.cfg = cfg
+        _check(self.L.vp_fw_create(C.byref(cfg), gpu, C.byref(self.h)),
+               "vp_fw_create")
+
+    def dump(self):
+        """By flow index: alloc, ts, FlowId bytes (16), int_devices."""
+        n = self.cfg.max_flows
+        alloc = np.zeros(n, np.uint8)
+        ts = np.zeros(n, np.int64)
+        keys = np.zeros(n * 16, np.uint8)
+        dev = np.zeros(n, np.uint32)
+        P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
+        _check(self.L.vp_fw_dump(self.h, P(alloc), P(ts), P(keys), P(dev)),
+               "vp_fw_dump")
+        return alloc, ts, keys.reshape(n, 16), dev

@@ -120,6 +120,29 @@ def nat_lan_trace(n_packets: int, n_flows: int, order: str = "rr",
     return frames, lens, in_dev, now
 
 
+def fw_trace(n_packets: int, n_flows: int, order: str = "rr",
+             slot: int = 64, lan_dev: int = 0, wan_dev: int = 1,
+             reply_every: int = 0, start: int = 0, seed: int = 0x5EED):
+    """vigfw trace: LAN->WAN packets of the vignat flows (flow i: 10.0.0.0 +
+    (i >> 16) : i & 0xFFFF -> 0.0.0.0:0); with reply_every = k, every k-th
+    packet is instead the WAN->LAN reply of its flow (addresses and ports
+    swapped, arriving on wan_dev)."""
+    fl = flow_order(n_packets, n_flows, order, seed, start)
+    a_ip = ip4(10, 0, 0, 0) + (fl >> 16)
+    a_port = fl & 0xFFFF
+    z = np.zeros_like(fl)
+    in_dev = np.full(n_packets, lan_dev, dtype=np.uint16)
+    rep = np.zeros(n_packets, bool)
+    if reply_every:
+        rep = (np.arange(start, start + n_packets) % reply_every) == reply_every - 1
+        in_dev[rep] = wan_dev
+    frames, lens = udp_frames(np.where(rep, z, a_ip), np.where(rep, a_ip, z),
+                              np.where(rep, z, a_port), np.where(rep, a_port, z),
+                              slot=slot)
+    now = (NOW0 + np.arange(start, start + n_packets, dtype=np.int64))
+    return frames, lens, in_dev, now
+
+
 def bridge_trace(n_packets: int, n_stations: int, slot: int = 64,
                  start: int = 0, flood_pattern: bool = False):
     """vigbridge config 3: frame p from station p mod N (on port (k & 1)) to
