@@ -23,7 +23,7 @@ def main():
     B, NF = 1 << 24, 1 << 20
     dev = torch.device("cuda:0")
     variants = {"full": (None, {}), "perlane": (None, {"VIGPATH_COALESCED": "0"})}
-    for v in ("NOPROBE", "NOINLINE", "NT", "NOFRAME"):
+    for v in ("NOPROBE", "NOINLINE", "NT", "NOFRAME", "STRIDED"):
         p = os.path.join(ROOT, "vigor_amd", "abl", "libvigpath_%s.so" % v)
         if os.path.exists(p):  # NOFRAME lives in the per-lane kernel
             variants[v] = (p, {"VIGPATH_COALESCED": "0"} if v == "NOFRAME"

@@ -214,7 +214,11 @@ __device__ __forceinline__ void wave_lds_sync() {
 // memory counters drain in issue order (MI355X_MICROARCH.md §Per-instruction
 // cycle constants), so rows can be consumed while the prefetch is still in
 // flight and the frame stream's HBM latency hides under the probes. The grid
-// is persistent (resident_grid()), each wave striding over tiles.
+// is persistent (resident_grid()); each block owns one contiguous range of
+// tiles, its four waves interleaved over it: measured 12 % faster than
+// dealing tiles round-robin over all waves (tools/ablate.py STRIDED), as
+// every block streams its own DRAM pages and its packets' table rows stay
+// near each other in its XCD's L2.
 template <class Issue, class Finish>
 __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
                                                const uint16_t *len,
@@ -226,7 +230,6 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t first = p0 & ~63u;
   const uint32_t tiles = (p1 - first + 63) / 64;
-  const uint32_t nwaves = gridDim.x * 4;
   uint4 r[4];
   uint32_t m_in = 0, m_len = 0;
   auto fetch = [&](uint32_t tile) {
@@ -242,9 +245,16 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
     m_in = p < n_all ? in_dev[p] : 0u;
     m_len = p < n_all ? len[p] : 0u;
   };
+#ifdef VP_ABL_STRIDED  // diagnostic: tiles dealt round-robin over all waves
   uint32_t tile = blockIdx.x * 4 + wv;
-  if (tile < tiles) fetch(tile);
-  for (; tile < tiles; tile += nwaves) {
+  const uint32_t tend = tiles, tstep = gridDim.x * 4;
+#else
+  const uint32_t per_b = (tiles + gridDim.x - 1) / gridDim.x;
+  uint32_t tile = blockIdx.x * per_b + wv;
+  const uint32_t tend = min(tiles, blockIdx.x * per_b + per_b), tstep = 4;
+#endif
+  if (tile < tend) fetch(tile);
+  for (; tile < tend; tile += tstep) {
     const uint32_t tb = first + tile * 64;
     uint4 *g = reinterpret_cast<uint4 *>(frames + (size_t)tb * 64);
 #pragma unroll
@@ -273,7 +283,7 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
                             : make_uint4(0, 0, 0, 0);
       }
     }
-    if (tile + nwaves < tiles) fetch(tile + nwaves);
+    if (tile + tstep < tend) fetch(tile + tstep);
     uint4 row[4] = {};
     if (rows) {  // S is free: f is in registers
       wave_lds_sync();

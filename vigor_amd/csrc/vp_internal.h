@@ -25,6 +25,11 @@ namespace vp {
 
 int hip_fail(hipError_t e, const char *what, const char *file, int line);
 
+// Wait for `s` to drain by polling (a packet-processing host thread polls,
+// as DPDK's lcores do): a blocking wait adds tens of microseconds of wake-up
+// latency to every batch's control-block read-back.
+hipError_t stream_wait(hipStream_t s);
+
 struct Comm;  // vp_comm.hip: collectives between the ranks of one NF
 constexpr int kMaxRanks = 64;
 
@@ -62,6 +67,8 @@ struct FlowTable {
   uint32_t *lastg = nullptr;  // touch-reduce partial maxima (small tables)
   Ctl *ctl = nullptr;
   Ctl h_ctl{};                     // last copy read back
+  Ctl *h_pin = nullptr;            // page-locked landing buffer for h_ctl
+  uint32_t *ttotal = nullptr;  // touch-reduce entry count (device)
   uint64_t ts_floor = UINT64_MAX;  // lower bound of min ts over live indices
   // expiry workspace (sized cap)
   uint64_t *ekey = nullptr, *ekey2 = nullptr;

@@ -37,6 +37,13 @@ int lb_dump(vp_ctx *c, uint8_t *f_alloc, int64_t *f_ts, uint8_t *f_keys,
             uint32_t *f_backend, uint8_t *b_alloc, int64_t *b_ts, uint32_t *b_ip,
             uint8_t *b_mac, uint16_t *b_nic);
 
+hipError_t stream_wait(hipStream_t s) {
+  hipError_t e;
+  while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+  }
+  return e;
+}
+
 static bool is_pow2(uint32_t v) { return v && !(v & (v - 1)); }
 
 template <class T>

@@ -75,9 +75,10 @@ int cub_reserve(vp_ctx *c, size_t bytes) {
 }
 
 int read_ctl(vp_ctx *c, FlowTable &t) {
-  VP_HIP(hipMemcpyAsync(&t.h_ctl, t.ctl, sizeof(Ctl), hipMemcpyDeviceToHost,
+  VP_HIP(hipMemcpyAsync(t.h_pin, t.ctl, sizeof(Ctl), hipMemcpyDeviceToHost,
                         c->stream));
-  VP_HIP(hipStreamSynchronize(c->stream));
+  VP_HIP(stream_wait(c->stream));
+  t.h_ctl = *t.h_pin;
   return 0;
 }
 
@@ -117,6 +118,8 @@ int tbl_alloc(vp_ctx *c, FlowTable &t, uint32_t cap) {
   VP_TRY(dalloc(&t.stack, cap));
   VP_TRY(dalloc(&t.lastg, cap));
   VP_TRY(dalloc(&t.ctl, 1));
+  VP_HIP(hipHostMalloc((void **)&t.h_pin, sizeof(Ctl), hipHostMallocDefault));
+  VP_TRY(dalloc(&t.ttotal, 1));
   VP_TRY(dalloc(&t.ekey, cap));
   VP_TRY(dalloc(&t.ekey2, cap));
   VP_TRY(dalloc(&t.eidx, cap));
@@ -136,6 +139,8 @@ void tbl_free(FlowTable &t) {
                   t.birth, t.stack,   t.lastg,   t.ctl,   t.ekey,
                   t.ekey2, t.eidx,    t.eidx2};
   for (void *p : ptrs) hipFree(p);
+  hipFree(t.ttotal);
+  if (t.h_pin) hipHostFree(t.h_pin);
   t = FlowTable{};
 }
 
@@ -295,14 +300,19 @@ int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
 }
 
 // ---------------------------------------------------------- touch log --
-// The index space is cut into chunks of 2^kChunkBits indices (one LDS tile of
-// last-toucher positions per chunk). Pass 1 counts each log span's touches
-// per chunk, an exclusive scan turns the counts into (chunk, span) offsets,
-// pass 2 scatters (index-in-chunk, position) pairs into chunk order, pass 3
+// The index space is cut into chunks of 2^cb indices (one LDS tile of
+// last-toucher positions per chunk; cb is chosen per table so that there are
+// about 512 chunks, enough blocks to fill the chip in pass 3). The log is cut
+// into spans of `span` entries. Pass 1 counts each span's touches per chunk,
+// an exclusive scan turns the counts into (chunk, span) offsets, pass 2
+// scatters one packed word per touch into chunk order:
+//   (index within chunk) << 20 | (position within span)
+// and pass 3 recovers each word's span from the chunk's span offsets (LDS),
 // keeps the largest position per index with LDS atomics and writes ts/tseq.
-// About 24 B of streaming traffic per packet, no global atomics.
-constexpr uint32_t kChunkBits = 12;
-constexpr uint32_t kSpan = 16384;  // log entries per pass-1/2 block
+// About 16 B of streaming traffic per packet, no global atomics.
+constexpr uint32_t kPosBits = 20;  // position within a span (span <= 2^20)
+constexpr uint32_t kMaxChunkBits = 12;
+constexpr uint32_t kMaxSpans = 8192;  // pass-3 LDS offset table (+1)
 
 // Lanes holding chunk `ch` (valid `v`) that share the first valid lane's
 // chunk are served by one LDS atomic (traffic with locality would otherwise
@@ -325,13 +335,14 @@ __device__ __forceinline__ uint32_t chunk_reserve(uint32_t *ctr, uint32_t ch,
 }
 
 __global__ __launch_bounds__(256) void touch_count(const uint32_t *log,
-                                                   uint32_t n, uint32_t nchunks,
+                                                   uint32_t n, uint32_t span,
+                                                   uint32_t cb, uint32_t nchunks,
                                                    uint32_t nspans,
                                                    uint32_t *hist) {
   extern __shared__ uint32_t cnt[];
   for (uint32_t b = threadIdx.x; b < nchunks; b += blockDim.x) cnt[b] = 0;
   __syncthreads();
-  const uint32_t s0 = blockIdx.x * kSpan, s1 = min(n, s0 + kSpan);
+  const uint32_t s0 = blockIdx.x * span, s1 = min(n, s0 + span);
   for (uint32_t j = s0 + threadIdx.x; j < s1; j += 4 * blockDim.x) {
     uint32_t k[4];
 #pragma unroll
@@ -340,8 +351,7 @@ __global__ __launch_bounds__(256) void touch_count(const uint32_t *log,
       k[u] = jj < s1 ? log[jj] : kNone;
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++)
-      chunk_reserve(cnt, k[u] >> kChunkBits, k[u] != kNone);
+    for (int u = 0; u < 4; u++) chunk_reserve(cnt, k[u] >> cb, k[u] != kNone);
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nchunks; b += blockDim.x)
@@ -349,15 +359,17 @@ __global__ __launch_bounds__(256) void touch_count(const uint32_t *log,
 }
 
 __global__ __launch_bounds__(256) void touch_scatter(const uint32_t *log,
-                                                     uint32_t n, uint32_t nchunks,
+                                                     uint32_t n, uint32_t span,
+                                                     uint32_t cb, uint32_t nchunks,
                                                      uint32_t nspans,
                                                      const uint32_t *off,
-                                                     uint2 *out) {
+                                                     uint32_t *out) {
   extern __shared__ uint32_t pos[];
   for (uint32_t b = threadIdx.x; b < nchunks; b += blockDim.x)
     pos[b] = off[(size_t)b * nspans + blockIdx.x];
   __syncthreads();
-  const uint32_t s0 = blockIdx.x * kSpan, s1 = min(n, s0 + kSpan);
+  const uint32_t cmask = (1u << cb) - 1;
+  const uint32_t s0 = blockIdx.x * span, s1 = min(n, s0 + span);
   for (uint32_t j = s0 + threadIdx.x; j < s1; j += 4 * blockDim.x) {
     uint32_t k[4];
 #pragma unroll
@@ -368,9 +380,8 @@ __global__ __launch_bounds__(256) void touch_scatter(const uint32_t *log,
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const bool v = k[u] != kNone;
-      const uint32_t at = chunk_reserve(pos, k[u] >> kChunkBits, v);
-      if (v)
-        out[at] = make_uint2(k[u] & ((1u << kChunkBits) - 1), j + u * blockDim.x);
+      const uint32_t at = chunk_reserve(pos, k[u] >> cb, v);
+      if (v) out[at] = ((k[u] & cmask) << kPosBits) | (j + u * blockDim.x - s0);
     }
   }
 }
@@ -380,39 +391,56 @@ __global__ void touch_total(const uint32_t *hist, const uint32_t *off,
   if (threadIdx.x == 0 && blockIdx.x == 0) *total = off[nh - 1] + hist[nh - 1];
 }
 
-// One block per (chunk, part). With one part per chunk the block owns its
-// indices and writes ts/tseq; with several (small tables: too few chunks to
-// fill the chip) the parts combine their maxima in `lastg` and
-// touch_finalize writes ts/tseq.
+// One block per (chunk, part); the part's words are taken in groups of 64
+// consecutive ones per wave instruction. A group's first span is found by a
+// wave-uniform binary search over the chunk's span offsets (LDS); each lane
+// then steps forward over the span boundaries inside the group. With one part
+// per chunk the block owns its indices and writes ts/tseq; with several
+// (small tables: too few chunks to fill the chip) the parts combine their
+// maxima in `lastg` and touch_finalize writes ts/tseq.
 __global__ __launch_bounds__(1024) void touch_reduce_k2(
-    const uint2 *in, const uint32_t *off, uint32_t nspans, uint32_t nchunks,
-    uint32_t split, const uint32_t *total, uint32_t cap, uint32_t p0,
-    NowSpec now, uint64_t seq_base, uint64_t *ts, uint64_t *tseq,
-    uint32_t *lastg) {
-  __shared__ uint32_t last[1u << kChunkBits];  // 1 + last position, 0 = none
+    const uint32_t *in, const uint32_t *off, uint32_t span, uint32_t nspans,
+    uint32_t cb, uint32_t nchunks, uint32_t split, const uint32_t *total,
+    uint32_t cap, uint32_t p0, NowSpec now, uint64_t seq_base, uint64_t *ts,
+    uint64_t *tseq, uint32_t *lastg) {
+  __shared__ uint32_t last[1u << kMaxChunkBits];  // 1 + last position, 0 = none
+  __shared__ uint32_t so[kMaxSpans + 1];          // this chunk's span offsets
   const uint32_t ch = blockIdx.x / split, part = blockIdx.x % split;
-  for (uint32_t i = threadIdx.x; i < (1u << kChunkBits); i += blockDim.x)
-    last[i] = 0;
+  const uint32_t csize = 1u << cb;
+  for (uint32_t i = threadIdx.x; i < csize; i += blockDim.x) last[i] = 0;
+  for (uint32_t s = threadIdx.x; s < nspans; s += blockDim.x)
+    so[s] = off[(size_t)ch * nspans + s];
+  if (threadIdx.x == 0)
+    so[nspans] = ch + 1 < nchunks ? off[(size_t)(ch + 1) * nspans] : *total;
   __syncthreads();
-  const uint32_t ca = off[(size_t)ch * nspans];
-  const uint32_t cb = ch + 1 < nchunks ? off[(size_t)(ch + 1) * nspans] : *total;
-  const uint32_t per = (cb - ca + split - 1) / split;
-  const uint32_t a = min(cb, ca + part * per), b = min(cb, a + per);
-  for (uint32_t j = a + threadIdx.x; j < b; j += 4 * blockDim.x) {
-    uint2 e[4];
+  const uint32_t ca = so[0], ce = so[nspans];
+  const uint32_t per = (ce - ca + split - 1) / split;
+  const uint32_t a = min(ce, ca + part * per), b = min(ce, a + per);
+  const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const uint32_t pmask = (1u << kPosBits) - 1;
+  constexpr uint32_t kU = 4;  // groups in flight per wave
+  for (uint32_t g0 = a + (threadIdx.x >> 6) * 64; g0 < b; g0 += kU * nw * 64) {
+    uint32_t e[kU], sp[kU];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const uint32_t jj = j + u * blockDim.x;
-      e[u] = jj < b ? in[jj] : make_uint2(0, 0xFFFFFFFFu);
+    for (uint32_t u = 0; u < kU; u++) {
+      const uint32_t j0 = g0 + u * nw * 64, jj = j0 + lane;
+      e[u] = jj < b ? in[jj] : kNone;
+      uint32_t lo = 0, hi = nspans;  // largest s with so[s] <= j0 (uniform)
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (so[mid] <= j0) lo = mid; else hi = mid;
+      }
+      while (lo + 1 < nspans && so[lo + 1] <= jj) lo++;
+      sp[u] = lo;
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++)
-      if (e[u].y != 0xFFFFFFFFu) atomicMax(&last[e[u].x], e[u].y + 1);
+    for (uint32_t u = 0; u < kU; u++)
+      if (e[u] != kNone)
+        atomicMax(&last[e[u] >> kPosBits], sp[u] * span + (e[u] & pmask) + 1);
   }
   __syncthreads();
-  const uint32_t base = ch << kChunkBits;
-  for (uint32_t i = threadIdx.x; i < (1u << kChunkBits) && base + i < cap;
-       i += blockDim.x) {
+  const uint32_t base = ch << cb;
+  for (uint32_t i = threadIdx.x; i < csize && base + i < cap; i += blockDim.x) {
     const uint32_t l = last[i];
     if (!l) continue;
     if (split > 1) {
@@ -443,11 +471,21 @@ int tbl_touch_reduce(vp_ctx *c, FlowTable &t, const uint32_t *log, uint32_t p0,
   Workspace &w = c->ws;
   const uint32_t n = p1 - p0;
   if (n == 0) return 0;
-  const uint32_t nchunks = (t.cap + (1u << kChunkBits) - 1) >> kChunkBits;
-  const uint32_t nspans = (n + kSpan - 1) / kSpan;
+  // ~512 chunks of 2^cb indices (64 <= 2^cb <= 4096)
+  uint32_t cb = 6;
+  while (cb < kMaxChunkBits && ((uint64_t)t.cap >> (cb + 1)) >= 512) cb++;
+  const uint32_t nchunks = (t.cap + (1u << cb) - 1) >> cb;
+  // spans of >= 16384 entries, at most kMaxSpans of them
+  uint32_t span = 16384;
+  while ((uint64_t)span * kMaxSpans < n) span <<= 1;
+  if (span > (1u << kPosBits)) return VP_ENOTSUP;
+  const uint32_t nspans = (n + span - 1) / span;
   const uint64_t nh = (uint64_t)nchunks * nspans;
+  const size_t lds = sizeof(uint32_t) * nchunks;
+  if (lds > 64 * 1024) return VP_ENOTSUP;
+  hipStream_t ts = c->stream;
   if (nh > w.hist_cap) {
-    VP_HIP(hipStreamSynchronize(c->stream));
+    VP_HIP(hipStreamSynchronize(ts));
     hipFree(w.hist);
     hipFree(w.hoff);
     w.hist = w.hoff = nullptr;
@@ -456,29 +494,28 @@ int tbl_touch_reduce(vp_ctx *c, FlowTable &t, const uint32_t *log, uint32_t p0,
     VP_TRY(dalloc(&w.hoff, nh));
     w.hist_cap = nh;
   }
-  uint32_t *hist = w.hist, *off = w.hoff;
-  uint2 *pairs = reinterpret_cast<uint2 *>(w.mkey);  // 4 words per packet
-  const size_t lds = sizeof(uint32_t) * nchunks;
-  if (lds > 64 * 1024) return VP_ENOTSUP;
-  touch_count<<<nspans, 256, lds, c->stream>>>(log + p0, n, nchunks, nspans, hist);
   size_t need = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, need, hist, off, (int)nh, c->stream);
+  hipcub::DeviceScan::ExclusiveSum(nullptr, need, w.hist, w.hoff, (int)nh, ts);
   VP_TRY(cub_reserve(c, need));
+  uint32_t *hist = w.hist, *off = w.hoff;
+  uint32_t *pairs = w.mkey;  // 4 words per packet available, 1 used
+  touch_count<<<nspans, 256, lds, ts>>>(log + p0, n, span, cb, nchunks, nspans,
+                                        hist);
   VP_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub_tmp, w.cub_bytes, hist, off,
-                                          (int)nh, c->stream));
-  touch_scatter<<<nspans, 256, lds, c->stream>>>(log + p0, n, nchunks, nspans, off,
-                                                 pairs);
-  touch_total<<<1, 64, 0, c->stream>>>(hist, off, (uint32_t)nh, &t.ctl->aux_count);
+                                          (int)nh, ts));
+  touch_scatter<<<nspans, 256, lds, ts>>>(log + p0, n, span, cb, nchunks, nspans,
+                                          off, pairs);
+  touch_total<<<1, 64, 0, ts>>>(hist, off, (uint32_t)nh, t.ttotal);
   // enough blocks to cover the chip, splitting chunks when there are few
   const uint32_t split = std::max<uint32_t>(1, 512 / nchunks);
   if (split > 1)
-    VP_HIP(hipMemsetAsync(t.lastg, 0, sizeof(uint32_t) * (size_t)t.cap, c->stream));
-  touch_reduce_k2<<<nchunks * split, 1024, 0, c->stream>>>(
-      pairs, off, nspans, nchunks, split, &t.ctl->aux_count, t.cap, p0, now,
+    VP_HIP(hipMemsetAsync(t.lastg, 0, sizeof(uint32_t) * (size_t)t.cap, ts));
+  touch_reduce_k2<<<nchunks * split, 1024, 0, ts>>>(
+      pairs, off, span, nspans, cb, nchunks, split, t.ttotal, t.cap, p0, now,
       seq_base, t.ts, t.tseq, t.lastg);
   if (split > 1)
-    touch_finalize<<<grid_for(t.cap), 256, 0, c->stream>>>(t.lastg, t.cap, p0, now,
-                                                           seq_base, t.ts, t.tseq);
+    touch_finalize<<<grid_for(t.cap), 256, 0, ts>>>(t.lastg, t.cap, p0, now,
+                                                   seq_base, t.ts, t.tseq);
   VP_HIP(hipGetLastError());
   return 0;
 }
@@ -701,7 +738,7 @@ int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
         tabs[i].t->ts_floor = std::min<uint64_t>(tabs[i].t->ts_floor, (uint64_t)ta);
     a0 = b1;
   }
-  VP_HIP(hipStreamSynchronize(c->stream));
+  VP_HIP(stream_wait(c->stream));
   c->seq += n;
   c->last_now = t_last;
   c->last_ms = ms;
