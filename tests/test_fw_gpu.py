@@ -140,3 +140,16 @@ def test_rejects_bad_config():
     cfg = vigor_amd.fw_config_from_args(args, 2, DEV_MACS[:2])
     with pytest.raises(vigor_amd.VigpathError):
         vigor_amd.Fw(cfg)  # map_allocate rejects a non power of two
+
+
+@pytest.mark.parametrize("n_flows", [3, 5000])
+def test_touch_bins_steady_state(n_flows):
+    """vigfw steady state (LAN hits + WAN replies) through the touch bins
+    (and their overflow fallback for a hot flow set): state equals the
+    oracle's."""
+    fw, o = make_pair(max_flows=1 << 16)
+    fr, ln, dv, now = T.fw_trace(n_flows, n_flows)
+    check_batches(fw, o, fr, ln, dv, now, 64, [])
+    fr, ln, dv, now = T.fw_trace(30_000, n_flows, start=n_flows, reply_every=3)
+    check_batches(fw, o, fr, ln, dv, now, 64, [])
+    check_state(fw, o, 1 << 16)

@@ -177,3 +177,21 @@ def test_host_pipeline_chunks(pinned, monkeypatch):
     np.testing.assert_array_equal(out, exp_out)
     np.testing.assert_array_equal(got, exp)
     check_state(nat, o, 256)
+
+
+@pytest.mark.parametrize("n_flows,order", [(4096, "uniform"), (3, "rr"),
+                                          (1 << 16, "rr")])
+def test_touch_bins_steady_state(n_flows, order):
+    """Steady-state batches (every packet a hit) fold their touches through
+    the classify kernel's touch bins; a hot flow set overflows a bin slice
+    and the fold falls back to the full log. Timestamps and LRU state must
+    equal the oracle's either way."""
+    nat, o = make_pair(max_flows=1 << 17)
+    fr, ln, dv, now = T.nat_lan_trace(n_flows, n_flows)  # warm-up: allocate
+    check_batches(nat, o, fr, ln, dv, now, 64, [])
+    for j in range(2):
+        start = n_flows + j * 40_000
+        fr, ln, dv, now = T.nat_lan_trace(40_000, n_flows, order=order,
+                                          start=start, seed=j)
+        check_batches(nat, o, fr, ln, dv, now, 64, [], affine=order == "rr")
+        check_state(nat, o, 1 << 17)

@@ -23,7 +23,9 @@ def main():
     B, NF = 1 << 24, 1 << 20
     dev = torch.device("cuda:0")
     variants = {"full": (None, {}), "perlane": (None, {"VIGPATH_COALESCED": "0"})}
-    for v in ("NOPROBE", "NOINLINE", "NT", "NOFRAME", "STRIDED"):
+    variants["bpc3"] = (None, {"VIGPATH_BLOCKS_PER_CU": "3"})
+    variants["bpc2"] = (None, {"VIGPATH_BLOCKS_PER_CU": "2"})
+    for v in ("NOPROBE", "NOINLINE", "NT", "NOFRAME", "STRIDED", "XCD", "OCC5"):
         p = os.path.join(ROOT, "vigor_amd", "abl", "libvigpath_%s.so" % v)
         if os.path.exists(p):  # NOFRAME lives in the per-lane kernel
             variants[v] = (p, {"VIGPATH_COALESCED": "0"} if v == "NOFRAME"
@@ -34,9 +36,13 @@ def main():
     out = torch.zeros(B, dtype=torch.int16, device=dev)
     buf = torch.empty(B * 64, dtype=torch.uint8, device=dev)
     nfs = {}
-    for name, (path, env) in variants.items():
-        os.environ.pop("VIGPATH_COALESCED", None)
+    def use_env(env):  # read at context creation and at every launch
+        for k in ("VIGPATH_COALESCED", "VIGPATH_BLOCKS_PER_CU"):
+            os.environ.pop(k, None)
         os.environ.update(env)
+
+    for name, (path, env) in variants.items():
+        use_env(env)
         cfg = vigor_amd.nat_config_from_args(
             bench.NAT_ARGS + ["--max-flows", str(NF)], 2, bench.DEV_MACS)
         nat = vigor_amd.Nat(cfg, 0, libpath=path)
@@ -48,6 +54,7 @@ def main():
     start = B
     for r in range(rounds):
         for name, nat in nfs.items():
+            use_env(variants[name][1])
             bank.fill(buf, start)
             torch.cuda.synchronize()
             t0 = time.perf_counter()

@@ -193,6 +193,50 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Lanes holding counter `ch` (valid `v`) that share the first valid lane's
+// counter are served by one LDS atomic (traffic with locality would otherwise
+// serialise a wave on one counter); the rest add individually. Returns this
+// lane's reserved position.
+__device__ __forceinline__ uint32_t group_reserve(uint32_t *ctr, uint32_t ch,
+                                                  bool v) {
+  const uint64_t vm = __ballot(v);
+  if (!vm) return 0;
+  const uint32_t lead = __shfl(ch, __ffsll((unsigned long long)vm) - 1);
+  const bool grp = v && ch == lead;
+  const uint64_t same = __ballot(grp);
+  const uint32_t first = __ffsll((unsigned long long)same) - 1;
+  uint32_t base = 0;
+  if (grp && __lane_id() == first)
+    base = atomicAdd(&ctr[ch], (uint32_t)__popcll(same));
+  base = __shfl(base, first);
+  if (grp) return base + (uint32_t)__popcll(same & ((1ull << __lane_id()) - 1ull));
+  return v ? atomicAdd(&ctr[ch], 1u) : 0;
+}
+
+// Touch bins: besides the per-packet touch log, the 64-byte classify kernels
+// sort each touch (flow index i of packet p) into one of kBins bins while
+// classifying, so the timestamp fold needs a single pass (touch_bins_reduce,
+// vp_table.hip) instead of count + scan + scatter + reduce. Index i belongs
+// to bin (i >> 4) & 255, at in-bin position ((i >> 12) << 4) | (i & 15): runs
+// of 16 consecutive indices per bin, so sequential flow sets spread over all
+// bins and the fold writes whole 128-byte runs of ts. Each block appends to
+// its own fixed-size slice of every bin (LDS cursors); a slice that fills up
+// sets *ovf and the host folds the full log instead.
+constexpr uint32_t kBins = 256;
+struct TouchBins {
+  uint32_t *ent;  // [block][bin][cap] entries (in-bin << pbits | position); null = off
+  uint32_t *cnt;  // [block][bin] entries written
+  uint32_t *ovf;  // set when a slice overflowed
+  uint32_t cap, pbits;
+};
+__device__ __forceinline__ uint32_t bin_of(uint32_t i) { return (i >> 4) & (kBins - 1); }
+__device__ __forceinline__ uint32_t bin_local(uint32_t i) {
+  return ((i >> 12) << 4) | (i & 15u);
+}
+__device__ __forceinline__ uint32_t bin_index(uint32_t bin, uint32_t local) {
+  return ((local >> 4) << 12) | (bin << 4) | (local & 15u);
+}
+
 // Packets [p0, p1) of a batch of n_all 64-byte slots, in tiles of 64
 // consecutive packets per wave (256-thread blocks, 4 waves): every global
 // load/store instruction moves 1 KiB contiguous (lane l <-> bytes
@@ -204,9 +248,11 @@ __device__ __forceinline__ void wave_lds_sync() {
 //   pend = issue(p, f, in, len, mine)  parse, hash, issue any per-lane read;
 //                                      pend.row = the 64-byte table row
 //                                      (bucket) this packet needs, or kNone;
-//   mod  = finish(pend, row, p, f, in, len)
+//   mod  = finish(pend, row, p, f, in, len, touch)
 //                                      consume the row, rewrite f, return
-//                                      true when f must be written back.
+//                                      true when f must be written back;
+//                                      touch = the flow index the packet
+//                                      logged (kNone if none), for the bins.
 // Rows are gathered cooperatively: four lanes fetch one row as 64 contiguous
 // bytes (one memory request per row instead of four 16-byte pieces per
 // lane) and the wave's LDS tile hands each lane its own row, the same
@@ -226,7 +272,9 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
                                                uint32_t p0, uint32_t p1,
                                                uint32_t n_all, uint4 *S,
                                                const uint4 *rows, Issue issue,
-                                               Finish finish) {
+                                               Finish finish,
+                                               const TouchBins &bins = TouchBins{},
+                                               uint32_t *cur = nullptr) {
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t first = p0 & ~63u;
   const uint32_t tiles = (p1 - first + 63) / 64;
@@ -249,9 +297,15 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
   uint32_t tile = blockIdx.x * 4 + wv;
   const uint32_t tend = tiles, tstep = gridDim.x * 4;
 #else
+#ifdef VP_ABL_XCD  // diagnostic: XCD x (= block % 8) owns the x-th eighth
+  const uint32_t rb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+#else
+  const uint32_t rb = blockIdx.x;
+#endif
   const uint32_t per_b = (tiles + gridDim.x - 1) / gridDim.x;
-  uint32_t tile = blockIdx.x * per_b + wv;
-  const uint32_t tend = min(tiles, blockIdx.x * per_b + per_b), tstep = 4;
+  uint32_t tile = rb * per_b + wv;
+  const uint32_t tend = min(tiles, rb * per_b + per_b), tstep = 4;
+  const uint32_t range0 = first + rb * per_b * 64;  // this block's first packet
 #endif
   if (tile < tend) fetch(tile);
   for (; tile < tend; tile += tstep) {
@@ -294,7 +348,18 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
       for (uint32_t k = 0; k < 4; k++) row[k] = S[chunk_swz(4 * lane + k)];
     }
     bool mod = false;
-    if (mine) mod = finish(pend, row, p, f, in, ln);
+    uint32_t touch = kNone;
+    if (mine) mod = finish(pend, row, p, f, in, ln, touch);
+#ifndef VP_ABL_STRIDED
+    if (bins.ent) {  // append to this block's slice of the touch's bin
+      const bool v = touch != kNone;
+      const uint32_t b = v ? bin_of(touch) : 0;
+      const uint32_t k = group_reserve(cur, b, v);
+      if (v && k < bins.cap)
+        bins.ent[((size_t)rb * kBins + b) * bins.cap + k] =
+            (bin_local(touch) << bins.pbits) | (p - range0);
+    }
+#endif
     if (mod) {
 #pragma unroll
       for (uint32_t k = 0; k < 4; k++)
@@ -310,6 +375,16 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
     }
     wave_lds_sync();  // the next tile overwrites S
   }
+#ifndef VP_ABL_STRIDED
+  if (bins.ent) {  // publish this block's slice sizes
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < kBins; b += blockDim.x) {
+      const uint32_t c = cur[b];
+      bins.cnt[(size_t)rb * kBins + b] = c < bins.cap ? c : bins.cap;
+      if (c > bins.cap) *bins.ovf = 1;
+    }
+  }
+#endif
 }
 
 // Checksums of a 64-byte IHL=5 frame with total_length <= 50 (so every byte

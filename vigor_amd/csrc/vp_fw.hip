@@ -94,14 +94,14 @@ __device__ __forceinline__ void fw_key(bool wan, uint32_t sp, uint32_t dp,
 }
 
 // Generic (byte-addressed) phase A: IP options, any slot size.
-__device__ void fw_generic_a(const FwArgs &a, const uint32_t *T, uint32_t p,
-                             uint32_t in, uint32_t len) {
+__device__ uint32_t fw_generic_a(const FwArgs &a, const uint32_t *T, uint32_t p,
+                                 uint32_t in, uint32_t len) {
   GFrame f{a.frames + (size_t)p * a.slot, a.slot};
   const L34 h = parse_l34(f, len);
   if (!h.ok) {  // not IPv4 / not TCP-UDP: drop (fw_main.c:29-40)
     a.out[p] = (uint16_t)in;
     a.log[p] = kNone;
-    return;
+    return kNone;
   }
   const uint32_t proto = f.r8(h.ip + 9);
   const uint32_t sp = f.r16(h.l4), dp = f.r16(h.l4 + 2);
@@ -119,7 +119,7 @@ __device__ void fw_generic_a(const FwArgs &a, const uint32_t *T, uint32_t p,
     else
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
     a.log[p] = kNone;  // phase B / C write the real entry
-    return;
+    return kNone;
   }
   a.log[p] = idx;
   const uint32_t dst = wan ? (w3 >> 8) : a.wan;
@@ -127,6 +127,7 @@ __device__ void fw_generic_a(const FwArgs &a, const uint32_t *T, uint32_t p,
   fw_macs(a, dst, mw);
   set_macs(f, mw);
   a.out[p] = (uint16_t)dst;
+  return idx;
 }
 
 // Phase A, 64-byte slots in registers (frames64_tiles): fw_issue parses and
@@ -171,10 +172,10 @@ __device__ __forceinline__ FwPend fw_issue(const FwArgs &a, const uint32_t *T,
 __device__ __forceinline__ bool fw_finish(const FwArgs &a, const uint32_t *T,
                                           const FwPend &P, const uint4 *row,
                                           uint32_t p, RFrame &f, uint32_t in,
-                                          uint32_t len) {
+                                          uint32_t len, uint32_t &touch) {
   if (P.kind == kFwDone) return false;
   if (P.kind == kFwGeneric) {
-    fw_generic_a(a, T, p, in, len);  // writes global memory itself
+    touch = fw_generic_a(a, T, p, in, len);  // writes global memory itself
     return false;
   }
   const uint32_t proto = f.w[5] >> 24;
@@ -197,6 +198,7 @@ __device__ __forceinline__ bool fw_finish(const FwArgs &a, const uint32_t *T,
     return false;
   }
   a.log[p] = idx;
+  touch = idx;
   const uint32_t dst = wan ? (w3 >> 8) : a.wan;
   uint32_t mw[3];
   fw_macs(a, dst, mw);
@@ -222,10 +224,13 @@ __global__ __launch_bounds__(256) void fw_classify(FwArgs a) {
 }
 
 // Phase A for 64-byte slots: LDS-staged coalesced frame I/O.
-__global__ __launch_bounds__(256, 4) void fw_classify64(FwArgs a, uint32_t n_all) {
+__global__ __launch_bounds__(256, 4) void fw_classify64(FwArgs a, uint32_t n_all,
+                                                       TouchBins bins) {
   __shared__ uint32_t T[kFwTabs * 256];
   __shared__ uint4 stage[4][256];
-  fw_load_tables(T, a.crc_tab);
+  __shared__ uint32_t cur[kBins];
+  for (uint32_t i = threadIdx.x; i < kBins; i += blockDim.x) cur[i] = 0;
+  fw_load_tables(T, a.crc_tab);  // (its barrier also covers cur)
   frames64_tiles(
       a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
       reinterpret_cast<const uint4 *>(a.t.bk),
@@ -233,7 +238,10 @@ __global__ __launch_bounds__(256, 4) void fw_classify64(FwArgs a, uint32_t n_all
         return fw_issue(a, T, p, f, in, len, mine);
       },
       [&](const FwPend &P, const uint4 *row, uint32_t p, RFrame &f, uint32_t in,
-          uint32_t len) { return fw_finish(a, T, P, row, p, f, in, len); });
+          uint32_t len, uint32_t &touch) {
+        return fw_finish(a, T, P, row, p, f, in, len, touch);
+      },
+      bins, cur);
 }
 
 // ------------------------------------------------------------- phase B --
@@ -344,21 +352,31 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.wan = c->fw.wan_device;
   a.n_dev = c->fw.n_devices;
 
+  // 64-byte slots: the classify launch also bins its touches (TouchBins)
+  const bool tiles64 = p1 > p0 && b->slot == 64 && c->coalesced_io;
+  BinsPlan bp{};
+  if (tiles64) VP_TRY(tbl_bins_plan(c, t, (const void *)fw_classify64, p0, p1, &bp));
   VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 8, c->stream));  // + defer
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   if (p1 > p0) {
-    if (b->slot == 64 && c->coalesced_io) {
+    if (tiles64) {
       const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
       fw_classify64<<<resident_grid((const void *)fw_classify64, (tiles + 3) / 4), 256,
-                      0, c->stream>>>(a, b->n);
+                      0, c->stream>>>(a, b->n, bp.bins);
     } else {
       fw_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
     }
     VP_HIP(hipGetLastError());
   }
   VP_HIP(hipEventRecord(c->ev1, c->stream));
-  VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));  // optimistic fold
+  // optimistic fold (redone below over the completed log when phase B/C
+  // run or a touch bin overflowed)
+  if (bp.on)
+    VP_TRY(tbl_bins_reduce(c, t, bp, p0, now, seq0));
+  else
+    VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
   VP_TRY(read_ctl(c, t));
+  const bool refold = bp.on && t.h_ctl.touch_ovf;
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
   *ms += kms;
@@ -386,7 +404,8 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     fw_defer_finish<<<grid_for(ndefer), 256, 0, c->stream>>>(a, w.defer, ndefer);
     VP_HIP(hipGetLastError());
   }
-  if (nmiss || ndefer) VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
+  if (nmiss || ndefer || refold)
+    VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
   if (nmiss || ndefer) VP_TRY(read_ctl(c, t));
   return 0;
 }

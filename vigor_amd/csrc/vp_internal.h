@@ -49,7 +49,7 @@ struct Ctl {
   uint32_t new_count;
   uint32_t aux_count;
   uint32_t max_disp;  // longest insert probe (buckets) since last check
-  uint32_t pad;
+  uint32_t touch_ovf;  // a touch-bin slice overflowed (vp_device.h TouchBins)
 };
 
 // One device table (see vp_table.h).
@@ -100,6 +100,8 @@ struct Workspace {
   uint32_t *skey = nullptr, *sval = nullptr;
   uint32_t *hist = nullptr, *hoff = nullptr;  // touch-reduce (chunk x span)
   uint64_t hist_cap = 0;
+  uint32_t *bins_ent = nullptr, *bins_cnt = nullptr;  // touch bins (TouchBins)
+  size_t bins_ent_n = 0, bins_cnt_n = 0;
   void *cub_tmp = nullptr;
   size_t cub_bytes = 0;
   // host staging for the host-batch entry points

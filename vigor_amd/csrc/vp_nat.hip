@@ -90,39 +90,40 @@ __device__ __forceinline__ void macs_for(const NatArgs &a, uint32_t dst,
 #else
 #define VP_GENERIC_FN __device__  // inlined: measured faster (tools/ablate.py)
 #endif
-VP_GENERIC_FN void nat_generic_a(const NatArgs &a, const uint32_t *T, uint32_t p,
-                              uint32_t in, uint32_t len) {
+VP_GENERIC_FN uint32_t nat_generic_a(const NatArgs &a, const uint32_t *T,
+                                       uint32_t p, uint32_t in, uint32_t len) {
   GFrame f{a.frames + (size_t)p * a.slot, a.slot};
   L34 h = parse_l34(f, len);
   if (!h.ok) {
     a.out[p] = (uint16_t)in;
     a.log[p] = kNone;
-    return;
+    return kNone;
   }
   const uint32_t proto = f.r8(h.ip + 9);
   const uint32_t sp = f.r16(h.l4), dp = f.r16(h.l4 + 2);
   const uint32_t sip = f.r32(h.ip + 12), dip = f.r32(h.ip + 16);
-  uint32_t dst;
+  uint32_t dst, logged;
   if (in == a.wan) {
     const int idx = (int)dp - (int)a.start_port;
     if (idx < 0 || idx >= (int)a.t.cap) {  // reference UB range: unallocated
       a.out[p] = (uint16_t)in;
       a.log[p] = kNone;
-      return;
+      return kNone;
     }
     const uint32_t s = a.t.slot_of[idx];
     if (s == kNone) {
       a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
       a.log[p] = kNone;  // phase C writes the real entry
-      return;
+      return kNone;
     }
     const uint4 fk = tbl_key_of(a.t, (uint32_t)idx);
     const uint32_t k0 = fk.x, k1 = fk.y, k2 = fk.z, k3 = fk.w;
     a.log[p] = (uint32_t)idx;  // rejuvenated before the anti-spoof check
     if ((k2 != sip) | ((k0 >> 16) != sp) | (((k3 >> 16) & 0xFF) != proto)) {
       a.out[p] = (uint16_t)in;
-      return;
+      return (uint32_t)idx;
     }
+    logged = (uint32_t)idx;
     f.w32(h.ip + 16, k1);
     f.w16(h.l4 + 2, (uint16_t)(k0 & 0xFFFF));
     dst = k3 & 0xFFFF;
@@ -133,9 +134,10 @@ VP_GENERIC_FN void nat_generic_a(const NatArgs &a, const uint32_t *T, uint32_t p
     if (idx == kNone) {
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
       a.log[p] = kNone;  // phase B writes the real entry
-      return;
+      return kNone;
     }
     a.log[p] = idx;
+    logged = idx;
     f.w32(h.ip + 12, a.ext_ip);
     f.w16(h.l4, (uint16_t)(a.start_port + idx));
     dst = a.wan;
@@ -145,6 +147,7 @@ VP_GENERIC_FN void nat_generic_a(const NatArgs &a, const uint32_t *T, uint32_t p
   macs_for(a, dst, mw);
   set_macs(f, mw);
   a.out[p] = (uint16_t)dst;
+  return logged;
 }
 
 // Phase A for one packet whose 64-byte slot is in registers, in two halves
@@ -213,10 +216,10 @@ __device__ __forceinline__ NatPend nat_issue(const NatArgs &a, const uint32_t *T
 __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
                                            const NatPend &P, const uint4 *row,
                                            uint32_t p, RFrame &f, uint32_t in,
-                                           uint32_t len) {
+                                           uint32_t len, uint32_t &touch) {
   if (P.kind == kPendDone) return false;
   if (P.kind == kPendGeneric) {
-    nat_generic_a(a, T, p, in, len);  // writes global memory itself
+    touch = nat_generic_a(a, T, p, in, len);  // writes global memory itself
     return false;
   }
   const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
@@ -235,6 +238,7 @@ __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
     }
     const uint4 k = reinterpret_cast<const uint4 *>(a.t.bk + (s >> 2))[s & 3];
     a.log[p] = idx;  // rejuvenated before the anti-spoof check
+    touch = idx;
     if ((k.z != sip) | ((k.x >> 16) != sp) | (((k.w >> 16) & 0xFF) != proto)) {
       a.out[p] = (uint16_t)in;  // nat_main.c:55-60
       return false;
@@ -260,6 +264,7 @@ __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
       return false;
     }
     a.log[p] = idx;
+    touch = idx;
     f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
     f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
     dst = a.wan;
@@ -309,7 +314,8 @@ __global__ __launch_bounds__(256) void nat_classify(NatArgs a) {
     }
     const NatPend P = nat_issue(a, T, p, f, in, len, true);
     const uint4 row[4] = {};
-    asm volatile("" ::"v"(nat_finish(a, T, P, row, p, f, in, len)
+    uint32_t touch;
+    asm volatile("" ::"v"(nat_finish(a, T, P, row, p, f, in, len, touch)
                               ? f.w[6] ^ f.w[10] : 0u));
 #else
     const NatPend P = nat_issue(a, T, p, f, in, len, true);
@@ -321,7 +327,8 @@ __global__ __launch_bounds__(256) void nat_classify(NatArgs a) {
       row[2] = q[2];
       row[3] = q[3];
     }
-    if (nat_finish(a, T, P, row, p, f, in, len)) {
+    uint32_t touch;
+    if (nat_finish(a, T, P, row, p, f, in, len, touch)) {
       st_stream(fp, make_uint4(f.w[0], f.w[1], f.w[2], f.w[3]));
       st_stream(fp + 1, make_uint4(f.w[4], f.w[5], f.w[6], f.w[7]));
       st_stream(fp + 2, make_uint4(f.w[8], f.w[9], f.w[10], f.w[11]));
@@ -334,10 +341,18 @@ __global__ __launch_bounds__(256) void nat_classify(NatArgs a) {
 
 // Phase A for 64-byte slots: LDS-staged 1 KiB-contiguous frame I/O
 // (frames64_tiles, vp_device.h); each wave owns 64 consecutive packets.
-__global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_all) {
+#if defined(VP_ABL_OCC5)  // diagnostic: 5 blocks per CU (96 VGPRs, spills)
+#define VP_NAT64_MINB 5
+#else
+#define VP_NAT64_MINB 4
+#endif
+__global__ __launch_bounds__(256, VP_NAT64_MINB) void nat_classify64(NatArgs a, uint32_t n_all,
+                                                                TouchBins bins) {
   __shared__ uint32_t T[15 * 256];
   __shared__ uint4 stage[4][256];
-  load_crc_tables(T, a.crc_tab);
+  __shared__ uint32_t cur[kBins];
+  for (uint32_t i = threadIdx.x; i < kBins; i += blockDim.x) cur[i] = 0;
+  load_crc_tables(T, a.crc_tab);  // (its barrier also covers cur)
   frames64_tiles(
       a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
       reinterpret_cast<const uint4 *>(a.t.bk),
@@ -345,7 +360,10 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
         return nat_issue(a, T, p, f, in, len, mine);
       },
       [&](const NatPend &P, const uint4 *row, uint32_t p, RFrame &f, uint32_t in,
-          uint32_t len) { return nat_finish(a, T, P, row, p, f, in, len); });
+          uint32_t len, uint32_t &touch) {
+        return nat_finish(a, T, P, row, p, f, in, len, touch);
+      },
+      bins, cur);
 }
 
 // ------------------------------------------------------------- phase B --
@@ -474,13 +492,17 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.start_port = c->nat.start_port;
   a.n_dev = c->nat.n_devices;
 
+  // 64-byte slots: the classify launch also bins its touches (TouchBins)
+  const bool tiles64 = p1 > p0 && b->slot == 64 && c->coalesced_io;
+  BinsPlan bp{};
+  if (tiles64) VP_TRY(tbl_bins_plan(c, t, (const void *)nat_classify64, p0, p1, &bp));
   VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 8, c->stream));  // + defer
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   if (p1 > p0) {
-    if (b->slot == 64 && c->coalesced_io) {
+    if (tiles64) {
       const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
       nat_classify64<<<resident_grid((const void *)nat_classify64, (tiles + 3) / 4),
-                       256, 0, c->stream>>>(a, b->n);
+                       256, 0, c->stream>>>(a, b->n, bp.bins);
     } else {
       nat_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
     }
@@ -488,9 +510,14 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   }
   VP_HIP(hipEventRecord(c->ev1, c->stream));
   // Optimistic: fold phase A's touches right away (queued packets logged
-  // kNone); if B/C run, the fold is redone over the completed log.
-  VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
+  // kNone); if B/C run, or a touch bin overflowed, the fold is redone over
+  // the completed log.
+  if (bp.on)
+    VP_TRY(tbl_bins_reduce(c, t, bp, p0, now, seq0));
+  else
+    VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
   VP_TRY(read_ctl(c, t));
+  const bool refold = bp.on && t.h_ctl.touch_ovf;
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
   *ms += kms;
@@ -532,7 +559,8 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     nat_defer_finish<<<grid_for(ndefer), 256, 0, c->stream>>>(a, w.defer, ndefer);
     VP_HIP(hipGetLastError());
   }
-  if (nmiss || ndefer) VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
+  if (nmiss || ndefer || refold)
+    VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
   if (union_n || ndefer) VP_TRY(read_ctl(c, t));
   return 0;
 }

@@ -161,6 +161,22 @@ int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
 int tbl_touch_reduce(vp_ctx *c, FlowTable &t, const uint32_t *log, uint32_t p0,
                      uint32_t p1, const NowSpec &now, uint64_t seq_base);
 
+// Touch bins for one 64-byte classify launch over [p0, p1) of `kernel`
+// (vp_device.h TouchBins). plan->on is false when the launch cannot bin
+// (unaligned segment, table or range too large, VIGPATH_TOUCH_BINS=0); then
+// pass plan->bins (ent = null) to the kernel and fold with tbl_touch_reduce.
+struct BinsPlan {
+  bool on;
+  uint32_t grid, range, L;
+  TouchBins bins;
+};
+int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
+                  uint32_t p1, BinsPlan *plan);
+// Fold the bins into ts/tseq. Exact unless a slice overflowed (the launch
+// sets t.ctl->touch_ovf; read_ctl, then fold the log with tbl_touch_reduce).
+int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
+                    const NowSpec &now, uint64_t seq_base);
+
 // Exact min ts over allocated indices -> t.ts_floor (~0 if none).
 int tbl_exact_floor(vp_ctx *c, FlowTable &t);
 

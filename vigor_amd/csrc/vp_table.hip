@@ -29,31 +29,32 @@ uint32_t resident_grid(const void *kernel, uint64_t work_blocks) {
   struct Entry {
     const void *kernel;
     int dev;
-    uint32_t blocks;
+    uint32_t cus, per;
   };
   static std::mutex mu;
   static std::vector<Entry> cache;
   int dev = 0;
   (void)hipGetDevice(&dev);
-  uint32_t blocks = 0;
+  uint32_t cus = 0, per = 0;
   {
     std::lock_guard<std::mutex> g(mu);
     for (const Entry &e : cache)
-      if (e.kernel == kernel && e.dev == dev) blocks = e.blocks;
-    if (!blocks) {
-      int cus = 0, per = 0;
-      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+      if (e.kernel == kernel && e.dev == dev) cus = e.cus, per = e.per;
+    if (!cus) {
+      int c = 0, p = 0;
+      if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) !=
               hipSuccess ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) !=
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&p, kernel, 256, 0) !=
               hipSuccess)
         (void)hipGetLastError();
-      const char *env = getenv("VIGPATH_BLOCKS_PER_CU");
-      if (env && atoi(env) > 0) per = atoi(env);
-      blocks = (uint32_t)std::max(1, std::max(cus, 1) * std::max(per, 1));
-      cache.push_back(Entry{kernel, dev, blocks});
+      cus = (uint32_t)std::max(c, 1);
+      per = (uint32_t)std::max(p, 1);
+      cache.push_back(Entry{kernel, dev, cus, per});
     }
   }
-  const uint64_t g = std::min<uint64_t>(work_blocks, blocks);
+  const char *env = getenv("VIGPATH_BLOCKS_PER_CU");  // diagnostics
+  if (env && atoi(env) > 0) per = (uint32_t)atoi(env);
+  const uint64_t g = std::min<uint64_t>(work_blocks, (uint64_t)cus * per);
   return (uint32_t)std::max<uint64_t>(g, 1);
 }
 
@@ -314,26 +315,6 @@ constexpr uint32_t kPosBits = 20;  // position within a span (span <= 2^20)
 constexpr uint32_t kMaxChunkBits = 12;
 constexpr uint32_t kMaxSpans = 8192;  // pass-3 LDS offset table (+1)
 
-// Lanes holding chunk `ch` (valid `v`) that share the first valid lane's
-// chunk are served by one LDS atomic (traffic with locality would otherwise
-// serialise a wave on one counter); the rest add individually. Returns this
-// lane's reserved position.
-__device__ __forceinline__ uint32_t chunk_reserve(uint32_t *ctr, uint32_t ch,
-                                                  bool v) {
-  const uint64_t vm = __ballot(v);
-  if (!vm) return 0;
-  const uint32_t lead = __shfl(ch, __ffsll((unsigned long long)vm) - 1);
-  const bool grp = v && ch == lead;
-  const uint64_t same = __ballot(grp);
-  const uint32_t first = __ffsll((unsigned long long)same) - 1;
-  uint32_t base = 0;
-  if (grp && __lane_id() == first)
-    base = atomicAdd(&ctr[ch], (uint32_t)__popcll(same));
-  base = __shfl(base, first);
-  if (grp) return base + (uint32_t)__popcll(same & ((1ull << __lane_id()) - 1ull));
-  return v ? atomicAdd(&ctr[ch], 1u) : 0;
-}
-
 __global__ __launch_bounds__(256) void touch_count(const uint32_t *log,
                                                    uint32_t n, uint32_t span,
                                                    uint32_t cb, uint32_t nchunks,
@@ -351,7 +332,7 @@ __global__ __launch_bounds__(256) void touch_count(const uint32_t *log,
       k[u] = jj < s1 ? log[jj] : kNone;
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++) chunk_reserve(cnt, k[u] >> cb, k[u] != kNone);
+    for (int u = 0; u < 4; u++) group_reserve(cnt, k[u] >> cb, k[u] != kNone);
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nchunks; b += blockDim.x)
@@ -380,7 +361,7 @@ __global__ __launch_bounds__(256) void touch_scatter(const uint32_t *log,
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const bool v = k[u] != kNone;
-      const uint32_t at = chunk_reserve(pos, k[u] >> cb, v);
+      const uint32_t at = group_reserve(pos, k[u] >> cb, v);
       if (v) out[at] = ((k[u] & cmask) << kPosBits) | (j + u * blockDim.x - s0);
     }
   }
@@ -516,6 +497,115 @@ int tbl_touch_reduce(vp_ctx *c, FlowTable &t, const uint32_t *log, uint32_t p0,
   if (split > 1)
     touch_finalize<<<grid_for(t.cap), 256, 0, ts>>>(t.lastg, t.cap, p0, now,
                                                    seq_base, t.ts, t.tseq);
+  VP_HIP(hipGetLastError());
+  return 0;
+}
+
+// ---------------------------------------------------------- touch bins --
+// Single-pass fold of the touch bins a 64-byte classify launch filled
+// (TouchBins, vp_device.h): one block per bin keeps the largest position per
+// in-bin index in LDS, reading every source block's slice of its bin, then
+// writes ts/tseq in runs of 16 consecutive indices. About 8 B of traffic per
+// packet (one write while classifying, one read here).
+constexpr uint32_t kBinLocalMax = 16384;  // in-bin indices held in LDS
+
+__global__ __launch_bounds__(1024) void touch_bins_reduce(
+    const uint32_t *ent, const uint32_t *cnt, uint32_t nsrc, uint32_t cap,
+    uint32_t pbits, uint32_t range, uint32_t L, uint32_t tcap, uint32_t p0,
+    NowSpec now, uint64_t seq_base, uint64_t *ts, uint64_t *tseq) {
+  __shared__ uint32_t last[kBinLocalMax];  // 1 + position in the launch, 0 = none
+  const uint32_t bin = blockIdx.x;
+  for (uint32_t i = threadIdx.x; i < L; i += blockDim.x) last[i] = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const uint32_t pmask = (1u << pbits) - 1;
+  constexpr uint32_t kU = 4;  // source slices in flight per wave
+  for (uint32_t s0 = threadIdx.x >> 6; s0 < nsrc; s0 += kU * nw) {
+    uint32_t n[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) {
+      const uint32_t sb = s0 + u * nw;
+      n[u] = sb < nsrc ? cnt[(size_t)sb * kBins + bin] : 0;
+    }
+    for (uint32_t k = 0;; k += 64) {
+      bool any = false;
+      uint32_t e[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; u++) {
+        const uint32_t sb = s0 + u * nw;
+        any |= k < n[u];
+        e[u] = k + lane < n[u] ? ent[((size_t)sb * kBins + bin) * cap + k + lane] : 0;
+      }
+      if (!any) break;
+#pragma unroll
+      for (uint32_t u = 0; u < kU; u++)
+        if (k + lane < n[u])
+          atomicMax(&last[e[u] >> pbits], (s0 + u * nw) * range + (e[u] & pmask) + 1);
+    }
+  }
+  __syncthreads();
+  for (uint32_t l = threadIdx.x; l < L; l += blockDim.x) {
+    const uint32_t v = last[l];
+    const uint32_t i = bin_index(bin, l);
+    if (!v || i >= tcap) continue;
+    const uint32_t p = p0 + v - 1;
+    ts[i] = (uint64_t)now.at(p);
+    tseq[i] = seq_base + p;
+  }
+}
+
+static uint32_t ceil_log2(uint64_t v) {
+  uint32_t b = 0;
+  while ((1ull << b) < v) b++;
+  return b;
+}
+
+int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
+                  uint32_t p1, BinsPlan *plan) {
+  Workspace &w = c->ws;
+  *plan = BinsPlan{};
+  const char *env = getenv("VIGPATH_TOUCH_BINS");  // diagnostics: 0 = off
+  if ((env && !atoi(env)) || (p0 & 63) || p1 <= p0) return 0;
+  const uint32_t tiles = (p1 - p0 + 63) / 64;
+  const uint32_t grid = resident_grid(kernel, (tiles + 3) / 4);
+  const uint32_t per_b = (tiles + grid - 1) / grid;
+  const uint32_t range = per_b * 64;
+  const uint32_t L = ((t.cap + 4095) >> 12) << 4;
+  const uint32_t pbits = std::max<uint32_t>(1, ceil_log2(range));
+  if (L > kBinLocalMax || ceil_log2(L) + pbits > 32) return 0;
+  // twice a uniform share of a block's packets per bin, in 64-entry lines
+  const uint32_t cap = ((2 * range / kBins + 32) + 15) & ~15u;
+  const size_t ne = (size_t)grid * kBins * cap, nc = (size_t)grid * kBins;
+  if (ne > w.bins_ent_n) {
+    VP_HIP(hipStreamSynchronize(c->stream));
+    hipFree(w.bins_ent);
+    w.bins_ent = nullptr;
+    w.bins_ent_n = 0;
+    VP_TRY(dalloc(&w.bins_ent, ne));
+    w.bins_ent_n = ne;
+  }
+  if (nc > w.bins_cnt_n) {
+    VP_HIP(hipStreamSynchronize(c->stream));
+    hipFree(w.bins_cnt);
+    w.bins_cnt = nullptr;
+    w.bins_cnt_n = 0;
+    VP_TRY(dalloc(&w.bins_cnt, nc));
+    w.bins_cnt_n = nc;
+  }
+  VP_HIP(hipMemsetAsync(&t.ctl->touch_ovf, 0, 4, c->stream));
+  plan->on = true;
+  plan->grid = grid;
+  plan->range = range;
+  plan->L = L;
+  plan->bins = TouchBins{w.bins_ent, w.bins_cnt, &t.ctl->touch_ovf, cap, pbits};
+  return 0;
+}
+
+int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
+                    const NowSpec &now, uint64_t seq_base) {
+  touch_bins_reduce<<<kBins, 1024, 0, c->stream>>>(
+      plan.bins.ent, plan.bins.cnt, plan.grid, plan.bins.cap, plan.bins.pbits,
+      plan.range, plan.L, t.cap, p0, now, seq_base, t.ts, t.tseq);
   VP_HIP(hipGetLastError());
   return 0;
 }
