@@ -41,15 +41,16 @@ struct Ctl {
   uint32_t fresh_next;  // first never-allocated index
   uint32_t n_live;
   uint32_t n_tomb;
-  uint32_t miss_count;
-  uint32_t defer_count;
+  uint32_t miss_count;   // } reset together at the start of a segment
+  uint32_t defer_count;  // }
+  uint32_t touch_ovf;    // } a touch-bin slice overflowed (TouchBins)
   uint32_t exp_count;
   uint32_t tomb_reused;
   uint64_t min_ts;
   uint32_t new_count;
   uint32_t aux_count;
   uint32_t max_disp;  // longest insert probe (buckets) since last check
-  uint32_t touch_ovf;  // a touch-bin slice overflowed (vp_device.h TouchBins)
+  uint32_t pad;
 };
 
 // One device table (see vp_table.h).

@@ -496,7 +496,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   const bool tiles64 = p1 > p0 && b->slot == 64 && c->coalesced_io;
   BinsPlan bp{};
   if (tiles64) VP_TRY(tbl_bins_plan(c, t, (const void *)nat_classify64, p0, p1, &bp));
-  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 8, c->stream));  // + defer
+  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 12, c->stream));  // + defer, ovf
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   if (p1 > p0) {
     if (tiles64) {

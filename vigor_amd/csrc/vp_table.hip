@@ -519,28 +519,32 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const uint32_t pmask = (1u << pbits) - 1;
-  constexpr uint32_t kU = 4;  // source slices in flight per wave
-  for (uint32_t s0 = threadIdx.x >> 6; s0 < nsrc; s0 += kU * nw) {
-    uint32_t n[kU];
-#pragma unroll
-    for (uint32_t u = 0; u < kU; u++) {
-      const uint32_t sb = s0 + u * nw;
-      n[u] = sb < nsrc ? cnt[(size_t)sb * kBins + bin] : 0;
-    }
-    for (uint32_t k = 0;; k += 64) {
-      bool any = false;
-      uint32_t e[kU];
+  constexpr uint32_t kU = 8;  // source slices in flight per wave
+  // wave w takes slices w, w + nw, ...; 64 of them per round, their sizes
+  // loaded by one instruction (lane l <-> slice w + l * nw)
+  for (uint32_t r0 = threadIdx.x >> 6; r0 < nsrc; r0 += 64 * nw) {
+    const uint32_t my = r0 + lane * nw;
+    const uint32_t nv = my < nsrc ? cnt[(size_t)my * kBins + bin] : 0;
+    for (uint32_t i = 0; i < 64; i += kU) {
+      uint32_t n[kU], e[kU];
 #pragma unroll
       for (uint32_t u = 0; u < kU; u++) {
-        const uint32_t sb = s0 + u * nw;
-        any |= k < n[u];
-        e[u] = k + lane < n[u] ? ent[((size_t)sb * kBins + bin) * cap + k + lane] : 0;
+        n[u] = __shfl(nv, i + u);
+        const uint32_t sb = r0 + (i + u) * nw;
+        e[u] = lane < n[u] ? ent[((size_t)sb * kBins + bin) * cap + lane] : 0;
       }
-      if (!any) break;
 #pragma unroll
-      for (uint32_t u = 0; u < kU; u++)
-        if (k + lane < n[u])
-          atomicMax(&last[e[u] >> pbits], (s0 + u * nw) * range + (e[u] & pmask) + 1);
+      for (uint32_t u = 0; u < kU; u++) {
+        const uint32_t sb = r0 + (i + u) * nw;
+        if (lane < n[u])
+          atomicMax(&last[e[u] >> pbits], sb * range + (e[u] & pmask) + 1);
+        for (uint32_t k = 64; k < n[u]; k += 64) {  // slices longer than 64
+          if (k + lane < n[u]) {
+            const uint32_t x = ent[((size_t)sb * kBins + bin) * cap + k + lane];
+            atomicMax(&last[x >> pbits], sb * range + (x & pmask) + 1);
+          }
+        }
+      }
     }
   }
   __syncthreads();
@@ -592,8 +596,7 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
     VP_TRY(dalloc(&w.bins_cnt, nc));
     w.bins_cnt_n = nc;
   }
-  VP_HIP(hipMemsetAsync(&t.ctl->touch_ovf, 0, 4, c->stream));
-  plan->on = true;
+  plan->on = true;  // (the segment's counter reset clears touch_ovf)
   plan->grid = grid;
   plan->range = range;
   plan->L = L;
