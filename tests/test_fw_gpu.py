@@ -153,3 +153,19 @@ def test_touch_bins_steady_state(n_flows):
     fr, ln, dv, now = T.fw_trace(30_000, n_flows, start=n_flows, reply_every=3)
     check_batches(fw, o, fr, ln, dv, now, 64, [])
     check_state(fw, o, 1 << 16)
+
+
+def test_multiplicative_home_buckets_reprobe(monkeypatch):
+    """VIGPATH_MIX=1 at load 0.65: full home buckets finish in fw_reprobe
+    (LAN hits, WAN replies and new flows alike)."""
+    monkeypatch.setenv("VIGPATH_MIX", "1")
+    fw, o = make_pair(max_flows=4096)
+    fr, ln, dv, now = T.fw_trace(4000, 4000)
+    check_batches(fw, o, fr, ln, dv, now, 64, [1500])
+    fr, ln, dv, now = T.fw_trace(50_000, 4000, start=4000, reply_every=3)
+    check_batches(fw, o, fr, ln, dv, now, 64, [20_000])
+    check_state(fw, o, 4096)
+    rng = np.random.default_rng(3)
+    fr, ln, dv, now = mixed_fw_trace(rng, 5000, 3500)
+    check_batches(fw, o, fr, ln, dv, now + 10**8, 64, [2500])
+    check_state(fw, o, 4096)

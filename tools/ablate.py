@@ -25,7 +25,7 @@ def main():
     variants = {"full": (None, {}), "perlane": (None, {"VIGPATH_COALESCED": "0"})}
     variants["bpc3"] = (None, {"VIGPATH_BLOCKS_PER_CU": "3"})
     variants["bpc2"] = (None, {"VIGPATH_BLOCKS_PER_CU": "2"})
-    for v in ("NOPROBE", "NOINLINE", "NT", "NOFRAME", "STRIDED", "XCD", "OCC5"):
+    for v in ("NOPROBE", "NOINLINE", "NT", "NOFRAME"):
         p = os.path.join(ROOT, "vigor_amd", "abl", "libvigpath_%s.so" % v)
         if os.path.exists(p):  # NOFRAME lives in the per-lane kernel
             variants[v] = (p, {"VIGPATH_COALESCED": "0"} if v == "NOFRAME"

@@ -18,7 +18,9 @@ out = torch.zeros(B, dtype=torch.int16, device=dev)
 buf = torch.empty(B * 64, dtype=torch.uint8, device=dev)
 libs = [None] + [os.path.join(ROOT, "vigor_amd", "abl", x)
                  for x in sys.argv[1:]]
-for nf in (1 << 14, 1 << 16, 1 << 18, 1 << 20, 1 << 22):
+SIZES = [int(x) for x in os.environ.get("SWEEP_FLOWS", "").split(",") if x] or \
+    [1 << 14, 1 << 16, 1 << 18, 1 << 20, 1 << 22]
+for nf in SIZES:
     for lp in libs:
         cfg = vigor_amd.nat_config_from_args(
             bench.NAT_ARGS + ["--max-flows", str(nf)], 2, bench.DEV_MACS)

@@ -223,6 +223,14 @@ __device__ __forceinline__ uint32_t group_reserve(uint32_t *ctr, uint32_t ch,
 // its own fixed-size slice of every bin (LDS cursors); a slice that fills up
 // sets *ovf and the host folds the full log instead.
 constexpr uint32_t kBins = 256;
+// finish() may set touch = kReprobe instead of an index: the packet leaves
+// the wave and is queued on the block's reprobe slice (TileQueue).
+constexpr uint32_t kReprobe = 0xFFFFFFFDu;
+struct TileQueue {
+  uint32_t *ent;    // [block][range] packet positions; null = off
+  uint32_t *cnt;    // [block] entries queued
+  uint32_t *total;  // += every block's count (one atomic per block)
+};
 struct TouchBins {
   uint32_t *ent;  // [block][bin][cap] entries (in-bin << pbits | position); null = off
   uint32_t *cnt;  // [block][bin] entries written
@@ -252,7 +260,9 @@ __device__ __forceinline__ uint32_t bin_index(uint32_t bin, uint32_t local) {
 //                                      consume the row, rewrite f, return
 //                                      true when f must be written back;
 //                                      touch = the flow index the packet
-//                                      logged (kNone if none), for the bins.
+//                                      logged (kNone if none), for the bins,
+//                                      or kReprobe to queue the packet on the
+//                                      block's reprobe slice (rq).
 // Rows are gathered cooperatively: four lanes fetch one row as 64 contiguous
 // bytes (one memory request per row instead of four 16-byte pieces per
 // lane) and the wave's LDS tile hands each lane its own row, the same
@@ -262,9 +272,10 @@ __device__ __forceinline__ uint32_t bin_index(uint32_t bin, uint32_t local) {
 // flight and the frame stream's HBM latency hides under the probes. The grid
 // is persistent (resident_grid()); each block owns one contiguous range of
 // tiles, its four waves interleaved over it: measured 12 % faster than
-// dealing tiles round-robin over all waves (tools/ablate.py STRIDED), as
-// every block streams its own DRAM pages and its packets' table rows stay
-// near each other in its XCD's L2.
+// dealing tiles round-robin over all waves, and 10 % faster than an
+// XCD-aware range order, as every block streams its own DRAM
+// pages and its packets' table rows stay near each other in its XCD's L2.
+// `cur` is kBins + 1 LDS counters, zeroed by the kernel before its barrier.
 template <class Issue, class Finish>
 __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
                                                const uint16_t *len,
@@ -273,8 +284,9 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
                                                uint32_t n_all, uint4 *S,
                                                const uint4 *rows, Issue issue,
                                                Finish finish,
-                                               const TouchBins &bins = TouchBins{},
-                                               uint32_t *cur = nullptr) {
+                                               const TouchBins &bins,
+                                               const TileQueue &rq,
+                                               uint32_t *cur) {
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t first = p0 & ~63u;
   const uint32_t tiles = (p1 - first + 63) / 64;
@@ -293,20 +305,11 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
     m_in = p < n_all ? in_dev[p] : 0u;
     m_len = p < n_all ? len[p] : 0u;
   };
-#ifdef VP_ABL_STRIDED  // diagnostic: tiles dealt round-robin over all waves
-  uint32_t tile = blockIdx.x * 4 + wv;
-  const uint32_t tend = tiles, tstep = gridDim.x * 4;
-#else
-#ifdef VP_ABL_XCD  // diagnostic: XCD x (= block % 8) owns the x-th eighth
-  const uint32_t rb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-#else
   const uint32_t rb = blockIdx.x;
-#endif
   const uint32_t per_b = (tiles + gridDim.x - 1) / gridDim.x;
   uint32_t tile = rb * per_b + wv;
   const uint32_t tend = min(tiles, rb * per_b + per_b), tstep = 4;
   const uint32_t range0 = first + rb * per_b * 64;  // this block's first packet
-#endif
   if (tile < tend) fetch(tile);
   for (; tile < tend; tile += tstep) {
     const uint32_t tb = first + tile * 64;
@@ -350,7 +353,12 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
     bool mod = false;
     uint32_t touch = kNone;
     if (mine) mod = finish(pend, row, p, f, in, ln, touch);
-#ifndef VP_ABL_STRIDED
+    if (rq.ent) {  // queue on this block's reprobe slice
+      const bool v = touch == kReprobe;
+      const uint32_t k = group_reserve(cur, kBins, v);
+      if (v) rq.ent[(size_t)rb * per_b * 64 + k] = p;
+    }
+    if (touch == kReprobe) touch = kNone;
     if (bins.ent) {  // append to this block's slice of the touch's bin
       const bool v = touch != kNone;
       const uint32_t b = v ? bin_of(touch) : 0;
@@ -359,7 +367,6 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
         bins.ent[((size_t)rb * kBins + b) * bins.cap + k] =
             (bin_local(touch) << bins.pbits) | (p - range0);
     }
-#endif
     if (mod) {
 #pragma unroll
       for (uint32_t k = 0; k < 4; k++)
@@ -375,16 +382,19 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
     }
     wave_lds_sync();  // the next tile overwrites S
   }
-#ifndef VP_ABL_STRIDED
+  if (bins.ent || rq.ent) __syncthreads();
   if (bins.ent) {  // publish this block's slice sizes
-    __syncthreads();
     for (uint32_t b = threadIdx.x; b < kBins; b += blockDim.x) {
       const uint32_t c = cur[b];
       bins.cnt[(size_t)rb * kBins + b] = c < bins.cap ? c : bins.cap;
       if (c > bins.cap) *bins.ovf = 1;
     }
   }
-#endif
+  if (rq.ent && threadIdx.x == 0) {
+    const uint32_t c = cur[kBins];
+    rq.cnt[rb] = c;
+    if (c) atomicAdd(rq.total, c);
+  }
 }
 
 // Checksums of a 64-byte IHL=5 frame with total_length <= 50 (so every byte

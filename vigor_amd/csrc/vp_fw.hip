@@ -62,6 +62,8 @@ struct FwArgs {
   const uint32_t *macw;  // per device: d_addr|s_addr header words
   uint32_t *miss;
   uint32_t *defer;
+  uint32_t *reprobe;
+  uint32_t tileq;  // 64-byte tiles: reprobes go to the block's TileQueue slice
   uint16_t wan, n_dev;
 };
 
@@ -186,9 +188,16 @@ __device__ __forceinline__ bool fw_finish(const FwArgs &a, const uint32_t *T,
   fw_key(wan, sp, dp, sip, dip, proto, key);
   bool done;
   uint32_t w3 = 0;
-  uint32_t idx = bucket_match<0xFFu>(row[0], row[1], row[2], row[3], key, &done, &w3);
-  if (!done)  // the home bucket is full of other keys: rest of the path
-    idx = tbl_probe_from<0xFFu>(a.t, (P.row + 1) & a.t.bmask, key, a.t.bmask, &w3);
+  const uint32_t idx =
+      bucket_match<0xFFu>(row[0], row[1], row[2], row[3], key, &done, &w3);
+  if (!done) {  // the home bucket is full of other keys: fw_reprobe walks on
+    a.log[p] = kNone;
+    if (a.tileq)
+      touch = kReprobe;
+    else
+      a.reprobe[wave_append(&a.t.ctl->reprobe_count, true)] = p;
+    return false;
+  }
   if (idx == kNone) {
     if (wan)
       a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
@@ -225,11 +234,11 @@ __global__ __launch_bounds__(256) void fw_classify(FwArgs a) {
 
 // Phase A for 64-byte slots: LDS-staged coalesced frame I/O.
 __global__ __launch_bounds__(256, 4) void fw_classify64(FwArgs a, uint32_t n_all,
-                                                       TouchBins bins) {
+                                                       TouchBins bins, TileQueue rq) {
   __shared__ uint32_t T[kFwTabs * 256];
   __shared__ uint4 stage[4][256];
-  __shared__ uint32_t cur[kBins];
-  for (uint32_t i = threadIdx.x; i < kBins; i += blockDim.x) cur[i] = 0;
+  __shared__ uint32_t cur[kBins + 1];
+  for (uint32_t i = threadIdx.x; i <= kBins; i += blockDim.x) cur[i] = 0;
   fw_load_tables(T, a.crc_tab);  // (its barrier also covers cur)
   frames64_tiles(
       a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
@@ -241,7 +250,59 @@ __global__ __launch_bounds__(256, 4) void fw_classify64(FwArgs a, uint32_t n_all
           uint32_t len, uint32_t &touch) {
         return fw_finish(a, T, P, row, p, f, in, len, touch);
       },
-      bins, cur);
+      bins, rq, cur);
+}
+
+// Packets whose home bucket held three other keys: the rest of the probe
+// path, then phase A's handling (fw_generic_a from the next bucket on).
+__device__ void fw_reprobe_one(const FwArgs &a, uint32_t p) {
+  {
+    const uint32_t in = a.in_dev[p];
+    GFrame f{a.frames + (size_t)p * a.slot, a.slot};
+    const L34 h = parse_l34(f, a.len[p]);
+    const uint32_t proto = f.r8(h.ip + 9);
+    const uint32_t sp = f.r16(h.l4), dp = f.r16(h.l4 + 2);
+    const uint32_t sip = f.r32(h.ip + 12), dip = f.r32(h.ip + 16);
+    const bool wan = in == a.wan;
+    uint32_t key[4];
+    fw_key(wan, sp, dp, sip, dip, proto, key);
+    const uint32_t hh = wan ? fw_hash(a.crc_tab, dp, sp, dip, sip, proto)
+                            : fw_hash(a.crc_tab, sp, dp, sip, dip, proto);
+    const uint32_t b = home_bucket(hh, a.t.bmask, a.t.mix);
+    uint32_t w3 = 0;
+    const uint32_t idx =
+        tbl_probe_from<0xFFu>(a.t, (b + 1) & a.t.bmask, key, a.t.bmask, &w3);
+    const bool miss = idx == kNone;
+    const uint32_t at_d = wave_append(&a.t.ctl->defer_count, miss && wan);
+    const uint32_t at_m = wave_append(&a.t.ctl->miss_count, miss && !wan);
+    if (miss) {
+      if (wan)
+        a.defer[at_d] = p;
+      else
+        a.miss[at_m] = p;
+      return;
+    }
+    a.log[p] = idx;
+    const uint32_t dst = wan ? (w3 >> 8) : a.wan;
+    uint32_t mw[3];
+    fw_macs(a, dst, mw);
+    set_macs(f, mw);
+    a.out[p] = (uint16_t)dst;
+  }
+}
+
+// The queue: per-block slices (cnt != null) or one list of n positions.
+__global__ void fw_reprobe(FwArgs a, const uint32_t *list, uint32_t n,
+                           const uint32_t *cnt, uint32_t range, uint32_t nblk) {
+  if (cnt) {
+    for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x)
+      for (uint32_t k = threadIdx.x; k < cnt[b]; k += blockDim.x)
+        fw_reprobe_one(a, list[(size_t)b * range + k]);
+    return;
+  }
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += gridDim.x * blockDim.x)
+    fw_reprobe_one(a, list[j]);
 }
 
 // ------------------------------------------------------------- phase B --
@@ -349,20 +410,28 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.macw = c->macw;
   a.miss = w.miss;
   a.defer = w.defer;
+  a.reprobe = w.reprobe;
   a.wan = c->fw.wan_device;
   a.n_dev = c->fw.n_devices;
 
   // 64-byte slots: the classify launch also bins its touches (TouchBins)
   const bool tiles64 = p1 > p0 && b->slot == 64 && c->coalesced_io;
   BinsPlan bp{};
-  if (tiles64) VP_TRY(tbl_bins_plan(c, t, (const void *)fw_classify64, p0, p1, &bp));
-  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 12, c->stream));  // + defer, ovf
+  uint32_t grid64 = 0, range64 = 0;
+  TileQueue rq{};
+  if (tiles64) {
+    VP_TRY(tbl_bins_plan(c, t, (const void *)fw_classify64, p0, p1, &bp));
+    const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
+    grid64 = resident_grid((const void *)fw_classify64, (tiles + 3) / 4);
+    range64 = (tiles + grid64 - 1) / grid64 * 64;
+    rq = TileQueue{w.reprobe, w.reprobe_cnt, &t.ctl->reprobe_count};
+    a.tileq = 1;
+  }
+  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   if (p1 > p0) {
     if (tiles64) {
-      const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
-      fw_classify64<<<resident_grid((const void *)fw_classify64, (tiles + 3) / 4), 256,
-                      0, c->stream>>>(a, b->n, bp.bins);
+      fw_classify64<<<grid64, 256, 0, c->stream>>>(a, b->n, bp.bins, rq);
     } else {
       fw_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
     }
@@ -376,7 +445,18 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   else
     VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
   VP_TRY(read_ctl(c, t));
-  const bool refold = bp.on && t.h_ctl.touch_ovf;
+  bool refold = bp.on && t.h_ctl.touch_ovf;
+  if (const uint32_t nre = t.h_ctl.reprobe_count) {
+    if (tiles64)
+      fw_reprobe<<<std::min<uint32_t>(grid64, 2048), 256, 0, c->stream>>>(
+          a, w.reprobe, nre, w.reprobe_cnt, range64, grid64);
+    else
+      fw_reprobe<<<grid_for(nre), 256, 0, c->stream>>>(a, w.reprobe, nre, nullptr, 0,
+                                                      0);
+    VP_HIP(hipGetLastError());
+    VP_TRY(read_ctl(c, t));  // the walk may have found new flows
+    refold = true;           // its hits are in the log, not in the bins
+  }
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
   *ms += kms;

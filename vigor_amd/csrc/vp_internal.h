@@ -41,9 +41,10 @@ struct Ctl {
   uint32_t fresh_next;  // first never-allocated index
   uint32_t n_live;
   uint32_t n_tomb;
-  uint32_t miss_count;   // } reset together at the start of a segment
-  uint32_t defer_count;  // }
-  uint32_t touch_ovf;    // } a touch-bin slice overflowed (TouchBins)
+  uint32_t miss_count;     // } reset together at the start of a segment
+  uint32_t defer_count;    // }
+  uint32_t touch_ovf;      // } a touch-bin slice overflowed (TouchBins)
+  uint32_t reprobe_count;  // } home bucket full of other keys (vp_nat.hip)
   uint32_t exp_count;
   uint32_t tomb_reused;
   uint64_t min_ts;
@@ -81,6 +82,8 @@ struct Workspace {
   uint32_t *miss = nullptr;
   uint32_t *miss_sorted = nullptr;
   uint32_t *defer = nullptr;
+  uint32_t *reprobe = nullptr;  // packets whose probe continues past the home bucket
+  uint32_t *reprobe_cnt = nullptr;  // per classify block (TileQueue)
   uint32_t *mkey = nullptr;  // 4 words per miss
   uint32_t *mhash = nullptr;
   uint32_t *first = nullptr;

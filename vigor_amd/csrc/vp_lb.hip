@@ -285,7 +285,8 @@ __global__ __launch_bounds__(256) void lb_classify64(LbArgs a, uint32_t n_all) {
         return NoPend{kNone};
       },
       [&](NoPend, const uint4 *, uint32_t p, RFrame &f, uint32_t in, uint32_t len,
-          uint32_t &) { return lb_fast(a, T, p, f, in, len); });
+          uint32_t &) { return lb_fast(a, T, p, f, in, len); },
+      TouchBins{}, TileQueue{}, nullptr);
 }
 
 __global__ __launch_bounds__(256) void lb_classify(LbArgs a) {

@@ -64,6 +64,8 @@ struct NatArgs {
   uint32_t wan_macw0, wan_macw1, wan_macw2;
   uint32_t *miss;
   uint32_t *defer;
+  uint32_t *reprobe;
+  uint32_t tileq;  // 64-byte tiles: reprobes go to the block's TileQueue slice
   uint32_t ext_ip;
   uint16_t wan, start_port, n_dev;
 };
@@ -254,9 +256,16 @@ __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
     const uint32_t idx = P.b & (a.t.cap - 1);
 #else
     bool done;
-    uint32_t idx = bucket_match(row[0], row[1], row[2], row[3], key, &done);
-    if (!done)  // the home bucket is full of other keys: rest of the path
-      idx = tbl_probe_from(a.t, (P.b + 1) & a.t.bmask, key, a.t.bmask);
+    const uint32_t idx = bucket_match(row[0], row[1], row[2], row[3], key, &done);
+    if (!done) {  // the home bucket is full of other keys: nat_reprobe walks
+      // the rest of the path, so this wave does not wait for a dependent read
+      a.log[p] = kNone;
+      if (a.tileq)
+        touch = kReprobe;
+      else
+        a.reprobe[wave_append(&a.t.ctl->reprobe_count, true)] = p;
+      return false;
+    }
 #endif
     if (idx == kNone) {  // new flow, or not yet visible: phase B
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
@@ -341,17 +350,12 @@ __global__ __launch_bounds__(256) void nat_classify(NatArgs a) {
 
 // Phase A for 64-byte slots: LDS-staged 1 KiB-contiguous frame I/O
 // (frames64_tiles, vp_device.h); each wave owns 64 consecutive packets.
-#if defined(VP_ABL_OCC5)  // diagnostic: 5 blocks per CU (96 VGPRs, spills)
-#define VP_NAT64_MINB 5
-#else
-#define VP_NAT64_MINB 4
-#endif
-__global__ __launch_bounds__(256, VP_NAT64_MINB) void nat_classify64(NatArgs a, uint32_t n_all,
-                                                                TouchBins bins) {
+__global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_all,
+                                                        TouchBins bins, TileQueue rq) {
   __shared__ uint32_t T[15 * 256];
   __shared__ uint4 stage[4][256];
-  __shared__ uint32_t cur[kBins];
-  for (uint32_t i = threadIdx.x; i < kBins; i += blockDim.x) cur[i] = 0;
+  __shared__ uint32_t cur[kBins + 1];
+  for (uint32_t i = threadIdx.x; i <= kBins; i += blockDim.x) cur[i] = 0;
   load_crc_tables(T, a.crc_tab);  // (its barrier also covers cur)
   frames64_tiles(
       a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
@@ -363,7 +367,7 @@ __global__ __launch_bounds__(256, VP_NAT64_MINB) void nat_classify64(NatArgs a, 
           uint32_t len, uint32_t &touch) {
         return nat_finish(a, T, P, row, p, f, in, len, touch);
       },
-      bins, cur);
+      bins, rq, cur);
 }
 
 // ------------------------------------------------------------- phase B --
@@ -415,6 +419,46 @@ __global__ void nat_miss_finish(NatArgs a, const uint32_t *list, uint32_t n,
     }
     nat_write_lan(a, p, idx);
   }
+}
+
+// LAN packets whose home bucket held three other keys: the rest of the probe
+// path (map_get's find_key walk, map-impl-pow2.c:629-732), then the same
+// hit / miss handling as phase A.
+__device__ void nat_reprobe_one(const NatArgs &a, uint32_t p) {
+  {
+    GFrame f{a.frames + (size_t)p * a.slot, a.slot};
+    const L34 h = parse_l34(f, a.len[p]);
+    const uint32_t proto = f.r8(h.ip + 9), in = a.in_dev[p];
+    const uint32_t sp = f.r16(h.l4), dp = f.r16(h.l4 + 2);
+    const uint32_t sip = f.r32(h.ip + 12), dip = f.r32(h.ip + 16);
+    const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
+    const uint32_t hh = flowid_hash(a.crc_tab, sp, dp, sip, dip, in, proto);
+    const uint32_t b = home_bucket(hh, a.t.bmask, a.t.mix);
+    const uint32_t idx = tbl_probe_from(a.t, (b + 1) & a.t.bmask, key, a.t.bmask);
+    const bool miss = idx == kNone;  // new flow, or not yet visible: phase B
+    const uint32_t at = wave_append(&a.t.ctl->miss_count, miss);
+    if (miss) {
+      a.miss[at] = p;
+      return;
+    }
+    a.log[p] = idx;
+    nat_write_lan(a, p, idx);
+  }
+}
+
+// The queue: per-block slices (cnt != null: slice b holds cnt[b] positions
+// at list + b * range) or one list of n positions.
+__global__ void nat_reprobe(NatArgs a, const uint32_t *list, uint32_t n,
+                            const uint32_t *cnt, uint32_t range, uint32_t nblk) {
+  if (cnt) {
+    for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x)
+      for (uint32_t k = threadIdx.x; k < cnt[b]; k += blockDim.x)
+        nat_reprobe_one(a, list[(size_t)b * range + k]);
+    return;
+  }
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += gridDim.x * blockDim.x)
+    nat_reprobe_one(a, list[j]);
 }
 
 // ------------------------------------------------------------- phase C --
@@ -487,22 +531,31 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.wan_macw2 = c->wan_macw[2];
   a.miss = w.miss;
   a.defer = w.defer;
+  a.reprobe = w.reprobe;
   a.ext_ip = c->nat.external_addr;
   a.wan = c->nat.wan_device;
   a.start_port = c->nat.start_port;
   a.n_dev = c->nat.n_devices;
 
   // 64-byte slots: the classify launch also bins its touches (TouchBins)
+  // and queues reprobes per block (TileQueue)
   const bool tiles64 = p1 > p0 && b->slot == 64 && c->coalesced_io;
   BinsPlan bp{};
-  if (tiles64) VP_TRY(tbl_bins_plan(c, t, (const void *)nat_classify64, p0, p1, &bp));
-  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 12, c->stream));  // + defer, ovf
+  uint32_t grid64 = 0, range64 = 0;
+  TileQueue rq{};
+  if (tiles64) {
+    VP_TRY(tbl_bins_plan(c, t, (const void *)nat_classify64, p0, p1, &bp));
+    const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
+    grid64 = resident_grid((const void *)nat_classify64, (tiles + 3) / 4);
+    range64 = (tiles + grid64 - 1) / grid64 * 64;
+    rq = TileQueue{w.reprobe, w.reprobe_cnt, &t.ctl->reprobe_count};
+    a.tileq = 1;
+  }
+  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   if (p1 > p0) {
     if (tiles64) {
-      const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
-      nat_classify64<<<resident_grid((const void *)nat_classify64, (tiles + 3) / 4),
-                       256, 0, c->stream>>>(a, b->n, bp.bins);
+      nat_classify64<<<grid64, 256, 0, c->stream>>>(a, b->n, bp.bins, rq);
     } else {
       nat_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
     }
@@ -517,7 +570,18 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   else
     VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
   VP_TRY(read_ctl(c, t));
-  const bool refold = bp.on && t.h_ctl.touch_ovf;
+  bool refold = bp.on && t.h_ctl.touch_ovf;
+  if (const uint32_t nre = t.h_ctl.reprobe_count) {
+    if (tiles64)
+      nat_reprobe<<<std::min<uint32_t>(grid64, 2048), 256, 0, c->stream>>>(
+          a, w.reprobe, nre, w.reprobe_cnt, range64, grid64);
+    else
+      nat_reprobe<<<grid_for(nre), 256, 0, c->stream>>>(a, w.reprobe, nre, nullptr,
+                                                       0, 0);
+    VP_HIP(hipGetLastError());
+    VP_TRY(read_ctl(c, t));  // the walk may have found new flows
+    refold = true;           // its hits are in the log, not in the bins
+  }
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
   *ms += kms;

@@ -64,12 +64,13 @@ static void ws_release(Workspace &w) {
                   w.first, w.rank,        w.rep,   w.assign, w.scratch,
                   w.log,   w.iota,        w.skey,  w.sval,
                   w.log2,  w.defer_sorted, w.aux,  w.aux_sorted, w.rlist,
-                  w.unow};
+                  w.unow,  w.reprobe,     w.reprobe_cnt};
   for (void *p : ptrs) hipFree(p);
   w.miss = w.miss_sorted = w.defer = w.mkey = w.mhash = w.first = w.rank =
       w.rep = w.assign = w.scratch = w.log = w.iota = w.skey = w.sval = nullptr;
   w.log2 = w.defer_sorted = w.aux = w.aux_sorted = w.rlist = nullptr;
   w.unow = nullptr;
+  w.reprobe = w.reprobe_cnt = nullptr;
   w.cap_n = 0;
 }
 
@@ -84,6 +85,8 @@ int ws_reserve(vp_ctx *c, uint32_t n) {
   VP_TRY(dalloc(&w.miss, cap));
   VP_TRY(dalloc(&w.miss_sorted, cap));
   VP_TRY(dalloc(&w.defer, cap));
+  VP_TRY(dalloc(&w.reprobe, cap + 128));  // per-block slices end on tile bounds
+  VP_TRY(dalloc(&w.reprobe_cnt, 4096));   // >= any resident grid
   VP_TRY(dalloc(&w.mkey, 4ull * cap));
   VP_TRY(dalloc(&w.mhash, cap));
   VP_TRY(dalloc(&w.first, cap));
