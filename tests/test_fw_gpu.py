@@ -159,6 +159,7 @@ def test_multiplicative_home_buckets_reprobe(monkeypatch):
     """VIGPATH_MIX=1 at load 0.65: full home buckets finish in fw_reprobe
     (LAN hits, WAN replies and new flows alike)."""
     monkeypatch.setenv("VIGPATH_MIX", "1")
+    monkeypatch.setenv("VIGPATH_SPARSE", "-1")  # load 2/3: many reprobes
     fw, o = make_pair(max_flows=4096)
     fr, ln, dv, now = T.fw_trace(4000, 4000)
     check_batches(fw, o, fr, ln, dv, now, 64, [1500])

@@ -197,21 +197,28 @@ def test_touch_bins_steady_state(n_flows, order):
         check_state(nat, o, 1 << 17)
 
 
-@pytest.mark.parametrize("order", ["rr", "uniform"])
-def test_multiplicative_home_buckets_reprobe(order, monkeypatch):
+@pytest.mark.parametrize("order,slot", [("rr", 64), ("uniform", 64), ("rr", 128)])
+def test_multiplicative_home_buckets_reprobe(order, slot, monkeypatch):
     """With the multiplicative home-bucket spread (VIGPATH_MIX=1, the layout
     the table rebuilds into for clustering key sets) a full home bucket is
     common at load 0.65: those packets leave the classify wave and finish in
-    nat_reprobe. Outputs and state equal the oracle's."""
+    nat_reprobe (per-block slices for 64-byte tiles, one list for the
+    per-lane path of wider slots). Outputs and state equal the oracle's."""
     monkeypatch.setenv("VIGPATH_MIX", "1")
+    monkeypatch.setenv("VIGPATH_SPARSE", "-1")  # load 2/3: many reprobes
+    def wide(fr):  # 64-byte slots -> `slot`-byte slots, zero padded
+        w = np.zeros((fr.size // 64, slot), np.uint8)
+        w[:, :64] = fr.reshape(-1, 64)
+        return w.reshape(-1)
+
     nat, o = make_pair(max_flows=4096)
     fr, ln, dv, now = T.nat_lan_trace(4000, 4000)
-    check_batches(nat, o, fr, ln, dv, now, 64, [1000])
+    check_batches(nat, o, wide(fr), ln, dv, now, slot, [1000])
     fr, ln, dv, now = T.nat_lan_trace(60_000, 4000, order=order, start=4000)
-    check_batches(nat, o, fr, ln, dv, now, 64, [30_000])
+    check_batches(nat, o, wide(fr), ln, dv, now, slot, [30_000])
     check_state(nat, o, 4096)
     rng = np.random.default_rng(9)
     fr, ln, dv, now = mixed_nat_trace(rng, 5000, 3000, max_idx=4096)
     now = now + 10**8
-    check_batches(nat, o, fr, ln, dv, now, 64, [2000])
+    check_batches(nat, o, wide(fr), ln, dv, now, slot, [2000])
     check_state(nat, o, 4096)

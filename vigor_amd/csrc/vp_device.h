@@ -397,6 +397,131 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
   }
 }
 
+// Wave-cooperative 64-byte row gather (wave-uniform call): lane L receives
+// the 64 bytes at base + row_L * stride (row_L == kNone: zeros). Four lanes
+// fetch each row as one contiguous request and the wave's LDS tile S
+// (256 x 16 B) hands every lane its own row, as in frames64_tiles. A lane
+// loading its own row as four 16-byte pieces costs four requests instead.
+__device__ __forceinline__ void wave_gather64(const uint8_t *base, size_t stride,
+                                              uint32_t row, uint4 *S, uint4 out[4]) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint4 q[4];
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t r = __shfl(row, 16 * j + (lane >> 2));
+    q[j] = r != kNone
+               ? reinterpret_cast<const uint4 *>(base + (size_t)r * stride)[lane & 3]
+               : make_uint4(0, 0, 0, 0);
+  }
+  wave_lds_sync();  // earlier readers of S are done
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = q[j];
+  wave_lds_sync();
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) out[k] = S[chunk_swz(4 * lane + k)];
+}
+
+// The inverse: the lanes with `st` store their 64 bytes at base + row * stride,
+// four lanes per row.
+__device__ __forceinline__ void wave_scatter64(uint8_t *base, size_t stride,
+                                               uint32_t row, bool st, const uint4 v[4],
+                                               uint4 *S) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t m = __ballot(st);
+  if (!m) return;
+  wave_lds_sync();
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) S[chunk_swz(4 * lane + k)] = v[k];
+  wave_lds_sync();
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t c = 64 * j + lane;
+    const uint32_t r = __shfl(row, c >> 2);
+    if ((m >> (c >> 2)) & 1ull)
+      reinterpret_cast<uint4 *>(base + (size_t)r * stride)[lane & 3] = S[chunk_swz(c)];
+  }
+}
+
+// Reprobes: the packets a classify kernel queued because their home bucket
+// held three other keys (touch == kReprobe), finished on the same register
+// path with the probe walked on bucket by bucket (map_get's find_key,
+// map-impl-pow2.c:629-732). Frames and buckets come in by wave_gather64, one
+// request per row; finish() answering kReprobe again asks for the next bucket
+// (it must leave no other trace in that case). Up to 64 packets per wave
+// (act); wave-uniform call. Returns the lane's touch (kNone if none).
+template <class Issue, class Finish>
+__device__ __forceinline__ uint32_t reprobe_wave(uint8_t *frames, uint32_t slot,
+                                                 const uint16_t *len,
+                                                 const uint16_t *in_dev,
+                                                 const uint8_t *buckets, uint32_t bmask,
+                                                 uint32_t p, bool act, uint4 *S,
+                                                 Issue issue, Finish finish) {
+  uint4 fr[4];
+  wave_gather64(frames, slot, act ? p : kNone, S, fr);
+  RFrame f;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) {
+    f.w[4 * k] = fr[k].x;
+    f.w[4 * k + 1] = fr[k].y;
+    f.w[4 * k + 2] = fr[k].z;
+    f.w[4 * k + 3] = fr[k].w;
+  }
+  const uint32_t in = act ? in_dev[p] : 0u, ln = act ? len[p] : 0u;
+  const auto pend = issue(p, f, in, ln, act);
+  uint32_t want = act ? pend.row : kNone;
+  bool live = act, mod = false;
+  uint32_t touch = kNone;
+  for (uint32_t step = 0;; step++) {
+    uint4 row[4];
+    wave_gather64(buckets, 64, live ? want : kNone, S, row);
+    if (live) {
+      touch = kNone;
+      mod = finish(pend, row, p, f, in, ln, touch);
+    }
+    live = live && touch == kReprobe && step < bmask;
+    if (!__ballot(live)) break;
+    if (live) want = (want + 1) & bmask;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++)
+    fr[k] = make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
+  wave_scatter64(frames, slot, p, mod, fr, S);
+  return touch == kReprobe ? kNone : touch;
+}
+
+// The reprobe queue: slice b holds cnt[b] packets at list + b * range (one
+// slice per classify block), or with cnt == null slice b is the b-th run of
+// `range` packets of one list of n.
+__device__ __forceinline__ uint32_t reprobe_slice_len(const uint32_t *cnt, uint32_t n,
+                                                      uint32_t range, uint32_t b) {
+  return cnt ? cnt[b] : (n - b * range < range ? n - b * range : range);
+}
+
+// The reprobe kernels' loop: each block works whole slices, its waves 64
+// packets at a time (`lane_fn(p, act)` runs reprobe_wave). The segment's
+// touches were already folded into ts/tseq without these packets, so each
+// touch raises tseq[i] to its sequence (atomicMax); tbl_reprobe_stamp then
+// gives ts[i] the time of the packet that won (last toucher, exact).
+template <class LaneFn>
+__device__ __forceinline__ void reprobe_slices(const uint32_t *list, const uint32_t *cnt,
+                                               uint32_t n, uint32_t range,
+                                               uint32_t nblk, uint64_t *tseq,
+                                               uint64_t seq_base, LaneFn lane_fn) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const uint32_t nb = reprobe_slice_len(cnt, n, range, b);
+    for (uint32_t k0 = 64 * wv; k0 < nb; k0 += blockDim.x) {  // wave-uniform
+      const uint32_t k = k0 + lane;
+      const bool act = k < nb;
+      const uint32_t p = act ? list[(size_t)b * range + k] : 0u;
+      const uint32_t touch = lane_fn(p, act);
+      if (touch != kNone)
+        atomicMax(reinterpret_cast<unsigned long long *>(tseq + touch),
+                  (unsigned long long)(seq_base + p));
+    }
+  }
+}
+
 // Checksums of a 64-byte IHL=5 frame with total_length <= 50 (so every byte
 // the L4 sum covers lies in the slot). Same arithmetic as set_checksums.
 __device__ inline void fast_checksums(RFrame &f, uint32_t proto, uint32_t tl) {

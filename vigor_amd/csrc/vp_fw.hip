@@ -190,8 +190,8 @@ __device__ __forceinline__ bool fw_finish(const FwArgs &a, const uint32_t *T,
   uint32_t w3 = 0;
   const uint32_t idx =
       bucket_match<0xFFu>(row[0], row[1], row[2], row[3], key, &done, &w3);
-  if (!done) {  // the home bucket is full of other keys: fw_reprobe walks on
-    a.log[p] = kNone;
+  if (!done) {  // the bucket is full of other keys: fw_reprobe walks on,
+    a.log[p] = kNone;  // so this wave does not wait for a dependent read
     if (a.tileq)
       touch = kReprobe;
     else
@@ -253,56 +253,30 @@ __global__ __launch_bounds__(256, 4) void fw_classify64(FwArgs a, uint32_t n_all
       bins, rq, cur);
 }
 
-// Packets whose home bucket held three other keys: the rest of the probe
-// path, then phase A's handling (fw_generic_a from the next bucket on).
-__device__ void fw_reprobe_one(const FwArgs &a, uint32_t p) {
-  {
-    const uint32_t in = a.in_dev[p];
-    GFrame f{a.frames + (size_t)p * a.slot, a.slot};
-    const L34 h = parse_l34(f, a.len[p]);
-    const uint32_t proto = f.r8(h.ip + 9);
-    const uint32_t sp = f.r16(h.l4), dp = f.r16(h.l4 + 2);
-    const uint32_t sip = f.r32(h.ip + 12), dip = f.r32(h.ip + 16);
-    const bool wan = in == a.wan;
-    uint32_t key[4];
-    fw_key(wan, sp, dp, sip, dip, proto, key);
-    const uint32_t hh = wan ? fw_hash(a.crc_tab, dp, sp, dip, sip, proto)
-                            : fw_hash(a.crc_tab, sp, dp, sip, dip, proto);
-    const uint32_t b = home_bucket(hh, a.t.bmask, a.t.mix);
-    uint32_t w3 = 0;
-    const uint32_t idx =
-        tbl_probe_from<0xFFu>(a.t, (b + 1) & a.t.bmask, key, a.t.bmask, &w3);
-    const bool miss = idx == kNone;
-    const uint32_t at_d = wave_append(&a.t.ctl->defer_count, miss && wan);
-    const uint32_t at_m = wave_append(&a.t.ctl->miss_count, miss && !wan);
-    if (miss) {
-      if (wan)
-        a.defer[at_d] = p;
-      else
-        a.miss[at_m] = p;
-      return;
-    }
-    a.log[p] = idx;
-    const uint32_t dst = wan ? (w3 >> 8) : a.wan;
-    uint32_t mw[3];
-    fw_macs(a, dst, mw);
-    set_macs(f, mw);
-    a.out[p] = (uint16_t)dst;
-  }
-}
-
-// The queue: per-block slices (cnt != null) or one list of n positions.
-__global__ void fw_reprobe(FwArgs a, const uint32_t *list, uint32_t n,
-                           const uint32_t *cnt, uint32_t range, uint32_t nblk) {
-  if (cnt) {
-    for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x)
-      for (uint32_t k = threadIdx.x; k < cnt[b]; k += blockDim.x)
-        fw_reprobe_one(a, list[(size_t)b * range + k]);
-    return;
-  }
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
-       j += gridDim.x * blockDim.x)
-    fw_reprobe_one(a, list[j]);
+// Packets whose home bucket held three other keys finish here, queued per
+// classify block (TileQueue): phase A's register path with the probe walked
+// on bucket by bucket (reprobe_wave); their touches join the block's bins.
+__global__ __launch_bounds__(256) void fw_reprobe(FwArgs a, const uint32_t *list,
+                                                  const uint32_t *cnt, uint32_t n,
+                                                  uint32_t range, uint32_t nblk,
+                                                  uint64_t seq_base) {
+  __shared__ uint32_t T[kFwTabs * 256];
+  __shared__ uint4 stage[4][256];
+  fw_load_tables(T, a.crc_tab);
+  a.tileq = 1;  // a full bucket answers kReprobe: reprobe_wave walks on
+  uint4 *S = stage[threadIdx.x >> 6];
+  reprobe_slices(list, cnt, n, range, nblk, a.t.tseq, seq_base, [&](uint32_t p, bool act) {
+    return reprobe_wave(
+        a.frames, a.slot, a.len, a.in_dev, reinterpret_cast<const uint8_t *>(a.t.bk),
+        a.t.bmask, p, act, S,
+        [&](uint32_t q, const RFrame &f, uint32_t in, uint32_t len, bool mine) {
+          return fw_issue(a, T, q, f, in, len, mine);
+        },
+        [&](const FwPend &P, const uint4 *row, uint32_t q, RFrame &f, uint32_t in,
+            uint32_t len, uint32_t &touch) {
+          return fw_finish(a, T, P, row, q, f, in, len, touch);
+        });
+  });
 }
 
 // ------------------------------------------------------------- phase B --
@@ -445,18 +419,17 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   else
     VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
   VP_TRY(read_ctl(c, t));
-  bool refold = bp.on && t.h_ctl.touch_ovf;
-  if (const uint32_t nre = t.h_ctl.reprobe_count) {
-    if (tiles64)
-      fw_reprobe<<<std::min<uint32_t>(grid64, 2048), 256, 0, c->stream>>>(
-          a, w.reprobe, nre, w.reprobe_cnt, range64, grid64);
-    else
-      fw_reprobe<<<grid_for(nre), 256, 0, c->stream>>>(a, w.reprobe, nre, nullptr, 0,
-                                                      0);
+  // reprobes come only from the 64-byte tiles (fw_generic_a walks in place)
+  const uint32_t nre = t.h_ctl.reprobe_count;
+  if (nre) {  // probes past a full home bucket: finish them, patch the fold
+    fw_reprobe<<<std::min<uint32_t>(grid64, 2048), 256, 0, c->stream>>>(
+        a, w.reprobe, w.reprobe_cnt, nre, range64, grid64, seq0);
     VP_HIP(hipGetLastError());
+    VP_TRY(tbl_reprobe_stamp(c, t, w.reprobe, w.reprobe_cnt, nre, range64, grid64,
+                             w.log, now, seq0));
     VP_TRY(read_ctl(c, t));  // the walk may have found new flows
-    refold = true;           // its hits are in the log, not in the bins
   }
+  const bool refold = bp.on && t.h_ctl.touch_ovf != 0;
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
   *ms += kms;

@@ -50,8 +50,8 @@ struct Ctl {
   uint64_t min_ts;
   uint32_t new_count;
   uint32_t aux_count;
-  uint32_t max_disp;  // longest insert probe (buckets) since last check
-  uint32_t pad;
+  uint32_t max_disp;    // longest insert probe (buckets) since last check
+  uint32_t disp_count;  // inserts that passed their home bucket (since rebuild)
 };
 
 // One device table (see vp_table.h).
@@ -60,6 +60,7 @@ struct FlowTable {
   uint32_t bmask = 0;  // buckets - 1
   uint32_t cap = 0;
   uint32_t mix = 0;    // home-bucket mode (vp_table.h home_bucket)
+  uint64_t ins_since = 0;  // inserts since the last rebuild (mode check)
   uint32_t *slot_of = nullptr;
   uint32_t *hash_of = nullptr;
   uint64_t *ts = nullptr;

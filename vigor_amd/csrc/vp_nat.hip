@@ -257,8 +257,8 @@ __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
 #else
     bool done;
     const uint32_t idx = bucket_match(row[0], row[1], row[2], row[3], key, &done);
-    if (!done) {  // the home bucket is full of other keys: nat_reprobe walks
-      // the rest of the path, so this wave does not wait for a dependent read
+    if (!done) {  // the bucket is full of other keys: nat_reprobe walks the
+      // rest of the path, so this wave does not wait for a dependent read
       a.log[p] = kNone;
       if (a.tileq)
         touch = kReprobe;
@@ -294,6 +294,55 @@ __device__ __forceinline__ void load_crc_tables(uint32_t *T, const uint32_t *g) 
   __syncthreads();
 }
 
+// One packet, its slot's first 64 bytes in registers (any slot size; frames
+// outside the fast path take nat_generic_a). Returns the logged index.
+__device__ __forceinline__ uint32_t nat_lane(const NatArgs &a, const uint32_t *T,
+                                             uint32_t p) {
+#ifdef VP_ABL_NOFRAME  // diagnostic: synthesise the bench trace's frame
+  uint4 *fp = reinterpret_cast<uint4 *>(a.frames + (size_t)(p & 63) * a.slot);
+#else
+  uint4 *fp = reinterpret_cast<uint4 *>(a.frames + (size_t)p * a.slot);
+#endif
+  RFrame f;
+  const uint4 c0 = ld_stream(fp), c1 = ld_stream(fp + 1), c2 = ld_stream(fp + 2),
+              c3 = ld_stream(fp + 3);
+  f.w[0] = c0.x; f.w[1] = c0.y; f.w[2] = c0.z; f.w[3] = c0.w;
+  f.w[4] = c1.x; f.w[5] = c1.y; f.w[6] = c1.z; f.w[7] = c1.w;
+  f.w[8] = c2.x; f.w[9] = c2.y; f.w[10] = c2.z; f.w[11] = c2.w;
+  f.w[12] = c3.x; f.w[13] = c3.y; f.w[14] = c3.z; f.w[15] = c3.w;
+  const uint32_t in = a.in_dev[p], len = a.len[p];
+  uint32_t touch = kNone;
+#ifdef VP_ABL_NOFRAME
+  {
+    const uint32_t fl = p & (a.t.cap - 1), v = fl >> 16;
+    f.set16(34, bswap16((uint16_t)(fl & 0xFFFF)));
+    f.set32at2(26, 10u | (((v >> 8) & 0xFF) << 16) | ((v & 0xFF) << 24));
+  }
+  const NatPend P = nat_issue(a, T, p, f, in, len, true);
+  const uint4 row[4] = {};
+  asm volatile("" ::"v"(nat_finish(a, T, P, row, p, f, in, len, touch)
+                            ? f.w[6] ^ f.w[10] : 0u));
+#else
+  const NatPend P = nat_issue(a, T, p, f, in, len, true);
+  uint4 row[4] = {};
+  if (P.row != kNone) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(a.t.bk + P.row);
+    row[0] = q[0];
+    row[1] = q[1];
+    row[2] = q[2];
+    row[3] = q[3];
+  }
+  if (nat_finish(a, T, P, row, p, f, in, len, touch)) {
+    st_stream(fp, make_uint4(f.w[0], f.w[1], f.w[2], f.w[3]));
+    st_stream(fp + 1, make_uint4(f.w[4], f.w[5], f.w[6], f.w[7]));
+    st_stream(fp + 2, make_uint4(f.w[8], f.w[9], f.w[10], f.w[11]));
+    if ((f.w[5] >> 24) == 6)
+      st_stream(fp + 3, make_uint4(f.w[12], f.w[13], f.w[14], f.w[15]));
+  }
+#endif
+  return touch;
+}
+
 // Phase A, any slot size: one packet per lane, grid-stride, the first 64
 // bytes of the slot as four 16-byte loads per lane.
 __global__ __launch_bounds__(256) void nat_classify(NatArgs a) {
@@ -301,51 +350,8 @@ __global__ __launch_bounds__(256) void nat_classify(NatArgs a) {
   load_crc_tables(T, a.crc_tab);
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t p = a.p0 + blockIdx.x * blockDim.x + threadIdx.x; p < a.p1;
-       p += stride) {
-#ifdef VP_ABL_NOFRAME  // diagnostic: synthesise the bench trace's frame
-    uint4 *fp = reinterpret_cast<uint4 *>(a.frames + (size_t)(p & 63) * a.slot);
-#else
-    uint4 *fp = reinterpret_cast<uint4 *>(a.frames + (size_t)p * a.slot);
-#endif
-    RFrame f;
-    const uint4 c0 = ld_stream(fp), c1 = ld_stream(fp + 1), c2 = ld_stream(fp + 2),
-                c3 = ld_stream(fp + 3);
-    f.w[0] = c0.x; f.w[1] = c0.y; f.w[2] = c0.z; f.w[3] = c0.w;
-    f.w[4] = c1.x; f.w[5] = c1.y; f.w[6] = c1.z; f.w[7] = c1.w;
-    f.w[8] = c2.x; f.w[9] = c2.y; f.w[10] = c2.z; f.w[11] = c2.w;
-    f.w[12] = c3.x; f.w[13] = c3.y; f.w[14] = c3.z; f.w[15] = c3.w;
-    const uint32_t in = a.in_dev[p], len = a.len[p];
-#ifdef VP_ABL_NOFRAME
-    {
-      const uint32_t fl = p & (a.t.cap - 1), v = fl >> 16;
-      f.set16(34, bswap16((uint16_t)(fl & 0xFFFF)));
-      f.set32at2(26, 10u | (((v >> 8) & 0xFF) << 16) | ((v & 0xFF) << 24));
-    }
-    const NatPend P = nat_issue(a, T, p, f, in, len, true);
-    const uint4 row[4] = {};
-    uint32_t touch;
-    asm volatile("" ::"v"(nat_finish(a, T, P, row, p, f, in, len, touch)
-                              ? f.w[6] ^ f.w[10] : 0u));
-#else
-    const NatPend P = nat_issue(a, T, p, f, in, len, true);
-    uint4 row[4] = {};
-    if (P.row != kNone) {
-      const uint4 *q = reinterpret_cast<const uint4 *>(a.t.bk + P.row);
-      row[0] = q[0];
-      row[1] = q[1];
-      row[2] = q[2];
-      row[3] = q[3];
-    }
-    uint32_t touch;
-    if (nat_finish(a, T, P, row, p, f, in, len, touch)) {
-      st_stream(fp, make_uint4(f.w[0], f.w[1], f.w[2], f.w[3]));
-      st_stream(fp + 1, make_uint4(f.w[4], f.w[5], f.w[6], f.w[7]));
-      st_stream(fp + 2, make_uint4(f.w[8], f.w[9], f.w[10], f.w[11]));
-      if ((f.w[5] >> 24) == 6)
-        st_stream(fp + 3, make_uint4(f.w[12], f.w[13], f.w[14], f.w[15]));
-    }
-#endif
-  }
+       p += stride)
+    nat_lane(a, T, p);
 }
 
 // Phase A for 64-byte slots: LDS-staged 1 KiB-contiguous frame I/O
@@ -421,44 +427,32 @@ __global__ void nat_miss_finish(NatArgs a, const uint32_t *list, uint32_t n,
   }
 }
 
-// LAN packets whose home bucket held three other keys: the rest of the probe
-// path (map_get's find_key walk, map-impl-pow2.c:629-732), then the same
-// hit / miss handling as phase A.
-__device__ void nat_reprobe_one(const NatArgs &a, uint32_t p) {
-  {
-    GFrame f{a.frames + (size_t)p * a.slot, a.slot};
-    const L34 h = parse_l34(f, a.len[p]);
-    const uint32_t proto = f.r8(h.ip + 9), in = a.in_dev[p];
-    const uint32_t sp = f.r16(h.l4), dp = f.r16(h.l4 + 2);
-    const uint32_t sip = f.r32(h.ip + 12), dip = f.r32(h.ip + 16);
-    const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
-    const uint32_t hh = flowid_hash(a.crc_tab, sp, dp, sip, dip, in, proto);
-    const uint32_t b = home_bucket(hh, a.t.bmask, a.t.mix);
-    const uint32_t idx = tbl_probe_from(a.t, (b + 1) & a.t.bmask, key, a.t.bmask);
-    const bool miss = idx == kNone;  // new flow, or not yet visible: phase B
-    const uint32_t at = wave_append(&a.t.ctl->miss_count, miss);
-    if (miss) {
-      a.miss[at] = p;
-      return;
-    }
-    a.log[p] = idx;
-    nat_write_lan(a, p, idx);
-  }
-}
-
-// The queue: per-block slices (cnt != null: slice b holds cnt[b] positions
-// at list + b * range) or one list of n positions.
-__global__ void nat_reprobe(NatArgs a, const uint32_t *list, uint32_t n,
-                            const uint32_t *cnt, uint32_t range, uint32_t nblk) {
-  if (cnt) {
-    for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x)
-      for (uint32_t k = threadIdx.x; k < cnt[b]; k += blockDim.x)
-        nat_reprobe_one(a, list[(size_t)b * range + k]);
-    return;
-  }
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
-       j += gridDim.x * blockDim.x)
-    nat_reprobe_one(a, list[j]);
+// LAN packets whose home bucket held three other keys finish here: phase A's
+// register path with the probe walked on bucket by bucket (reprobe_wave, one
+// cooperative 64-byte request per frame and per bucket). Slices per classify
+// block (cnt, 64-byte tiles) or runs of 256 of one list (cnt == null, the
+// per-lane classify path).
+__global__ __launch_bounds__(256) void nat_reprobe(NatArgs a, const uint32_t *list,
+                                                   const uint32_t *cnt, uint32_t n,
+                                                   uint32_t range, uint32_t nblk,
+                                                   uint64_t seq_base) {
+  __shared__ uint32_t T[15 * 256];
+  __shared__ uint4 stage[4][256];
+  load_crc_tables(T, a.crc_tab);
+  a.tileq = 1;  // a full bucket answers kReprobe: reprobe_wave walks on
+  uint4 *S = stage[threadIdx.x >> 6];
+  reprobe_slices(list, cnt, n, range, nblk, a.t.tseq, seq_base, [&](uint32_t p, bool act) {
+    return reprobe_wave(
+        a.frames, a.slot, a.len, a.in_dev, reinterpret_cast<const uint8_t *>(a.t.bk),
+        a.t.bmask, p, act, S,
+        [&](uint32_t q, const RFrame &f, uint32_t in, uint32_t len, bool mine) {
+          return nat_issue(a, T, q, f, in, len, mine);
+        },
+        [&](const NatPend &P, const uint4 *row, uint32_t q, RFrame &f, uint32_t in,
+            uint32_t len, uint32_t &touch) {
+          return nat_finish(a, T, P, row, q, f, in, len, touch);
+        });
+  });
 }
 
 // ------------------------------------------------------------- phase C --
@@ -570,18 +564,20 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   else
     VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
   VP_TRY(read_ctl(c, t));
-  bool refold = bp.on && t.h_ctl.touch_ovf;
-  if (const uint32_t nre = t.h_ctl.reprobe_count) {
-    if (tiles64)
-      nat_reprobe<<<std::min<uint32_t>(grid64, 2048), 256, 0, c->stream>>>(
-          a, w.reprobe, nre, w.reprobe_cnt, range64, grid64);
-    else
-      nat_reprobe<<<grid_for(nre), 256, 0, c->stream>>>(a, w.reprobe, nre, nullptr,
-                                                       0, 0);
+  const uint32_t nre = t.h_ctl.reprobe_count;
+  if (nre) {  // probes past a full home bucket: finish them, patch the fold
+    const uint32_t *rcnt = tiles64 ? w.reprobe_cnt : nullptr;
+    const uint32_t range = tiles64 ? range64 : 256;
+    const uint32_t nblk = tiles64 ? grid64 : (nre + 255) / 256;
+    nat_reprobe<<<std::min<uint32_t>(nblk, 2048), 256, 0, c->stream>>>(
+        a, w.reprobe, rcnt, nre, range, nblk, seq0);
     VP_HIP(hipGetLastError());
+    VP_TRY(tbl_reprobe_stamp(c, t, w.reprobe, rcnt, nre, range, nblk, w.log, now,
+                             seq0));
     VP_TRY(read_ctl(c, t));  // the walk may have found new flows
-    refold = true;           // its hits are in the log, not in the bins
   }
+  // the log fold redoes it all when a bin slice overflowed
+  const bool refold = bp.on && t.h_ctl.touch_ovf != 0;
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
   *ms += kms;

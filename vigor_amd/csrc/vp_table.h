@@ -172,6 +172,12 @@ struct BinsPlan {
 };
 int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
                   uint32_t p1, BinsPlan *plan);
+// ts of the indices the reprobe kernels touched (after their tseq atomicMax;
+// the queue as in reprobe_slices, vp_device.h).
+int tbl_reprobe_stamp(vp_ctx *c, FlowTable &t, const uint32_t *list,
+                      const uint32_t *cnt, uint32_t n, uint32_t range, uint32_t nblk,
+                      const uint32_t *log, const NowSpec &now, uint64_t seq_base);
+
 // Fold the bins into ts/tseq. Exact unless a slice overflowed (the launch
 // sets t.ctl->touch_ovf; read_ctl, then fold the log with tbl_touch_reduce).
 int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,

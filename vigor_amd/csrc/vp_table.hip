@@ -103,9 +103,16 @@ static uint64_t tbl_entries(const FlowTable &t) {
 
 int tbl_alloc(vp_ctx *c, FlowTable &t, uint32_t cap) {
   (void)c;
-  // load factor <= ~0.7 of the entries; tombstones purged at 0.85
+  // one bucket (3 entries) per index: load <= 1/3, so a random key set puts
+  // ~2 % of its keys past their home bucket (~13 % at load 2/3, each one a
+  // reprobe); 64 B of HBM per index. Tombstones purged at 0.85.
   uint64_t nb = 64;
-  while (nb * kBucketEntries * 7 < 10ull * cap) nb <<= 1;
+  while (nb < cap) nb <<= 1;
+  if (const char *sp = getenv("VIGPATH_SPARSE")) {  // diagnostics: 2^k x buckets
+    const int k = atoi(sp);
+    if (k > 0) nb <<= std::min(k, 3);
+    if (k < 0) nb = std::max<uint64_t>(64, nb >> std::min(-k, 3));
+  }
   t.bmask = (uint32_t)(nb - 1);
   t.cap = cap;
   const char *mix = getenv("VIGPATH_MIX");  // diagnostics: start in mode 1
@@ -149,9 +156,10 @@ void tbl_free(FlowTable &t) {
 // map_put position; the key is known to be absent) and store key + index.
 // Returns the entry id. Concurrent claimers race on the index word only.
 __device__ uint32_t tbl_insert(const TableDev &t, uint32_t h, const uint32_t *k,
-                               uint32_t idx, bool *reused_tomb) {
+                               uint32_t idx, bool *reused_tomb, uint32_t *disp) {
   uint32_t b = home_bucket(h, t.bmask, t.mix);
   for (uint32_t d = 0;; d++) {
+    if (d == 1) *disp += 1;  // past the home bucket
     if (d == 8) atomicMax(&t.ctl->max_disp, d);  // clustering signal
     for (uint32_t e = 0; e < kBucketEntries; e++) {
       uint32_t *w = &t.bk[b].idx[e];
@@ -221,6 +229,7 @@ __global__ void nk_alloc(NkArgs m) {
   const uint32_t stack_top = t.ctl->stack_top;
   const uint32_t fresh = t.ctl->fresh_next;
   const uint32_t free_total = stack_top + (t.cap - fresh);
+  uint32_t disp = 0;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m.n;
        j += gridDim.x * blockDim.x) {
     if (!m.first[j]) continue;
@@ -232,13 +241,16 @@ __global__ void nk_alloc(NkArgs m) {
     const uint32_t idx =
         r < stack_top ? t.stack[stack_top - 1 - r] : fresh + (r - stack_top);
     bool tomb = false;
-    const uint32_t e = tbl_insert(t, m.mhash[j], m.mkey + 4 * (size_t)j, idx, &tomb);
+    const uint32_t e =
+        tbl_insert(t, m.mhash[j], m.mkey + 4 * (size_t)j, idx, &tomb, &disp);
     if (tomb) atomicAdd(&t.ctl->tomb_reused, 1u);
     t.slot_of[idx] = e;
     t.hash_of[idx] = m.mhash[j];
     t.birth[idx] = m.seq_base + m.pos[j];
     m.assign[j] = idx;
   }
+  for (uint32_t o = 32; o > 0; o >>= 1) disp += __shfl_xor(disp, o);
+  if ((threadIdx.x & 63) == 0 && disp) atomicAdd(&t.ctl->disp_count, disp);
 }
 
 __global__ void nk_commit(NkArgs m) {
@@ -292,7 +304,12 @@ int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
   VP_HIP(hipGetLastError());
   VP_TRY(read_ctl(c, t));
   if (n_new) *n_new = t.h_ctl.new_count;
-  if (t.h_ctl.max_disp && !t.mix) {  // masked layout clusters for these keys
+  // The masked layout is exact-structured for GF(2)-linear key sets: either
+  // well spread or clustered (a long probe, or a quarter of the keys past
+  // their home bucket). Clustered: rebuild into the multiplicative layout.
+  t.ins_since += t.h_ctl.new_count;
+  if (!t.mix && (t.h_ctl.max_disp ||
+                 (t.ins_since >= 4096 && 10ull * t.h_ctl.disp_count > t.ins_since))) {
     t.mix = 1;
     VP_HIP(hipMemsetAsync(&t.ctl->max_disp, 0, 4, c->stream));
     VP_TRY(tbl_rebuild(c, t));
@@ -613,6 +630,31 @@ int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
   return 0;
 }
 
+// After a reprobe kernel raised tseq[i] to the sequence of its packets'
+// touches: the packet whose sequence won writes ts[i] (exactly one per index).
+__global__ void reprobe_stamp(const uint32_t *list, const uint32_t *cnt, uint32_t n,
+                              uint32_t range, uint32_t nblk, const uint32_t *log,
+                              NowSpec now, uint64_t seq_base, uint64_t *ts,
+                              const uint64_t *tseq) {
+  for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const uint32_t nb = reprobe_slice_len(cnt, n, range, b);
+    for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x) {
+      const uint32_t p = list[(size_t)b * range + k];
+      const uint32_t i = log[p];
+      if (i != kNone && tseq[i] == seq_base + p) ts[i] = (uint64_t)now.at(p);
+    }
+  }
+}
+
+int tbl_reprobe_stamp(vp_ctx *c, FlowTable &t, const uint32_t *list,
+                      const uint32_t *cnt, uint32_t n, uint32_t range, uint32_t nblk,
+                      const uint32_t *log, const NowSpec &now, uint64_t seq_base) {
+  reprobe_stamp<<<std::min<uint32_t>(nblk, 2048), 256, 0, c->stream>>>(
+      list, cnt, n, range, nblk, log, now, seq_base, t.ts, t.tseq);
+  VP_HIP(hipGetLastError());
+  return 0;
+}
+
 // ---------------------------------------------------------------- expiry --
 
 __global__ void tbl_min_ts(TableDev t) {
@@ -698,7 +740,8 @@ __global__ void rb_insert(TableDev t, const uint32_t *keys) {
        i += gridDim.x * blockDim.x) {
     if (t.slot_of[i] == kNone) continue;
     bool tomb = false;
-    t.slot_of[i] = tbl_insert(t, t.hash_of[i], keys + 4 * (size_t)i, i, &tomb);
+    uint32_t disp = 0;
+    t.slot_of[i] = tbl_insert(t, t.hash_of[i], keys + 4 * (size_t)i, i, &tomb, &disp);
   }
 }
 
@@ -710,6 +753,8 @@ static int tbl_rebuild(vp_ctx *c, FlowTable &t) {
                         c->stream));
   rb_insert<<<grid_for(t.cap), 256, 0, c->stream>>>(tbl_dev(t), keys);
   VP_HIP(hipMemsetAsync(&t.ctl->n_tomb, 0, 4, c->stream));
+  VP_HIP(hipMemsetAsync(&t.ctl->disp_count, 0, 4, c->stream));
+  t.ins_since = 0;
   VP_HIP(hipStreamSynchronize(c->stream));
   VP_HIP(hipFree(keys));
   return 0;
