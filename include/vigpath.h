@@ -1,7 +1,7 @@
 /*
  * vigpath — MI355X-native implementation of Vigor's per-packet receive path
  * (parse -> CRC32C flow hash -> libVig map probe -> state update -> header
- * rewrite + IPv4/L4 checksum) for vignat, vigbridge, viglb and vigfw.
+ * rewrite + IPv4/L4 checksum) for vignat, vigbridge, viglb, vigfw and vigpol.
  *
  * C ABI only: plain pointers and sizes, no HIP or torch types. Two layers:
  *
@@ -103,6 +103,16 @@ typedef struct vp_fw_config {
   uint8_t endpoint_macs[VP_MAX_DEVICES][6];
 } vp_fw_config;
 
+/* vigpol/policer_config.h:8-24 (policer_config.c:17-93 parses it). */
+typedef struct vp_pol_config {
+  uint16_t lan_device;
+  uint16_t wan_device;
+  uint64_t rate;         /* B/s, > 0 */
+  uint64_t burst;        /* B, > 0 */
+  uint32_t dyn_capacity; /* power of two (map.c:73, -DCAPACITY_POW2) */
+  uint16_t n_devices;    /* rte_eth_dev_count_avail() */
+} vp_pol_config;
+
 /* Create an NF instance whose state lives in HBM of HIP device `gpu`.
  * Returns 0 and *out, or VP_EINVAL for a configuration the reference's
  * nf_init would reject (non power-of-two capacities, ...). */
@@ -110,6 +120,7 @@ int vp_nat_create(const vp_nat_config *cfg, int gpu, vp_ctx **out);
 int vp_bridge_create(const vp_bridge_config *cfg, int gpu, vp_ctx **out);
 int vp_lb_create(const vp_lb_config *cfg, int gpu, vp_ctx **out);
 int vp_fw_create(const vp_fw_config *cfg, int gpu, vp_ctx **out);
+int vp_pol_create(const vp_pol_config *cfg, int gpu, vp_ctx **out);
 void vp_destroy(vp_ctx *ctx);
 
 /* ------------------------------------------------------------ batches -- */
@@ -208,6 +219,13 @@ int vp_lb_dump(vp_ctx *ctx, uint8_t *f_alloc, int64_t *f_ts, uint8_t *f_keys,
  * int_devices vector, fw_flowmanager.c:61-64; 0 where not allocated). */
 int vp_fw_dump(vp_ctx *ctx, uint8_t *alloc, int64_t *ts, uint8_t *keys,
                uint32_t *int_dev);
+
+/* vigpol state by index i < dyn_capacity: alloc[i], ts[i], keys[i] (dyn_keys:
+ * the destination address, raw network-order u32), bucket_size[i] and
+ * bucket_time[i] (dyn_vals, vigpol/dynamic_value.h:7-10; meaningful where
+ * allocated). */
+int vp_pol_dump(vp_ctx *ctx, uint8_t *alloc, int64_t *ts, uint32_t *keys,
+                uint64_t *bucket_size, int64_t *bucket_time);
 
 /* Number of live flows / learned MACs / flows+backends. */
 int64_t vp_live_count(vp_ctx *ctx);

@@ -12,6 +12,7 @@
  *   vigbridge/bridge_main.c:29-128, 292-329
  *   viglb/lb_main.c:13-68, lb_balancer.c:22-237
  *   vigfw/fw_main.c:21-80, fw_flowmanager.c:38-86
+ *   vigpol/policer_main.c:21-145
  *   codegen/main.ml:163-206, 328-401, 444-486 (generated _eq/_hash/_allocate)
  * libVig is reached only through orc_lv.h, so the same glue runs over the
  * restated libVig (liborc.so) or the reference's own (oracle/_ref).
@@ -344,7 +345,7 @@ static void set_macs(struct pkt *p, uint32_t eth, const uint8_t *src,
 }
 
 /* ---------------------------------------------------------------- NFs -- */
-enum nf_kind { NF_NAT = 1, NF_BRIDGE = 2, NF_LB = 3, NF_FW = 4 };
+enum nf_kind { NF_NAT = 1, NF_BRIDGE = 2, NF_LB = 3, NF_FW = 4, NF_POL = 5 };
 
 struct nat_state {
   orc_nat_cfg cfg;
@@ -360,6 +361,20 @@ struct fw_state {
   struct lv_vector *int_devices;
   struct lv_dchain *heap;
 };
+/* vigpol/dataspec.ml:5-11: dyn_map, dyn_keys, dyn_heap, dyn_vals */
+struct pol_state {
+  orc_pol_cfg cfg;
+  struct lv_map *dyn_map;
+  struct lv_vector *dyn_keys;
+  struct lv_dchain *dyn_heap;
+  struct lv_vector *dyn_vals;
+};
+/* vigpol/dynamic_value.h:7-10 */
+struct PolValue {
+  uint64_t bucket_size;
+  int64_t bucket_time;
+};
+static void PolValue_allocate(void *k) { memset(k, 0, sizeof(struct PolValue)); }
 struct bridge_state {
   orc_bridge_cfg cfg;
   struct lv_map *dyn_map;
@@ -389,6 +404,7 @@ struct orc_nf {
     struct bridge_state br;
     struct lb_state lb;
     struct fw_state fw;
+    struct pol_state pol;
   } u;
 };
 
@@ -592,6 +608,110 @@ void orc_fw_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *keys,
     memcpy(keys + (size_t)16 * i, k, 13);
     lv_vector_borrow(s->int_devices, i, &k);
     int_dev[i] = alloc[i] ? *(uint32_t *)k : 0;
+  }
+  free(order);
+  free(fre);
+}
+
+/* ---- vigpol ---- */
+orc_nf *orc_pol_create(const orc_pol_cfg *cfg) {
+  if (cfg->n_devices == 0 || cfg->rate == 0 || cfg->burst == 0) return NULL;
+  orc_nf *nf = calloc(1, sizeof *nf);
+  if (!nf) return NULL;
+  nf->kind = NF_POL;
+  struct pol_state *s = &nf->u.pol;
+  s->cfg = *cfg;
+  /* alloc_state(capacity, dev_count): vigpol/dataspec.ml:5-11 */
+  if (!lv_map_allocate(IpAddr_eq, IpAddr_hash, cfg->dyn_capacity, &s->dyn_map) ||
+      !lv_vector_allocate(sizeof(uint32_t), cfg->dyn_capacity, U32_init,
+                          &s->dyn_keys) ||
+      !lv_dchain_allocate((int)cfg->dyn_capacity, &s->dyn_heap) ||
+      !lv_vector_allocate(sizeof(struct PolValue), cfg->dyn_capacity,
+                          PolValue_allocate, &s->dyn_vals)) {
+    free(nf);
+    return NULL;
+  }
+  return nf;
+}
+
+#define ORC_NS_PER_S 1000000000ul /* VIGOR_TIME_SECONDS_MULTIPLIER, vigor-time.h:10 */
+
+/* policer_check_tb, vigpol/policer_main.c:34-111 (u64 arithmetic as there) */
+static int pol_check_tb(struct pol_state *s, uint32_t dst, uint16_t size,
+                        int64_t time) {
+  int index = -1;
+  if (lv_map_get(s->dyn_map, &dst, &index)) {
+    lv_dchain_rejuvenate_index(s->dyn_heap, index, time);
+    struct PolValue *v;
+    lv_vector_borrow(s->dyn_vals, index, (void **)&v);
+    uint64_t time_u = (uint64_t)time;
+    uint64_t time_diff = time_u - (uint64_t)v->bucket_time;
+    if (time_diff < s->cfg.burst * ORC_NS_PER_S / s->cfg.rate) {
+      uint64_t added = time_diff * s->cfg.rate / ORC_NS_PER_S;
+      v->bucket_size += added;
+      if (v->bucket_size > s->cfg.burst) v->bucket_size = s->cfg.burst;
+    } else {
+      v->bucket_size = s->cfg.burst;
+    }
+    v->bucket_time = (int64_t)time_u;
+    int fwd = 0;
+    if (v->bucket_size > size) {
+      v->bucket_size -= size;
+      fwd = 1;
+    }
+    lv_vector_return(s->dyn_vals, index, v);
+    return fwd;
+  }
+  if (size > s->cfg.burst) return 0; /* unknown flow larger than burst */
+  if (!lv_dchain_allocate_new_index(s->dyn_heap, &index, time)) return 0;
+  uint32_t *key;
+  struct PolValue *v;
+  lv_vector_borrow(s->dyn_keys, index, (void **)&key);
+  lv_vector_borrow(s->dyn_vals, index, (void **)&v);
+  *key = dst;
+  v->bucket_size = s->cfg.burst - size;
+  v->bucket_time = time;
+  lv_map_put(s->dyn_map, key, index);
+  lv_vector_return(s->dyn_keys, index, key);
+  lv_vector_return(s->dyn_vals, index, v);
+  return 1;
+}
+
+/* nf_process, vigpol/policer_main.c:120-145; expiry (policer_expire_entries,
+ * :21-32) only after the IPv4 header parsed. */
+static int pol_process(struct pol_state *s, uint16_t device, struct pkt *p,
+                       uint16_t len, int64_t now) {
+  uint32_t eth = borrow(p, 14);
+  uint32_t ip;
+  if (!get_ipv4(p, eth, &ip)) return device;
+  uint64_t exp_time = ORC_NS_PER_S * s->cfg.burst / s->cfg.rate;
+  int64_t min_time = (int64_t)((uint64_t)now - exp_time);
+  lv_expire_items_single_map(s->dyn_heap, s->dyn_keys, s->dyn_map, min_time);
+  if (device == s->cfg.lan_device) return s->cfg.wan_device;
+  if (device == s->cfg.wan_device)
+    return pol_check_tb(s, rd32(p, ip + 16), len, now) ? s->cfg.lan_device
+                                                         : s->cfg.wan_device;
+  return device;
+}
+
+void orc_pol_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint32_t *keys,
+                  uint64_t *bucket_size, int64_t *bucket_time) {
+  struct pol_state *s = &nf->u.pol;
+  int n = (int)s->cfg.dyn_capacity;
+  int *order = malloc(sizeof(int) * (size_t)n);
+  int *fre = malloc(sizeof(int) * (size_t)n);
+  int na, nfree;
+  lv_dchain_dump(s->dyn_heap, n, order, &na, fre, &nfree, ts);
+  for (int i = 0; i < n; i++) {
+    alloc[i] = (uint8_t)lv_dchain_is_index_allocated(s->dyn_heap, i);
+    void *k;
+    lv_vector_borrow(s->dyn_keys, i, &k);
+    keys[i] = *(uint32_t *)k;
+    lv_vector_return(s->dyn_keys, i, k);
+    lv_vector_borrow(s->dyn_vals, i, &k);
+    bucket_size[i] = ((struct PolValue *)k)->bucket_size;
+    bucket_time[i] = ((struct PolValue *)k)->bucket_time;
+    lv_vector_return(s->dyn_vals, i, k);
   }
   free(order);
   free(fre);
@@ -940,6 +1060,12 @@ void orc_destroy(orc_nf *nf) {
       lv_vector_free(nf->u.fw.int_devices);
       lv_dchain_free(nf->u.fw.heap);
       break;
+    case NF_POL:
+      lv_map_free(nf->u.pol.dyn_map);
+      lv_vector_free(nf->u.pol.dyn_keys);
+      lv_dchain_free(nf->u.pol.dyn_heap);
+      lv_vector_free(nf->u.pol.dyn_vals);
+      break;
   }
   free(nf);
 }
@@ -956,6 +1082,8 @@ int orc_process(orc_nf *nf, uint16_t device, uint8_t *frame, uint16_t len,
       return lb_process(&nf->u.lb, device, &p, now);
     case NF_FW:
       return fw_process(&nf->u.fw, device, &p, now);
+    case NF_POL:
+      return pol_process(&nf->u.pol, device, &p, len, now);
   }
   return device;
 }

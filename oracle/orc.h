@@ -2,7 +2,7 @@
  * ORACLE — TEST INFRASTRUCTURE ONLY.
  *
  * CPU restatement of Vigor's per-packet path (nf.c dispatch -> nf_process of
- * vignat / vigbridge / viglb / vigfw -> nf-util parse + DPDK 20.08 checksum -> libVig).
+ * vignat / vigbridge / viglb / vigfw / vigpol -> nf-util parse + DPDK 20.08 checksum -> libVig).
  * Only tests/, bench.py's cpu_baseline leg and __graft_entry__.smoke() may
  * load it, and only as the checker (or the timed CPU baseline). The product
  * path (vigor_amd/, include/vigpath.h) never links, loads or calls it.
@@ -75,7 +75,18 @@ typedef struct {
   uint8_t endpoint_macs[ORC_MAX_DEV][6];
 } orc_fw_cfg;
 
+/* vigpol/policer_config.h:8-24 */
+typedef struct {
+  uint16_t lan_device;
+  uint16_t wan_device;
+  uint64_t rate;         /* B/s */
+  uint64_t burst;        /* B */
+  uint32_t dyn_capacity; /* power of two (map.c:73) */
+  uint16_t n_devices;
+} orc_pol_cfg;
+
 orc_nf *orc_nat_create(const orc_nat_cfg *cfg);
+orc_nf *orc_pol_create(const orc_pol_cfg *cfg);
 orc_nf *orc_fw_create(const orc_fw_cfg *cfg);
 orc_nf *orc_bridge_create(const orc_bridge_cfg *cfg);
 orc_nf *orc_lb_create(const orc_lb_cfg *cfg);
@@ -113,6 +124,10 @@ void orc_nat_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *keys);
 /* vigfw: alloc, ts, FlowId bytes (13 + zero padding), int_devices. */
 void orc_fw_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *keys,
                  uint32_t *int_dev);
+/* vigpol: alloc, ts, dyn_keys (u32 dst address, raw), dyn_vals
+ * (DynamicValue {bucket_size, bucket_time}, vigpol/dynamic_value.h:7-10). */
+void orc_pol_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint32_t *keys,
+                  uint64_t *bucket_size, int64_t *bucket_time);
 void orc_bridge_dump(orc_nf *nf, uint8_t *alloc, int64_t *ts, uint8_t *macs,
                      uint16_t *port);
 void orc_lb_dump(orc_nf *nf, uint8_t *f_alloc, int64_t *f_ts, uint8_t *f_keys,

@@ -47,6 +47,12 @@ class FwCfg(C.Structure):
                 ("endpoint_macs", (C.c_uint8 * 6) * MAX_DEV)]
 
 
+class PolCfg(C.Structure):
+    _fields_ = [("lan_device", C.c_uint16), ("wan_device", C.c_uint16),
+                ("rate", C.c_uint64), ("burst", C.c_uint64),
+                ("dyn_capacity", C.c_uint32), ("n_devices", C.c_uint16)]
+
+
 def _ptr(a):
     return C.c_void_p(a.ctypes.data) if a is not None else None
 
@@ -81,6 +87,9 @@ def lib(ref: bool = False):
     L.orc_fw_flowid_hash.restype = C.c_uint32
     L.orc_fw_flowid_hash.argtypes = [C.c_uint16, C.c_uint16, C.c_uint32,
                                      C.c_uint32, C.c_uint8]
+    L.orc_pol_create.restype = C.c_void_p
+    L.orc_pol_create.argtypes = [C.POINTER(PolCfg)]
+    L.orc_pol_dump.argtypes = [C.c_void_p] * 6
     L.orc_destroy.argtypes = [C.c_void_p]
     L.orc_process.restype = C.c_int
     L.orc_process.argtypes = [C.c_void_p, C.c_uint16, C.c_void_p, C.c_uint16,
@@ -141,8 +150,14 @@ def fw_cfg(wan=1, expire_us=60_000_000, max_flows=65536, device_macs=(),
     return c
 
 
+def pol_cfg(lan=1, wan=0, rate=375_000_000, burst=3_750_000_000,
+            capacity=65536, n_devices=2):
+    """vigpol defaults of vigpol/Makefile:5 (NF_ARGS)."""
+    return PolCfg(lan, wan, rate, burst, capacity, n_devices)
+
+
 class Oracle:
-    """One NF instance in the oracle. kind: 'nat' | 'bridge' | 'lb' | 'fw'."""
+    """One NF instance in the oracle: 'nat' | 'bridge' | 'lb' | 'fw' | 'pol'."""
 
     def __init__(self, kind: str, cfg, ref: bool = False, statics=None):
         self.L = lib(ref)
@@ -165,6 +180,8 @@ class Oracle:
             self.h = self.L.orc_lb_create(C.byref(cfg))
         elif kind == "fw":
             self.h = self.L.orc_fw_create(C.byref(cfg))
+        elif kind == "pol":
+            self.h = self.L.orc_pol_create(C.byref(cfg))
         else:
             raise ValueError(kind)
         if not self.h:
@@ -214,6 +231,16 @@ class Oracle:
         dev = np.zeros(max_flows, np.uint32)
         self.L.orc_fw_dump(self.h, _ptr(alloc), _ptr(ts), _ptr(keys), _ptr(dev))
         return alloc, ts, keys.reshape(max_flows, 16), dev
+
+    def pol_dump(self, cap):
+        alloc = np.zeros(cap, np.uint8)
+        ts = np.zeros(cap, np.int64)
+        keys = np.zeros(cap, np.uint32)
+        size = np.zeros(cap, np.uint64)
+        btime = np.zeros(cap, np.int64)
+        self.L.orc_pol_dump(self.h, _ptr(alloc), _ptr(ts), _ptr(keys),
+                            _ptr(size), _ptr(btime))
+        return alloc, ts, keys, size, btime
 
     def bridge_dump(self, cap):
         alloc = np.zeros(cap, np.uint8)

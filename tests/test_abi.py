@@ -14,7 +14,7 @@ from vigor_amd import config as cfgmod
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHIMS = {nf: os.path.join(ROOT, "vigor_amd", "libvig%s_nf.so" % nf)
-         for nf in ("nat", "bridge", "lb", "fw")}
+         for nf in ("nat", "bridge", "lb", "fw", "pol")}
 NF_H = ["nf_init", "nf_process", "nf_config_init", "nf_config_usage",
         "nf_config_print", "config"]
 
@@ -173,3 +173,34 @@ def test_fw_config_parse_semantics():
                 ["--extip", "1.2.3.4"]):
         with pytest.raises(ValueError):
             cfgmod.fw_config_from_args(bad, 2, [])
+
+
+class PolNfConfig(C.Structure):
+    """vigpol/policer_config.h:9-24 as the shim defines it."""
+    _fields_ = [("lan_device", C.c_uint16), ("wan_device", C.c_uint16),
+                ("rate", C.c_uint64), ("burst", C.c_uint64),
+                ("dyn_capacity", C.c_uint32)]
+
+
+def test_pol_shim_parses_like_reference():
+    """policer_config.c:20-93: defaults, then the options."""
+    os.environ["VIGPATH_NB_DEVICES"] = "3"
+    L = C.CDLL(SHIMS["pol"])
+    _init(L, [])
+    cfg = PolNfConfig.in_dll(L, "config")
+    assert (cfg.lan_device, cfg.wan_device, cfg.rate, cfg.burst,
+            cfg.dyn_capacity) == (1, 0, 1000000, 100000, 128)
+    _init(L, ["--lan", "2", "--wan", "1", "--rate", "375000000", "--burst",
+              "3750000000", "--capacity", "65536"])
+    assert (cfg.lan_device, cfg.wan_device, cfg.rate, cfg.burst,
+            cfg.dyn_capacity) == (2, 1, 375000000, 3750000000, 65536)
+
+
+def test_pol_config_parse_semantics():
+    c = vigor_amd.pol_config_from_args(["--wan", "1", "--lan=0"], 2)
+    assert (c.lan_device, c.wan_device, c.rate, c.burst, c.dyn_capacity) == \
+        (0, 1, 1000000, 100000, 128)
+    for bad in (["--burst", "0"], ["--wan", "5"], ["--capacity", "0"],
+                ["--rate", "12x"], ["--bogus", "1"]):
+        with pytest.raises(ValueError):
+            vigor_amd.pol_config_from_args(bad, 2)

@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 
 import orc
-from tracegen import mixed_fw_trace, mixed_nat_trace
+from tracegen import mixed_fw_trace, mixed_nat_trace, mixed_pol_trace
 from vigor_amd import traces as T
 
 HAVE_REF = os.path.isdir("/root/reference/libvig/verified")
@@ -398,3 +398,63 @@ def test_fw_trace_matches_reference(seed, max_flows, expire_us, n_flows):
     np.testing.assert_array_equal(t0[a0 == 1], t1[a1 == 1])
     np.testing.assert_array_equal(k0, k1)
     np.testing.assert_array_equal(d0, d1)
+
+
+def pol_oracle(ref, cap=64, rate=1_000_000, burst=1000, n_dev=3, lan=1, wan=0):
+    return orc.Oracle("pol", orc.pol_cfg(lan=lan, wan=wan, rate=rate, burst=burst,
+                                         capacity=cap, n_devices=n_dev), ref=ref)
+
+
+@pytest.mark.parametrize("ref", IMPLS)
+def test_pol_semantics_kat(ref):
+    """policer_main.c:34-145 by hand (rate 1 B/us, burst 1000 B): a new
+    destination takes burst - size; a refill adds time_diff * rate / 1e9;
+    a packet passes only while bucket > size; after burst/rate of silence the
+    bucket is full again; LAN packets pass unpoliced; frames are untouched."""
+    o = pol_oracle(ref)
+    f, _ = T.udp_frames(np.array([T.ip4(9, 9, 9, 9)]), np.array([T.ip4(10, 0, 0, 1)]),
+                        np.array([53]), np.array([80]))
+    fr = bytearray(f.tobytes())
+    orig = bytes(fr)
+    t = T.NOW0
+    assert o.process(0, fr, length=600, now=t) == 1       # new: 1000-600 = 400
+    assert o.process(0, fr, length=400, now=t) == 0       # 400 > 400 fails
+    assert o.process(0, fr, length=399, now=t) == 1       # 1 left
+    assert o.process(0, fr, length=64, now=t + 100_000) == 1  # +100 -> 101 - 64
+    alloc, ts, keys, size, btime = o.pol_dump(64)
+    assert alloc.sum() == 1 and size[0] == 37 and btime[0] == t + 100_000
+    assert keys[0] == 0x0100000A and ts[0] == t + 100_000  # raw (network order)
+    assert o.process(0, fr, length=1001, now=t + 100_001) == 0  # hit, > burst
+    assert o.process(1, fr, length=64, now=t + 100_002) == 0    # LAN -> WAN
+    assert o.process(2, fr, length=64, now=t + 100_003) == 2    # other: drop
+    assert bytes(fr) == orig
+    # burst/rate = 1 ms after the last touch the entry expires
+    g, _ = T.udp_frames(np.array([T.ip4(9, 9, 9, 9)]), np.array([T.ip4(10, 0, 0, 2)]),
+                        np.array([53]), np.array([80]))
+    fr2 = bytearray(g.tobytes())
+    assert o.process(0, fr2, length=1001, now=t + 2_000_000) == 0  # > burst, new
+    alloc, ts, keys, size, btime = o.pol_dump(64)
+    assert alloc.sum() == 0
+
+
+@needs_ref
+@pytest.mark.parametrize("seed,cap,n_dsts,burst,gap", [
+    (0, 64, 40, 3000, 500), (1, 16, 60, 1000, 2000), (2, 256, 300, 2000, 50),
+    (3, 64, 20, 1000, 10)])
+def test_pol_trace_matches_reference(seed, cap, n_dsts, burst, gap):
+    rng = np.random.default_rng(seed)
+    fr, ln, dv, now = mixed_pol_trace(rng, 6000, n_dsts, gap_ns=gap)
+    res = []
+    for ref in (False, True):
+        o = pol_oracle(ref, cap=cap, burst=burst)
+        f = fr.copy()
+        out = o.run(f, ln, dv, now, 64)
+        res.append((out, f, o.pol_dump(cap)))
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(res[0][1], fr)
+    (a0, t0, *v0), (a1, t1, *v1) = res[0][2], res[1][2]
+    np.testing.assert_array_equal(a0, a1)
+    np.testing.assert_array_equal(t0[a0 == 1], t1[a1 == 1])
+    for x, y in zip(v0, v1):
+        np.testing.assert_array_equal(x, y)
+    assert (res[0][0] == 1).sum() > 100 and (res[0][0] == 0).sum() > 100

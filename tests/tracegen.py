@@ -178,3 +178,33 @@ def mixed_fw_trace(rng, n, n_flows, n_dev=3, wan=1, slot=64, reply_frac=0.35,
     frames[(bad >= 0.06) & (bad < 0.08), 14] = 0x46  # IP options (generic path)
     now = T.NOW0 + np.cumsum(rng.integers(0, 3, n))
     return frames.reshape(-1), lens, in_dev, now.astype(np.int64)
+
+
+def mixed_pol_trace(rng, n, n_dsts, n_dev=3, lan=1, wan=0, slot=64,
+                    lan_frac=0.2, other_frac=0.05, gap_ns=2000, big=1400):
+    """vigpol stress: WAN packets to n_dsts destination addresses with random
+    sizes (some above the burst), LAN packets (forwarded, not policed),
+    packets from a third device (dropped), non-IPv4 / truncated frames (no
+    expiry runs for them, policer_main.c:124-130), monotone time with ties
+    and gaps long enough to refill buckets and expire entries."""
+    d = rng.integers(0, n_dsts, n)
+    sip = T.ip4(9, 9, 0, 0) + (d % 5)
+    dip = T.ip4(10, 0, 0, 0) + d
+    f, _ = T.udp_frames(sip, dip, 1000 + d % 13, np.full(n, 80), slot=slot)
+    frames = f.reshape(n, slot)
+    lens = rng.integers(60, big, n).astype(np.uint16)
+    lens[rng.random(n) < 0.3] = 64
+    frames[:, 16] = 0  # total_length = 46 <= every size (nf-util.h:140)
+    frames[:, 17] = 46
+    in_dev = np.full(n, wan, np.uint16)
+    r = rng.random(n)
+    in_dev[r < lan_frac] = lan
+    if n_dev > 2:
+        in_dev[(r >= lan_frac) & (r < lan_frac + other_frac)] = 2
+    bad = rng.random(n)
+    frames[bad < 0.02, 12] = 0x86                          # not IPv4
+    frames[(bad >= 0.02) & (bad < 0.03), 14] = 0x44        # ihl < 5
+    frames[(bad >= 0.03) & (bad < 0.04), 16] = 0x40        # total_length > len
+    frames[(bad >= 0.04) & (bad < 0.06), 14] = 0x46        # IP options
+    now = T.NOW0 + np.cumsum(rng.integers(0, gap_ns, n))
+    return frames.reshape(-1), lens, in_dev, now.astype(np.int64)

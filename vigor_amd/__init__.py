@@ -68,6 +68,13 @@ class FwConfigC(C.Structure):
                 ("device_macs", MacTable), ("endpoint_macs", MacTable)]
 
 
+class PolConfigC(C.Structure):
+    """vp_pol_config (vigpol/policer_config.h:8-24)."""
+    _fields_ = [("lan_device", C.c_uint16), ("wan_device", C.c_uint16),
+                ("rate", C.c_uint64), ("burst", C.c_uint64),
+                ("dyn_capacity", C.c_uint32), ("n_devices", C.c_uint16)]
+
+
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                            C.c_size_t)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t)
@@ -88,7 +95,7 @@ class DevBatchC(C.Structure):
 
 # every symbol include/vigpath.h declares
 EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_fw_create",
-           "vp_destroy", "vp_process_device", "vp_process_batch",
+           "vp_pol_create", "vp_pol_dump", "vp_destroy", "vp_process_device", "vp_process_batch",
            "vp_process_host", "vp_nat_dump", "vp_bridge_dump", "vp_lb_dump",
            "vp_fw_dump", "vp_comm_unique_id", "vp_attach_rccl",
            "vp_attach_comm", "vp_sync_state", "vp_live_count",
@@ -114,6 +121,11 @@ def lib(path: str | None = None):
                                C.POINTER(C.c_void_p)]
     L.vp_fw_dump.argtypes = [C.c_void_p] * 5
     L.vp_fw_dump.restype = C.c_int
+    L.vp_pol_create.restype = C.c_int
+    L.vp_pol_create.argtypes = [C.POINTER(PolConfigC), C.c_int,
+                                C.POINTER(C.c_void_p)]
+    L.vp_pol_dump.argtypes = [C.c_void_p] * 6
+    L.vp_pol_dump.restype = C.c_int
     L.vp_nat_create.argtypes = [C.POINTER(NatConfigC), C.c_int,
                                 C.POINTER(C.c_void_p)]
     L.vp_bridge_create.argtypes = [C.POINTER(BridgeConfigC), C.c_int,
@@ -162,6 +174,7 @@ def _check(rc: int, what: str):
         raise VigpathError(rc, what)
 
 
-from .nf import Bridge, Fw, Lb, Nat, NfBase  # noqa: E402,F401
+from .nf import Bridge, Fw, Lb, Nat, NfBase, Pol  # noqa: E402,F401
 from .config import (bridge_config_from_args, fw_config_from_args,  # noqa
-                     lb_config_from_args, nat_config_from_args)
+                     lb_config_from_args, nat_config_from_args,
+                     pol_config_from_args)

@@ -8,6 +8,8 @@ semantics (host side; the C shims in csrc/vp_nf_*.c do the same in C).
             --backend-capacity --cht-height --backend-expiration --wan)
   vigfw     vigfw/fw_config.c:17-82      (--eth-dest --expire --max-flows
             --wan)
+  vigpol    vigpol/policer_config.c:17-93 (--lan --wan --rate --burst
+            --capacity)
 
 The reference calls exit(EXIT_FAILURE) on a bad option; here a ValueError is
 raised with the same message.
@@ -16,7 +18,8 @@ from __future__ import annotations
 
 import re
 
-from . import BridgeConfigC, BridgeRuleC, FwConfigC, LbConfigC, NatConfigC
+from . import (BridgeConfigC, BridgeRuleC, FwConfigC, LbConfigC, NatConfigC,
+               PolConfigC)
 
 
 def _parse_int(s: str, name: str, nxt: str = "") -> tuple[int, str]:
@@ -201,6 +204,39 @@ def fw_config_from_args(argv, n_devices: int, device_macs) -> FwConfigC:
             c.wan_device = _parse_int(v, "wan-dev")[0] & 0xFFFF
             if c.wan_device >= n_devices:
                 raise ValueError("WAN device does not exist.")
+        else:
+            raise ValueError("Unknown option.")
+    return c
+
+
+def pol_config_from_args(argv, n_devices: int) -> PolConfigC:
+    """policer_config.c:17-93: defaults LAN 1, WAN 0, rate 1 MB/s, burst
+    100 kB, capacity 128; devices must exist, rate/burst/capacity > 0."""
+    c = PolConfigC()
+    c.n_devices = n_devices
+    c.lan_device, c.wan_device = 1, 0
+    c.rate, c.burst, c.dyn_capacity = 1_000_000, 100_000, 128
+    for k, v in _split(argv):
+        if k == "lan":
+            c.lan_device = _parse_int(v, "lan")[0] & 0xFFFF
+            if c.lan_device >= n_devices:
+                raise ValueError("Invalid LAN device.")
+        elif k == "wan":
+            c.wan_device = _parse_int(v, "wan")[0] & 0xFFFF
+            if c.wan_device >= n_devices:
+                raise ValueError("Invalid WAN device.")
+        elif k == "rate":
+            c.rate = _parse_int(v, "rate")[0] & 0xFFFFFFFFFFFFFFFF
+            if c.rate == 0:
+                raise ValueError("Policer rate must be strictly positive.")
+        elif k == "burst":
+            c.burst = _parse_int(v, "burst")[0] & 0xFFFFFFFFFFFFFFFF
+            if c.burst == 0:
+                raise ValueError("Policer burst size must be strictly positive.")
+        elif k == "capacity":
+            c.dyn_capacity = _parse_int(v, "capacity")[0] & 0xFFFFFFFF
+            if c.dyn_capacity <= 0:
+                raise ValueError("Flow table size must be strictly positive.")
         else:
             raise ValueError("Unknown option.")
     return c

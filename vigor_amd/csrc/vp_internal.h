@@ -33,7 +33,7 @@ hipError_t stream_wait(hipStream_t s);
 struct Comm;  // vp_comm.hip: collectives between the ranks of one NF
 constexpr int kMaxRanks = 64;
 
-enum Kind { KIND_NAT = 1, KIND_BRIDGE = 2, KIND_LB = 3, KIND_FW = 4 };
+enum Kind { KIND_NAT = 1, KIND_BRIDGE = 2, KIND_LB = 3, KIND_FW = 4, KIND_POL = 5 };
 
 // Device control block of one table (dchain + map bookkeeping).
 struct Ctl {
@@ -143,6 +143,9 @@ struct vp_ctx {
   vp::FlowTable ft2;      // viglb backends (ip_to_backend_id + dchain)
   vp_lb_config lb{};
   vp_fw_config fw{};
+  vp_pol_config pol{};
+  uint64_t *pol_size = nullptr;  // vigpol dyn_vals: bucket_size by index
+  int64_t *pol_time = nullptr;   //                  bucket_time by index
   uint4 *be_rec = nullptr;  // viglb backends[]: {ip, mac0-3, mac4-5|nic<<16, 0}
   uint32_t *cht = nullptr;  // viglb CHT, cht[bucket * backend_capacity + prio]
   uint32_t *dmacw = nullptr;  // per device: {s_addr[0..1] << 16, s_addr[2..5]}

@@ -1,0 +1,371 @@
+// vigpol on MI355X: batch classification + per-destination token buckets.
+//
+// Reference behaviour (paths relative to the reference repository):
+//   nf_process            vigpol/policer_main.c:120-145
+//   policer_check_tb      vigpol/policer_main.c:34-111
+//   expiry                vigpol/policer_main.c:21-32 (only for packets whose
+//                         IPv4 header parsed: nf_process returns before it
+//                         otherwise)
+//   state                 vigpol/dataspec.ml:5-11 (dyn_map, dyn_keys,
+//                         dyn_heap, dyn_vals)
+// Same segment structure as the other NFs, one more phase:
+//   phase A  parse; LAN packets go out on the WAN device, packets from other
+//            devices and non-IPv4 frames are dropped; WAN packets look their
+//            destination address up: a hit is recorded, a miss is queued
+//            (sizes <= burst may allocate, larger ones may not);
+//   phase B  allocating misses: de-duplicated, ranked and given dchain
+//            indices in packet order (tbl_new_keys); a later packet of an
+//            allocated address is a hit of that index;
+//   phase C  misses larger than the burst: a hit iff an earlier packet of the
+//            segment allocated their address, dropped otherwise;
+//   phase T  token buckets: every policed packet (index known) is sorted by
+//            (index, packet order) and one lane per index replays its
+//            packets through policer_check_tb's arithmetic in order. The
+//            bucket is a serial recurrence per address (refill, clamp,
+//            conditional take), so it is replayed, not scanned.
+// Frames are never written (the policer only decides the output device).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <vector>
+
+#include "vp_table.h"
+
+namespace vp {
+
+int ws_reserve(vp_ctx *c, uint32_t n);  // vp_runtime.hip
+
+// ip_addr_hash (generated for vigpol/ip_addr.h:6-8): crc32c_u32(0, addr);
+// four byte-position tables of a 4-byte message.
+constexpr uint32_t kPolTabs = 4;
+constexpr uint64_t kNsPerS = 1000000000ull;  // VIGOR_TIME_SECONDS_MULTIPLIER
+
+__device__ __forceinline__ uint32_t pol_hash(const uint32_t *T, uint32_t a) {
+  return T[a & 0xFF] ^ T[256 + ((a >> 8) & 0xFF)] ^ T[512 + ((a >> 16) & 0xFF)] ^
+         T[768 + (a >> 24)];
+}
+
+struct PolArgs {
+  const uint8_t *frames;
+  const uint16_t *len;
+  const uint16_t *in_dev;
+  uint16_t *out;
+  uint32_t *log;   // touch log (rejuvenations)
+  uint32_t *pidx;  // policed packets: their index (kNone otherwise)
+  uint64_t seq_base;
+  uint32_t slot, p0, p1;
+  TableDev t;
+  const uint32_t *crc_tab;
+  uint32_t *miss;   // allocating misses (size <= burst)
+  uint32_t *defer;  // misses larger than the burst
+  uint64_t burst, rate, thr;  // thr = burst * 1e9 / rate (u64, as the reference)
+  uint16_t lan, wan;
+};
+
+// nf_then_get_rte_ipv4_header (nf-util.h:122-151): the dst address offset,
+// or 0 when the header does not parse.
+__device__ __forceinline__ uint32_t pol_ipv4(const GFrame &f, uint32_t total) {
+  const uint16_t unread = (uint16_t)(total - 14);
+  if (!(f.r16(12) == bswap16(0x0800)) | (unread < 20)) return 0;
+  const uint8_t ihl = f.r8(14) & 0x0F;
+  if ((ihl < 5) | (unread < bswap16(f.r16(16)))) return 0;
+  return 14 + 16;
+}
+
+// Phase A: one packet per lane.
+__global__ __launch_bounds__(256) void pol_classify(PolArgs a) {
+  __shared__ uint32_t T[kPolTabs * 256];
+  for (uint32_t i = threadIdx.x; i < kPolTabs * 256; i += blockDim.x)
+    T[i] = a.crc_tab[i];
+  __syncthreads();
+  for (uint32_t p = a.p0 + blockIdx.x * blockDim.x + threadIdx.x; p < a.p1;
+       p += gridDim.x * blockDim.x) {
+    const uint32_t in = a.in_dev[p], len = a.len[p];
+    const GFrame f{const_cast<uint8_t *>(a.frames) + (size_t)p * a.slot, a.slot};
+    const uint32_t dipo = pol_ipv4(f, len);
+    a.log[p] = kNone;
+    a.pidx[p] = kNone;
+    if (!dipo) {  // not IPv4: dropped before the expiry (policer_main.c:126-130)
+      a.out[p] = (uint16_t)in;
+      continue;
+    }
+    if (in == a.lan) {  // outgoing: not policed (policer_main.c:134-136)
+      a.out[p] = a.wan;
+      continue;
+    }
+    if (in != a.wan) {  // unknown port (policer_main.c:141-144)
+      a.out[p] = (uint16_t)in;
+      continue;
+    }
+    const uint32_t dst = f.r32(dipo);
+    const uint32_t key[4] = {dst, 0, 0, 0};
+    const uint32_t idx = tbl_probe(a.t, pol_hash(T, dst), key);
+    if (idx != kNone) {
+      a.log[p] = idx;
+      a.pidx[p] = idx;
+    } else if (len <= a.burst) {
+      a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
+    } else {
+      a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
+    }
+  }
+}
+
+// ------------------------------------------------------------- phase B --
+
+__global__ void pol_miss_keys(PolArgs a, const uint32_t *list, uint32_t n,
+                              uint32_t *mkey, uint32_t *mhash) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += gridDim.x * blockDim.x) {
+    const uint32_t p = list[j];
+    const GFrame f{const_cast<uint8_t *>(a.frames) + (size_t)p * a.slot, a.slot};
+    const uint32_t dst = f.r32(30);
+    uint32_t *k = mkey + 4 * (size_t)j;
+    k[0] = dst;
+    k[1] = k[2] = k[3] = 0;
+    mhash[j] = pol_hash(a.crc_tab, dst);
+  }
+}
+
+// Allocating misses: the first sighting of an address took a free index (or
+// the table was full: dropped, policer_main.c:84-89); later sightings are
+// hits of that index.
+__global__ void pol_miss_finish(PolArgs a, const uint32_t *list, uint32_t n,
+                                const uint32_t *scratch, const uint32_t *rep,
+                                const uint32_t *assign) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += gridDim.x * blockDim.x) {
+    const uint32_t p = list[j];
+    const uint32_t idx = assign[scratch[rep[j]]];
+    if (idx == kNone) {
+      a.out[p] = a.wan;
+      continue;
+    }
+    a.log[p] = idx;
+    a.pidx[p] = idx;
+  }
+}
+
+// ------------------------------------------------------------- phase C --
+// Misses larger than the burst (policer_main.c:79-82): a hit iff an earlier
+// packet of the segment allocated the address.
+__global__ void pol_defer_finish(PolArgs a, const uint32_t *list, uint32_t n) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += gridDim.x * blockDim.x) {
+    const uint32_t p = list[j];
+    const GFrame f{const_cast<uint8_t *>(a.frames) + (size_t)p * a.slot, a.slot};
+    const uint32_t dst = f.r32(30);
+    const uint32_t key[4] = {dst, 0, 0, 0};
+    const uint32_t idx = tbl_probe(a.t, pol_hash(a.crc_tab, dst), key);
+    if (idx == kNone || !tbl_allocated_before(a.t, idx, a.seq_base + p)) {
+      a.out[p] = a.wan;
+      continue;
+    }
+    a.log[p] = idx;
+    a.pidx[p] = idx;
+  }
+}
+
+// ------------------------------------------------------------- phase T --
+
+// Sort keys: the packet's index, or `cap` (sorts last) when not policed.
+__global__ void pol_sort_keys(const uint32_t *pidx, uint32_t p0, uint32_t n,
+                              uint32_t cap, uint32_t *key) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += gridDim.x * blockDim.x) {
+    const uint32_t k = pidx[p0 + i];
+    key[i] = k == kNone ? cap : k;
+  }
+}
+
+// One lane per run of equal indices in the sorted list: policer_check_tb's
+// bucket arithmetic over the run's packets in packet order. The run's first
+// packet is the allocation when the index was born at it
+// (policer_main.c:91-100: bucket = burst - size, time = now).
+__global__ void pol_buckets(PolArgs a, const uint32_t *skey, const uint32_t *sval,
+                            uint32_t n, uint32_t cap, NowSpec now,
+                            uint64_t *bsize, int64_t *btime) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += gridDim.x * blockDim.x) {
+    const uint32_t k = skey[i];
+    if (k >= cap || (i > 0 && skey[i - 1] == k)) continue;
+    uint64_t size = bsize[k];
+    uint64_t btu = (uint64_t)btime[k];
+    for (uint32_t j = i; j < n && skey[j] == k; j++) {
+      const uint32_t p = sval[j];
+      const uint64_t len = a.len[p];
+      const uint64_t tu = (uint64_t)now.at(p);
+      bool fwd;
+      if (j == i && a.t.birth[k] == a.seq_base + p) {
+        size = a.burst - len;  // new flow: forwarded (policer_main.c:91-103)
+        fwd = true;
+      } else {  // policer_main.c:39-72
+        const uint64_t diff = tu - btu;
+        if (diff < a.thr) {
+          size += diff * a.rate / kNsPerS;
+          if (size > a.burst) size = a.burst;
+        } else {
+          size = a.burst;
+        }
+        fwd = size > len;
+        if (fwd) size -= len;
+      }
+      btu = tu;
+      a.out[p] = fwd ? a.lan : a.wan;
+    }
+    bsize[k] = size;
+    btime[k] = (int64_t)btu;
+  }
+}
+
+// The last packet of [0, n) whose IPv4 header parses (-1 if none): packets
+// after it run no expiry (policer_main.c:124-132). One block walks back from
+// the end 256 packets at a time.
+__global__ __launch_bounds__(256) void pol_last_ipv4(const uint8_t *frames,
+                                                     uint32_t slot,
+                                                     const uint16_t *len,
+                                                     uint32_t n, int32_t *out) {
+  __shared__ int32_t found;
+  if (threadIdx.x == 0) found = -1;
+  __syncthreads();
+  for (int64_t base = (int64_t)n - 1; base >= 0; base -= blockDim.x) {
+    const int64_t p = base - threadIdx.x;
+    if (p >= 0) {
+      const GFrame f{const_cast<uint8_t *>(frames) + (size_t)p * slot, slot};
+      if (pol_ipv4(f, len[p])) atomicMax(&found, (int32_t)p);
+    }
+    __syncthreads();
+    if (found >= 0) break;
+  }
+  if (threadIdx.x == 0) *out = found;
+}
+
+// =============================================================== host ==
+
+// policer_expire_entries (policer_main.c:21-32): exp_time and the cutoff in
+// unsigned 64-bit arithmetic.
+static inline int64_t pol_cutoff(const vp_ctx *c, int64_t t) {
+  const uint64_t exp_time = kNsPerS * c->pol.burst / c->pol.rate;
+  return (int64_t)((uint64_t)t - exp_time);
+}
+
+static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
+                       uint32_t p0, uint32_t p1, float *ms, int *launches,
+                       uint32_t *allocated) {
+  FlowTable &t = c->ft;
+  Workspace &w = c->ws;
+  PolArgs a{};
+  a.frames = b->frames;
+  a.len = b->len;
+  a.in_dev = b->in_dev;
+  a.out = b->out_dev;
+  a.log = w.log;
+  a.pidx = w.aux;
+  const uint64_t seq0 = c->seq;
+  a.seq_base = seq0;
+  a.slot = b->slot;
+  a.p0 = p0;
+  a.p1 = p1;
+  a.t = tbl_dev(t);
+  a.crc_tab = c->crc_tab;
+  a.miss = w.miss;
+  a.defer = w.defer;
+  a.burst = c->pol.burst;
+  a.rate = c->pol.rate;
+  a.thr = c->pol.burst * kNsPerS / c->pol.rate;
+  a.lan = c->pol.lan_device;
+  a.wan = c->pol.wan_device;
+  const uint32_t n = p1 - p0;
+
+  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
+  VP_HIP(hipEventRecord(c->ev0, c->stream));
+  pol_classify<<<grid_for(n), 256, 0, c->stream>>>(a);
+  VP_HIP(hipGetLastError());
+  VP_HIP(hipEventRecord(c->ev1, c->stream));
+  VP_TRY(read_ctl(c, t));
+  float kms = 0.f;
+  VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
+  *ms += kms;
+  *launches += 1;
+  const uint32_t nmiss = t.h_ctl.miss_count, ndefer = t.h_ctl.defer_count;
+  if (nmiss) {
+    size_t need = 0;
+    hipcub::DeviceRadixSort::SortKeys(nullptr, need, w.miss, w.miss_sorted,
+                                      (int)nmiss, 0, 32, c->stream);
+    VP_TRY(cub_reserve(c, need));
+    VP_HIP(hipcub::DeviceRadixSort::SortKeys(w.cub_tmp, w.cub_bytes, w.miss,
+                                             w.miss_sorted, (int)nmiss, 0, 32,
+                                             c->stream));
+    pol_miss_keys<<<grid_for(nmiss), 256, 0, c->stream>>>(a, w.miss_sorted, nmiss,
+                                                          w.mkey, w.mhash);
+    VP_HIP(hipGetLastError());
+    VP_TRY(tbl_new_keys(c, t, NewKeys{nmiss, w.miss_sorted}, c->seq, nullptr));
+    pol_miss_finish<<<grid_for(nmiss), 256, 0, c->stream>>>(
+        a, w.miss_sorted, nmiss, w.scratch, w.rep, w.assign);
+    VP_HIP(hipGetLastError());
+    *allocated |= 1u;
+  }
+  if (ndefer) {
+    a.t = tbl_dev(t);  // a rebuild during phase B may have changed the layout
+    pol_defer_finish<<<grid_for(ndefer), 256, 0, c->stream>>>(a, w.defer, ndefer);
+    VP_HIP(hipGetLastError());
+  }
+  // phase T: (index, packet) pairs sorted by index; radix sort is stable, so
+  // each index's packets stay in packet order
+  a.t = tbl_dev(t);
+  uint32_t bits = 1;
+  while ((1ull << bits) <= t.cap) bits++;
+  pol_sort_keys<<<grid_for(n), 256, 0, c->stream>>>(w.aux, p0, n, t.cap, w.rank);
+  VP_HIP(hipGetLastError());
+  size_t need = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, need, w.rank, w.skey, w.iota + p0,
+                                     w.sval, (int)n, 0, (int)bits, c->stream);
+  VP_TRY(cub_reserve(c, need));
+  VP_HIP(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, w.cub_bytes, w.rank, w.skey,
+                                            w.iota + p0, w.sval, (int)n, 0,
+                                            (int)bits, c->stream));
+  pol_buckets<<<grid_for(n), 256, 0, c->stream>>>(a, w.skey, w.sval, n, t.cap, now,
+                                                  c->pol_size, c->pol_time);
+  VP_HIP(hipGetLastError());
+  VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
+  if (nmiss || ndefer) VP_TRY(read_ctl(c, t));
+  return 0;
+}
+
+int pol_process_device(vp_ctx *c, const vp_dev_batch *b) {
+  // expiries only up to the batch's last IPv4 packet
+  uint32_t exp_end = b->n;
+  if (b->n && b->frames && b->len && b->slot >= 64) {
+    VP_TRY(ws_reserve(c, b->n));
+    int32_t *d_last = reinterpret_cast<int32_t *>(&c->ft.ctl->aux_count);
+    pol_last_ipv4<<<1, 256, 0, c->stream>>>(b->frames, b->slot, b->len, b->n,
+                                            d_last);
+    VP_HIP(hipGetLastError());
+    int32_t last = -1;
+    VP_HIP(hipMemcpyAsync(&last, d_last, 4, hipMemcpyDeviceToHost, c->stream));
+    VP_HIP(hipStreamSynchronize(c->stream));
+    exp_end = (uint32_t)(last + 1);
+  }
+  ExpiringTable tabs[1] = {{&c->ft, pol_cutoff}};
+  return run_batch(c, b, tabs, 1, pol_segment, exp_end);
+}
+
+// State by index: alloc, ts, dyn_keys (u32 address), dyn_vals.
+int pol_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint32_t *keys,
+             uint64_t *bucket_size, int64_t *bucket_time) {
+  const uint32_t cap = c->ft.cap;
+  std::vector<uint32_t> k(4ull * cap);
+  VP_TRY(tbl_dump(c, c->ft, alloc, ts, k.data()));
+  for (uint32_t i = 0; i < cap; i++) keys[i] = k[4ull * i];
+  VP_HIP(hipMemcpy(bucket_size, c->pol_size, 8ull * cap, hipMemcpyDeviceToHost));
+  VP_HIP(hipMemcpy(bucket_time, c->pol_time, 8ull * cap, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+void build_pol_tables(std::vector<uint32_t> &tab) {
+  tab.assign(kPolTabs * 256, 0);
+  for (uint32_t j = 0; j < kPolTabs; j++)
+    build_position_table(&tab[j * 256], (int)j, 4);
+}
+
+}  // namespace vp

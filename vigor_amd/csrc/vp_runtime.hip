@@ -33,6 +33,10 @@ void lb_fill_cht(uint32_t height, uint32_t bcap, std::vector<uint32_t> &cht);
 int fw_process_device(vp_ctx *c, const vp_dev_batch *b);
 void build_fw_tables(std::vector<uint32_t> &tab);
 int fw_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *keys, uint32_t *int_dev);
+int pol_process_device(vp_ctx *c, const vp_dev_batch *b);
+void build_pol_tables(std::vector<uint32_t> &tab);
+int pol_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint32_t *keys,
+             uint64_t *bucket_size, int64_t *bucket_time);
 int lb_dump(vp_ctx *c, uint8_t *f_alloc, int64_t *f_ts, uint8_t *f_keys,
             uint32_t *f_backend, uint8_t *b_alloc, int64_t *b_ts, uint32_t *b_ip,
             uint8_t *b_mac, uint16_t *b_nic);
@@ -103,6 +107,7 @@ int ws_reserve(vp_ctx *c, uint32_t n) {
     VP_TRY(dalloc(&w.aux_sorted, cap));
     VP_TRY(dalloc(&w.rlist, cap));
   }
+  if (c->kind == KIND_POL) VP_TRY(dalloc(&w.aux, cap));  // policed indices
   VP_TRY(dalloc(&w.iota, cap));
   VP_TRY(dalloc(&w.skey, cap));
   VP_TRY(dalloc(&w.sval, cap));
@@ -144,7 +149,7 @@ static void free_all(vp_ctx *c) {
                   w.bins_ent, w.bins_cnt,
                   w.d_out,   w.d_now,    c->crc_tab, c->macw,
                   c->st_bk,  c->st_val,  c->be_rec,   c->cht,   c->dmacw,
-                  w.sbuf,    w.rbuf};
+                  w.sbuf,    w.rbuf,     c->pol_size, c->pol_time};
   for (void *p : ptrs) hipFree(p);
   if (w.h_frames) hipHostFree(w.h_frames);
   if (w.h_meta) hipHostFree(w.h_meta);
@@ -238,6 +243,21 @@ static int fw_init(vp_ctx *c, const vp_fw_config *cfg) {
   for (int d = 0; d < cfg->n_devices; d++)
     mac_words(cfg->endpoint_macs[d], cfg->device_macs[d], &mw[3 * d]);
   VP_TRY(upload(&c->macw, mw));
+  return 0;
+}
+
+static int pol_init(vp_ctx *c, const vp_pol_config *cfg) {
+  c->kind = KIND_POL;
+  c->pol = *cfg;
+  VP_TRY(tbl_alloc(c, c->ft, cfg->dyn_capacity));
+  std::vector<uint32_t> tab;
+  build_pol_tables(tab);
+  VP_TRY(upload(&c->crc_tab, tab));
+  // dyn_vals (DynamicValue_allocate zero-fills, vigpol/dataspec.ml:8)
+  VP_TRY(dalloc(&c->pol_size, cfg->dyn_capacity));
+  VP_TRY(dalloc(&c->pol_time, cfg->dyn_capacity));
+  VP_HIP(hipMemset(c->pol_size, 0, 8ull * cfg->dyn_capacity));
+  VP_HIP(hipMemset(c->pol_time, 0, 8ull * cfg->dyn_capacity));
   return 0;
 }
 
@@ -487,6 +507,26 @@ int vp_fw_create(const vp_fw_config *cfg, int gpu, vp_ctx **out) {
   return 0;
 }
 
+int vp_pol_create(const vp_pol_config *cfg, int gpu, vp_ctx **out) {
+  if (!cfg || !out) return VP_EINVAL;
+  // policer_config.c:44-77: devices < rte_eth_dev_count_avail(), rate and
+  // burst strictly positive; map.c:73 (CAPACITY_POW2)
+  if (!is_pow2(cfg->dyn_capacity) || cfg->dyn_capacity > (1u << 30) ||
+      cfg->n_devices == 0 || cfg->n_devices > VP_MAX_DEVICES ||
+      cfg->lan_device >= cfg->n_devices || cfg->wan_device >= cfg->n_devices ||
+      cfg->rate == 0 || cfg->burst == 0)
+    return VP_EINVAL;
+  vp_ctx *c = new vp_ctx();
+  int rc = ctx_common(c, gpu);
+  if (!rc) rc = pol_init(c, cfg);
+  if (rc) {
+    free_all(c);
+    return rc;
+  }
+  *out = c;
+  return 0;
+}
+
 void vp_destroy(vp_ctx *ctx) { free_all(ctx); }
 
 int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
@@ -512,6 +552,9 @@ int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
       break;
     case KIND_FW:
       rc = fw_process_device(c, b);
+      break;
+    case KIND_POL:
+      rc = pol_process_device(c, b);
       break;
     default:
       break;
@@ -611,6 +654,15 @@ int vp_fw_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *keys,
     return VP_EINVAL;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
   return fw_dump(c, alloc, ts, keys, int_dev);
+}
+
+int vp_pol_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint32_t *keys,
+                uint64_t *bucket_size, int64_t *bucket_time) {
+  if (!c || c->kind != KIND_POL || !alloc || !ts || !keys || !bucket_size ||
+      !bucket_time)
+    return VP_EINVAL;
+  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  return pol_dump(c, alloc, ts, keys, bucket_size, bucket_time);
 }
 
 int64_t vp_live_count(vp_ctx *c) {

@@ -212,9 +212,11 @@ using SegmentFn = int (*)(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
                           uint32_t p0, uint32_t p1, float *kernel_ms,
                           int *launches, uint32_t *allocated);
 // Validates the batch, then cuts it where any table may expire an entry and
-// runs the exact expiries between segments (see vp_nat.hip header).
+// runs the exact expiries between segments (see vp_nat.hip header). Only
+// packets [0, exp_end) run an expiry (vigpol expires after the IPv4 parse
+// only); the others leave the tables as they are.
 int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
-              SegmentFn seg);
+              SegmentFn seg, uint32_t exp_end = UINT32_MAX);
 
 // ------------------------------------------------- multi-GPU new keys --
 // (run_batch_sharded, vp_table.hip) Gather every rank's count of local new

@@ -807,7 +807,7 @@ static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
                              ExpiringTable *tabs, int ntabs, SegmentFn seg);
 
 int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
-              SegmentFn seg) {
+              SegmentFn seg, uint32_t exp_end) {
   if (c->comm) return run_batch_sharded(c, b, tabs, ntabs, seg);
   c->off = 0;
   const uint32_t n = b->n;
@@ -842,7 +842,13 @@ int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
   float ms = 0.f;
   int launches = 0;
   uint32_t a0 = 0;
+  const uint32_t ne = std::min(n, exp_end);  // packets that may expire
   while (a0 < n) {
+    if (a0 >= ne) {  // the rest runs no expiry: one segment
+      uint32_t allocated = 0;
+      VP_TRY(seg(c, b, now, a0, n, &ms, &launches, &allocated));
+      break;
+    }
     const int64_t ta = at(a0);
     auto lim = [&](int i) { return std::min<uint64_t>(tabs[i].t->ts_floor, (uint64_t)ta); };
     auto safe = [&](uint32_t p) {
@@ -861,8 +867,8 @@ int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
       }
     }
     uint32_t b1 = n;
-    if (!safe(n - 1)) {  // first unsafe packet (cutoffs are monotone in time)
-      uint32_t lo = a0 + 1, hi = n - 1;
+    if (!safe(ne - 1)) {  // first unsafe packet (cutoffs are monotone in time)
+      uint32_t lo = a0 + 1, hi = ne - 1;
       while (lo < hi) {
         const uint32_t mid = lo + (hi - lo) / 2;
         if (safe(mid)) lo = mid + 1; else hi = mid;

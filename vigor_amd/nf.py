@@ -13,7 +13,7 @@ import ctypes as C
 import numpy as np
 
 from . import (BridgeConfigC, DevBatchC, FwConfigC, LbConfigC, NatConfigC,
-               _check, lib)
+               PolConfigC, _check, lib)
 
 
 def _dptr(t):
@@ -199,3 +199,29 @@ class Fw(NfBase):
         _check(self.L.vp_fw_dump(self.h, P(alloc), P(ts), P(keys), P(dev)),
                "vp_fw_dump")
         return alloc, ts, keys.reshape(n, 16), dev
+
+
+class Pol(NfBase):
+    """vigpol (vigpol/policer_main.c): per-destination token buckets on the
+    WAN device; frames are never rewritten."""
+    kind = "pol"
+
+    def __init__(self, cfg: PolConfigC, gpu: int = 0, libpath=None):
+        super().__init__(libpath)
+        self.cfg = cfg
+        _check(self.L.vp_pol_create(C.byref(cfg), gpu, C.byref(self.h)),
+               "vp_pol_create")
+
+    def dump(self):
+        """By index: alloc, ts, dyn_keys (raw u32 address), bucket_size,
+        bucket_time."""
+        n = self.cfg.dyn_capacity
+        alloc = np.zeros(n, np.uint8)
+        ts = np.zeros(n, np.int64)
+        keys = np.zeros(n, np.uint32)
+        size = np.zeros(n, np.uint64)
+        btime = np.zeros(n, np.int64)
+        P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
+        _check(self.L.vp_pol_dump(self.h, P(alloc), P(ts), P(keys), P(size),
+                                  P(btime)), "vp_pol_dump")
+        return alloc, ts, keys, size, btime
