@@ -1,5 +1,5 @@
 """Side benchmarks for the other NFs on the path (BASELINE configs 3 and 4,
-and vigfw, SURVEY.md §8(f);
+and vigfw / vigpol, SURVEY.md §8(f);
 the headline line is bench.py's vignat). One JSON line per workload:
 device-resident Mpps over pre-generated batches, kernel time of the
 classification kernel, and the oracle's 1-core rate on a sample.
@@ -169,6 +169,39 @@ def bench_fw(args, dev):
                              "kind": "port"} if cpu else None}
 
 
+def bench_pol(args, dev):
+    """vigpol 64 B, 1M destinations, the reference's own NF_ARGS rate and
+    burst (vigpol/Makefile:5: 375 MB/s, 3.75 GB): warm-up allocates every
+    destination, then steady state (every packet a hit, replayed through its
+    token bucket)."""
+    import orc
+    N = args.flows
+    argv = ["--lan", "1", "--wan", "0", "--rate", "375000000", "--burst",
+            "3750000000", "--capacity", str(N)]
+    pol = vigor_amd.Pol(vigor_amd.pol_config_from_args(argv, 2), gpu=0)
+    B = args.batch
+    gen = lambda s: T.pol_trace(B, N, start=s)  # noqa
+    t0 = time.perf_counter()
+    warm = [to_dev(gen(w * B), dev) for w in range(max(1, N // B))]
+    run(pol, warm, B, dev)
+    warm_s = time.perf_counter() - t0
+    base = len(warm) * B
+    batches = [to_dev(gen(base + k * B), dev) for k in range(args.steps)]
+    mpps, kmpps, out = run(pol, batches, B, dev)
+    cpu = None
+    if not args.no_cpu:
+        ocfg = orc.pol_cfg(lan=1, wan=0, capacity=N, n_devices=2)
+        cpu = cpu_rate("pol", ocfg, [T.pol_trace(N, N)],
+                       [T.pol_trace(1 << 21, N, start=N)])
+    return {"workload": "vigpol 64B, %d destinations" % N,
+            "value": round(mpps, 1), "unit": "Mpps", "kernel_mpps": round(kmpps, 1),
+            "kernel": "pol_classify", "batch_packets": B, "steps": args.steps,
+            "warm_s": round(warm_s, 2),
+            "forwarded": int((out == 1).sum().item()),
+            "cpu_baseline": {"value": round(cpu, 2), "unit": "Mpps", "cores": 1,
+                             "kind": "port"} if cpu else None}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1 << 22)
@@ -176,7 +209,7 @@ def main():
     ap.add_argument("--stations", type=int, default=1 << 20)
     ap.add_argument("--flows", type=int, default=1 << 20)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--only", default="bridge,flood,lb,fw")
+    ap.add_argument("--only", default="bridge,flood,lb,fw,pol")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     todo = args.only.split(",")
@@ -188,6 +221,8 @@ def main():
         print(json.dumps(bench_lb(args, dev)), flush=True)
     if "fw" in todo:
         print(json.dumps(bench_fw(args, dev)), flush=True)
+    if "pol" in todo:
+        print(json.dumps(bench_pol(args, dev)), flush=True)
 
 
 if __name__ == "__main__":

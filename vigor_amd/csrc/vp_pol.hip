@@ -50,8 +50,8 @@ struct PolArgs {
   const uint16_t *len;
   const uint16_t *in_dev;
   uint16_t *out;
-  uint32_t *log;   // touch log (rejuvenations)
-  uint32_t *pidx;  // policed packets: their index (kNone otherwise)
+  uint32_t *pidx;  // policed packets: their index (kNone otherwise); every
+                   // policed packet rejuvenates it (policer_main.c:38)
   uint64_t seq_base;
   uint32_t slot, p0, p1;
   TableDev t;
@@ -72,6 +72,18 @@ __device__ __forceinline__ uint32_t pol_ipv4(const GFrame &f, uint32_t total) {
   return 14 + 16;
 }
 
+// The same predicate on a slot's first 48 bytes in three 16-byte loads
+// (slots are >= 64 B and 16-B aligned): the dst address, or 0.
+__device__ __forceinline__ uint32_t pol_ipv4_w(const uint4 *s, uint32_t total,
+                                               uint32_t *dst) {
+  const uint4 h0 = s[0], h1 = s[1], h2 = s[2];
+  const uint16_t unread = (uint16_t)(total - 14);
+  const uint32_t ihl = (h0.w >> 16) & 0x0F;
+  const uint16_t tl = bswap16((uint16_t)(h1.x & 0xFFFF));
+  *dst = (h1.w >> 16) | (h2.x << 16);  // bytes 30-33
+  return ((h0.w & 0xFFFF) == 0x0008) & (unread >= 20) & (ihl >= 5) & (unread >= tl);
+}
+
 // Phase A: one packet per lane.
 __global__ __launch_bounds__(256) void pol_classify(PolArgs a) {
   __shared__ uint32_t T[kPolTabs * 256];
@@ -81,11 +93,11 @@ __global__ __launch_bounds__(256) void pol_classify(PolArgs a) {
   for (uint32_t p = a.p0 + blockIdx.x * blockDim.x + threadIdx.x; p < a.p1;
        p += gridDim.x * blockDim.x) {
     const uint32_t in = a.in_dev[p], len = a.len[p];
-    const GFrame f{const_cast<uint8_t *>(a.frames) + (size_t)p * a.slot, a.slot};
-    const uint32_t dipo = pol_ipv4(f, len);
-    a.log[p] = kNone;
+    uint32_t dst;
+    const bool v4 = pol_ipv4_w(
+        reinterpret_cast<const uint4 *>(a.frames + (size_t)p * a.slot), len, &dst);
     a.pidx[p] = kNone;
-    if (!dipo) {  // not IPv4: dropped before the expiry (policer_main.c:126-130)
+    if (!v4) {  // not IPv4: dropped before the expiry (policer_main.c:126-130)
       a.out[p] = (uint16_t)in;
       continue;
     }
@@ -97,11 +109,9 @@ __global__ __launch_bounds__(256) void pol_classify(PolArgs a) {
       a.out[p] = (uint16_t)in;
       continue;
     }
-    const uint32_t dst = f.r32(dipo);
     const uint32_t key[4] = {dst, 0, 0, 0};
     const uint32_t idx = tbl_probe(a.t, pol_hash(T, dst), key);
     if (idx != kNone) {
-      a.log[p] = idx;
       a.pidx[p] = idx;
     } else if (len <= a.burst) {
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
@@ -141,7 +151,6 @@ __global__ void pol_miss_finish(PolArgs a, const uint32_t *list, uint32_t n,
       a.out[p] = a.wan;
       continue;
     }
-    a.log[p] = idx;
     a.pidx[p] = idx;
   }
 }
@@ -161,7 +170,6 @@ __global__ void pol_defer_finish(PolArgs a, const uint32_t *list, uint32_t n) {
       a.out[p] = a.wan;
       continue;
     }
-    a.log[p] = idx;
     a.pidx[p] = idx;
   }
 }
@@ -181,18 +189,21 @@ __global__ void pol_sort_keys(const uint32_t *pidx, uint32_t p0, uint32_t n,
 // One lane per run of equal indices in the sorted list: policer_check_tb's
 // bucket arithmetic over the run's packets in packet order. The run's first
 // packet is the allocation when the index was born at it
-// (policer_main.c:91-100: bucket = burst - size, time = now).
+// (policer_main.c:91-100: bucket = burst - size, time = now). The run's last
+// packet is the index's last rejuvenation: the lane stamps ts/tseq itself
+// (no touch-log fold for vigpol).
 __global__ void pol_buckets(PolArgs a, const uint32_t *skey, const uint32_t *sval,
                             uint32_t n, uint32_t cap, NowSpec now,
-                            uint64_t *bsize, int64_t *btime) {
+                            uint64_t *bsize, int64_t *btime, uint32_t p0) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += gridDim.x * blockDim.x) {
     const uint32_t k = skey[i];
     if (k >= cap || (i > 0 && skey[i - 1] == k)) continue;
     uint64_t size = bsize[k];
     uint64_t btu = (uint64_t)btime[k];
+    uint32_t p = p0;
     for (uint32_t j = i; j < n && skey[j] == k; j++) {
-      const uint32_t p = sval[j];
+      p = sval[j];
       const uint64_t len = a.len[p];
       const uint64_t tu = (uint64_t)now.at(p);
       bool fwd;
@@ -215,6 +226,8 @@ __global__ void pol_buckets(PolArgs a, const uint32_t *skey, const uint32_t *sva
     }
     bsize[k] = size;
     btime[k] = (int64_t)btu;
+    a.t.ts[k] = btu;
+    a.t.tseq[k] = a.seq_base + p;
   }
 }
 
@@ -259,8 +272,7 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.len = b->len;
   a.in_dev = b->in_dev;
   a.out = b->out_dev;
-  a.log = w.log;
-  a.pidx = w.aux;
+  a.pidx = w.log;
   const uint64_t seq0 = c->seq;
   a.seq_base = seq0;
   a.slot = b->slot;
@@ -315,7 +327,7 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.t = tbl_dev(t);
   uint32_t bits = 1;
   while ((1ull << bits) <= t.cap) bits++;
-  pol_sort_keys<<<grid_for(n), 256, 0, c->stream>>>(w.aux, p0, n, t.cap, w.rank);
+  pol_sort_keys<<<grid_for(n), 256, 0, c->stream>>>(w.log, p0, n, t.cap, w.rank);
   VP_HIP(hipGetLastError());
   size_t need = 0;
   hipcub::DeviceRadixSort::SortPairs(nullptr, need, w.rank, w.skey, w.iota + p0,
@@ -325,9 +337,8 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
                                             w.iota + p0, w.sval, (int)n, 0,
                                             (int)bits, c->stream));
   pol_buckets<<<grid_for(n), 256, 0, c->stream>>>(a, w.skey, w.sval, n, t.cap, now,
-                                                  c->pol_size, c->pol_time);
+                                                  c->pol_size, c->pol_time, p0);
   VP_HIP(hipGetLastError());
-  VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
   if (nmiss || ndefer) VP_TRY(read_ctl(c, t));
   return 0;
 }

@@ -107,7 +107,6 @@ int ws_reserve(vp_ctx *c, uint32_t n) {
     VP_TRY(dalloc(&w.aux_sorted, cap));
     VP_TRY(dalloc(&w.rlist, cap));
   }
-  if (c->kind == KIND_POL) VP_TRY(dalloc(&w.aux, cap));  // policed indices
   VP_TRY(dalloc(&w.iota, cap));
   VP_TRY(dalloc(&w.skey, cap));
   VP_TRY(dalloc(&w.sval, cap));

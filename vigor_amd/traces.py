@@ -143,6 +143,21 @@ def fw_trace(n_packets: int, n_flows: int, order: str = "rr",
     return frames, lens, in_dev, now
 
 
+def pol_trace(n_packets: int, n_dsts: int, order: str = "rr",
+              slot: int = 64, wan_dev: int = 0, start: int = 0,
+              seed: int = 0x5EED):
+    """vigpol trace: 64 B packets arriving on the WAN device (the policed
+    direction), destination i = 10.0.0.0 + i (a /8 of subscribers), one
+    source; time advances 1 ns per packet like the vignat trace."""
+    d = flow_order(n_packets, n_dsts, order, seed, start)
+    z = np.zeros_like(d)
+    frames, lens = udp_frames(np.full_like(d, ip4(192, 168, 0, 1)),
+                              ip4(10, 0, 0, 0) + d, z + 53, z + 80, slot=slot)
+    in_dev = np.full(n_packets, wan_dev, dtype=np.uint16)
+    now = (NOW0 + np.arange(start, start + n_packets, dtype=np.int64))
+    return frames, lens, in_dev, now
+
+
 def bridge_trace(n_packets: int, n_stations: int, slot: int = 64,
                  start: int = 0, flood_pattern: bool = False):
     """vigbridge config 3: frame p from station p mod N (on port (k & 1)) to
