@@ -12,7 +12,8 @@
  *       void nf_config_init(int argc, char **argv); nf_config_usage();
  *       nf_config_print(); FLOOD_FRAME
  *     exported by the per-NF shim libraries libvignat_nf.so /
- *     libvigbridge_nf.so / libviglb_nf.so (one NF per binary, as the
+ *     libvigbridge_nf.so / libviglb_nf.so / libvigfw_nf.so /
+ *     libvigpol_nf.so (one NF per binary, as the
  *     reference builds one NF per binary, Makefile.dpdk). They link unchanged
  *     against the reference's nf.c (nf.c:143-216). See INTEGRATION.md.
  *

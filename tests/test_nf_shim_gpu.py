@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import orc
-from tracegen import mixed_fw_trace, mixed_nat_trace
+from tracegen import mixed_fw_trace, mixed_nat_trace, mixed_pol_trace
 from vigor_amd import traces as T
 
 pytestmark = pytest.mark.gpu
@@ -95,3 +95,32 @@ def test_fw_loop_matches_oracle(tmp_path, batch):
     f, e = frames.reshape(n, 64), exp.reshape(n, 64)
     for i in range(n):
         assert f[i, :ln[i]].tobytes() == e[i, :ln[i]].tobytes(), i
+
+
+@pytest.mark.parametrize("batch", [0, 700])
+def test_pol_loop_matches_oracle(tmp_path, batch):
+    """host/nf_loop_pol: nf.c's loop linked against libvigpol_nf.so (frames
+    up to 1.4 kB in 1536-byte buffers, so every mbuf holds its length)."""
+    rng = np.random.default_rng(5)
+    n = 3000 if batch else 400
+    slot = 1536
+    fr, ln, dv, now = mixed_pol_trace(rng, n, 100, slot=slot, gap_ns=1500)
+    cfg = orc.pol_cfg(lan=1, wan=0, rate=1_000_000, burst=1500, capacity=64,
+                      n_devices=3)
+    exp = fr.copy()
+    exp_out = orc.Oracle("pol", cfg).run(exp, ln, dv, now, slot)
+    tin, tout = tmp_path / "t.in", tmp_path / "t.out"
+    write_trace(tin, fr, ln, dv, now, slot)
+    cmd = [LOOP + "_pol", str(tin), str(tout)]
+    if batch:
+        cmd += ["--batch", str(batch)]
+    args = ["--lan", "1", "--wan", "0", "--rate", "1000000", "--burst", "1500",
+            "--capacity", "64"]
+    env = dict(os.environ, VIGPATH_NB_DEVICES="3")
+    r = subprocess.run(cmd + ["--"] + args, capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    out, frames = read_out(tout, n, slot)
+    np.testing.assert_array_equal(out, exp_out)
+    assert (out == 1).sum() > 50 and (out == 0).sum() > 50
+    np.testing.assert_array_equal(frames, fr)  # the policer never writes

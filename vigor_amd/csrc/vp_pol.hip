@@ -346,7 +346,16 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
 int pol_process_device(vp_ctx *c, const vp_dev_batch *b) {
   // expiries only up to the batch's last IPv4 packet
   uint32_t exp_end = b->n;
-  if (b->n && b->frames && b->len && b->slot >= 64) {
+  // With affine time the whole batch may be free of expiries (the cutoff
+  // of its last packet is below every live stamp): then run_batch makes one
+  // segment whatever exp_end is, and the search is skipped.
+  bool may_expire = true;
+  if (b->n && !b->now && b->now_step >= 0 && b->now0 >= 0) {
+    const int64_t t_last = b->now0 + (int64_t)(b->n - 1) * b->now_step;
+    may_expire = pol_cutoff(c, t_last) >
+                 (int64_t)std::min<uint64_t>(c->ft.ts_floor, (uint64_t)b->now0);
+  }
+  if (may_expire && b->n && b->frames && b->len && b->slot >= 64) {
     VP_TRY(ws_reserve(c, b->n));
     int32_t *d_last = reinterpret_cast<int32_t *>(&c->ft.ctl->aux_count);
     pol_last_ipv4<<<1, 256, 0, c->stream>>>(b->frames, b->slot, b->len, b->n,
