@@ -99,3 +99,23 @@ def test_config_rejects_like_reference():
     cfg = vigor_amd.pol_config_from_args(["--capacity", "100"], 2)
     with pytest.raises(vigor_amd.VigpathError):
         vigor_amd.Pol(cfg, gpu=0)  # not a power of two (map.c:73)
+
+
+def test_steady_state_grouping_path():
+    """Segments without misses and with short runs take the grouping path
+    (per-index hit counts from phase A, scan + scatter, per-lane insertion
+    sort); uniformly random order puts each run's packets out of order in
+    the scatter. A hot address (run > 64) in the last batch sends that
+    segment to the radix-sort path instead. Both must equal the oracle."""
+    rng = np.random.default_rng(21)
+    n_dst, n = 5000, 60000
+    d = np.concatenate([np.arange(n_dst), rng.integers(0, n_dst, n - n_dst)])
+    d[-3000::7] = 17  # hot address in the last batch
+    f, _ = T.udp_frames(np.full(n, T.ip4(9, 9, 9, 9)), T.ip4(10, 0, 0, 0) + d,
+                        np.full(n, 53), np.full(n, 80))
+    ln = rng.integers(60, 900, n).astype(np.uint16)
+    dv = np.zeros(n, np.uint16)
+    now = (T.NOW0 + np.cumsum(rng.integers(0, 40, n))).astype(np.int64)
+    pol, o = make_pair(cap=8192, rate=2_000_000, burst=2000)
+    check_batches(pol, o, f.copy(), ln, dv, now, 64, [n_dst, 25000, 45000])
+    check_state(pol, o, 8192)

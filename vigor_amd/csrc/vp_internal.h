@@ -146,6 +146,8 @@ struct vp_ctx {
   vp_pol_config pol{};
   uint64_t *pol_size = nullptr;  // vigpol dyn_vals: bucket_size by index
   int64_t *pol_time = nullptr;   //                  bucket_time by index
+  uint32_t *pol_cnt = nullptr;   // hits per index in a segment (grouping)
+  uint32_t *pol_off = nullptr;   // exclusive scan of pol_cnt
   uint4 *be_rec = nullptr;  // viglb backends[]: {ip, mac0-3, mac4-5|nic<<16, 0}
   uint32_t *cht = nullptr;  // viglb CHT, cht[bucket * backend_capacity + prio]
   uint32_t *dmacw = nullptr;  // per device: {s_addr[0..1] << 16, s_addr[2..5]}

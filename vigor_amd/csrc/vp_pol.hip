@@ -18,11 +18,17 @@
 //            allocated address is a hit of that index;
 //   phase C  misses larger than the burst: a hit iff an earlier packet of the
 //            segment allocated their address, dropped otherwise;
-//   phase T  token buckets: every policed packet (index known) is sorted by
-//            (index, packet order) and one lane per index replays its
+//   phase T  token buckets: every policed packet (index known) is grouped
+//            by index in packet order and one lane per index replays its
 //            packets through policer_check_tb's arithmetic in order. The
 //            bucket is a serial recurrence per address (refill, clamp,
-//            conditional take), so it is replayed, not scanned.
+//            conditional take), so it is replayed, not scanned. Grouping:
+//            phase A counts hits per index (atomicAdd: the packet's rank in
+//            its run, in arbitrary order); when the segment had no misses
+//            and no run is longer than kRunMax, a scan + scatter groups the
+//            runs and each lane puts its run back in packet order (insertion
+//            sort of <= kRunMax positions); otherwise a stable radix sort of
+//            (index, packet) pairs does it.
 // Frames are never written (the policer only decides the output device).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -59,8 +65,13 @@ struct PolArgs {
   uint32_t *miss;   // allocating misses (size <= burst)
   uint32_t *defer;  // misses larger than the burst
   uint64_t burst, rate, thr;  // thr = burst * 1e9 / rate (u64, as the reference)
+  uint32_t *cnt;     // hits per index in this segment (phase A)
+  uint32_t *rnk;     // a hit's rank in its index's run (arbitrary order)
+  uint32_t *maxrun;  // longest run (ctl->aux_count)
   uint16_t lan, wan;
 };
+
+constexpr uint32_t kRunMax = 64;  // longest run the grouping path sorts per lane
 
 // nf_then_get_rte_ipv4_header (nf-util.h:122-151): the dst address offset,
 // or 0 when the header does not parse.
@@ -90,6 +101,7 @@ __global__ __launch_bounds__(256) void pol_classify(PolArgs a) {
   for (uint32_t i = threadIdx.x; i < kPolTabs * 256; i += blockDim.x)
     T[i] = a.crc_tab[i];
   __syncthreads();
+  uint32_t lmax = 0;
   for (uint32_t p = a.p0 + blockIdx.x * blockDim.x + threadIdx.x; p < a.p1;
        p += gridDim.x * blockDim.x) {
     const uint32_t in = a.in_dev[p], len = a.len[p];
@@ -113,12 +125,17 @@ __global__ __launch_bounds__(256) void pol_classify(PolArgs a) {
     const uint32_t idx = tbl_probe(a.t, pol_hash(T, dst), key);
     if (idx != kNone) {
       a.pidx[p] = idx;
+      const uint32_t r = atomicAdd(&a.cnt[idx], 1u);
+      a.rnk[p] = r;
+      lmax = max(lmax, r + 1);
     } else if (len <= a.burst) {
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
     } else {
       a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
     }
   }
+  for (int o = 32; o > 0; o >>= 1) lmax = max(lmax, (uint32_t)__shfl_xor((int)lmax, o));
+  if (__lane_id() == 0 && lmax) atomicMax(a.maxrun, lmax);
 }
 
 // ------------------------------------------------------------- phase B --
@@ -192,22 +209,20 @@ __global__ void pol_sort_keys(const uint32_t *pidx, uint32_t p0, uint32_t n,
 // (policer_main.c:91-100: bucket = burst - size, time = now). The run's last
 // packet is the index's last rejuvenation: the lane stamps ts/tseq itself
 // (no touch-log fold for vigpol).
-__global__ void pol_buckets(PolArgs a, const uint32_t *skey, const uint32_t *sval,
-                            uint32_t n, uint32_t cap, NowSpec now,
-                            uint64_t *bsize, int64_t *btime, uint32_t p0) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += gridDim.x * blockDim.x) {
-    const uint32_t k = skey[i];
-    if (k >= cap || (i > 0 && skey[i - 1] == k)) continue;
-    uint64_t size = bsize[k];
-    uint64_t btu = (uint64_t)btime[k];
-    uint32_t p = p0;
-    for (uint32_t j = i; j < n && skey[j] == k; j++) {
-      p = sval[j];
+template <class Next>
+__device__ __forceinline__ void pol_replay(const PolArgs &a, uint32_t k,
+                                           uint32_t c, Next next, const NowSpec &now,
+                                           uint64_t *bsize, int64_t *btime) {
+  uint64_t size = bsize[k];
+  uint64_t btu = (uint64_t)btime[k];
+  uint32_t p = 0;
+  for (uint32_t j = 0; j < c; j++) {
+    p = next(j);
+    {
       const uint64_t len = a.len[p];
       const uint64_t tu = (uint64_t)now.at(p);
       bool fwd;
-      if (j == i && a.t.birth[k] == a.seq_base + p) {
+      if (j == 0 && a.t.birth[k] == a.seq_base + p) {
         size = a.burst - len;  // new flow: forwarded (policer_main.c:91-103)
         fwd = true;
       } else {  // policer_main.c:39-72
@@ -224,10 +239,59 @@ __global__ void pol_buckets(PolArgs a, const uint32_t *skey, const uint32_t *sva
       btu = tu;
       a.out[p] = fwd ? a.lan : a.wan;
     }
-    bsize[k] = size;
-    btime[k] = (int64_t)btu;
-    a.t.ts[k] = btu;
-    a.t.tseq[k] = a.seq_base + p;
+  }
+  bsize[k] = size;
+  btime[k] = (int64_t)btu;
+  a.t.ts[k] = btu;
+  a.t.tseq[k] = a.seq_base + p;
+}
+
+// Sorted (index, packet) pairs: one lane per run.
+__global__ void pol_buckets(PolArgs a, const uint32_t *skey, const uint32_t *sval,
+                            uint32_t n, uint32_t cap, NowSpec now,
+                            uint64_t *bsize, int64_t *btime) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += gridDim.x * blockDim.x) {
+    const uint32_t k = skey[i];
+    if (k >= cap || (i > 0 && skey[i - 1] == k)) continue;
+    uint32_t c = 1;
+    while (i + c < n && skey[i + c] == k) c++;
+    pol_replay(a, k, c, [&](uint32_t j) { return sval[i + j]; }, now, bsize, btime);
+  }
+}
+
+// Grouping path: hits scattered to their index's run (off = exclusive scan
+// of cnt), in arbitrary order inside the run.
+__global__ void pol_scatter(const uint32_t *pidx, const uint32_t *rnk, uint32_t p0,
+                            uint32_t p1, const uint32_t *off, uint32_t *grouped) {
+  for (uint32_t p = p0 + blockIdx.x * blockDim.x + threadIdx.x; p < p1;
+       p += gridDim.x * blockDim.x) {
+    const uint32_t k = pidx[p];
+    if (k != kNone) grouped[off[k] + rnk[p]] = p;
+  }
+}
+
+// One lane per index with hits: its run (<= kRunMax positions) put back in
+// packet order by an insertion sort, then replayed.
+__global__ void pol_runs(PolArgs a, const uint32_t *cnt, const uint32_t *off,
+                         const uint32_t *grouped, uint32_t cap, NowSpec now,
+                         uint64_t *bsize, int64_t *btime) {
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < cap;
+       k += gridDim.x * blockDim.x) {
+    const uint32_t c = cnt[k];
+    if (c == 0) continue;
+    uint32_t q[kRunMax];
+    const uint32_t *g = grouped + off[k];
+    for (uint32_t j = 0; j < c; j++) {
+      const uint32_t v = g[j];
+      uint32_t i = j;
+      while (i > 0 && q[i - 1] > v) {
+        q[i] = q[i - 1];
+        i--;
+      }
+      q[i] = v;
+    }
+    pol_replay(a, k, c, [&](uint32_t j) { return q[j]; }, now, bsize, btime);
   }
 }
 
@@ -287,9 +351,14 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.thr = c->pol.burst * kNsPerS / c->pol.rate;
   a.lan = c->pol.lan_device;
   a.wan = c->pol.wan_device;
+  a.cnt = c->pol_cnt;
+  a.rnk = w.aux;
+  a.maxrun = &t.ctl->aux_count;
   const uint32_t n = p1 - p0;
 
   VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
+  VP_HIP(hipMemsetAsync(a.maxrun, 0, 4, c->stream));
+  VP_HIP(hipMemsetAsync(c->pol_cnt, 0, 4ull * t.cap, c->stream));
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   pol_classify<<<grid_for(n), 256, 0, c->stream>>>(a);
   VP_HIP(hipGetLastError());
@@ -322,9 +391,26 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     pol_defer_finish<<<grid_for(ndefer), 256, 0, c->stream>>>(a, w.defer, ndefer);
     VP_HIP(hipGetLastError());
   }
-  // phase T: (index, packet) pairs sorted by index; radix sort is stable, so
-  // each index's packets stay in packet order
   a.t = tbl_dev(t);
+  if (!nmiss && !ndefer && t.h_ctl.aux_count <= kRunMax) {
+    // phase T, grouping path: every policed packet was a phase-A hit and
+    // counted; runs are short
+    size_t need = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, need, c->pol_cnt, c->pol_off,
+                                     (int)t.cap, c->stream);
+    VP_TRY(cub_reserve(c, need));
+    VP_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub_tmp, w.cub_bytes, c->pol_cnt,
+                                            c->pol_off, (int)t.cap, c->stream));
+    pol_scatter<<<grid_for(n), 256, 0, c->stream>>>(w.log, w.aux, p0, p1,
+                                                    c->pol_off, w.sval);
+    pol_runs<<<grid_for(t.cap), 256, 0, c->stream>>>(a, c->pol_cnt, c->pol_off,
+                                                     w.sval, t.cap, now,
+                                                     c->pol_size, c->pol_time);
+    VP_HIP(hipGetLastError());
+    return 0;
+  }
+  // phase T, sorting path: (index, packet) pairs sorted by index; radix sort
+  // is stable, so each index's packets stay in packet order
   uint32_t bits = 1;
   while ((1ull << bits) <= t.cap) bits++;
   pol_sort_keys<<<grid_for(n), 256, 0, c->stream>>>(w.log, p0, n, t.cap, w.rank);
@@ -337,7 +423,7 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
                                             w.iota + p0, w.sval, (int)n, 0,
                                             (int)bits, c->stream));
   pol_buckets<<<grid_for(n), 256, 0, c->stream>>>(a, w.skey, w.sval, n, t.cap, now,
-                                                  c->pol_size, c->pol_time, p0);
+                                                  c->pol_size, c->pol_time);
   VP_HIP(hipGetLastError());
   if (nmiss || ndefer) VP_TRY(read_ctl(c, t));
   return 0;

@@ -107,6 +107,7 @@ int ws_reserve(vp_ctx *c, uint32_t n) {
     VP_TRY(dalloc(&w.aux_sorted, cap));
     VP_TRY(dalloc(&w.rlist, cap));
   }
+  if (c->kind == KIND_POL) VP_TRY(dalloc(&w.aux, cap));  // hit ranks (vp_pol.hip)
   VP_TRY(dalloc(&w.iota, cap));
   VP_TRY(dalloc(&w.skey, cap));
   VP_TRY(dalloc(&w.sval, cap));
@@ -148,7 +149,8 @@ static void free_all(vp_ctx *c) {
                   w.bins_ent, w.bins_cnt,
                   w.d_out,   w.d_now,    c->crc_tab, c->macw,
                   c->st_bk,  c->st_val,  c->be_rec,   c->cht,   c->dmacw,
-                  w.sbuf,    w.rbuf,     c->pol_size, c->pol_time};
+                  w.sbuf,    w.rbuf,     c->pol_size, c->pol_time,
+                  c->pol_cnt, c->pol_off};
   for (void *p : ptrs) hipFree(p);
   if (w.h_frames) hipHostFree(w.h_frames);
   if (w.h_meta) hipHostFree(w.h_meta);
@@ -257,6 +259,8 @@ static int pol_init(vp_ctx *c, const vp_pol_config *cfg) {
   VP_TRY(dalloc(&c->pol_time, cfg->dyn_capacity));
   VP_HIP(hipMemset(c->pol_size, 0, 8ull * cfg->dyn_capacity));
   VP_HIP(hipMemset(c->pol_time, 0, 8ull * cfg->dyn_capacity));
+  VP_TRY(dalloc(&c->pol_cnt, cfg->dyn_capacity));
+  VP_TRY(dalloc(&c->pol_off, cfg->dyn_capacity));
   return 0;
 }
 
