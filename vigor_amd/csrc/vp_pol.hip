@@ -260,10 +260,20 @@ __global__ void pol_buckets(PolArgs a, const uint32_t *skey, const uint32_t *sva
   }
 }
 
+// The grouping path applies when phase A found no misses and no run longer
+// than kRunMax. Its kernels are enqueued right behind phase A, before the
+// host has read the counts back, and check them on the device: in steady
+// state the replay overlaps the control read-back instead of following it.
+__device__ __forceinline__ bool pol_grouping_ok(const Ctl *ctl) {
+  return (ctl->miss_count | ctl->defer_count) == 0 && ctl->aux_count <= kRunMax;
+}
+
 // Grouping path: hits scattered to their index's run (off = exclusive scan
 // of cnt), in arbitrary order inside the run.
 __global__ void pol_scatter(const uint32_t *pidx, const uint32_t *rnk, uint32_t p0,
-                            uint32_t p1, const uint32_t *off, uint32_t *grouped) {
+                            uint32_t p1, const uint32_t *off, uint32_t *grouped,
+                            const Ctl *ctl) {
+  if (!pol_grouping_ok(ctl)) return;
   for (uint32_t p = p0 + blockIdx.x * blockDim.x + threadIdx.x; p < p1;
        p += gridDim.x * blockDim.x) {
     const uint32_t k = pidx[p];
@@ -276,6 +286,7 @@ __global__ void pol_scatter(const uint32_t *pidx, const uint32_t *rnk, uint32_t 
 __global__ void pol_runs(PolArgs a, const uint32_t *cnt, const uint32_t *off,
                          const uint32_t *grouped, uint32_t cap, NowSpec now,
                          uint64_t *bsize, int64_t *btime) {
+  if (!pol_grouping_ok(a.t.ctl)) return;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < cap;
        k += gridDim.x * blockDim.x) {
     const uint32_t c = cnt[k];
@@ -363,6 +374,20 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   pol_classify<<<grid_for(n), 256, 0, c->stream>>>(a);
   VP_HIP(hipGetLastError());
   VP_HIP(hipEventRecord(c->ev1, c->stream));
+  {  // phase T, grouping path (speculative: no-ops unless pol_grouping_ok)
+    size_t need = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, need, c->pol_cnt, c->pol_off,
+                                     (int)t.cap, c->stream);
+    VP_TRY(cub_reserve(c, need));
+    VP_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub_tmp, w.cub_bytes, c->pol_cnt,
+                                            c->pol_off, (int)t.cap, c->stream));
+    pol_scatter<<<grid_for(n), 256, 0, c->stream>>>(w.log, w.aux, p0, p1,
+                                                    c->pol_off, w.sval, t.ctl);
+    pol_runs<<<grid_for(t.cap), 256, 0, c->stream>>>(a, c->pol_cnt, c->pol_off,
+                                                     w.sval, t.cap, now,
+                                                     c->pol_size, c->pol_time);
+    VP_HIP(hipGetLastError());
+  }
   VP_TRY(read_ctl(c, t));
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
@@ -392,23 +417,9 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     VP_HIP(hipGetLastError());
   }
   a.t = tbl_dev(t);
-  if (!nmiss && !ndefer && t.h_ctl.aux_count <= kRunMax) {
-    // phase T, grouping path: every policed packet was a phase-A hit and
-    // counted; runs are short
-    size_t need = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, need, c->pol_cnt, c->pol_off,
-                                     (int)t.cap, c->stream);
-    VP_TRY(cub_reserve(c, need));
-    VP_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub_tmp, w.cub_bytes, c->pol_cnt,
-                                            c->pol_off, (int)t.cap, c->stream));
-    pol_scatter<<<grid_for(n), 256, 0, c->stream>>>(w.log, w.aux, p0, p1,
-                                                    c->pol_off, w.sval);
-    pol_runs<<<grid_for(t.cap), 256, 0, c->stream>>>(a, c->pol_cnt, c->pol_off,
-                                                     w.sval, t.cap, now,
-                                                     c->pol_size, c->pol_time);
-    VP_HIP(hipGetLastError());
-    return 0;
-  }
+  // the grouping path already ran (every policed packet was a counted
+  // phase-A hit and runs are short): nothing left
+  if (!nmiss && !ndefer && t.h_ctl.aux_count <= kRunMax) return 0;
   // phase T, sorting path: (index, packet) pairs sorted by index; radix sort
   // is stable, so each index's packets stay in packet order
   uint32_t bits = 1;
