@@ -1,0 +1,108 @@
+"""Golden cases: per-NF 4,096-packet traces whose expected outputs were
+produced by the oracle glue over the REFERENCE's own libVig (oracle/_ref,
+compiled from /root/reference/libvig/verified by oracle/Makefile), stored in
+tests/golden/<name>.npz by tests/golden/make_golden.py. The GPU box has no
+reference: these fixtures carry its answers there."""
+import os
+
+import numpy as np
+
+import orc
+from tracegen import (mixed_bridge_trace, mixed_fw_trace, mixed_lb_trace,
+                      mixed_nat_trace, mixed_pol_trace)
+from vigor_amd import traces as T
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+N = 4096
+DEV3 = [T.mac("02:03:04:05:06:07"), T.mac("12:13:14:15:16:17"),
+        T.mac("22:23:24:25:26:27")]
+END3 = [T.mac("01:23:45:67:89:00"), T.mac("01:23:45:67:89:01"),
+        T.mac("01:23:45:67:89:02")]
+LB_MACS = [bytes([0x10 * d + i for i in range(6)]) for d in range(3)]
+
+# name -> (kind, table capacity, trace builder); configs below
+CASES = {
+    "nat_churn": ("nat", 64, lambda: mixed_nat_trace(np.random.default_rng(101), N, 100)),
+    "fw_churn": ("fw", 64, lambda: mixed_fw_trace(np.random.default_rng(102), N, 100)),
+    "bridge_churn": ("bridge", 64,
+                     lambda: mixed_bridge_trace(np.random.default_rng(103), N, 80)),
+    "lb_churn": ("lb", 64, lambda: mixed_lb_trace(np.random.default_rng(104), N, 200, 20)),
+    "pol_churn": ("pol", 16, lambda: mixed_pol_trace(np.random.default_rng(105), N, 60,
+                                                     gap_ns=2000)),
+}
+
+
+def oracle(name, ref=False):
+    kind, cap, _ = CASES[name]
+    if kind == "nat":
+        cfg = orc.nat_cfg(wan=1, start_port=0, ext_ip=T.ip4(192, 168, 4, 2),
+                          expire_us=2, max_flows=cap, device_macs=DEV3[:2],
+                          endpoint_macs=END3[:2], n_devices=2)
+    elif kind == "fw":
+        cfg = orc.fw_cfg(wan=1, expire_us=3, max_flows=cap, device_macs=DEV3,
+                         endpoint_macs=END3, n_devices=3)
+    elif kind == "bridge":
+        cfg = orc.BridgeCfg(expiration_time=2, dyn_capacity=cap, n_devices=3)
+    elif kind == "lb":
+        cfg = orc.LbCfg(flow_capacity=cap, flow_expiration_time=3,
+                        backend_capacity=32, cht_height=97,
+                        backend_expiration_time=3_600_000, wan_device=2,
+                        n_devices=3)
+        for d in range(3):
+            cfg.device_macs[d][:] = list(LB_MACS[d])
+    else:
+        cfg = orc.pol_cfg(lan=1, wan=0, rate=1_000_000, burst=1000, capacity=cap,
+                          n_devices=3)
+    return orc.Oracle(kind, cfg, ref=ref)
+
+
+def gpu(name):
+    import vigor_amd
+    kind, cap, _ = CASES[name]
+    if kind == "nat":
+        args = ["--wan", "1", "--expire", "2", "--starting-port", "0",
+                "--max-flows", str(cap), "--extip", "192.168.4.2"]
+        for d in range(2):
+            args += ["--eth-dest", "%d,%s" % (d, END3[d].hex(":"))]
+        return vigor_amd.Nat(vigor_amd.nat_config_from_args(args, 2, DEV3[:2]))
+    if kind == "fw":
+        args = ["--wan", "1", "--expire", "3", "--max-flows", str(cap)]
+        for d in range(3):
+            args += ["--eth-dest", "%d,%s" % (d, END3[d].hex(":"))]
+        return vigor_amd.Fw(vigor_amd.fw_config_from_args(args, 3, DEV3))
+    if kind == "bridge":
+        return vigor_amd.Bridge(vigor_amd.bridge_config_from_args(
+            ["--expire", "2", "--capacity", str(cap)], 3, []))
+    if kind == "lb":
+        args = ["--flow-capacity", str(cap), "--backend-capacity", "32",
+                "--cht-height", "97", "--flow-expiration", "3",
+                "--backend-expiration", "3600000", "--wan", "2"]
+        return vigor_amd.Lb(vigor_amd.lb_config_from_args(args, 3, LB_MACS))
+    args = ["--lan", "1", "--wan", "0", "--rate", "1000000", "--burst", "1000",
+            "--capacity", str(cap)]
+    return vigor_amd.Pol(vigor_amd.pol_config_from_args(args, 3))
+
+
+def oracle_state(name, o):
+    """(alloc, ts where allocated) of the NF's main table."""
+    kind, cap, _ = CASES[name]
+    if kind == "lb":
+        d = o.lb_dump(cap, 32)[0]
+    else:
+        d = getattr(o, kind + "_dump")(cap)
+    alloc, ts = d[0], d[1]
+    return alloc, np.where(alloc == 1, ts, 0)
+
+
+def gpu_state(name, nf):
+    kind = CASES[name][0]
+    d = nf.dump()
+    if kind == "lb":
+        d = d[0]
+    alloc, ts = d[0], d[1]
+    return alloc, np.where(alloc == 1, ts, 0)
+
+
+def load(name):
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}

@@ -1,0 +1,55 @@
+"""Golden fixtures (tests/golden/*.npz, made by tests/golden/make_golden.py
+from the oracle glue over the REFERENCE's own libVig, oracle/_ref): the
+restated oracle and the GPU path must both reproduce them bit-exact: out
+ports, every frame byte, and which indices are allocated with their
+timestamps. These run where the reference is absent (the GPU box)."""
+import numpy as np
+import pytest
+
+import golden_cases as G
+from gpuh import run_gpu
+
+NAMES = sorted(G.CASES)
+
+
+def check(name, out, frames, alloc, ts):
+    g = G.load(name)
+    bad = np.nonzero(out != g["out_dev"])[0]
+    assert bad.size == 0, "%s: out port mismatch at %s" % (name, bad[:10])
+    badf = np.nonzero((frames.reshape(-1, 64) != g["out_frames"].reshape(-1, 64))
+                      .any(axis=1))[0]
+    assert badf.size == 0, "%s: frame mismatch at %s" % (name, badf[:10])
+    np.testing.assert_array_equal(alloc, g["alloc"])
+    np.testing.assert_array_equal(ts, g["ts"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_fixture_made_by_reference_libvig(name):
+    g = G.load(name)
+    assert str(g["impl"]) == "reference"
+    assert g["lens"].shape[0] == G.N and g["frames"].size == G.N * 64
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_restated_oracle_reproduces_golden(name):
+    g = G.load(name)
+    o = G.oracle(name, ref=False)
+    fr = g["frames"].copy()
+    out = o.run(fr, g["lens"], g["in_dev"], g["now"], 64)
+    check(name, out, fr, *G.oracle_state(name, o))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+def test_gpu_reproduces_golden(name):
+    """Two batches (split at packet 1500) through vp_process_device."""
+    g = G.load(name)
+    nf = G.gpu(name)
+    fr = g["frames"]
+    outs, frames = [], []
+    for a, b in ((0, 1500), (1500, G.N)):
+        f, o = run_gpu(nf, fr[a * 64:b * 64], g["lens"][a:b], g["in_dev"][a:b],
+                       g["now"][a:b], 64)
+        frames.append(f)
+        outs.append(o)
+    check(name, np.concatenate(outs), np.concatenate(frames), *G.gpu_state(name, nf))
