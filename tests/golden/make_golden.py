@@ -31,6 +31,20 @@ def main():
         print(name, kind, "packets", ln.shape[0], "dropped-or-flooded",
               int((out == dv).sum() + (out == 0xFFFF).sum()), "live", int(alloc.sum()))
 
+    # configs[1] at full size: digest + head/tail frames
+    fr, ln, dv, now = G.big_trace()
+    o = G.big_oracle(ref=True)
+    out = o.run(fr, ln, dv, now, 64)
+    dig = G.orc.digest(fr, 64, ln, out, ref=True)
+    k = 1024 * 64
+    np.savez_compressed(os.path.join(HERE, "nat_1m_digest.npz"),
+                        digest=np.array(dig, np.uint64), n=np.array(ln.shape[0]),
+                        head_frames=fr[:k], tail_frames=fr[-k:],
+                        head_out=out[:1024], tail_out=out[-1024:],
+                        live=np.array(o.L.orc_nat_flow_count(o.h)),
+                        impl=np.array(o.L.orc_impl_name().decode()))
+    print("nat_1m_digest", hex(dig), "live", o.L.orc_nat_flow_count(o.h))
+
 
 if __name__ == "__main__":
     main()

@@ -106,3 +106,34 @@ def gpu_state(name, nf):
 def load(name):
     with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
         return {k: z[k] for k in z.files}
+
+
+# BASELINE configs[1] at full table size: vignat, 1M flows, the bench's own
+# trace shape (round robin, now_p = 1e9 + p); 2^21 packets = every flow
+# allocated once, then hit once. Stored as a digest (FNV-1a-64 over
+# out_port || frame, orc_digest) plus the first and last 1,024 frames.
+BIG_FLOWS = 1 << 20
+BIG_PACKETS = 1 << 21
+BIG_NAT_ARGS = ["--expire", "60000000", "--starting-port", "0", "--wan", "1",
+                "--extip", "192.168.4.2", "--eth-dest", "0,90:e2:ba:55:12:20",
+                "--eth-dest", "1,90:e2:ba:55:12:21"]
+BIG_DEV = [T.mac("02:00:00:00:00:00"), T.mac("02:00:00:00:00:01")]
+BIG_END = [T.mac("90:e2:ba:55:12:20"), T.mac("90:e2:ba:55:12:21")]
+
+
+def big_trace():
+    return T.nat_lan_trace(BIG_PACKETS, BIG_FLOWS)
+
+
+def big_oracle(ref=False):
+    cfg = orc.nat_cfg(wan=1, start_port=0, ext_ip=T.ip4(192, 168, 4, 2),
+                      expire_us=60_000_000, max_flows=BIG_FLOWS,
+                      device_macs=BIG_DEV, endpoint_macs=BIG_END, n_devices=2)
+    return orc.Oracle("nat", cfg, ref=ref)
+
+
+def big_gpu():
+    import vigor_amd
+    cfg = vigor_amd.nat_config_from_args(
+        BIG_NAT_ARGS + ["--max-flows", str(BIG_FLOWS)], 2, BIG_DEV)
+    return vigor_amd.Nat(cfg)

@@ -53,3 +53,40 @@ def test_gpu_reproduces_golden(name):
         frames.append(f)
         outs.append(o)
     check(name, np.concatenate(outs), np.concatenate(frames), *G.gpu_state(name, nf))
+
+
+def _big_check(fr, out, live):
+    import orc
+    g = G.load("nat_1m_digest")
+    assert str(g["impl"]) == "reference"
+    k = 1024 * 64
+    np.testing.assert_array_equal(out[:1024], g["head_out"])
+    np.testing.assert_array_equal(out[-1024:], g["tail_out"])
+    np.testing.assert_array_equal(fr[:k], g["head_frames"])
+    np.testing.assert_array_equal(fr[-k:], g["tail_frames"])
+    lens = np.full(out.shape[0], 60, np.uint16)
+    assert orc.digest(fr, 64, lens, out) == int(g["digest"])
+    assert live == int(g["live"])
+
+
+def test_restated_oracle_reproduces_1m_digest():
+    fr, ln, dv, now = G.big_trace()
+    o = G.big_oracle()
+    out = o.run(fr, ln, dv, now, 64)
+    _big_check(fr, out, o.L.orc_nat_flow_count(o.h))
+
+
+@pytest.mark.gpu
+def test_gpu_reproduces_1m_digest():
+    """BASELINE configs[1] table size through vp_process_device: 1M new
+    flows then 1M hits (two 2^20-packet batches, affine time)."""
+    fr, ln, dv, now = G.big_trace()
+    nat = G.big_gpu()
+    h = G.BIG_PACKETS // 2
+    frames, outs = [], []
+    for a in (0, h):
+        f, o = run_gpu(nat, fr[a * 64:(a + h) * 64], ln[a:a + h], dv[a:a + h],
+                       now[a:a + h], 64, affine=(int(now[a]), 1))
+        frames.append(f)
+        outs.append(o)
+    _big_check(np.concatenate(frames), np.concatenate(outs), nat.live_count())
