@@ -93,16 +93,34 @@ def cpu_baseline(n_flows: int, sample: int):
                                      T.mac("90:e2:ba:55:12:21")])
     o = orc.Oracle("nat", cfg)
     fr, ln, dv, now = T.nat_lan_trace(n_flows, n_flows)
-    o.run(fr, ln, dv, now, SLOT)
-    chunk = 1 << 22
-    total, t = 0, 0.0
-    while total < sample:
-        fr, ln, dv, now = T.nat_lan_trace(chunk, n_flows, start=n_flows + total)
-        t0 = time.perf_counter()
+    # one core, as the reference runs (nf.c:38, 142; SURVEY.md §8(d) taskset):
+    # this thread is pinned to the first CPU it may use while it runs
+    mask = os.sched_getaffinity(0)
+    core = min(mask)
+    os.sched_setaffinity(0, {core})
+    try:
         o.run(fr, ln, dv, now, SLOT)
-        t += time.perf_counter() - t0
-        total += chunk
-    return total / t / 1e6, total
+        chunk = 1 << 22
+        total, t = 0, 0.0
+        while total < sample:
+            fr, ln, dv, now = T.nat_lan_trace(chunk, n_flows, start=n_flows + total)
+            t0 = time.perf_counter()
+            o.run(fr, ln, dv, now, SLOT)
+            t += time.perf_counter() - t0
+            total += chunk
+    finally:
+        os.sched_setaffinity(0, mask)
+    return total / t / 1e6, total, core
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def main():
@@ -225,12 +243,13 @@ def main():
     if rank == 0:
         cpu = None
         if not args.no_cpu and world == 1:
-            cmpps, sample = cpu_baseline(args.flows, args.cpu_sample)
+            cmpps, sample, core = cpu_baseline(args.flows, args.cpu_sample)
             cpu = {"value": round(cmpps, 3), "unit": "Mpps", "cores": 1,
                    "kind": "port",
                    "sample": "%d steady-state packets of the same trace "
                              "(64B, %d flows warm, round robin), oracle/"
-                             "liborc.so, 1 thread" % (sample, args.flows)}
+                             "liborc.so, 1 thread pinned to cpu %d (%s)"
+                             % (sample, args.flows, core, cpu_model())}
         line = {
             "metric": METRIC, "value": round(mpps, 2), "unit": "Mpps",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
