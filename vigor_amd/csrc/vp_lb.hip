@@ -559,8 +559,7 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   VP_HIP(hipGetLastError());
   VP_HIP(hipEventRecord(c->ev1, c->stream));
   VP_TRY(tbl_touch_reduce(c, c->ft, w.log, p0, p1, now, c->seq));  // optimistic
-  VP_TRY(read_ctl(c, c->ft2));
-  VP_TRY(read_ctl(c, c->ft));
+  VP_TRY(read_ctl2(c, c->ft2, c->ft));
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
   *ms += kms;
@@ -618,8 +617,7 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
             lb_resolve<<<grid_for(rl.size()), 256, 0, c->stream>>>(a, w.rlist,
                                                                   (uint32_t)rl.size());
             VP_HIP(hipGetLastError());
-            VP_TRY(read_ctl(c, c->ft2));
-            VP_TRY(read_ctl(c, c->ft));
+            VP_TRY(read_ctl2(c, c->ft2, c->ft));
             const uint32_t rm = c->ft.h_ctl.miss_count, rs = c->ft.h_ctl.defer_count;
             const uint32_t rh = c->ft2.h_ctl.miss_count;
             VP_TRY(sort_list(c, w.miss, w.miss_sorted, rm));

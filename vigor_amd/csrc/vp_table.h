@@ -198,6 +198,7 @@ int tbl_dump(vp_ctx *c, FlowTable &t, uint8_t *alloc, int64_t *ts,
              uint32_t *keys);
 
 int read_ctl(vp_ctx *c, FlowTable &t);
+int read_ctl2(vp_ctx *c, FlowTable &a, FlowTable &b);
 
 // ---------------------------------------------------------- batch driver --
 // A table whose entries expire, and the cutoff for a packet at time t (the

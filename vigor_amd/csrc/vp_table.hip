@@ -83,6 +83,18 @@ int read_ctl(vp_ctx *c, FlowTable &t) {
   return 0;
 }
 
+// Both tables' control blocks with one wait (viglb reads its two together).
+int read_ctl2(vp_ctx *c, FlowTable &a, FlowTable &b) {
+  VP_HIP(hipMemcpyAsync(a.h_pin, a.ctl, sizeof(Ctl), hipMemcpyDeviceToHost,
+                        c->stream));
+  VP_HIP(hipMemcpyAsync(b.h_pin, b.ctl, sizeof(Ctl), hipMemcpyDeviceToHost,
+                        c->stream));
+  VP_HIP(stream_wait(c->stream));
+  a.h_ctl = *a.h_pin;
+  b.h_ctl = *b.h_pin;
+  return 0;
+}
+
 TableDev tbl_dev(const FlowTable &t) {
   return TableDev{t.bk, t.bmask, t.cap,   t.mix,   t.slot_of, t.hash_of,
                   t.ts, t.tseq,  t.birth, t.stack, t.ctl};
