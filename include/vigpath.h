@@ -146,8 +146,11 @@ typedef struct vp_dev_batch {
 } vp_dev_batch;
 
 /* Process one device-resident batch on HIP stream `stream` (a hipStream_t,
- * or NULL for the context's own stream). Synchronous: returns after the
- * results are in device memory and the NF state is updated. */
+ * or NULL for the context's own stream). Returns after the results (frames,
+ * out_dev) are in device memory. In steady state the fold of the flow
+ * timestamps may still be running on the context's stream when it returns;
+ * it is ordered before every later call on this context (dumps, counts,
+ * the next batch) and before work enqueued on `stream` afterwards. */
 int vp_process_device(vp_ctx *ctx, const vp_dev_batch *batch, void *stream);
 
 /* Host-resident batch shaped like a DPDK rx burst: frames[i] -> mbuf data of

@@ -133,6 +133,10 @@ struct vp_ctx {
   int gpu = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t evc = nullptr;  // control-block copy (read_ctl_post / _wait)
+  // The last segment left only its timestamp fold running on `stream`
+  // (results complete): run_batch returns without waiting for it.
+  bool fold_pending = false;
   float last_ms = 0.f;
   int last_launches = 0;
   uint64_t seq = 0;       // packets processed so far (global packet order)

@@ -556,6 +556,8 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     VP_HIP(hipGetLastError());
   }
   VP_HIP(hipEventRecord(c->ev1, c->stream));
+  // phase A's counts are copied out before the fold and waited for alone
+  VP_TRY(read_ctl_post(c, t));
   // Optimistic: fold phase A's touches right away (queued packets logged
   // kNone); if B/C run, or a touch bin overflowed, the fold is redone over
   // the completed log.
@@ -563,7 +565,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     VP_TRY(tbl_bins_reduce(c, t, bp, p0, now, seq0));
   else
     VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
-  VP_TRY(read_ctl(c, t));
+  VP_TRY(read_ctl_wait(c, t));
   const uint32_t nre = t.h_ctl.reprobe_count;
   if (nre) {  // probes past a full home bucket: finish them, patch the fold
     const uint32_t *rcnt = tiles64 ? w.reprobe_cnt : nullptr;
@@ -622,6 +624,10 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   if (nmiss || ndefer || refold)
     VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
   if (union_n || ndefer) VP_TRY(read_ctl(c, t));
+  // steady state (every packet a phase-A hit): the frames and ports are
+  // complete (the control copy waited for phase A); only the fold of the
+  // stamps may still run
+  c->fold_pending = !c->comm && !nre && !nmiss && !ndefer && !union_n && !refold;
   return 0;
 }
 

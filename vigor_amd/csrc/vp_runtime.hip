@@ -134,6 +134,7 @@ static int ctx_common(vp_ctx *c, int gpu) {
   VP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   VP_HIP(hipEventCreate(&c->ev0));
   VP_HIP(hipEventCreate(&c->ev1));
+  VP_HIP(hipEventCreateWithFlags(&c->evc, hipEventDisableTiming));
   return 0;
 }
 
@@ -163,6 +164,7 @@ static void free_all(vp_ctx *c) {
   delete c->comm;
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->evc) hipEventDestroy(c->evc);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -671,6 +673,7 @@ int vp_pol_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint32_t *keys,
 int64_t vp_live_count(vp_ctx *c) {
   if (!c) return VP_EINVAL;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  if (hipStreamSynchronize(c->stream) != hipSuccess) return VP_EIO;
   Ctl h{};
   if (hipMemcpy(&h, c->ft.ctl, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)
     return VP_EIO;

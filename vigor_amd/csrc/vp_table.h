@@ -199,6 +199,8 @@ int tbl_dump(vp_ctx *c, FlowTable &t, uint8_t *alloc, int64_t *ts,
 
 int read_ctl(vp_ctx *c, FlowTable &t);
 int read_ctl2(vp_ctx *c, FlowTable &a, FlowTable &b);
+int read_ctl_post(vp_ctx *c, FlowTable &t);
+int read_ctl_wait(vp_ctx *c, FlowTable &t);
 
 // ---------------------------------------------------------- batch driver --
 // A table whose entries expire, and the cutoff for a packet at time t (the

@@ -83,6 +83,25 @@ int read_ctl(vp_ctx *c, FlowTable &t) {
   return 0;
 }
 
+// The control block as of the work enqueued so far, copied behind it; the
+// caller may enqueue more (the timestamp fold) before waiting for the copy
+// alone, so the host learns phase A's counts while the fold runs.
+int read_ctl_post(vp_ctx *c, FlowTable &t) {
+  VP_HIP(hipMemcpyAsync(t.h_pin, t.ctl, sizeof(Ctl), hipMemcpyDeviceToHost,
+                        c->stream));
+  VP_HIP(hipEventRecord(c->evc, c->stream));
+  return 0;
+}
+
+int read_ctl_wait(vp_ctx *c, FlowTable &t) {
+  hipError_t e;
+  while ((e = hipEventQuery(c->evc)) == hipErrorNotReady) {
+  }
+  VP_HIP(e);
+  t.h_ctl = *t.h_pin;
+  return 0;
+}
+
 // Both tables' control blocks with one wait (viglb reads its two together).
 int read_ctl2(vp_ctx *c, FlowTable &a, FlowTable &b) {
   VP_HIP(hipMemcpyAsync(a.h_pin, a.ctl, sizeof(Ctl), hipMemcpyDeviceToHost,
@@ -858,6 +877,7 @@ int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
   while (a0 < n) {
     if (a0 >= ne) {  // the rest runs no expiry: one segment
       uint32_t allocated = 0;
+      c->fold_pending = false;
       VP_TRY(seg(c, b, now, a0, n, &ms, &launches, &allocated));
       break;
     }
@@ -888,13 +908,18 @@ int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
       b1 = lo;
     }
     uint32_t allocated = 0;
+    c->fold_pending = false;
     VP_TRY(seg(c, b, now, a0, b1, &ms, &launches, &allocated));
     for (int i = 0; i < ntabs; i++)
       if (allocated & (1u << i))
         tabs[i].t->ts_floor = std::min<uint64_t>(tabs[i].t->ts_floor, (uint64_t)ta);
     a0 = b1;
   }
-  VP_HIP(stream_wait(c->stream));
+  // Results are complete once every segment's work is; a trailing timestamp
+  // fold alone may keep running (ordered before any later call on the
+  // stream, and before the caller's stream through vp_process_device).
+  if (!c->fold_pending) VP_HIP(stream_wait(c->stream));
+  c->fold_pending = false;
   c->seq += n;
   c->last_now = t_last;
   c->last_ms = ms;
