@@ -412,13 +412,14 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     VP_HIP(hipGetLastError());
   }
   VP_HIP(hipEventRecord(c->ev1, c->stream));
+  VP_TRY(read_ctl_post(c, t));  // phase A's counts, waited for alone
   // optimistic fold (redone below over the completed log when phase B/C
   // run or a touch bin overflowed)
   if (bp.on)
     VP_TRY(tbl_bins_reduce(c, t, bp, p0, now, seq0));
   else
     VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
-  VP_TRY(read_ctl(c, t));
+  VP_TRY(read_ctl_wait(c, t));
   // reprobes come only from the 64-byte tiles (fw_generic_a walks in place)
   const uint32_t nre = t.h_ctl.reprobe_count;
   if (nre) {  // probes past a full home bucket: finish them, patch the fold
@@ -460,6 +461,8 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   if (nmiss || ndefer || refold)
     VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
   if (nmiss || ndefer) VP_TRY(read_ctl(c, t));
+  // steady state: frames and ports complete, only the stamp fold may run
+  c->fold_pending = !nre && !nmiss && !ndefer && !refold;
   return 0;
 }
 
