@@ -80,9 +80,16 @@ class FlowBank:
         fv[:, 34:36] = v[:, 6:8]
 
 
+CPU_SAMPLES = 5
+
+
 def cpu_baseline(n_flows: int, sample: int):
-    """The oracle on one core over the same trace shape: warm every flow,
-    then time `sample` steady-state packets."""
+    """The oracle (clean-room restatement of nf.c + vignat + libVig) on one
+    core over the same trace shape, built on this host with the reference's
+    flags (-O3 -march=native, hardware crc32: oracle/Makefile `native`): warm
+    every flow, then time CPU_SAMPLES samples of sample / CPU_SAMPLES
+    steady-state packets each. Returns (median Mpps, [Mpps per sample],
+    packets, core)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import orc
 
@@ -91,26 +98,54 @@ def cpu_baseline(n_flows: int, sample: int):
                       device_macs=DEV_MACS,
                       endpoint_macs=[T.mac("90:e2:ba:55:12:20"),
                                      T.mac("90:e2:ba:55:12:21")])
-    o = orc.Oracle("nat", cfg)
+    o = orc.Oracle("nat", cfg, ref="native")
     fr, ln, dv, now = T.nat_lan_trace(n_flows, n_flows)
     # one core, as the reference runs (nf.c:38, 142; SURVEY.md §8(d) taskset):
     # this thread is pinned to the first CPU it may use while it runs
     mask = os.sched_getaffinity(0)
     core = min(mask)
     os.sched_setaffinity(0, {core})
+    rates = []
     try:
         o.run(fr, ln, dv, now, SLOT)
-        chunk = 1 << 22
-        total, t = 0, 0.0
-        while total < sample:
-            fr, ln, dv, now = T.nat_lan_trace(chunk, n_flows, start=n_flows + total)
+        per = max(1, sample // CPU_SAMPLES)
+        pos = n_flows
+        for _ in range(CPU_SAMPLES):
+            fr, ln, dv, now = T.nat_lan_trace(per, n_flows, start=pos)
             t0 = time.perf_counter()
             o.run(fr, ln, dv, now, SLOT)
-            t += time.perf_counter() - t0
-            total += chunk
+            rates.append(per / (time.perf_counter() - t0) / 1e6)
+            pos += per
     finally:
         os.sched_setaffinity(0, mask)
-    return total / t / 1e6, total, core
+    return float(np.median(rates)), rates, per * CPU_SAMPLES, core
+
+
+def golden_batch_digest(flows: int, batch: int):
+    """The reference's digest of one steady-state batch of this exact shape
+    (tests/golden/nat_bench_shape.npz, made by tests/golden/make_golden.py
+    from the oracle over the reference's own libVig), or None."""
+    path = os.path.join(ROOT, "tests", "golden", "nat_bench_shape.npz")
+    if not os.path.exists(path) or flows != 1 << 20 or batch != 1 << 24:
+        return None
+    with np.load(path, allow_pickle=False) as z:
+        return int(z["batch_digest"][-1])
+
+
+def launch_ranks(n: int) -> int:
+    """--gpus N > 1 without a torch.distributed environment: start one rank
+    per GPU as child processes (torch.distributed.run), before anything here
+    touches the GPU, and return their exit code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def cpu_model() -> str:
@@ -132,11 +167,15 @@ def main():
     ap.add_argument("--flows", type=int, default=None,
                     help="default: 1M (config 2) on one GPU, 16M (config 5) "
                          "over N > 1 GPUs")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 24)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 26)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.flows is None:
@@ -215,6 +254,17 @@ def main():
         elapsed = float(t.item())
     # every packet hit (steady state) and went out on the WAN port
     assert int((out != 1).sum().item()) == 0
+    # the last timed batch, byte for byte, against the reference's output of
+    # the same batch (after timing; the golden exists for the default shape)
+    want = golden_batch_digest(args.flows, B) if world == 1 else None
+    parity = None
+    if want is not None:
+        got = T.batch_digest(bufs[-1].cpu().numpy(), out.cpu().numpy().view(np.uint16),
+                             SLOT)
+        parity = {"batch_digest": "%016x" % got, "golden": "%016x" % want,
+                  "match": got == want,
+                  "source": "tests/golden/nat_bench_shape.npz (reference libVig)"}
+        assert got == want, "timed batch differs from the reference: %s" % parity
 
     total_pkts = B * args.steps * world
     mpps = total_pkts / elapsed / 1e6
@@ -243,13 +293,17 @@ def main():
     if rank == 0:
         cpu = None
         if not args.no_cpu and world == 1:
-            cmpps, sample, core = cpu_baseline(args.flows, args.cpu_sample)
+            cmpps, rates, sample, core = cpu_baseline(args.flows, args.cpu_sample)
             cpu = {"value": round(cmpps, 3), "unit": "Mpps", "cores": 1,
                    "kind": "port",
-                   "sample": "%d steady-state packets of the same trace "
-                             "(64B, %d flows warm, round robin), oracle/"
-                             "liborc.so, 1 thread pinned to cpu %d (%s)"
-                             % (sample, args.flows, core, cpu_model())}
+                   "samples": [round(r, 3) for r in rates],
+                   "spread": round((max(rates) - min(rates)) / cmpps, 4),
+                   "sample": "median of %d samples, %d steady-state packets in "
+                             "all, of the same trace (64B, %d flows warm, round "
+                             "robin); oracle restatement built here -O3 "
+                             "-march=native with hardware crc32 (oracle/"
+                             "liborc_native.so), 1 thread pinned to cpu %d (%s)"
+                             % (len(rates), sample, args.flows, core, cpu_model())}
         line = {
             "metric": METRIC, "value": round(mpps, 2), "unit": "Mpps",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -276,6 +330,7 @@ def main():
                          "kernel_mpps": round(pkts_per_launch / per_launch_s
                                               / 1e6, 1)},
             "cpu_baseline": cpu,
+            "parity": parity,
             "new_flow_mpps": round(new_flow_mpps, 2) if new_flow_mpps else None,
         }
         print(json.dumps(line), flush=True)

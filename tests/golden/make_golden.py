@@ -14,6 +14,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
 import golden_cases as G  # noqa: E402
+from vigor_amd import traces as T  # noqa: E402
 
 
 def main():
@@ -44,6 +45,46 @@ def main():
                         live=np.array(o.L.orc_nat_flow_count(o.h)),
                         impl=np.array(o.L.orc_impl_name().decode()))
     print("nat_1m_digest", hex(dig), "live", o.L.orc_nat_flow_count(o.h))
+
+    # the bench's shape: 1M flows, 2^24-packet batches (bench.py)
+    o = G.nat_oracle(G.BENCH_FLOWS, ref=True)
+    digs = []
+    for k in range(G.BENCH_BATCHES):
+        acc = [0]
+
+        def add(p0, fr, out, k=k, acc=acc):
+            acc[0] += T.batch_digest(fr, out, 64, p0 - k * G.BENCH_BATCH)
+        G.run_oracle_chunks(o, G.BENCH_BATCH, G.BENCH_FLOWS, k * G.BENCH_BATCH, add)
+        digs.append(acc[0] % (1 << 64))
+    alloc, ts, _ = o.nat_dump(G.BENCH_FLOWS)
+    sd = T.state_digest(alloc, ts)
+    np.savez_compressed(os.path.join(HERE, "nat_bench_shape.npz"),
+                        batch_digest=np.array(digs, np.uint64),
+                        state_digest=np.array(sd, np.uint64),
+                        live=np.array(o.L.orc_nat_flow_count(o.h)),
+                        impl=np.array(o.L.orc_impl_name().decode()))
+    print("nat_bench_shape", [hex(d) for d in digs], hex(sd))
+
+    # configs[4] at full table size: 16M flows
+    o = G.nat_oracle(G.F16M_FLOWS, ref=True)
+    acc = [0]
+    ends = {}
+
+    def add16(p0, fr, out):
+        acc[0] += T.batch_digest(fr, out, 64, p0)
+        if p0 == 0:
+            ends["head_frames"], ends["head_out"] = fr[:1024 * 64].copy(), out[:1024].copy()
+        if p0 + out.shape[0] == G.F16M_PACKETS:
+            ends["tail_frames"], ends["tail_out"] = fr[-1024 * 64:].copy(), out[-1024:].copy()
+    G.run_oracle_chunks(o, G.F16M_PACKETS, G.F16M_FLOWS, 0, add16)
+    alloc, ts, _ = o.nat_dump(G.F16M_FLOWS)
+    sd = T.state_digest(alloc, ts)
+    np.savez_compressed(os.path.join(HERE, "nat_16m_digest.npz"),
+                        digest=np.array(acc[0] % (1 << 64), np.uint64),
+                        state_digest=np.array(sd, np.uint64),
+                        live=np.array(o.L.orc_nat_flow_count(o.h)),
+                        impl=np.array(o.L.orc_impl_name().decode()), **ends)
+    print("nat_16m_digest", hex(acc[0] % (1 << 64)), hex(sd))
 
 
 if __name__ == "__main__":

@@ -137,3 +137,50 @@ def big_gpu():
     cfg = vigor_amd.nat_config_from_args(
         BIG_NAT_ARGS + ["--max-flows", str(BIG_FLOWS)], 2, BIG_DEV)
     return vigor_amd.Nat(cfg)
+
+
+# The bench's own shape (bench.py, BASELINE configs[1]): 1M flows, batches of
+# 2^24 packets (every flow touched 16 times per batch, so steady-state
+# batches fold their stamps through the touch bins), round robin, now_p =
+# 1e9 + p. Batch 0 allocates every flow, batch 1 is all hits. Stored: each
+# batch's batch_digest (positions local to the batch), the state_digest of
+# (alloc, ts) after batch 1, and the live count.
+BENCH_FLOWS = 1 << 20
+BENCH_BATCH = 1 << 24
+BENCH_BATCHES = 2
+
+# BASELINE configs[4] at full table size: 16M flows, 2^25 packets (every
+# flow allocated once, then hit once), round robin. Stored: batch_digest over
+# the whole trace (global positions), state_digest, live count, and the first
+# and last 1,024 output frames.
+F16M_FLOWS = 1 << 24
+F16M_PACKETS = 1 << 25
+
+CHUNK = 1 << 22
+
+
+def nat_oracle(flows, ref=False):
+    cfg = orc.nat_cfg(wan=1, start_port=0, ext_ip=T.ip4(192, 168, 4, 2),
+                      expire_us=60_000_000, max_flows=flows,
+                      device_macs=BIG_DEV, endpoint_macs=BIG_END, n_devices=2)
+    return orc.Oracle("nat", cfg, ref=ref)
+
+
+def nat_gpu(flows, gpu=0):
+    import vigor_amd
+    cfg = vigor_amd.nat_config_from_args(
+        BIG_NAT_ARGS + ["--max-flows", str(flows)], 2, BIG_DEV)
+    return vigor_amd.Nat(cfg, gpu=gpu)
+
+
+def run_oracle_chunks(o, n_packets, n_flows, start=0, on_chunk=None):
+    """Run the round-robin trace [start, start + n_packets) through oracle o
+    in chunks; on_chunk(p0, frames, out) sees every chunk's output."""
+    p = start
+    while p < start + n_packets:
+        m = min(CHUNK, start + n_packets - p)
+        fr, ln, dv, now = T.nat_lan_trace(m, n_flows, start=p)
+        out = o.run(fr, ln, dv, now, 64)
+        if on_chunk:
+            on_chunk(p, fr, out)
+        p += m

@@ -57,22 +57,28 @@ def _ptr(a):
     return C.c_void_p(a.ctypes.data) if a is not None else None
 
 
-def build(ref: bool = False) -> str:
-    target = "ref" if ref else "all"
-    subprocess.run(["make", "-s", "-C", ORC_DIR, target], check=True)
-    return os.path.join(ORC_DIR, "_ref", "liborc_ref.so") if ref else \
-        os.path.join(ORC_DIR, "liborc.so")
+# ref: False = the restatement (portable build, the checker); True = the
+# reference's own libVig (oracle/_ref, this container only); "native" = the
+# restatement built -O3 -march=native with the hardware crc32 instruction on
+# the host that runs it (the CPU baseline, as the reference is built).
+_PATHS = {False: "liborc.so", True: os.path.join("_ref", "liborc_ref.so"),
+          "native": "liborc_native.so"}
+_TARGETS = {False: "all", True: "ref", "native": "native"}
+
+
+def build(ref=False) -> str:
+    subprocess.run(["make", "-s", "-C", ORC_DIR, _TARGETS[ref]], check=True)
+    return os.path.join(ORC_DIR, _PATHS[ref])
 
 
 _LIBS = {}
 
 
-def lib(ref: bool = False):
+def lib(ref=False):
     if ref in _LIBS:
         return _LIBS[ref]
-    path = os.path.join(ORC_DIR, "_ref", "liborc_ref.so") if ref else \
-        os.path.join(ORC_DIR, "liborc.so")
-    if not os.path.exists(path):
+    path = os.path.join(ORC_DIR, _PATHS[ref])
+    if ref == "native" or not os.path.exists(path):
         build(ref)
     L = C.CDLL(path)
     L.orc_nat_create.restype = C.c_void_p

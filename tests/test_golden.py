@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 import golden_cases as G
+from vigor_amd import traces as T
 from gpuh import run_gpu
 
 NAMES = sorted(G.CASES)
@@ -90,3 +91,77 @@ def test_gpu_reproduces_1m_digest():
         frames.append(f)
         outs.append(o)
     _big_check(np.concatenate(frames), np.concatenate(outs), nat.live_count())
+
+
+# ---- the bench's own shape (BASELINE configs[1]; bench.py) ----------------
+
+def _bench_golden():
+    g = G.load("nat_bench_shape")
+    assert str(g["impl"]) == "reference"
+    return g
+
+
+def test_restated_oracle_reproduces_bench_shape():
+    g = _bench_golden()
+    o = G.nat_oracle(G.BENCH_FLOWS)
+    for k in range(G.BENCH_BATCHES):
+        acc = [0]
+
+        def add(p0, fr, out, k=k):
+            acc[0] += T.batch_digest(fr, out, 64, p0 - k * G.BENCH_BATCH)
+        G.run_oracle_chunks(o, G.BENCH_BATCH, G.BENCH_FLOWS, k * G.BENCH_BATCH, add)
+        assert acc[0] % (1 << 64) == int(g["batch_digest"][k]), k
+    alloc, ts, _ = o.nat_dump(G.BENCH_FLOWS)
+    assert T.state_digest(alloc, ts) == int(g["state_digest"])
+
+
+@pytest.mark.gpu
+def test_gpu_reproduces_bench_shape():
+    """bench.py's workload through vp_process_device: 2^24-packet batches
+    over 1M flows (affine time), batch 0 allocating every flow and batch 1
+    in steady state, where each flow is touched 16 times and the stamps fold
+    through the touch bins. Every output byte (batch digest) and the whole
+    table state (alloc + ts digest) equal the reference's."""
+    import torch
+    g = _bench_golden()
+    nat = G.nat_gpu(G.BENCH_FLOWS)
+    d = torch.device("cuda:0")
+    B = G.BENCH_BATCH
+    lens = torch.full((B,), 60, dtype=torch.int16, device=d)
+    ind = torch.zeros(B, dtype=torch.int16, device=d)
+    out = torch.zeros(B, dtype=torch.int16, device=d)
+    for k in range(G.BENCH_BATCHES):
+        fr, _, _, _ = T.nat_lan_trace(B, G.BENCH_FLOWS, start=k * B)
+        f = torch.from_numpy(fr).to(d)
+        del fr
+        nat.process_device(f, lens, ind, out, 64, now0=T.NOW0 + k * B, now_step=1)
+        torch.cuda.synchronize()
+        dig = T.batch_digest(f.cpu().numpy(), out.cpu().numpy().view(np.uint16), 64)
+        assert dig == int(g["batch_digest"][k]), "batch %d digest" % k
+        del f
+    alloc, ts, _ = nat.dump()
+    assert T.state_digest(alloc, ts) == int(g["state_digest"])
+    assert nat.live_count() == int(g["live"])
+
+
+# ---- BASELINE configs[4] table size (16M flows) ---------------------------
+
+def _16m_golden():
+    g = G.load("nat_16m_digest")
+    assert str(g["impl"]) == "reference"
+    return g
+
+
+def test_restated_oracle_reproduces_16m_digest():
+    g = _16m_golden()
+    o = G.nat_oracle(G.F16M_FLOWS)
+    acc = [0]
+
+    def add(p0, fr, out):
+        acc[0] += T.batch_digest(fr, out, 64, p0)
+        if p0 == 0:
+            np.testing.assert_array_equal(fr[:1024 * 64], g["head_frames"])
+    G.run_oracle_chunks(o, G.F16M_PACKETS, G.F16M_FLOWS, 0, add)
+    assert acc[0] % (1 << 64) == int(g["digest"])
+    alloc, ts, _ = o.nat_dump(G.F16M_FLOWS)
+    assert T.state_digest(alloc, ts) == int(g["state_digest"])

@@ -222,3 +222,29 @@ def test_multiplicative_home_buckets_reprobe(order, slot, monkeypatch):
     now = now + 10**8
     check_batches(nat, o, wide(fr), ln, dv, now, slot, [2000])
     check_state(nat, o, 4096)
+
+
+def test_now_buffer_reusable_after_return():
+    """vp_process_device with a per-packet time array: the array may be
+    overwritten (or freed) as soon as the call returns, with no
+    synchronisation, and the timestamps the batch leaves behind must still be
+    the ones it carried (the steady-state fold must not read it late)."""
+    import torch
+    nat, o = make_pair(max_flows=1 << 16)
+    n_flows = 4096
+    fr, ln, dv, now = T.nat_lan_trace(n_flows, n_flows)
+    check_batches(nat, o, fr, ln, dv, now, 64, [])
+    d = torch.device("cuda:0")
+    B = 1 << 18  # steady state: every packet a hit, touch bins
+    fr, ln, dv, now = T.nat_lan_trace(B, n_flows, start=n_flows)
+    o.run(fr.copy(), ln, dv, now, 64)
+    f = torch.from_numpy(fr).to(d)
+    l_ = torch.from_numpy(ln.view(np.int16)).to(d)
+    i_ = torch.from_numpy(dv.view(np.int16)).to(d)
+    out = torch.zeros(B, dtype=torch.int16, device=d)
+    nt = torch.from_numpy(now).to(d)
+    nat.process_device(f, l_, i_, out, 64, now=nt)
+    nt.fill_(0)  # on torch's stream, unordered with the library's
+    del nt
+    torch.cuda.synchronize()
+    check_state(nat, o, 1 << 16)

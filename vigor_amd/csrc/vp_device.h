@@ -220,9 +220,15 @@ __device__ __forceinline__ uint32_t group_reserve(uint32_t *ctr, uint32_t ch,
 // to bin (i >> 4) & 255, at in-bin position ((i >> 12) << 4) | (i & 15): runs
 // of 16 consecutive indices per bin, so sequential flow sets spread over all
 // bins and the fold writes whole 128-byte runs of ts. Each block appends to
-// its own fixed-size slice of every bin (LDS cursors); a slice that fills up
-// sets *ovf and the host folds the full log instead.
+// its own fixed-size slice of every bin (LDS cursors). With bins on, the
+// classify kernels write no per-packet touch log: a touch that finds its
+// slice full is logged alone (olog[p] = index) and queued on the block's
+// overflow slice (oent/ocnt), and *ovf tells the host to apply the queued
+// touches after the fold (tbl_late_touches, vp_table.hip).
 constexpr uint32_t kBins = 256;
+constexpr uint32_t kCurReprobe = kBins;       // LDS cursor of the reprobe queue
+constexpr uint32_t kCurOverflow = kBins + 1;  // LDS cursor of the overflow queue
+constexpr uint32_t kCurs = kBins + 2;
 // finish() may set touch = kReprobe instead of an index: the packet leaves
 // the wave and is queued on the block's reprobe slice (TileQueue).
 constexpr uint32_t kReprobe = 0xFFFFFFFDu;
@@ -235,8 +241,16 @@ struct TouchBins {
   uint32_t *ent;  // [block][bin][cap] entries (in-bin << pbits | position); null = off
   uint32_t *cnt;  // [block][bin] entries written
   uint32_t *ovf;  // set when a slice overflowed
+  uint32_t *oent;  // [block][range] positions of overflowed touches
+  uint32_t *ocnt;  // [block] overflowed touches queued
+  uint32_t *olog;  // olog[p] = index of an overflowed touch
   uint32_t cap, pbits;
 };
+// Touch-log entry of packet p; `log` is null in the classify kernels that
+// bin their touches.
+__device__ __forceinline__ void log_put(uint32_t *log, uint32_t p, uint32_t v) {
+  if (log) log[p] = v;
+}
 __device__ __forceinline__ uint32_t bin_of(uint32_t i) { return (i >> 4) & (kBins - 1); }
 __device__ __forceinline__ uint32_t bin_local(uint32_t i) {
   return ((i >> 12) << 4) | (i & 15u);
@@ -258,7 +272,10 @@ __device__ __forceinline__ uint32_t bin_index(uint32_t bin, uint32_t local) {
 //                                      (bucket) this packet needs, or kNone;
 //   mod  = finish(pend, row, p, f, in, len, touch)
 //                                      consume the row, rewrite f, return
-//                                      true when f must be written back;
+//                                      the mask of the 16-byte chunks of f
+//                                      that must be written back (bit k =
+//                                      bytes 16k..16k+15; a UDP rewrite leaves
+//                                      chunk 3 alone);
 //                                      touch = the flow index the packet
 //                                      logged (kNone if none), for the bins,
 //                                      or kReprobe to queue the packet on the
@@ -275,7 +292,7 @@ __device__ __forceinline__ uint32_t bin_index(uint32_t bin, uint32_t local) {
 // dealing tiles round-robin over all waves, and 10 % faster than an
 // XCD-aware range order, as every block streams its own DRAM
 // pages and its packets' table rows stay near each other in its XCD's L2.
-// `cur` is kBins + 1 LDS counters, zeroed by the kernel before its barrier.
+// `cur` is kCurs LDS counters, zeroed by the kernel before its barrier.
 template <class Issue, class Finish>
 __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
                                                const uint16_t *len,
@@ -350,12 +367,12 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
 #pragma unroll
       for (uint32_t k = 0; k < 4; k++) row[k] = S[chunk_swz(4 * lane + k)];
     }
-    bool mod = false;
+    uint32_t mod = 0;
     uint32_t touch = kNone;
     if (mine) mod = finish(pend, row, p, f, in, ln, touch);
     if (rq.ent) {  // queue on this block's reprobe slice
       const bool v = touch == kReprobe;
-      const uint32_t k = group_reserve(cur, kBins, v);
+      const uint32_t k = group_reserve(cur, kCurReprobe, v);
       if (v) rq.ent[(size_t)rb * per_b * 64 + k] = p;
     }
     if (touch == kReprobe) touch = kNone;
@@ -363,9 +380,16 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
       const bool v = touch != kNone;
       const uint32_t b = v ? bin_of(touch) : 0;
       const uint32_t k = group_reserve(cur, b, v);
-      if (v && k < bins.cap)
+      const bool fits = k < bins.cap;
+      if (v && fits)
         bins.ent[((size_t)rb * kBins + b) * bins.cap + k] =
             (bin_local(touch) << bins.pbits) | (p - range0);
+      const bool spill = v && !fits;  // slice full: log this touch alone
+      const uint32_t o = group_reserve(cur, kCurOverflow, spill);
+      if (spill) {
+        bins.olog[p] = touch;
+        bins.oent[(size_t)rb * per_b * 64 + o] = p;
+      }
     }
     if (mod) {
 #pragma unroll
@@ -373,12 +397,16 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
         S[chunk_swz(4 * lane + k)] =
             make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
     }
-    const uint64_t modmask = __ballot(mod);
+    // chunk c (lane-contiguous) is part c % 4 = lane % 4 of packet c / 4
+    const uint32_t part = lane & 3;
+    const uint64_t m0 = __ballot(mod & 1u), m1 = __ballot(mod & 2u),
+                   m2 = __ballot(mod & 4u), m3 = __ballot(mod & 8u);
+    const uint64_t partmask = part == 0 ? m0 : part == 1 ? m1 : part == 2 ? m2 : m3;
     wave_lds_sync();
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) {
       const uint32_t c = 64 * j + lane;
-      if ((modmask >> (c >> 2)) & 1ull) g[c] = S[chunk_swz(c)];
+      if ((partmask >> (c >> 2)) & 1ull) g[c] = S[chunk_swz(c)];
     }
     wave_lds_sync();  // the next tile overwrites S
   }
@@ -387,11 +415,15 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
     for (uint32_t b = threadIdx.x; b < kBins; b += blockDim.x) {
       const uint32_t c = cur[b];
       bins.cnt[(size_t)rb * kBins + b] = c < bins.cap ? c : bins.cap;
-      if (c > bins.cap) *bins.ovf = 1;
+    }
+    if (threadIdx.x == 0) {
+      const uint32_t o = cur[kCurOverflow];
+      bins.ocnt[rb] = o;
+      if (o) *bins.ovf = 1;
     }
   }
   if (rq.ent && threadIdx.x == 0) {
-    const uint32_t c = cur[kBins];
+    const uint32_t c = cur[kCurReprobe];
     rq.cnt[rb] = c;
     if (c) atomicAdd(rq.total, c);
   }

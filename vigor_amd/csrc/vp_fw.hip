@@ -102,7 +102,7 @@ __device__ uint32_t fw_generic_a(const FwArgs &a, const uint32_t *T, uint32_t p,
   const L34 h = parse_l34(f, len);
   if (!h.ok) {  // not IPv4 / not TCP-UDP: drop (fw_main.c:29-40)
     a.out[p] = (uint16_t)in;
-    a.log[p] = kNone;
+    log_put(a.log, p, kNone);
     return kNone;
   }
   const uint32_t proto = f.r8(h.ip + 9);
@@ -120,10 +120,10 @@ __device__ uint32_t fw_generic_a(const FwArgs &a, const uint32_t *T, uint32_t p,
       a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
     else
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
-    a.log[p] = kNone;  // phase B / C write the real entry
+    log_put(a.log, p, kNone);  // phase B / C write the real entry
     return kNone;
   }
-  a.log[p] = idx;
+  log_put(a.log, p, idx);
   const uint32_t dst = wan ? (w3 >> 8) : a.wan;
   uint32_t mw[3];
   fw_macs(a, dst, mw);
@@ -159,7 +159,7 @@ __device__ __forceinline__ FwPend fw_issue(const FwArgs &a, const uint32_t *T,
                   ((proto == 6) | (proto == 17)) & ((uint32_t)(len - 34) >= 4u);
   if (!ok) {
     a.out[p] = (uint16_t)in;
-    a.log[p] = kNone;
+    log_put(a.log, p, kNone);
     return P;
   }
   const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
@@ -191,7 +191,7 @@ __device__ __forceinline__ bool fw_finish(const FwArgs &a, const uint32_t *T,
   const uint32_t idx =
       bucket_match<0xFFu>(row[0], row[1], row[2], row[3], key, &done, &w3);
   if (!done) {  // the bucket is full of other keys: fw_reprobe walks on,
-    a.log[p] = kNone;  // so this wave does not wait for a dependent read
+    log_put(a.log, p, kNone);  // so this wave does not wait for a dependent read
     if (a.tileq)
       touch = kReprobe;
     else
@@ -203,10 +203,10 @@ __device__ __forceinline__ bool fw_finish(const FwArgs &a, const uint32_t *T,
       a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
     else
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
-    a.log[p] = kNone;
+    log_put(a.log, p, kNone);
     return false;
   }
-  a.log[p] = idx;
+  log_put(a.log, p, idx);
   touch = idx;
   const uint32_t dst = wan ? (w3 >> 8) : a.wan;
   uint32_t mw[3];
@@ -237,8 +237,8 @@ __global__ __launch_bounds__(256, 4) void fw_classify64(FwArgs a, uint32_t n_all
                                                        TouchBins bins, TileQueue rq) {
   __shared__ uint32_t T[kFwTabs * 256];
   __shared__ uint4 stage[4][256];
-  __shared__ uint32_t cur[kBins + 1];
-  for (uint32_t i = threadIdx.x; i <= kBins; i += blockDim.x) cur[i] = 0;
+  __shared__ uint32_t cur[kCurs];
+  for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
   fw_load_tables(T, a.crc_tab);  // (its barrier also covers cur)
   frames64_tiles(
       a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
@@ -247,8 +247,8 @@ __global__ __launch_bounds__(256, 4) void fw_classify64(FwArgs a, uint32_t n_all
         return fw_issue(a, T, p, f, in, len, mine);
       },
       [&](const FwPend &P, const uint4 *row, uint32_t p, RFrame &f, uint32_t in,
-          uint32_t len, uint32_t &touch) {
-        return fw_finish(a, T, P, row, p, f, in, len, touch);
+          uint32_t len, uint32_t &touch) -> uint32_t {
+        return fw_finish(a, T, P, row, p, f, in, len, touch) ? 0x1u : 0u;  // MACs
       },
       bins, rq, cur);
 }
@@ -405,7 +405,9 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   if (p1 > p0) {
     if (tiles64) {
-      fw_classify64<<<grid64, 256, 0, c->stream>>>(a, b->n, bp.bins, rq);
+      FwArgs a64 = a;
+      if (bp.on) a64.log = nullptr;  // touches go to the bins only
+      fw_classify64<<<grid64, 256, 0, c->stream>>>(a64, b->n, bp.bins, rq);
     } else {
       fw_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
     }
@@ -413,8 +415,7 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   }
   VP_HIP(hipEventRecord(c->ev1, c->stream));
   VP_TRY(read_ctl_post(c, t));  // phase A's counts, waited for alone
-  // optimistic fold (redone below over the completed log when phase B/C
-  // run or a touch bin overflowed)
+  // fold phase A's touches; queued packets follow as late touches
   if (bp.on)
     VP_TRY(tbl_bins_reduce(c, t, bp, p0, now, seq0));
   else
@@ -430,7 +431,10 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
                              w.log, now, seq0));
     VP_TRY(read_ctl(c, t));  // the walk may have found new flows
   }
-  const bool refold = bp.on && t.h_ctl.touch_ovf != 0;
+  const bool ovf = bp.on && t.h_ctl.touch_ovf != 0;
+  if (ovf)  // touches that found their bin slice full, logged alone
+    VP_TRY(tbl_late_touches(c, t, bp.bins.oent, bp.bins.ocnt, 0, range64, grid64,
+                            w.log, now, seq0));
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
   *ms += kms;
@@ -451,18 +455,21 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     fw_miss_finish<<<grid_for(nmiss), 256, 0, c->stream>>>(
         a, w.miss_sorted, nmiss, w.mkey, w.scratch, w.rep, w.assign);
     VP_HIP(hipGetLastError());
+    VP_TRY(tbl_late_touches(c, t, w.miss_sorted, nullptr, nmiss, 256,
+                            (nmiss + 255) / 256, w.log, now, seq0));
     *allocated |= 1u;
   }
   if (ndefer) {
     a.t = tbl_dev(t);  // a rebuild during phase B may have changed the layout
     fw_defer_finish<<<grid_for(ndefer), 256, 0, c->stream>>>(a, w.defer, ndefer);
     VP_HIP(hipGetLastError());
+    VP_TRY(tbl_late_touches(c, t, w.defer, nullptr, ndefer, 256, (ndefer + 255) / 256,
+                            w.log, now, seq0));
   }
-  if (nmiss || ndefer || refold)
-    VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
   if (nmiss || ndefer) VP_TRY(read_ctl(c, t));
   // steady state: frames and ports complete, only the stamp fold may run
-  c->fold_pending = !nre && !nmiss && !ndefer && !refold;
+  // (not when it reads the caller's time array)
+  c->fold_pending = !b->now && !nre && !nmiss && !ndefer && !ovf;
   return 0;
 }
 

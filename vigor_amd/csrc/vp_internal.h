@@ -106,6 +106,7 @@ struct Workspace {
   uint32_t *hist = nullptr, *hoff = nullptr;  // touch-reduce (chunk x span)
   uint64_t hist_cap = 0;
   uint32_t *bins_ent = nullptr, *bins_cnt = nullptr;  // touch bins (TouchBins)
+  uint32_t *ovf_q = nullptr, *ovf_cnt = nullptr;  // overflowed touches per block
   size_t bins_ent_n = 0, bins_cnt_n = 0;
   void *cub_tmp = nullptr;
   size_t cub_bytes = 0;

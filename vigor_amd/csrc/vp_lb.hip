@@ -285,7 +285,11 @@ __global__ __launch_bounds__(256) void lb_classify64(LbArgs a, uint32_t n_all) {
         return NoPend{kNone};
       },
       [&](NoPend, const uint4 *, uint32_t p, RFrame &f, uint32_t in, uint32_t len,
-          uint32_t &) { return lb_fast(a, T, p, f, in, len); },
+          uint32_t &) -> uint32_t {
+        // dst address, MACs and checksums: bytes 0-47, and the TCP checksum
+        if (!lb_fast(a, T, p, f, in, len)) return 0u;
+        return (f.w[5] >> 24) == 6 ? 0xFu : 0x7u;
+      },
       TouchBins{}, TileQueue{}, nullptr);
 }
 

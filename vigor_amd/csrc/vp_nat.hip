@@ -98,7 +98,7 @@ VP_GENERIC_FN uint32_t nat_generic_a(const NatArgs &a, const uint32_t *T,
   L34 h = parse_l34(f, len);
   if (!h.ok) {
     a.out[p] = (uint16_t)in;
-    a.log[p] = kNone;
+    log_put(a.log, p, kNone);
     return kNone;
   }
   const uint32_t proto = f.r8(h.ip + 9);
@@ -109,18 +109,18 @@ VP_GENERIC_FN uint32_t nat_generic_a(const NatArgs &a, const uint32_t *T,
     const int idx = (int)dp - (int)a.start_port;
     if (idx < 0 || idx >= (int)a.t.cap) {  // reference UB range: unallocated
       a.out[p] = (uint16_t)in;
-      a.log[p] = kNone;
+      log_put(a.log, p, kNone);
       return kNone;
     }
     const uint32_t s = a.t.slot_of[idx];
     if (s == kNone) {
       a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
-      a.log[p] = kNone;  // phase C writes the real entry
+      log_put(a.log, p, kNone);  // phase C writes the real entry
       return kNone;
     }
     const uint4 fk = tbl_key_of(a.t, (uint32_t)idx);
     const uint32_t k0 = fk.x, k1 = fk.y, k2 = fk.z, k3 = fk.w;
-    a.log[p] = (uint32_t)idx;  // rejuvenated before the anti-spoof check
+    log_put(a.log, p, (uint32_t)idx);  // rejuvenated before the anti-spoof check
     if ((k2 != sip) | ((k0 >> 16) != sp) | (((k3 >> 16) & 0xFF) != proto)) {
       a.out[p] = (uint16_t)in;
       return (uint32_t)idx;
@@ -135,10 +135,10 @@ VP_GENERIC_FN uint32_t nat_generic_a(const NatArgs &a, const uint32_t *T,
                                    key);
     if (idx == kNone) {
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
-      a.log[p] = kNone;  // phase B writes the real entry
+      log_put(a.log, p, kNone);  // phase B writes the real entry
       return kNone;
     }
-    a.log[p] = idx;
+    log_put(a.log, p, idx);
     logged = idx;
     f.w32(h.ip + 12, a.ext_ip);
     f.w16(h.l4, (uint16_t)(a.start_port + idx));
@@ -187,7 +187,7 @@ __device__ __forceinline__ NatPend nat_issue(const NatArgs &a, const uint32_t *T
                   ((proto == 6) | (proto == 17)) & ((uint32_t)(len - 34) >= 4u);
   if (!ok) {
     a.out[p] = (uint16_t)in;
-    a.log[p] = kNone;
+    log_put(a.log, p, kNone);
     return P;
   }
   const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
@@ -196,7 +196,7 @@ __device__ __forceinline__ NatPend nat_issue(const NatArgs &a, const uint32_t *T
     const int idx = (int)dp - (int)a.start_port;
     if (idx < 0 || idx >= (int)a.t.cap) {
       a.out[p] = (uint16_t)in;
-      a.log[p] = kNone;
+      log_put(a.log, p, kNone);
       return P;
     }
     P.kind = kPendWan;
@@ -235,11 +235,11 @@ __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
     const uint32_t s = P.s;
     if (s == kNone) {  // maybe allocated earlier in this segment: phase C
       a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
-      a.log[p] = kNone;  // phase C writes the real entry
+      log_put(a.log, p, kNone);  // phase C writes the real entry
       return false;
     }
     const uint4 k = reinterpret_cast<const uint4 *>(a.t.bk + (s >> 2))[s & 3];
-    a.log[p] = idx;  // rejuvenated before the anti-spoof check
+    log_put(a.log, p, idx);  // rejuvenated before the anti-spoof check
     touch = idx;
     if ((k.z != sip) | ((k.x >> 16) != sp) | (((k.w >> 16) & 0xFF) != proto)) {
       a.out[p] = (uint16_t)in;  // nat_main.c:55-60
@@ -259,7 +259,7 @@ __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
     const uint32_t idx = bucket_match(row[0], row[1], row[2], row[3], key, &done);
     if (!done) {  // the bucket is full of other keys: nat_reprobe walks the
       // rest of the path, so this wave does not wait for a dependent read
-      a.log[p] = kNone;
+      log_put(a.log, p, kNone);
       if (a.tileq)
         touch = kReprobe;
       else
@@ -269,10 +269,10 @@ __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
 #endif
     if (idx == kNone) {  // new flow, or not yet visible: phase B
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
-      a.log[p] = kNone;  // phase B writes the real entry
+      log_put(a.log, p, kNone);  // phase B writes the real entry
       return false;
     }
-    a.log[p] = idx;
+    log_put(a.log, p, idx);
     touch = idx;
     f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
     f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
@@ -360,8 +360,8 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
                                                         TouchBins bins, TileQueue rq) {
   __shared__ uint32_t T[15 * 256];
   __shared__ uint4 stage[4][256];
-  __shared__ uint32_t cur[kBins + 1];
-  for (uint32_t i = threadIdx.x; i <= kBins; i += blockDim.x) cur[i] = 0;
+  __shared__ uint32_t cur[kCurs];
+  for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
   load_crc_tables(T, a.crc_tab);  // (its barrier also covers cur)
   frames64_tiles(
       a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
@@ -370,8 +370,11 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
         return nat_issue(a, T, p, f, in, len, mine);
       },
       [&](const NatPend &P, const uint4 *row, uint32_t p, RFrame &f, uint32_t in,
-          uint32_t len, uint32_t &touch) {
-        return nat_finish(a, T, P, row, p, f, in, len, touch);
+          uint32_t len, uint32_t &touch) -> uint32_t {
+        // a rewrite touches bytes 0-47; the TCP checksum (bytes 50-51) also
+        // dirties chunk 3 (the protocol byte is never rewritten)
+        if (!nat_finish(a, T, P, row, p, f, in, len, touch)) return 0u;
+        return (f.w[5] >> 24) == 6 ? 0xFu : 0x7u;
       },
       bins, rq, cur);
 }
@@ -549,7 +552,9 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   if (p1 > p0) {
     if (tiles64) {
-      nat_classify64<<<grid64, 256, 0, c->stream>>>(a, b->n, bp.bins, rq);
+      NatArgs a64 = a;
+      if (bp.on) a64.log = nullptr;  // touches go to the bins only
+      nat_classify64<<<grid64, 256, 0, c->stream>>>(a64, b->n, bp.bins, rq);
     } else {
       nat_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
     }
@@ -558,9 +563,9 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   VP_HIP(hipEventRecord(c->ev1, c->stream));
   // phase A's counts are copied out before the fold and waited for alone
   VP_TRY(read_ctl_post(c, t));
-  // Optimistic: fold phase A's touches right away (queued packets logged
-  // kNone); if B/C run, or a touch bin overflowed, the fold is redone over
-  // the completed log.
+  // Fold phase A's touches right away; the packets it queued (reprobes,
+  // overflowed bin entries, phase B/C) are applied on top of it afterwards
+  // as late touches (tbl_late_touches: last toucher still wins).
   if (bp.on)
     VP_TRY(tbl_bins_reduce(c, t, bp, p0, now, seq0));
   else
@@ -578,8 +583,10 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
                              seq0));
     VP_TRY(read_ctl(c, t));  // the walk may have found new flows
   }
-  // the log fold redoes it all when a bin slice overflowed
-  const bool refold = bp.on && t.h_ctl.touch_ovf != 0;
+  const bool ovf = bp.on && t.h_ctl.touch_ovf != 0;
+  if (ovf)  // touches that found their bin slice full, logged alone
+    VP_TRY(tbl_late_touches(c, t, bp.bins.oent, bp.bins.ocnt, 0, range64, grid64,
+                            w.log, now, seq0));
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
   *ms += kms;
@@ -614,20 +621,24 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
       nat_miss_finish<<<grid_for(nmiss), 256, 0, c->stream>>>(
           a, w.miss_sorted, nmiss, w.scratch, w.rep + union_off, w.assign);
       VP_HIP(hipGetLastError());
+      VP_TRY(tbl_late_touches(c, t, w.miss_sorted, nullptr, nmiss, 256,
+                              (nmiss + 255) / 256, w.log, now, seq0));
     }
     *allocated |= 1u;
   }
   if (ndefer) {
     nat_defer_finish<<<grid_for(ndefer), 256, 0, c->stream>>>(a, w.defer, ndefer);
     VP_HIP(hipGetLastError());
+    VP_TRY(tbl_late_touches(c, t, w.defer, nullptr, ndefer, 256, (ndefer + 255) / 256,
+                            w.log, now, seq0));
   }
-  if (nmiss || ndefer || refold)
-    VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
   if (union_n || ndefer) VP_TRY(read_ctl(c, t));
   // steady state (every packet a phase-A hit): the frames and ports are
   // complete (the control copy waited for phase A); only the fold of the
-  // stamps may still run
-  c->fold_pending = !c->comm && !nre && !nmiss && !ndefer && !union_n && !refold;
+  // stamps may still run — unless it reads the caller's time array, which
+  // the caller may reuse as soon as the call returns
+  c->fold_pending = !c->comm && !b->now && !nre && !nmiss && !ndefer && !union_n &&
+                    !ovf;
   return 0;
 }
 

@@ -178,8 +178,16 @@ int tbl_reprobe_stamp(vp_ctx *c, FlowTable &t, const uint32_t *list,
                       const uint32_t *cnt, uint32_t n, uint32_t range, uint32_t nblk,
                       const uint32_t *log, const NowSpec &now, uint64_t seq_base);
 
-// Fold the bins into ts/tseq. Exact unless a slice overflowed (the launch
-// sets t.ctl->touch_ovf; read_ctl, then fold the log with tbl_touch_reduce).
+// Touches applied after a fold, in any order: packets listed as in
+// reprobe_slices (slices per classify block with `cnt`, or runs of `range`
+// of one list of n), each with its index in log[p] (kNone: none); the last
+// toucher in packet order still wins (tseq atomicMax, then ts).
+int tbl_late_touches(vp_ctx *c, FlowTable &t, const uint32_t *list,
+                     const uint32_t *cnt, uint32_t n, uint32_t range, uint32_t nblk,
+                     const uint32_t *log, const NowSpec &now, uint64_t seq_base);
+
+// Fold the bins into ts/tseq. A touch that found its slice full was queued
+// instead (t.ctl->touch_ovf set; apply plan.bins.oent with tbl_late_touches).
 int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
                     const NowSpec &now, uint64_t seq_base);
 

@@ -648,7 +648,8 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   plan->grid = grid;
   plan->range = range;
   plan->L = L;
-  plan->bins = TouchBins{w.bins_ent, w.bins_cnt, &t.ctl->touch_ovf, cap, pbits};
+  plan->bins = TouchBins{w.bins_ent, w.bins_cnt, &t.ctl->touch_ovf, w.ovf_q,
+                         w.ovf_cnt, w.log, cap, pbits};
   return 0;
 }
 
@@ -675,6 +676,35 @@ __global__ void reprobe_stamp(const uint32_t *list, const uint32_t *cnt, uint32_
       if (i != kNone && tseq[i] == seq_base + p) ts[i] = (uint64_t)now.at(p);
     }
   }
+}
+
+// Late touches: every listed packet p with log[p] = i != kNone raises tseq[i]
+// to its sequence; reprobe_stamp then stamps ts[i] for the winner.
+__global__ void late_max(const uint32_t *list, const uint32_t *cnt, uint32_t n,
+                         uint32_t range, uint32_t nblk, const uint32_t *log,
+                         uint64_t seq_base, uint64_t *tseq) {
+  for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const uint32_t nb = reprobe_slice_len(cnt, n, range, b);
+    for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x) {
+      const uint32_t p = list[(size_t)b * range + k];
+      const uint32_t i = log[p];
+      if (i != kNone)
+        atomicMax(reinterpret_cast<unsigned long long *>(tseq + i),
+                  (unsigned long long)(seq_base + p));
+    }
+  }
+}
+
+int tbl_late_touches(vp_ctx *c, FlowTable &t, const uint32_t *list,
+                     const uint32_t *cnt, uint32_t n, uint32_t range, uint32_t nblk,
+                     const uint32_t *log, const NowSpec &now, uint64_t seq_base) {
+  if (nblk == 0) return 0;
+  const uint32_t g = std::min<uint32_t>(nblk, 2048);
+  late_max<<<g, 256, 0, c->stream>>>(list, cnt, n, range, nblk, log, seq_base, t.tseq);
+  reprobe_stamp<<<g, 256, 0, c->stream>>>(list, cnt, n, range, nblk, log, now,
+                                          seq_base, t.ts, t.tseq);
+  VP_HIP(hipGetLastError());
+  return 0;
 }
 
 int tbl_reprobe_stamp(vp_ctx *c, FlowTable &t, const uint32_t *list,

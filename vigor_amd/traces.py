@@ -209,3 +209,58 @@ def lb_heartbeats(n_backends: int, slot: int = 64, t0: int = NOW0 - 1000):
     in_dev = (b & 1).astype(np.uint16)
     now = t0 + b
     return frames, lens, in_dev, now
+
+
+FNV64_BASIS = 0xCBF29CE484222325
+FNV64_PRIME = 0x100000001B3
+
+
+def batch_digest(frames: np.ndarray, out_dev: np.ndarray, slot: int,
+                 p0: int = 0) -> int:
+    """Order-sensitive digest of one processed batch: the wrapping u64 sum over
+    packets p of an FNV-1a-style chain over 64-bit words, h = (h ^ w) * prime,
+    of the word (p | out_dev[p] << 32) and then the slot's 8-byte LE words,
+    finalised by splitmix64's mixer. Packet positions start at p0, so the
+    digests of consecutive pieces of a batch add up to the batch's digest.
+    Vectorised over packets (one pass per word): a 2^24-packet batch of 64 B
+    slots digests in about a second."""
+    n = out_dev.shape[0]
+    words = np.ascontiguousarray(frames.reshape(n, slot)).view("<u8")
+    prime = np.uint64(FNV64_PRIME)
+    h = np.full(n, FNV64_BASIS, np.uint64)
+    with np.errstate(over="ignore"):
+        w0 = (np.arange(p0, p0 + n, dtype=np.uint64) |
+              (out_dev.astype(np.uint64) << np.uint64(32)))
+        np.bitwise_xor(h, w0, out=h)
+        np.multiply(h, prime, out=h)
+        for j in range(slot // 8):
+            np.bitwise_xor(h, words[:, j], out=h)
+            np.multiply(h, prime, out=h)
+        return int(_avalanche(h).sum(dtype=np.uint64))
+
+
+def state_digest(alloc: np.ndarray, ts: np.ndarray) -> int:
+    """Digest of a table dump, same construction: per index i the words
+    (i | alloc[i] << 32) and ts[i] (0 where not allocated)."""
+    n = alloc.shape[0]
+    prime = np.uint64(FNV64_PRIME)
+    h = np.full(n, FNV64_BASIS, np.uint64)
+    t = np.where(alloc != 0, ts, 0).astype(np.int64).view(np.uint64)
+    with np.errstate(over="ignore"):
+        w0 = np.arange(n, dtype=np.uint64) | (alloc.astype(np.uint64) << np.uint64(32))
+        for w in (w0, t):
+            np.bitwise_xor(h, w, out=h)
+            np.multiply(h, prime, out=h)
+        return int(_avalanche(h).sum(dtype=np.uint64))
+
+
+def _avalanche(h: np.ndarray) -> np.ndarray:
+    """splitmix64's finaliser, so every bit of the per-packet hash feeds the
+    low bits of the sum."""
+    with np.errstate(over="ignore"):
+        np.bitwise_xor(h, h >> np.uint64(30), out=h)
+        np.multiply(h, np.uint64(0xBF58476D1CE4E5B9), out=h)
+        np.bitwise_xor(h, h >> np.uint64(27), out=h)
+        np.multiply(h, np.uint64(0x94D049BB133111EB), out=h)
+        np.bitwise_xor(h, h >> np.uint64(31), out=h)
+    return h
