@@ -168,13 +168,17 @@ int vp_process_host(vp_ctx *ctx, uint32_t n, const uint16_t *in_dev,
 /* -------------------------------------------------------- multi-GPU -- *
  * One vignat instance over N GPUs (one process and one context per GPU),
  * identical to a single nf.c processing the concatenation of the ranks'
- * slices (rank 0's packets first) of every global batch. Every rank keeps a
- * replica of the flow dictionary and allocator; new flows are all-gathered
- * and allocated identically everywhere; timestamps are per-rank partial
- * maxima merged (all-reduce MAX) only where an expiry may happen. After an
- * attach, vp_process_device is a collective: every rank calls it once per
- * global batch with its own slice (n may be 0), in the same order. See
- * DESIGN.md §6. */
+ * slices (rank 0's packets first) of every global batch. The allocator
+ * (dchain free list) is replicated; new flows are all-gathered and allocated
+ * identically everywhere; timestamps are per-rank partial maxima merged
+ * (all-reduce MAX) only where an expiry may happen. The flow dictionary is
+ * either replicated (VP_SHARD_REPLICATED, the default: every rank probes
+ * locally) or sharded by flow hash (VP_SHARD_OWNER: rank q's buckets hold
+ * the keys with owner(FlowId_hash) = q; a LAN packet whose key another rank
+ * owns is looked up there through an all-to-all of 16-byte keys and 4-byte
+ * replies). After an attach, vp_process_device is a collective: every rank
+ * calls it once per global batch with its own slice (n may be 0), in the
+ * same order. See DESIGN.md §6. */
 
 /* RCCL over xGMI: rank 0 creates the id, the host distributes it. */
 #define VP_COMM_ID_BYTES 128
@@ -190,8 +194,20 @@ typedef struct vp_comm_ops {
   int (*allgather)(void *user, const void *send, void *recv, size_t bytes);
   /* element-wise maximum over ranks of `count` u64 values (all < 2^63) */
   int (*allreduce_max_u64)(void *user, uint64_t *buf, size_t count);
+  /* personalised exchange (VP_SHARD_OWNER only; may be NULL otherwise):
+   * this rank sends send_bytes[q] bytes to rank q, the chunks consecutive in
+   * `send` in rank order, and receives recv_bytes[q] bytes from rank q into
+   * `recv`, laid out the same way */
+  int (*alltoallv)(void *user, const void *send, const size_t *send_bytes,
+                   void *recv, const size_t *recv_bytes);
 } vp_comm_ops;
 int vp_attach_comm(vp_ctx *ctx, const vp_comm_ops *ops, int nranks, int rank);
+
+/* Dictionary placement over the attached ranks (collective; call on every
+ * rank with the same mode after the attach and before the first batch). */
+#define VP_SHARD_REPLICATED 0
+#define VP_SHARD_OWNER 1
+int vp_shard_mode(vp_ctx *ctx, int mode);
 
 /* Collective: merge the ranks' timestamps so vp_nat_dump is exact on every
  * rank (the dictionary and allocator are identical everywhere already). */

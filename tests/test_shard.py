@@ -41,7 +41,17 @@ def _worker(rank, world, port, q):
         # element-wise max of u64 (< 2^63)
         vals = (C.c_uint64 * 4)(rank, 5 - rank, 1 << 62 if rank else 7, 3)
         rc2 = ops.allreduce_max_u64(None, C.addressof(vals), 4)
-        q.put((rank, rc, rc0, rc2, ag, list(vals)))
+        # personalised exchange: q + rank + 1 bytes between rank and q (the
+        # owner mode's key / answer all-to-alls), then an all-empty one
+        sb = [q_ + rank + 1 for q_ in range(world)]
+        data = [rank * 100 + q_ * 10 + i for q_ in range(world) for i in range(sb[q_])]
+        send = (C.c_uint8 * len(data))(*data)
+        recv = (C.c_uint8 * sum(sb))()
+        sz = (C.c_size_t * world)(*sb)
+        rc3 = ops.alltoallv(None, C.addressof(send), sz, C.addressof(recv), sz)
+        zero = (C.c_size_t * world)()
+        rc4 = ops.alltoallv(None, None, zero, None, zero)
+        q.put((rank, rc, rc0, rc2, ag, list(vals), rc3, rc4, list(recv)))
     finally:
         dist.destroy_process_group()
 
@@ -58,10 +68,14 @@ def test_torch_comm_collectives_world2():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, rc, rc0, rc2, ag, vals in res:
-        assert rc == rc0 == rc2 == 0
+    for rank, rc, rc0, rc2, ag, vals, rc3, rc4, a2a in res:
+        assert rc == rc0 == rc2 == rc3 == rc4 == 0
         assert ag == [0, 1, 2, 3, 4, 10, 11, 12, 13, 14]
         assert vals == [1, 5, 1 << 62, 3]
+        # chunk from q: q's bytes for `rank`, in rank order
+        want = [q_ * 100 + rank * 10 + i for q_ in range(world)
+                for i in range(q_ + rank + 1)]
+        assert a2a == want
 
 
 def test_slice_layout():
@@ -77,3 +91,4 @@ def test_attach_rejects_bad_arguments():
     assert L.vp_attach_comm(None, C.byref(ops), 2, 0) == -22
     assert L.vp_attach_rccl(None, None, 2, 0) == -22
     assert L.vp_sync_state(None) == -22
+    assert L.vp_shard_mode(None, 1) == -22

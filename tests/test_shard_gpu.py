@@ -60,7 +60,7 @@ def _worker(rank, world, port, spec, outdir):
             "0," + END_MACS[0].hex(":"), "--eth-dest", "1," + END_MACS[1].hex(":")]
     cfg = vigor_amd.nat_config_from_args(args, 2, DEV_MACS)
     nat = vigor_amd.Nat(cfg, gpu=0)
-    shard.attach_torch(nat, rank, world)
+    shard.attach_torch(nat, rank, world, mode=spec.get("mode", "replicated"))
     fr, ln, dv, now = _trace(spec)
     n = ln.shape[0]
     bounds = [0] + spec["cuts"] + [n]
@@ -137,7 +137,7 @@ def test_rccl_transport_single_rank():
     np.testing.assert_array_equal(gts[oa == 1], ots[oa == 1])
 
 
-@pytest.mark.parametrize("world,spec", [
+SPECS = [
     (2, dict(kind="rr", n=40_000, flows=1000, max_flows=65536,
              expire_us=60_000_000, cuts=[1000, 20_000], affine=True)),
     (3, dict(kind="mixed", seed=1, n=5000, flows=100, max_flows=64,
@@ -148,8 +148,15 @@ def test_rccl_transport_single_rank():
              expire_us=5, cuts=[1000, 1001, 3000])),
     (2, dict(kind="mixed", seed=7, n=6000, flows=300, max_flows=512,
              expire_us=4_295_000, cuts=[1234, 3000], ties=True)),
-])
-def test_sharded_nat_equals_single_nf(world, spec):
+]
+
+
+@pytest.mark.parametrize("mode", ["replicated", "owner"])
+@pytest.mark.parametrize("world,spec", SPECS)
+def test_sharded_nat_equals_single_nf(world, spec, mode):
+    """Both dictionary placements: replicated, and owner-sharded by flow hash
+    (LAN lookups of other ranks' keys through the all-to-all)."""
+    spec = dict(spec, mode=mode)
     res = run_sharded(spec, world)
     fr, ln, dv, now = _trace(spec)
     cfg = orc.nat_cfg(wan=1, start_port=0, ext_ip=T.ip4(192, 168, 4, 2),
@@ -175,3 +182,68 @@ def test_sharded_nat_equals_single_nf(world, spec):
     np.testing.assert_array_equal(res[0]["alloc"], oa)
     np.testing.assert_array_equal(res[0]["ts"][oa == 1], ots[oa == 1])
     np.testing.assert_array_equal(res[0]["keys"][oa == 1], ok[oa == 1])
+
+
+def _worker16m(rank, world, port, mode, outdir):
+    """BASELINE configs[4] table size over `world` ranks: 16M flows, the
+    round-robin trace in global batches of 2^24 packets (rank r ingests the
+    r-th contiguous slice), every flow allocated in batch 0 and hit in
+    batch 1. Each rank digests its own outputs at their global positions."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import golden_cases as G
+    from vigor_amd import shard
+    nat = G.nat_gpu(G.F16M_FLOWS)
+    shard.attach_torch(nat, rank, world, mode=mode)
+    d = torch.device("cuda:0")
+    GB = 1 << 24
+    per = GB // world
+    lens = torch.full((per,), 60, dtype=torch.int16, device=d)
+    ind = torch.zeros(per, dtype=torch.int16, device=d)
+    out = torch.zeros(per, dtype=torch.int16, device=d)
+    dig = 0
+    for k in range(G.F16M_PACKETS // GB):
+        s0 = k * GB + rank * per
+        fr, _, _, _ = T.nat_lan_trace(per, G.F16M_FLOWS, start=s0)
+        f = torch.from_numpy(fr).to(d)
+        del fr
+        nat.process_device(f, lens, ind, out, 64, now0=T.NOW0 + s0, now_step=1)
+        torch.cuda.synchronize()
+        dig += T.batch_digest(f.cpu().numpy(), out.cpu().numpy().view(np.uint16), 64, s0)
+        del f
+    nat.sync_state()
+    res = dict(digest=np.array(dig % (1 << 64), np.uint64))
+    if rank == 0:
+        a_, t_, _ = nat.dump()
+        res.update(state=np.array(T.state_digest(a_, t_), np.uint64),
+                   live=np.array(nat.live_count()))
+    np.savez(os.path.join(outdir, "r%d.npz" % rank), **res)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["replicated", "owner"])
+def test_sharded_16m_flows_equals_reference(mode):
+    """configs[4]'s table (16M flows) over 2 ranks sharing the GPU (gloo
+    transport): output bytes of all 2^25 packets and the merged table state
+    equal the reference's (tests/golden/nat_16m_digest.npz)."""
+    import golden_cases as G
+    g = G.load("nat_16m_digest")
+    assert str(g["impl"]) == "reference"
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        port = _free_port()
+        ps = [ctx.Process(target=_worker16m, args=(r, world, port, mode, d))
+              for r in range(world)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(timeout=400)
+        assert [p.exitcode for p in ps] == [0] * world
+        res = [dict(np.load(os.path.join(d, "r%d.npz" % r))) for r in range(world)]
+    assert sum(int(r["digest"]) for r in res) % (1 << 64) == int(g["digest"])
+    assert int(res[0]["state"]) == int(g["state_digest"])
+    assert int(res[0]["live"]) == int(g["live"])

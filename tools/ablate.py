@@ -25,11 +25,15 @@ def main():
     variants = {"full": (None, {}), "perlane": (None, {"VIGPATH_COALESCED": "0"})}
     variants["bpc3"] = (None, {"VIGPATH_BLOCKS_PER_CU": "3"})
     variants["bpc2"] = (None, {"VIGPATH_BLOCKS_PER_CU": "2"})
-    for v in ("NOPROBE", "NOINLINE", "NT", "NOFRAME"):
+    only = os.environ.get("ABLATE_ONLY")  # comma-separated variant names
+    for v in ("NOPROBE", "NOINLINE", "NT", "NOFRAME", "NTLD", "SC1ST", "NTSC"):
         p = os.path.join(ROOT, "vigor_amd", "abl", "libvigpath_%s.so" % v)
         if os.path.exists(p):  # NOFRAME lives in the per-lane kernel
             variants[v] = (p, {"VIGPATH_COALESCED": "0"} if v == "NOFRAME"
                            else {})
+    if only:
+        keep = set(only.split(",")) | {"full"}
+        variants = {k: v for k, v in variants.items() if k in keep}
     bank = bench.FlowBank(NF, 0, dev)
     lens = torch.full((B,), 60, dtype=torch.int16, device=dev)
     ind = torch.zeros(B, dtype=torch.int16, device=dev)

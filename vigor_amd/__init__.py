@@ -78,12 +78,18 @@ class PolConfigC(C.Structure):
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                            C.c_size_t)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t)
+ALLTOALLV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p,
+                           C.POINTER(C.c_size_t), C.c_void_p,
+                           C.POINTER(C.c_size_t))
+
+SHARD_REPLICATED, SHARD_OWNER = 0, 1  # vp_shard_mode
 
 
 class CommOpsC(C.Structure):
     """vp_comm_ops: host-memory collectives supplied by the caller."""
     _fields_ = [("user", C.c_void_p), ("allgather", ALLGATHER_FN),
-                ("allreduce_max_u64", ALLREDUCE_FN)]
+                ("allreduce_max_u64", ALLREDUCE_FN),
+                ("alltoallv", ALLTOALLV_FN)]
 
 
 class DevBatchC(C.Structure):
@@ -98,7 +104,7 @@ EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_fw_create",
            "vp_pol_create", "vp_pol_dump", "vp_destroy", "vp_process_device", "vp_process_batch",
            "vp_process_host", "vp_nat_dump", "vp_bridge_dump", "vp_lb_dump",
            "vp_fw_dump", "vp_comm_unique_id", "vp_attach_rccl",
-           "vp_attach_comm", "vp_sync_state", "vp_live_count",
+           "vp_attach_comm", "vp_shard_mode", "vp_sync_state", "vp_live_count",
            "vp_last_kernel_ms", "vp_version"]
 
 _libs = {}
@@ -158,6 +164,8 @@ def lib(path: str | None = None):
     L.vp_attach_comm.argtypes = [C.c_void_p, C.POINTER(CommOpsC), C.c_int,
                                  C.c_int]
     L.vp_attach_comm.restype = C.c_int
+    L.vp_shard_mode.argtypes = [C.c_void_p, C.c_int]
+    L.vp_shard_mode.restype = C.c_int
     L.vp_sync_state.argtypes = [C.c_void_p]
     L.vp_sync_state.restype = C.c_int
     L.vp_live_count.argtypes = [C.c_void_p]

@@ -19,6 +19,10 @@ struct Comm {
                             size_t bytes) = 0;
   // in place, element-wise max over ranks (values < 2^63)
   virtual int allreduce_max_u64_dev(vp_ctx *c, uint64_t *buf, size_t count) = 0;
+  // personalised exchange of device buffers: sbytes[q] bytes to rank q
+  // (chunks consecutive in rank order), rbytes[q] bytes from rank q
+  virtual int alltoallv_dev(vp_ctx *c, const void *send, const size_t *sbytes,
+                            void *recv, const size_t *rbytes) = 0;
 };
 
 }  // namespace vp

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "vp_comm.h"
+#include "vp_table.h"
 
 namespace vp {
 
@@ -58,6 +59,45 @@ struct RcclComm : Comm {
     VP_NCCL(ncclAllReduce(buf, buf, count, ncclUint64, ncclMax, comm, c->stream));
     return 0;
   }
+  // one grouped send/recv per peer: every pair of GPUs talks over its own
+  // xGMI link at once
+  int alltoallv_dev(vp_ctx *c, const void *send, const size_t *sbytes, void *recv,
+                    const size_t *rbytes) override {
+    const uint8_t *s = static_cast<const uint8_t *>(send);
+    uint8_t *d = static_cast<uint8_t *>(recv);
+    size_t so = 0, ro = 0;
+    std::vector<size_t> soff(n), roff(n);
+    for (int q = 0; q < n; q++) {
+      soff[q] = so;
+      roff[q] = ro;
+      so += sbytes[q];
+      ro += rbytes[q];
+    }
+    if (sbytes[r] != rbytes[r]) return VP_EINVAL;
+    if (sbytes[r])
+      VP_HIP(hipMemcpyAsync(d + roff[r], s + soff[r], sbytes[r],
+                            hipMemcpyDeviceToDevice, c->stream));
+    VP_NCCL(ncclGroupStart());
+    for (int q = 0; q < n; q++) {
+      if (q == r) continue;
+      if (sbytes[q]) {
+        ncclResult_t e = ncclSend(s + soff[q], sbytes[q], ncclUint8, q, comm, c->stream);
+        if (e != ncclSuccess) {
+          ncclGroupEnd();
+          return nccl_fail(e, "ncclSend");
+        }
+      }
+      if (rbytes[q]) {
+        ncclResult_t e = ncclRecv(d + roff[q], rbytes[q], ncclUint8, q, comm, c->stream);
+        if (e != ncclSuccess) {
+          ncclGroupEnd();
+          return nccl_fail(e, "ncclRecv");
+        }
+      }
+    }
+    VP_NCCL(ncclGroupEnd());
+    return 0;
+  }
 };
 
 // Caller-supplied host-memory collectives; device variants stage through
@@ -91,6 +131,25 @@ struct HostComm : Comm {
     VP_HIP(hipMemcpyAsync(buf, hs.data(), count * 8, hipMemcpyHostToDevice,
                           c->stream));
     VP_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+  }
+  int alltoallv_dev(vp_ctx *c, const void *send, const size_t *sbytes, void *recv,
+                    const size_t *rbytes) override {
+    if (!ops.alltoallv) return VP_ENOTSUP;
+    size_t st = 0, rt = 0;
+    for (int q = 0; q < n; q++) {
+      st += sbytes[q];
+      rt += rbytes[q];
+    }
+    hs.resize(st ? st : 1);
+    hr.resize(rt ? rt : 1);
+    if (st) VP_HIP(hipMemcpyAsync(hs.data(), send, st, hipMemcpyDeviceToHost, c->stream));
+    VP_HIP(hipStreamSynchronize(c->stream));
+    if (ops.alltoallv(ops.user, hs.data(), sbytes, hr.data(), rbytes)) return VP_EIO;
+    if (rt) {
+      VP_HIP(hipMemcpyAsync(recv, hr.data(), rt, hipMemcpyHostToDevice, c->stream));
+      VP_HIP(hipStreamSynchronize(c->stream));
+    }
     return 0;
   }
 };
@@ -147,6 +206,21 @@ int vp_attach_comm(vp_ctx *c, const vp_comm_ops *ops, int nranks, int rank) {
   m->r = rank;
   m->ops = *ops;
   c->comm = m;
+  return 0;
+}
+
+int vp_shard_mode(vp_ctx *c, int mode) {
+  if (!c || (mode != VP_SHARD_REPLICATED && mode != VP_SHARD_OWNER)) return VP_EINVAL;
+  if (mode == c->shard_mode) return 0;
+  // before the first batch, on an attached context (or a one-rank context
+  // for VP_SHARD_REPLICATED, which is the default)
+  if (!c->comm || c->seq != 0 || c->shard_mode != VP_SHARD_REPLICATED) return VP_EINVAL;
+  if (c->kind != KIND_NAT) return VP_ENOTSUP;
+  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  HostComm *h = dynamic_cast<HostComm *>(c->comm);
+  if (h && !h->ops.alltoallv) return VP_EINVAL;
+  VP_TRY(tbl_set_owner(c, c->ft, (uint32_t)c->comm->n, (uint32_t)c->comm->r));
+  c->shard_mode = mode;
   return 0;
 }
 

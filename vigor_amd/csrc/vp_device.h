@@ -156,6 +156,30 @@ __device__ __forceinline__ void st_stream(uint4 *p, uint4 v) {
 #endif
 }
 
+// Tile frame loads / stores of frames64_tiles. Ablation builds (tools/
+// ablate.py) change their cache policy: VP_ABL_NTLD loads non-temporal
+// (evict-first in L2), VP_ABL_SC1ST stores write-through (sc1: the line
+// leaves the XCD's L2), so the frame stream displaces fewer table rows.
+__device__ __forceinline__ uint4 tile_ld(const uint4 *p) {
+#if defined(VP_ABL_NTLD) || defined(VP_ABL_NTSC)
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void tile_st(uint4 *g, uint32_t c, uint4 v) {
+#if defined(VP_ABL_SC1ST) || defined(VP_ABL_NTSC)
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(g, 0, 4096, 0x00020000);
+  const v4u x = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)(c * 16), 0, 16);
+#else
+  g[c] = v;
+#endif
+}
+
 // ------------------------------------------------------------ fast frames --
 // The 64-byte slot held in 16 registers (LE words). Only compile-time word
 // indices are used so nothing spills to scratch.
@@ -214,21 +238,25 @@ __device__ __forceinline__ uint32_t group_reserve(uint32_t *ctr, uint32_t ch,
 }
 
 // Touch bins: besides the per-packet touch log, the 64-byte classify kernels
-// sort each touch (flow index i of packet p) into one of kBins bins while
-// classifying, so the timestamp fold needs a single pass (touch_bins_reduce,
-// vp_table.hip) instead of count + scan + scatter + reduce. Index i belongs
-// to bin (i >> 4) & 255, at in-bin position ((i >> 12) << 4) | (i & 15): runs
-// of 16 consecutive indices per bin, so sequential flow sets spread over all
-// bins and the fold writes whole 128-byte runs of ts. Each block appends to
+// sort each touch (flow index i of packet p) into one of 2^bbits bins (256 up
+// to kMaxBins, chosen per table so that a bin's indices fit one LDS tile)
+// while classifying, so the timestamp fold needs a single pass
+// (touch_bins_reduce, vp_table.hip) instead of count + scan + scatter +
+// reduce. Index i belongs to bin (i >> 4) & (2^bbits - 1), at in-bin position
+// ((i >> (4 + bbits)) << 4) | (i & 15): runs of 16 consecutive indices per
+// bin, so sequential flow sets spread over all bins and the fold writes whole
+// 128-byte runs of ts. Each block appends to
 // its own fixed-size slice of every bin (LDS cursors). With bins on, the
 // classify kernels write no per-packet touch log: a touch that finds its
 // slice full is logged alone (olog[p] = index) and queued on the block's
 // overflow slice (oent/ocnt), and *ovf tells the host to apply the queued
 // touches after the fold (tbl_late_touches, vp_table.hip).
-constexpr uint32_t kBins = 256;
-constexpr uint32_t kCurReprobe = kBins;       // LDS cursor of the reprobe queue
-constexpr uint32_t kCurOverflow = kBins + 1;  // LDS cursor of the overflow queue
-constexpr uint32_t kCurs = kBins + 2;
+constexpr uint32_t kMaxBins = 1024;
+constexpr uint32_t kCurReprobe = kMaxBins;       // LDS cursor of the reprobe queue
+constexpr uint32_t kCurOverflow = kMaxBins + 1;  // LDS cursor of the overflow queue
+constexpr uint32_t kCurDest = kMaxBins + 2;      // LDS cursors per owner rank (owner mode)
+constexpr uint32_t kMaxDest = 64;                // = kMaxRanks (vp_internal.h)
+constexpr uint32_t kCurs = kCurDest + kMaxDest;
 // finish() may set touch = kReprobe instead of an index: the packet leaves
 // the wave and is queued on the block's reprobe slice (TileQueue).
 constexpr uint32_t kReprobe = 0xFFFFFFFDu;
@@ -244,19 +272,22 @@ struct TouchBins {
   uint32_t *oent;  // [block][range] positions of overflowed touches
   uint32_t *ocnt;  // [block] overflowed touches queued
   uint32_t *olog;  // olog[p] = index of an overflowed touch
-  uint32_t cap, pbits;
+  uint32_t cap, pbits, bbits;
 };
 // Touch-log entry of packet p; `log` is null in the classify kernels that
 // bin their touches.
 __device__ __forceinline__ void log_put(uint32_t *log, uint32_t p, uint32_t v) {
   if (log) log[p] = v;
 }
-__device__ __forceinline__ uint32_t bin_of(uint32_t i) { return (i >> 4) & (kBins - 1); }
-__device__ __forceinline__ uint32_t bin_local(uint32_t i) {
-  return ((i >> 12) << 4) | (i & 15u);
+__device__ __forceinline__ uint32_t bin_of(uint32_t i, uint32_t bbits) {
+  return (i >> 4) & ((1u << bbits) - 1);
 }
-__device__ __forceinline__ uint32_t bin_index(uint32_t bin, uint32_t local) {
-  return ((local >> 4) << 12) | (bin << 4) | (local & 15u);
+__device__ __forceinline__ uint32_t bin_local(uint32_t i, uint32_t bbits) {
+  return ((i >> (4 + bbits)) << 4) | (i & 15u);
+}
+__device__ __forceinline__ uint32_t bin_index(uint32_t bin, uint32_t local,
+                                              uint32_t bbits) {
+  return ((local >> 4) << (4 + bbits)) | (bin << 4) | (local & 15u);
 }
 
 // Packets [p0, p1) of a batch of n_all 64-byte slots, in tiles of 64
@@ -316,7 +347,7 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) {
       const uint32_t c = 64 * j + lane;
-      r[j] = (c >> 2) < avail ? g[c] : make_uint4(0, 0, 0, 0);
+      r[j] = (c >> 2) < avail ? tile_ld(g + c) : make_uint4(0, 0, 0, 0);
     }
     const uint32_t p = tb + lane;
     m_in = p < n_all ? in_dev[p] : 0u;
@@ -378,12 +409,12 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
     if (touch == kReprobe) touch = kNone;
     if (bins.ent) {  // append to this block's slice of the touch's bin
       const bool v = touch != kNone;
-      const uint32_t b = v ? bin_of(touch) : 0;
+      const uint32_t b = v ? bin_of(touch, bins.bbits) : 0;
       const uint32_t k = group_reserve(cur, b, v);
       const bool fits = k < bins.cap;
       if (v && fits)
-        bins.ent[((size_t)rb * kBins + b) * bins.cap + k] =
-            (bin_local(touch) << bins.pbits) | (p - range0);
+        bins.ent[(((size_t)rb << bins.bbits) + b) * bins.cap + k] =
+            (bin_local(touch, bins.bbits) << bins.pbits) | (p - range0);
       const bool spill = v && !fits;  // slice full: log this touch alone
       const uint32_t o = group_reserve(cur, kCurOverflow, spill);
       if (spill) {
@@ -406,15 +437,15 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) {
       const uint32_t c = 64 * j + lane;
-      if ((partmask >> (c >> 2)) & 1ull) g[c] = S[chunk_swz(c)];
+      if ((partmask >> (c >> 2)) & 1ull) tile_st(g, c, S[chunk_swz(c)]);
     }
     wave_lds_sync();  // the next tile overwrites S
   }
   if (bins.ent || rq.ent) __syncthreads();
   if (bins.ent) {  // publish this block's slice sizes
-    for (uint32_t b = threadIdx.x; b < kBins; b += blockDim.x) {
+    for (uint32_t b = threadIdx.x; b < (1u << bins.bbits); b += blockDim.x) {
       const uint32_t c = cur[b];
-      bins.cnt[(size_t)rb * kBins + b] = c < bins.cap ? c : bins.cap;
+      bins.cnt[((size_t)rb << bins.bbits) + b] = c < bins.cap ? c : bins.cap;
     }
     if (threadIdx.x == 0) {
       const uint32_t o = cur[kCurOverflow];

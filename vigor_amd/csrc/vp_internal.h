@@ -52,6 +52,8 @@ struct Ctl {
   uint32_t aux_count;
   uint32_t max_disp;    // longest insert probe (buckets) since last check
   uint32_t disp_count;  // inserts that passed their home bucket (since rebuild)
+  uint32_t sh_live;     // entries in this rank's buckets (= n_live unless owner mode)
+  uint32_t own_new;     // owner mode: union keys this rank will insert (upper bound)
 };
 
 // One device table (see vp_table.h).
@@ -76,6 +78,10 @@ struct FlowTable {
   // expiry workspace (sized cap)
   uint64_t *ekey = nullptr, *ekey2 = nullptr;
   uint32_t *eidx = nullptr, *eidx2 = nullptr;
+  // owner-sharded mode (vp_shard_mode): this rank's buckets
+  // hold only the keys it owns; key by index is replicated in kv
+  uint4 *kv = nullptr;
+  uint32_t own_n = 0, own_r = 0;  // ranks, this rank (own_n == 0: off)
 };
 
 struct Workspace {
@@ -107,6 +113,19 @@ struct Workspace {
   uint64_t hist_cap = 0;
   uint32_t *bins_ent = nullptr, *bins_cnt = nullptr;  // touch bins (TouchBins)
   uint32_t *ovf_q = nullptr, *ovf_cnt = nullptr;  // overflowed touches per block
+  // owner mode: per-block slices of descriptors by owner rank, their counts
+  // and send offsets, per-packet routes, the exchanged keys and replies
+  uint4 *desc = nullptr;
+  size_t desc_n = 0;
+  uint32_t *dcnt = nullptr, *dbase = nullptr, *dtot = nullptr;
+  size_t dcnt_n = 0, dbase_n = 0, dtot_n = 0;
+  uint32_t *route = nullptr;
+  size_t route_n = 0;
+  uint4 *sendk = nullptr, *recvk = nullptr;
+  size_t sendk_n = 0, recvk_n = 0;
+  uint32_t *reply = nullptr, *rreply = nullptr;
+  size_t reply_n = 0, rreply_n = 0;
+  uint32_t *h_tot = nullptr;  // pinned landing buffer for dtot
   size_t bins_ent_n = 0, bins_cnt_n = 0;
   void *cub_tmp = nullptr;
   size_t cub_bytes = 0;
@@ -135,6 +154,7 @@ struct vp_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t evc = nullptr;  // control-block copy (read_ctl_post / _wait)
+  hipEvent_t ev2 = nullptr, ev3 = nullptr;  // owner mode: pass 2 timing
   // The last segment left only its timestamp fold running on `stream`
   // (results complete): run_batch returns without waiting for it.
   bool fold_pending = false;
@@ -168,6 +188,7 @@ struct vp_ctx {
   // multi-GPU (vp_attach_*): this rank's collectives, and during a batch the
   // global position of local packet 0 and the per-rank slice sizes
   vp::Comm *comm = nullptr;
+  int shard_mode = 0;  // VP_SHARD_REPLICATED / VP_SHARD_OWNER
   uint32_t off = 0;
   std::vector<uint32_t> rank_n;    // slice sizes of the current batch
   std::vector<uint32_t> rank_cnt;  // new keys per rank of the current segment

@@ -23,6 +23,7 @@
 #include <cstring>
 #include <vector>
 
+#include "vp_comm.h"
 #include "vp_table.h"
 
 namespace vp {
@@ -49,6 +50,27 @@ __device__ __forceinline__ uint32_t flowid_hash(const uint32_t *T, uint32_t sp,
          T[14 * 256 + (proto & 0xFF)];
 }
 
+// Owner mode (vp_shard_mode): a LAN packet whose FlowId is
+// owned by another rank leaves phase A as a 16-byte key in this block's
+// slice for that owner (desc), and route[p] says where its answer will be:
+//   route[p] = kRouteBit | owner << 24 | k   k-th key of the block's slice
+//            = index < 2^30                  a phase-A touch, frame done
+//            = kNone                         nothing left (drop, queued, ...)
+// After the exchange, pass 2 (nat_remote64 / nat_remote_lane) finishes the
+// routed packets from the owners' replies.
+constexpr uint32_t kRouteBit = 0x80000000u;
+constexpr uint32_t kRouted = 0xFFFFFFFBu;  // touch: the packet was routed
+struct Route {
+  uint32_t n, r;          // ranks, this rank (n == 0: single table)
+  uint4 *desc;            // [block][n][range] keys by owner
+  uint32_t *dcnt;         // [block][n] keys per slice
+  uint32_t *route;        // per packet
+  uint32_t *cur;          // the kernel's LDS cursors per owner
+  uint32_t first, range;  // packets of block b: [first + b * range, +range)
+  const uint32_t *dbase;  // pass 2: [block][n] offset of the slice's replies
+  const uint32_t *rreply; // pass 2: replies (index or kNone), in send order
+};
+
 struct NatArgs {
   uint8_t *frames;
   const uint16_t *len;
@@ -68,7 +90,22 @@ struct NatArgs {
   uint32_t tileq;  // 64-byte tiles: reprobes go to the block's TileQueue slice
   uint32_t ext_ip;
   uint16_t wan, start_port, n_dev;
+  Route own;
 };
+
+// Owner mode: hand the LAN packet with key `key` (hash h) to its owner if
+// that is another rank. Returns true when routed.
+__device__ __forceinline__ bool nat_route(const NatArgs &a, uint32_t p, uint32_t h,
+                                          const uint32_t key[4]) {
+  if (!a.own.n) return false;
+  const uint32_t o = owner_of(h, a.own.n);
+  if (o == a.own.r) return false;
+  const uint32_t k = atomicAdd(&a.own.cur[o], 1u);
+  a.own.desc[((size_t)blockIdx.x * a.own.n + o) * a.own.range + k] =
+      make_uint4(key[0], key[1], key[2], key[3]);
+  a.own.route[p] = kRouteBit | (o << 24) | k;
+  return true;
+}
 
 __device__ __forceinline__ void macs_for(const NatArgs &a, uint32_t dst,
                                          uint32_t mw[3]) {
@@ -131,8 +168,12 @@ VP_GENERIC_FN uint32_t nat_generic_a(const NatArgs &a, const uint32_t *T,
     dst = k3 & 0xFFFF;
   } else {
     const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
-    const uint32_t idx = tbl_probe(a.t, flowid_hash(T, sp, dp, sip, dip, in, proto),
-                                   key);
+    const uint32_t hh = flowid_hash(T, sp, dp, sip, dip, in, proto);
+    if (nat_route(a, p, hh, key)) {
+      log_put(a.log, p, kNone);  // pass 2 writes the real entry
+      return kRouted;
+    }
+    const uint32_t idx = tbl_probe(a.t, hh, key);
     if (idx == kNone) {
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
       log_put(a.log, p, kNone);  // phase B writes the real entry
@@ -157,7 +198,8 @@ VP_GENERIC_FN uint32_t nat_generic_a(const NatArgs &a, const uint32_t *T,
 // first dependent read — the home bucket of a LAN packet's FlowId, the
 // entry slot of a WAN packet's index — and nat_finish consumes it, rewrites
 // the frame and returns true when it must be stored back.
-enum : uint32_t { kPendDone = 0, kPendGeneric = 1, kPendLan = 2, kPendWan = 3 };
+enum : uint32_t { kPendDone = 0, kPendGeneric = 1, kPendLan = 2, kPendWan = 3,
+                  kPendRemote = 4 };
 struct NatPend {
   uint32_t kind;
   uint32_t row;  // LAN: home bucket, gathered by frames64_tiles; else kNone
@@ -206,6 +248,11 @@ __device__ __forceinline__ NatPend nat_issue(const NatArgs &a, const uint32_t *T
     // flow_manager_get_internal (nat_flowmanager.c:67-76): map_get's hash
     const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
     const uint32_t hh = flowid_hash(T, sp, dp, sip, dip, in, proto);
+    if (a.own.n && owner_of(hh, a.own.n) != a.own.r) {  // another rank's key
+      P.kind = kPendRemote;
+      P.b = hh;
+      return P;
+    }
     P.kind = kPendLan;
     P.b = home_bucket(hh, a.t.bmask, a.t.mix);
 #ifndef VP_ABL_NOPROBE  // diagnostic builds skip the read (tools/ablate.py)
@@ -230,6 +277,13 @@ __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
   const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
   uint32_t dst;
   uint32_t mw[3];
+  if (P.kind == kPendRemote) {
+    const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
+    nat_route(a, p, P.b, key);
+    log_put(a.log, p, kNone);  // pass 2 writes the real entry
+    touch = kRouted;
+    return false;
+  }
   if (P.kind == kPendWan) {
     const uint32_t idx = P.b;
     const uint32_t s = P.s;
@@ -238,7 +292,8 @@ __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
       log_put(a.log, p, kNone);  // phase C writes the real entry
       return false;
     }
-    const uint4 k = reinterpret_cast<const uint4 *>(a.t.bk + (s >> 2))[s & 3];
+    const uint4 k = a.t.kv ? a.t.kv[idx]  // owner mode: keys by index
+                           : reinterpret_cast<const uint4 *>(a.t.bk + (s >> 2))[s & 3];
     log_put(a.log, p, idx);  // rejuvenated before the anti-spoof check
     touch = idx;
     if ((k.z != sip) | ((k.x >> 16) != sp) | (((k.w >> 16) & 0xFF) != proto)) {
@@ -294,6 +349,24 @@ __device__ __forceinline__ void load_crc_tables(uint32_t *T, const uint32_t *g) 
   __syncthreads();
 }
 
+// Owner mode: the route of a packet phase A did not hand to another rank
+// (its touch, or nothing); returns the touch for this launch's bins.
+__device__ __forceinline__ uint32_t route_note(const NatArgs &a, uint32_t p,
+                                               uint32_t touch) {
+  if (!a.own.n) return touch;
+  if (touch == kRouted) return kNone;
+  a.own.route[p] = touch == kReprobe ? kNone : touch;
+  return touch == kReprobe ? kReprobe : kNone;  // pass 2 bins the touches
+}
+
+// Owner mode: publish this block's key count per owner (after a barrier).
+__device__ __forceinline__ void route_publish(const NatArgs &a, const uint32_t *cur) {
+  if (!a.own.n) return;
+  __syncthreads();
+  for (uint32_t o = threadIdx.x; o < a.own.n; o += blockDim.x)
+    a.own.dcnt[(size_t)blockIdx.x * a.own.n + o] = cur[o];
+}
+
 // One packet, its slot's first 64 bytes in registers (any slot size; frames
 // outside the fast path take nat_generic_a). Returns the logged index.
 __device__ __forceinline__ uint32_t nat_lane(const NatArgs &a, const uint32_t *T,
@@ -340,14 +413,26 @@ __device__ __forceinline__ uint32_t nat_lane(const NatArgs &a, const uint32_t *T
       st_stream(fp + 3, make_uint4(f.w[12], f.w[13], f.w[14], f.w[15]));
   }
 #endif
-  return touch;
+  return route_note(a, p, touch);
 }
 
 // Phase A, any slot size: one packet per lane, grid-stride, the first 64
 // bytes of the slot as four 16-byte loads per lane.
 __global__ __launch_bounds__(256) void nat_classify(NatArgs a) {
   __shared__ uint32_t T[15 * 256];
-  load_crc_tables(T, a.crc_tab);
+  __shared__ uint32_t dcur[kMaxDest];
+  if (a.own.n) {  // owner mode: block b takes packets [first + b * range, +range)
+    for (uint32_t o = threadIdx.x; o < kMaxDest; o += blockDim.x) dcur[o] = 0;
+    a.own.cur = dcur;
+  }
+  load_crc_tables(T, a.crc_tab);  // (its barrier also covers dcur)
+  if (a.own.n) {
+    const uint32_t b0 = a.own.first + blockIdx.x * a.own.range;
+    const uint32_t b1 = min(a.p1, b0 + a.own.range);
+    for (uint32_t p = b0 + threadIdx.x; p < b1; p += blockDim.x) nat_lane(a, T, p);
+    route_publish(a, dcur);
+    return;
+  }
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t p = a.p0 + blockIdx.x * blockDim.x + threadIdx.x; p < a.p1;
        p += stride)
@@ -362,6 +447,7 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
   __shared__ uint4 stage[4][256];
   __shared__ uint32_t cur[kCurs];
   for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
+  a.own.cur = cur + kCurDest;
   load_crc_tables(T, a.crc_tab);  // (its barrier also covers cur)
   frames64_tiles(
       a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
@@ -373,10 +459,13 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
           uint32_t len, uint32_t &touch) -> uint32_t {
         // a rewrite touches bytes 0-47; the TCP checksum (bytes 50-51) also
         // dirties chunk 3 (the protocol byte is never rewritten)
-        if (!nat_finish(a, T, P, row, p, f, in, len, touch)) return 0u;
+        const bool m = nat_finish(a, T, P, row, p, f, in, len, touch);
+        touch = route_note(a, p, touch);
+        if (!m) return 0u;
         return (f.w[5] >> 24) == 6 ? 0xFu : 0x7u;
       },
       bins, rq, cur);
+  route_publish(a, cur + kCurDest);
 }
 
 // ------------------------------------------------------------- phase B --
@@ -458,6 +547,203 @@ __global__ __launch_bounds__(256) void nat_reprobe(NatArgs a, const uint32_t *li
   });
 }
 
+// ------------------------------------------------------- owner mode --
+//  After pass 1 each block has a slice of keys per owner rank
+// (desc, dcnt). route_scan + route_base give every slice its offset in the
+// send buffer (grouped by owner, ranks in order, blocks in order inside),
+// route_pack gathers the slices there; the keys go to their owners
+// (all-to-all), nat_own_probe answers them against the owner's buckets, the
+// answers come back in the same order, and pass 2 finishes the packets.
+
+// Per owner o (one block each): exclusive scan over blocks of dcnt[.][o].
+__global__ __launch_bounds__(256) void route_scan(const uint32_t *dcnt, uint32_t nblk,
+                                                  uint32_t n, uint32_t *dbase,
+                                                  uint32_t *dtot) {
+  __shared__ uint32_t part[256];
+  const uint32_t o = blockIdx.x;
+  const uint32_t per = (nblk + 255) / 256;
+  const uint32_t b0 = threadIdx.x * per, b1 = min(nblk, b0 + per);
+  uint32_t sum = 0;
+  for (uint32_t b = b0; b < b1; b++) sum += dcnt[(size_t)b * n + o];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < 256; i++) {
+      const uint32_t v = part[i];
+      part[i] = acc;
+      acc += v;
+    }
+    dtot[o] = acc;
+  }
+  __syncthreads();
+  uint32_t acc = part[threadIdx.x];
+  for (uint32_t b = b0; b < b1; b++) {
+    dbase[(size_t)b * n + o] = acc;
+    acc += dcnt[(size_t)b * n + o];
+  }
+}
+
+// Owner o's chunk starts after the chunks of owners < o.
+__global__ void route_base(uint32_t *dbase, const uint32_t *dtot, uint32_t nblk,
+                           uint32_t n) {
+  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nblk * n;
+       x += gridDim.x * blockDim.x) {
+    const uint32_t o = x % n;
+    uint32_t start = 0;
+    for (uint32_t q = 0; q < o; q++) start += dtot[q];
+    dbase[x] += start;
+  }
+}
+
+// One block per source block: its slices into the send buffer.
+__global__ __launch_bounds__(256) void route_pack(const uint4 *desc, const uint32_t *dcnt,
+                                                  const uint32_t *dbase, uint32_t n,
+                                                  uint32_t range, uint4 *sendk) {
+  const uint32_t b = blockIdx.x;
+  for (uint32_t o = 0; o < n; o++) {
+    const uint32_t cnt = dcnt[(size_t)b * n + o], base = dbase[(size_t)b * n + o];
+    const uint4 *src = desc + ((size_t)b * n + o) * range;
+    for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) sendk[base + k] = src[k];
+  }
+}
+
+// The owner side of C1: map_get (find_key, map-impl-pow2.c:629-732) of every
+// received FlowId in this rank's buckets, a wave of 64 keys at a time, each
+// bucket fetched as one cooperative 64-byte request (wave_gather64). Answers
+// the index or kNone (a new flow: the ingest rank queues the packet for
+// phase B).
+__global__ __launch_bounds__(256) void nat_own_probe(TableDev t, const uint32_t *crc_tab,
+                                                     const uint4 *keys, uint32_t n,
+                                                     uint32_t *reply) {
+  __shared__ uint32_t T[15 * 256];
+  __shared__ uint4 stage[4][256];
+  load_crc_tables(T, crc_tab);
+  uint4 *S = stage[threadIdx.x >> 6];
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t base = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; base < n;
+       base += gridDim.x * 256) {  // wave-uniform
+    const uint32_t j = base + lane;
+    const bool act = j < n;
+    const uint4 k = act ? keys[j] : make_uint4(0, 0, 0, 0);
+    const uint32_t key[4] = {k.x, k.y, k.z, k.w};
+    const uint32_t h = flowid_hash(T, k.x & 0xFFFF, k.x >> 16, k.y, k.z, k.w & 0xFFFF,
+                                   (k.w >> 16) & 0xFF);
+    uint32_t b = home_bucket(h, t.bmask, t.mix), res = kNone;
+    bool live = act;
+    for (uint32_t step = 0;; step++) {
+      uint4 row[4];
+      wave_gather64(reinterpret_cast<const uint8_t *>(t.bk), 64, live ? b : kNone, S,
+                    row);
+      if (live) {
+        bool done;
+        const uint32_t idx = bucket_match(row[0], row[1], row[2], row[3], key, &done);
+        if (done) {
+          res = idx;
+          live = false;
+        } else {
+          b = (b + 1) & t.bmask;
+        }
+      }
+      if (!__ballot(live) || step >= t.bmask) break;
+    }
+    if (act) reply[j] = res;
+  }
+}
+
+// LAN rewrite of a routed packet whose index came back (register frame).
+__device__ __forceinline__ void nat_lan_fast(const NatArgs &a, RFrame &f, uint32_t p,
+                                             uint32_t idx) {
+  const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
+  const uint32_t proto = f.w[5] >> 24;
+  f.set32at2(26, a.ext_ip);
+  f.set16(34, (uint16_t)(a.start_port + idx));
+  fast_checksums(f, proto, tl);
+  f.w[0] = a.wan_macw0;
+  f.w[1] = a.wan_macw1;
+  f.w[2] = a.wan_macw2;
+  a.out[p] = a.wan;
+}
+
+// The answer for packet p's route (kRouteBit set).
+__device__ __forceinline__ uint32_t route_answer(const NatArgs &a, uint32_t p,
+                                                 uint32_t rt) {
+  const uint32_t o = (rt >> 24) & 63, k = rt & 0xFFFFFFu;
+  const uint32_t blk = (p - a.own.first) / a.own.range;
+  return a.own.rreply[a.own.dbase[(size_t)blk * a.own.n + o] + k];
+}
+
+// Pass 2 for 64-byte slots: the same coalesced tiles as pass 1; routed
+// packets are rewritten with their answer (or queued as phase-B misses) and
+// every touch of the segment, pass 1's included, goes to the touch bins.
+struct RemPend {
+  uint32_t row;  // (no table rows: always kNone)
+  uint32_t kind, idx;
+};
+__global__ __launch_bounds__(256, 4) void nat_remote64(NatArgs a, uint32_t n_all,
+                                                      TouchBins bins) {
+  __shared__ uint4 stage[4][256];
+  __shared__ uint32_t cur[kCurs];
+  for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
+  __syncthreads();
+  frames64_tiles(
+      a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6], nullptr,
+      [&](uint32_t p, const RFrame &, uint32_t, uint32_t, bool mine) {
+        RemPend P{kNone, 0, kNone};
+        if (!mine) return P;
+        const uint32_t rt = a.own.route[p];
+        if (rt == kNone) return P;
+        if (!(rt & kRouteBit)) {
+          P.kind = 1;  // pass 1's own touch
+          P.idx = rt;
+        } else {
+          P.kind = 2;
+          P.idx = route_answer(a, p, rt);
+        }
+        return P;
+      },
+      [&](const RemPend &P, const uint4 *, uint32_t p, RFrame &f, uint32_t in,
+          uint32_t len, uint32_t &touch) -> uint32_t {
+        if (P.kind == 0) return 0u;
+        if (P.kind == 1) {
+          touch = P.idx;
+          return 0u;
+        }
+        if (P.idx == kNone) {  // a new flow (or not yet visible): phase B
+          a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
+          log_put(a.log, p, kNone);
+          return 0u;
+        }
+        log_put(a.log, p, P.idx);
+        touch = P.idx;
+        const uint32_t et = f.w[3] & 0xFFFF, ihl = (f.w[3] >> 16) & 0x0F;
+        const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
+        if (!(et == 0x0008 && ihl == 5 && tl <= 50)) {  // byte path, in place
+          nat_write_lan(a, p, P.idx);
+          return 0u;
+        }
+        nat_lan_fast(a, f, p, P.idx);
+        return (f.w[5] >> 24) == 6 ? 0xFu : 0x7u;
+      },
+      bins, TileQueue{}, cur);
+}
+
+// Pass 2, any slot size: routed packets only, one lane each (byte path).
+__global__ void nat_remote_lane(NatArgs a) {
+  for (uint32_t p = a.p0 + blockIdx.x * blockDim.x + threadIdx.x; p < a.p1;
+       p += gridDim.x * blockDim.x) {
+    const uint32_t rt = a.own.route[p];
+    if (rt == kNone || !(rt & kRouteBit)) continue;
+    const uint32_t idx = route_answer(a, p, rt);
+    a.log[p] = idx;
+    if (idx == kNone) {
+      a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
+      continue;
+    }
+    nat_write_lan(a, p, idx);
+  }
+}
+
 // ------------------------------------------------------------- phase C --
 __global__ void nat_defer_finish(NatArgs a, const uint32_t *list, uint32_t n) {
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
@@ -503,6 +789,142 @@ static inline int64_t nat_cutoff(const vp_ctx *c, int64_t t) {
   return (int64_t)((uint64_t)t - e);
 }
 
+template <class T>
+static int grow_dev(T **p, size_t *have, size_t count, hipStream_t s) {
+  if (count <= *have && *p) return 0;
+  VP_HIP(hipStreamSynchronize(s));
+  hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  VP_HIP(hipMalloc((void **)p, sizeof(T) * std::max<size_t>(count, 1)));
+  *have = count;
+  return 0;
+}
+
+// Phase A in owner mode: pass 1 classifies what this rank can
+// answer and routes the other LAN keys to their owners, the keys and answers
+// cross in two all-to-alls, pass 2 finishes the routed packets and bins every
+// touch, then the fold. On return h_ctl holds phase A's counts.
+struct PhaseA {
+  BinsPlan bp;
+  bool tiles64;
+  uint32_t grid1, range1;  // pass 1 layout (reprobe slices)
+  float ms;
+};
+
+static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
+                             const NowSpec &now, uint32_t p0, uint32_t p1,
+                             uint64_t seq0, PhaseA *ph) {
+  FlowTable &t = c->ft;
+  Workspace &w = c->ws;
+  Comm &m = *c->comm;
+  const uint32_t n = (uint32_t)m.n, r = (uint32_t)m.r;
+  const uint32_t np = p1 - p0;
+  ph->tiles64 = np && b->slot == 64 && c->coalesced_io;
+  uint32_t first;
+  if (ph->tiles64) {
+    first = p0 & ~63u;
+    const uint32_t tiles = (p1 - first + 63) / 64;
+    ph->grid1 = resident_grid((const void *)nat_classify64, (tiles + 3) / 4);
+    ph->range1 = (tiles + ph->grid1 - 1) / ph->grid1 * 64;
+    VP_TRY(tbl_bins_plan(c, t, (const void *)nat_remote64, p0, p1, &ph->bp));
+  } else {
+    first = p0;
+    ph->grid1 = std::max<uint32_t>(1, std::min<uint32_t>(2048, (np + 255) / 256));
+    ph->range1 = std::max<uint32_t>(1, (np + ph->grid1 - 1) / ph->grid1);
+  }
+  if (ph->range1 >= (1u << 24) - 1) return VP_ENOTSUP;
+  const size_t slices = (size_t)ph->grid1 * n;
+  VP_TRY(grow_dev(&w.desc, &w.desc_n, slices * ph->range1, c->stream));
+  VP_TRY(grow_dev(&w.dcnt, &w.dcnt_n, slices, c->stream));
+  VP_TRY(grow_dev(&w.dbase, &w.dbase_n, slices, c->stream));
+  VP_TRY(grow_dev(&w.dtot, &w.dtot_n, kMaxDest, c->stream));
+  VP_TRY(grow_dev(&w.route, &w.route_n, b->n, c->stream));
+  if (!w.h_tot) VP_HIP(hipHostMalloc((void **)&w.h_tot, 4 * kMaxDest, hipHostMallocDefault));
+  a.own = Route{n, r, w.desc, w.dcnt, w.route, nullptr, first, ph->range1, w.dbase,
+                nullptr};
+
+  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
+  VP_HIP(hipEventRecord(c->ev0, c->stream));
+  if (np) {
+    if (ph->tiles64) {
+      NatArgs a1 = a;
+      a1.tileq = 1;
+      if (ph->bp.on) a1.log = nullptr;  // pass 2 bins every touch
+      nat_classify64<<<ph->grid1, 256, 0, c->stream>>>(
+          a1, b->n, TouchBins{}, TileQueue{w.reprobe, w.reprobe_cnt, &t.ctl->reprobe_count});
+    } else {
+      nat_classify<<<ph->grid1, 256, 0, c->stream>>>(a);
+    }
+    VP_HIP(hipGetLastError());
+  } else {
+    VP_HIP(hipMemsetAsync(w.dcnt, 0, sizeof(uint32_t) * slices, c->stream));
+  }
+  VP_HIP(hipEventRecord(c->ev1, c->stream));
+  route_scan<<<n, 256, 0, c->stream>>>(w.dcnt, ph->grid1, n, w.dbase, w.dtot);
+  route_base<<<grid_for(slices), 256, 0, c->stream>>>(w.dbase, w.dtot, ph->grid1, n);
+  VP_HIP(hipGetLastError());
+  VP_HIP(hipMemcpyAsync(w.h_tot, w.dtot, 4ull * n, hipMemcpyDeviceToHost, c->stream));
+  VP_HIP(stream_wait(c->stream));
+  // C1 sizes: M[q * n + o] = keys rank q sends to owner o
+  std::vector<uint32_t> M((size_t)n * n);
+  VP_TRY(m.allgather_host(c, w.h_tot, M.data(), 4ull * n));
+  uint64_t S = 0, R = 0;
+  std::vector<size_t> sk(n), rk(n), sr(n), rr(n);
+  for (uint32_t q = 0; q < n; q++) {
+    S += M[(size_t)r * n + q];
+    R += M[(size_t)q * n + r];
+    sk[q] = 16ull * M[(size_t)r * n + q];
+    rk[q] = 16ull * M[(size_t)q * n + r];
+    sr[q] = 4ull * M[(size_t)q * n + r];  // answers go back the way keys came
+    rr[q] = 4ull * M[(size_t)r * n + q];
+  }
+  VP_TRY(grow_dev(&w.sendk, &w.sendk_n, S, c->stream));
+  VP_TRY(grow_dev(&w.rreply, &w.rreply_n, S, c->stream));
+  VP_TRY(grow_dev(&w.recvk, &w.recvk_n, R, c->stream));
+  VP_TRY(grow_dev(&w.reply, &w.reply_n, R, c->stream));
+  a.own.rreply = w.rreply;
+  route_pack<<<ph->grid1, 256, 0, c->stream>>>(w.desc, w.dcnt, w.dbase, n, ph->range1,
+                                               w.sendk);
+  VP_HIP(hipGetLastError());
+  VP_TRY(m.alltoallv_dev(c, w.sendk, sk.data(), w.recvk, rk.data()));
+  if (R) {
+    nat_own_probe<<<grid_for(R, 256, 4096), 256, 0, c->stream>>>(
+        tbl_dev(t), c->crc_tab, w.recvk, (uint32_t)R, w.reply);
+    VP_HIP(hipGetLastError());
+  }
+  VP_TRY(m.alltoallv_dev(c, w.reply, sr.data(), w.rreply, rr.data()));
+  VP_HIP(hipEventRecord(c->ev2, c->stream));
+  if (np) {
+    if (ph->tiles64) {
+      NatArgs a2 = a;
+      uint32_t grid2 = ph->bp.grid;
+      if (ph->bp.on) {
+        a2.log = nullptr;
+      } else {
+        const uint32_t tiles = (p1 - first + 63) / 64;
+        grid2 = resident_grid((const void *)nat_remote64, (tiles + 3) / 4);
+      }
+      nat_remote64<<<grid2, 256, 0, c->stream>>>(a2, b->n, ph->bp.bins);
+    } else {
+      nat_remote_lane<<<grid_for(np), 256, 0, c->stream>>>(a);
+    }
+    VP_HIP(hipGetLastError());
+  }
+  VP_HIP(hipEventRecord(c->ev3, c->stream));
+  VP_TRY(read_ctl_post(c, t));
+  if (ph->bp.on)
+    VP_TRY(tbl_bins_reduce(c, t, ph->bp, p0, now, seq0));
+  else
+    VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
+  VP_TRY(read_ctl_wait(c, t));
+  float k1 = 0.f, k2 = 0.f;
+  VP_HIP(hipEventElapsedTime(&k1, c->ev0, c->ev1));
+  VP_HIP(hipEventElapsedTime(&k2, c->ev2, c->ev3));
+  ph->ms = k1 + k2;
+  return 0;
+}
+
 static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
                        uint32_t p0, uint32_t p1, float *ms, int *launches,
                        uint32_t *allocated) {
@@ -534,13 +956,16 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.start_port = c->nat.start_port;
   a.n_dev = c->nat.n_devices;
 
+  const bool owner = c->shard_mode == VP_SHARD_OWNER && c->comm;
+  PhaseA ph{};
+  if (owner) VP_TRY(nat_phase_a_owner(c, b, a, now, p0, p1, seq0, &ph));
   // 64-byte slots: the classify launch also bins its touches (TouchBins)
   // and queues reprobes per block (TileQueue)
-  const bool tiles64 = p1 > p0 && b->slot == 64 && c->coalesced_io;
-  BinsPlan bp{};
-  uint32_t grid64 = 0, range64 = 0;
+  const bool tiles64 = owner ? ph.tiles64 : p1 > p0 && b->slot == 64 && c->coalesced_io;
+  BinsPlan bp = ph.bp;
+  uint32_t grid64 = ph.grid1, range64 = ph.range1;
   TileQueue rq{};
-  if (tiles64) {
+  if (tiles64 && !owner) {
     VP_TRY(tbl_bins_plan(c, t, (const void *)nat_classify64, p0, p1, &bp));
     const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
     grid64 = resident_grid((const void *)nat_classify64, (tiles + 3) / 4);
@@ -548,6 +973,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     rq = TileQueue{w.reprobe, w.reprobe_cnt, &t.ctl->reprobe_count};
     a.tileq = 1;
   }
+  if (!owner) {
   VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   if (p1 > p0) {
@@ -571,6 +997,9 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   else
     VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
   VP_TRY(read_ctl_wait(c, t));
+  VP_HIP(hipEventElapsedTime(&ph.ms, c->ev0, c->ev1));
+  }  // !owner
+  a.own.n = 0;  // below: this rank's own table only
   const uint32_t nre = t.h_ctl.reprobe_count;
   if (nre) {  // probes past a full home bucket: finish them, patch the fold
     const uint32_t *rcnt = tiles64 ? w.reprobe_cnt : nullptr;
@@ -585,11 +1014,9 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   }
   const bool ovf = bp.on && t.h_ctl.touch_ovf != 0;
   if (ovf)  // touches that found their bin slice full, logged alone
-    VP_TRY(tbl_late_touches(c, t, bp.bins.oent, bp.bins.ocnt, 0, range64, grid64,
+    VP_TRY(tbl_late_touches(c, t, bp.bins.oent, bp.bins.ocnt, 0, bp.range, bp.grid,
                             w.log, now, seq0));
-  float kms = 0.f;
-  VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
-  *ms += kms;
+  *ms += ph.ms;
   *launches += 1;
   const uint32_t nmiss = t.h_ctl.miss_count, ndefer = t.h_ctl.defer_count;
 
@@ -610,7 +1037,9 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   if (union_n) {
     if (c->comm) {  // every rank allocates the union in global packet order
       VP_TRY(union_exchange(c, nmiss, now));
+      if (owner) VP_TRY(tbl_owner_reserve(c, t, union_n));
       VP_TRY(tbl_new_keys(c, t, NewKeys{union_n, w.skey}, c->seq, nullptr));
+      a.t = tbl_dev(t);  // the buckets may have been rebuilt
       union_stamp<<<grid_for(union_n), 256, 0, c->stream>>>(
           w.first, w.assign, w.skey, w.unow, union_n, c->seq, t.ts, t.tseq);
       VP_HIP(hipGetLastError());

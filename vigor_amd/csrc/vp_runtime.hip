@@ -138,6 +138,8 @@ static int ctx_common(vp_ctx *c, int gpu) {
   VP_HIP(hipEventCreate(&c->ev0));
   VP_HIP(hipEventCreate(&c->ev1));
   VP_HIP(hipEventCreateWithFlags(&c->evc, hipEventDisableTiming));
+  VP_HIP(hipEventCreate(&c->ev2));
+  VP_HIP(hipEventCreate(&c->ev3));
   return 0;
 }
 
@@ -154,8 +156,10 @@ static void free_all(vp_ctx *c) {
                   w.d_out,   w.d_now,    c->crc_tab, c->macw,
                   c->st_bk,  c->st_val,  c->be_rec,   c->cht,   c->dmacw,
                   w.sbuf,    w.rbuf,     c->pol_size, c->pol_time,
-                  c->pol_cnt, c->pol_off};
+                  c->pol_cnt, c->pol_off, w.desc, w.dcnt, w.dbase, w.dtot,
+                  w.route,   w.sendk,    w.recvk,  w.reply,  w.rreply};
   for (void *p : ptrs) hipFree(p);
+  if (w.h_tot) hipHostFree(w.h_tot);
   if (w.h_frames) hipHostFree(w.h_frames);
   if (w.h_meta) hipHostFree(w.h_meta);
   for (int i = 0; i < 2; i++) {
@@ -168,6 +172,8 @@ static void free_all(vp_ctx *c) {
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->evc) hipEventDestroy(c->evc);
+  if (c->ev2) hipEventDestroy(c->ev2);
+  if (c->ev3) hipEventDestroy(c->ev3);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }

@@ -39,7 +39,19 @@ struct TableDev {
   uint64_t *birth;
   uint32_t *stack;
   Ctl *ctl;
+  uint4 *kv;               // owner mode: key by index (replicated); else null
+  uint32_t own_n, own_r;   // owner mode: ranks and this rank; own_n == 0 off
 };
+
+// slot_of[] in owner mode: allocated, but its key lives in another rank's
+// buckets (entry ids are (bucket << 2) | e, always below this value).
+constexpr uint32_t kElsewhere = 0xFFFFFFFCu;
+
+// Owner rank of a key hash: the top bits (multiply-shift, so any rank
+// count), independent of the home bucket's low bits.
+__host__ __device__ __forceinline__ uint32_t owner_of(uint32_t h, uint32_t n) {
+  return (uint32_t)(((uint64_t)h * n) >> 32);
+}
 
 struct NowSpec {
   const int64_t *arr;
@@ -125,6 +137,7 @@ __device__ __forceinline__ uint32_t tbl_probe(const TableDev &t, uint32_t h,
 
 // Key words of an allocated index's entry.
 __device__ __forceinline__ uint4 tbl_key_of(const TableDev &t, uint32_t idx) {
+  if (t.kv) return t.kv[idx];
   const uint32_t e = t.slot_of[idx];
   return reinterpret_cast<const uint4 *>(t.bk + (e >> 2))[e & 3];
 }
@@ -200,6 +213,13 @@ int tbl_expire(vp_ctx *c, FlowTable &t, int64_t cutoff, uint32_t *n_out);
 
 // Purge tombstones (rebuild) once live + erased entries pass 85 %.
 int tbl_check_tombs(vp_ctx *c, FlowTable &t);
+
+// Owner mode (rank r of n): a fresh table keeps only the keys it owns in its
+// buckets (sized for 1/n of the keys) and every key by index in kv.
+int tbl_set_owner(vp_ctx *c, FlowTable &t, uint32_t n, uint32_t r);
+// Owner mode: grow the buckets, if needed, before inserting the union of n
+// new keys whose hashes are in ws.mhash.
+int tbl_owner_reserve(vp_ctx *c, FlowTable &t, uint32_t n);
 
 // Per index: alloc flag, ts, key words.
 int tbl_dump(vp_ctx *c, FlowTable &t, uint8_t *alloc, int64_t *ts,

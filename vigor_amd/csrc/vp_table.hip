@@ -115,8 +115,8 @@ int read_ctl2(vp_ctx *c, FlowTable &a, FlowTable &b) {
 }
 
 TableDev tbl_dev(const FlowTable &t) {
-  return TableDev{t.bk, t.bmask, t.cap,   t.mix,   t.slot_of, t.hash_of,
-                  t.ts, t.tseq,  t.birth, t.stack, t.ctl};
+  return TableDev{t.bk,  t.bmask, t.cap,   t.mix, t.slot_of, t.hash_of, t.ts,
+                  t.tseq, t.birth, t.stack, t.ctl, t.kv,      t.own_n,   t.own_r};
 }
 
 template <class T>
@@ -126,7 +126,7 @@ static int dalloc(T **p, size_t count) {
   return e == hipSuccess ? 0 : hip_fail(e, "hipMalloc", __FILE__, __LINE__);
 }
 
-static int tbl_rebuild(vp_ctx *c, FlowTable &t);
+static int tbl_rebuild(vp_ctx *c, FlowTable &t, uint64_t nb_new = 0);
 
 static uint64_t tbl_entries(const FlowTable &t) {
   return (uint64_t)(t.bmask + 1) * kBucketEntries;
@@ -179,6 +179,7 @@ void tbl_free(FlowTable &t) {
                   t.ekey2, t.eidx,    t.eidx2};
   for (void *p : ptrs) hipFree(p);
   hipFree(t.ttotal);
+  hipFree(t.kv);
   if (t.h_pin) hipHostFree(t.h_pin);
   t = FlowTable{};
 }
@@ -260,7 +261,7 @@ __global__ void nk_alloc(NkArgs m) {
   const uint32_t stack_top = t.ctl->stack_top;
   const uint32_t fresh = t.ctl->fresh_next;
   const uint32_t free_total = stack_top + (t.cap - fresh);
-  uint32_t disp = 0;
+  uint32_t disp = 0, ins = 0;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m.n;
        j += gridDim.x * blockDim.x) {
     if (!m.first[j]) continue;
@@ -271,17 +272,28 @@ __global__ void nk_alloc(NkArgs m) {
     }
     const uint32_t idx =
         r < stack_top ? t.stack[stack_top - 1 - r] : fresh + (r - stack_top);
-    bool tomb = false;
-    const uint32_t e =
-        tbl_insert(t, m.mhash[j], m.mkey + 4 * (size_t)j, idx, &tomb, &disp);
-    if (tomb) atomicAdd(&t.ctl->tomb_reused, 1u);
+    const uint32_t *key = m.mkey + 4 * (size_t)j;
+    // owner mode: every rank allocates, only the key's owner inserts it
+    const bool mine = !t.own_n || owner_of(m.mhash[j], t.own_n) == t.own_r;
+    uint32_t e = kElsewhere;
+    if (mine) {
+      bool tomb = false;
+      e = tbl_insert(t, m.mhash[j], key, idx, &tomb, &disp);
+      if (tomb) atomicAdd(&t.ctl->tomb_reused, 1u);
+      ins++;
+    }
+    if (t.kv) t.kv[idx] = make_uint4(key[0], key[1], key[2], key[3]);
     t.slot_of[idx] = e;
     t.hash_of[idx] = m.mhash[j];
     t.birth[idx] = m.seq_base + m.pos[j];
     m.assign[j] = idx;
   }
-  for (uint32_t o = 32; o > 0; o >>= 1) disp += __shfl_xor(disp, o);
+  for (uint32_t o = 32; o > 0; o >>= 1) {
+    disp += __shfl_xor(disp, o);
+    ins += __shfl_xor(ins, o);
+  }
   if ((threadIdx.x & 63) == 0 && disp) atomicAdd(&t.ctl->disp_count, disp);
+  if ((threadIdx.x & 63) == 0 && ins) atomicAdd(&t.ctl->sh_live, ins);
 }
 
 __global__ void nk_commit(NkArgs m) {
@@ -559,8 +571,8 @@ constexpr uint32_t kBinLocalMax = 16384;  // in-bin indices held in LDS
 
 __global__ __launch_bounds__(1024) void touch_bins_reduce(
     const uint32_t *ent, const uint32_t *cnt, uint32_t nsrc, uint32_t cap,
-    uint32_t pbits, uint32_t range, uint32_t L, uint32_t tcap, uint32_t p0,
-    NowSpec now, uint64_t seq_base, uint64_t *ts, uint64_t *tseq) {
+    uint32_t pbits, uint32_t bbits, uint32_t range, uint32_t L, uint32_t tcap,
+    uint32_t p0, NowSpec now, uint64_t seq_base, uint64_t *ts, uint64_t *tseq) {
   __shared__ uint32_t last[kBinLocalMax];  // 1 + position in the launch, 0 = none
   const uint32_t bin = blockIdx.x;
   for (uint32_t i = threadIdx.x; i < L; i += blockDim.x) last[i] = 0;
@@ -572,14 +584,14 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
   // loaded by one instruction (lane l <-> slice w + l * nw)
   for (uint32_t r0 = threadIdx.x >> 6; r0 < nsrc; r0 += 64 * nw) {
     const uint32_t my = r0 + lane * nw;
-    const uint32_t nv = my < nsrc ? cnt[(size_t)my * kBins + bin] : 0;
+    const uint32_t nv = my < nsrc ? cnt[((size_t)my << bbits) + bin] : 0;
     for (uint32_t i = 0; i < 64; i += kU) {
       uint32_t n[kU], e[kU];
 #pragma unroll
       for (uint32_t u = 0; u < kU; u++) {
         n[u] = __shfl(nv, i + u);
         const uint32_t sb = r0 + (i + u) * nw;
-        e[u] = lane < n[u] ? ent[((size_t)sb * kBins + bin) * cap + lane] : 0;
+        e[u] = lane < n[u] ? ent[(((size_t)sb << bbits) + bin) * cap + lane] : 0;
       }
 #pragma unroll
       for (uint32_t u = 0; u < kU; u++) {
@@ -588,7 +600,7 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
           atomicMax(&last[e[u] >> pbits], sb * range + (e[u] & pmask) + 1);
         for (uint32_t k = 64; k < n[u]; k += 64) {  // slices longer than 64
           if (k + lane < n[u]) {
-            const uint32_t x = ent[((size_t)sb * kBins + bin) * cap + k + lane];
+            const uint32_t x = ent[(((size_t)sb << bbits) + bin) * cap + k + lane];
             atomicMax(&last[x >> pbits], sb * range + (x & pmask) + 1);
           }
         }
@@ -598,7 +610,7 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
   __syncthreads();
   for (uint32_t l = threadIdx.x; l < L; l += blockDim.x) {
     const uint32_t v = last[l];
-    const uint32_t i = bin_index(bin, l);
+    const uint32_t i = bin_index(bin, l, bbits);
     if (!v || i >= tcap) continue;
     const uint32_t p = p0 + v - 1;
     ts[i] = (uint64_t)now.at(p);
@@ -622,12 +634,18 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   const uint32_t grid = resident_grid(kernel, (tiles + 3) / 4);
   const uint32_t per_b = (tiles + grid - 1) / grid;
   const uint32_t range = per_b * 64;
-  const uint32_t L = ((t.cap + 4095) >> 12) << 4;
+  // the fewest bins (>= 256) whose in-bin index range fits the fold's LDS
+  uint32_t bbits = 8;
+  while (bbits < 10 && (((uint64_t)t.cap + (16ull << bbits) - 1) >> (4 + bbits)) << 4 >
+                           kBinLocalMax)
+    bbits++;
+  const uint32_t nbins = 1u << bbits;
+  const uint32_t L = (uint32_t)((((uint64_t)t.cap + (16ull << bbits) - 1) >> (4 + bbits)) << 4);
   const uint32_t pbits = std::max<uint32_t>(1, ceil_log2(range));
   if (L > kBinLocalMax || ceil_log2(L) + pbits > 32) return 0;
   // twice a uniform share of a block's packets per bin, in 64-entry lines
-  const uint32_t cap = ((2 * range / kBins + 32) + 15) & ~15u;
-  const size_t ne = (size_t)grid * kBins * cap, nc = (size_t)grid * kBins;
+  const uint32_t cap = ((2 * range / nbins + 32) + 15) & ~15u;
+  const size_t ne = (size_t)grid * nbins * cap, nc = (size_t)grid * nbins;
   if (ne > w.bins_ent_n) {
     VP_HIP(hipStreamSynchronize(c->stream));
     hipFree(w.bins_ent);
@@ -649,15 +667,15 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   plan->range = range;
   plan->L = L;
   plan->bins = TouchBins{w.bins_ent, w.bins_cnt, &t.ctl->touch_ovf, w.ovf_q,
-                         w.ovf_cnt, w.log, cap, pbits};
+                         w.ovf_cnt, w.log, cap, pbits, bbits};
   return 0;
 }
 
 int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
                     const NowSpec &now, uint64_t seq_base) {
-  touch_bins_reduce<<<kBins, 1024, 0, c->stream>>>(
+  touch_bins_reduce<<<1u << plan.bins.bbits, 1024, 0, c->stream>>>(
       plan.bins.ent, plan.bins.cnt, plan.grid, plan.bins.cap, plan.bins.pbits,
-      plan.range, plan.L, t.cap, p0, now, seq_base, t.ts, t.tseq);
+      plan.bins.bbits, plan.range, plan.L, t.cap, p0, now, seq_base, t.ts, t.tseq);
   VP_HIP(hipGetLastError());
   return 0;
 }
@@ -767,6 +785,7 @@ __global__ void exp_gather_ts(const uint32_t *eidx, uint32_t n, const uint64_t *
 
 // Free in LRU order: the oldest is pushed first, so the youngest expired
 // index ends on top (double-chain-impl.c:1968-1981); erase the keys.
+// (Owner mode: every rank frees the index; only the key's owner erases it.)
 __global__ void exp_apply(TableDev t, const uint32_t *eidx, uint32_t n) {
   const uint32_t top = t.ctl->stack_top;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
@@ -774,24 +793,28 @@ __global__ void exp_apply(TableDev t, const uint32_t *eidx, uint32_t n) {
     const uint32_t idx = eidx[j];
     const uint32_t e = t.slot_of[idx];
     t.stack[top + j] = idx;
-    t.bk[e >> 2].idx[e & 3] = kTomb;
+    const bool own = e < kElsewhere;
+    if (own) t.bk[e >> 2].idx[e & 3] = kTomb;
     t.slot_of[idx] = kNone;
+    const uint32_t k = wave_append(&t.ctl->n_tomb, own);
+    (void)k;
   }
 }
 
-__global__ void exp_commit(Ctl *ctl, uint32_t n) {
+__global__ void exp_commit(Ctl *ctl, uint32_t n, uint32_t n_tomb_before) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     ctl->stack_top += n;
     ctl->n_live -= n;
-    ctl->n_tomb += n;
+    ctl->sh_live -= ctl->n_tomb - n_tomb_before;  // this rank's erasures
   }
 }
 
-// Rebuild (tombstone purge): keys of live indices out, clear, re-insert.
+// Rebuild (tombstone purge, layout change or growth): keys of this rank's
+// live indices out, clear, re-insert.
 __global__ void rb_collect(TableDev t, uint32_t *keys) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.cap;
        i += gridDim.x * blockDim.x) {
-    if (t.slot_of[i] == kNone) continue;
+    if (t.slot_of[i] >= kElsewhere) continue;
     const uint4 k = tbl_key_of(t, i);
     reinterpret_cast<uint4 *>(keys)[i] = k;
   }
@@ -799,17 +822,27 @@ __global__ void rb_collect(TableDev t, uint32_t *keys) {
 __global__ void rb_insert(TableDev t, const uint32_t *keys) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.cap;
        i += gridDim.x * blockDim.x) {
-    if (t.slot_of[i] == kNone) continue;
+    if (t.slot_of[i] >= kElsewhere) continue;
     bool tomb = false;
     uint32_t disp = 0;
     t.slot_of[i] = tbl_insert(t, t.hash_of[i], keys + 4 * (size_t)i, i, &tomb, &disp);
   }
 }
 
-static int tbl_rebuild(vp_ctx *c, FlowTable &t) {
-  uint32_t *keys = nullptr;
-  VP_TRY(dalloc(&keys, 4ull * t.cap));
-  rb_collect<<<grid_for(t.cap), 256, 0, c->stream>>>(tbl_dev(t), keys);
+// nb_new: bucket count afterwards (0 = unchanged).
+static int tbl_rebuild(vp_ctx *c, FlowTable &t, uint64_t nb_new) {
+  uint32_t *keys = reinterpret_cast<uint32_t *>(t.kv);  // owner mode: kv has them
+  if (!keys) {
+    VP_TRY(dalloc(&keys, 4ull * t.cap));
+    rb_collect<<<grid_for(t.cap), 256, 0, c->stream>>>(tbl_dev(t), keys);
+  }
+  if (nb_new && nb_new != (uint64_t)t.bmask + 1) {
+    VP_HIP(hipStreamSynchronize(c->stream));
+    VP_HIP(hipFree(t.bk));
+    t.bk = nullptr;
+    VP_TRY(dalloc(&t.bk, nb_new));
+    t.bmask = (uint32_t)(nb_new - 1);
+  }
   VP_HIP(hipMemsetAsync(t.bk, 0xFF, sizeof(Bucket) * ((size_t)t.bmask + 1),
                         c->stream));
   rb_insert<<<grid_for(t.cap), 256, 0, c->stream>>>(tbl_dev(t), keys);
@@ -817,8 +850,44 @@ static int tbl_rebuild(vp_ctx *c, FlowTable &t) {
   VP_HIP(hipMemsetAsync(&t.ctl->disp_count, 0, 4, c->stream));
   t.ins_since = 0;
   VP_HIP(hipStreamSynchronize(c->stream));
-  VP_HIP(hipFree(keys));
+  if (!t.kv) VP_HIP(hipFree(keys));
   return 0;
+}
+
+int tbl_set_owner(vp_ctx *c, FlowTable &t, uint32_t n, uint32_t r) {
+  // a fresh table: keys by index replicated, buckets sized for this rank's
+  // share (grown on demand, tbl_owner_reserve)
+  VP_TRY(dalloc(&t.kv, t.cap));
+  t.own_n = n;
+  t.own_r = r;
+  uint64_t nb = 64;
+  while (nb * n < t.cap) nb <<= 1;
+  return tbl_rebuild(c, t, nb);
+}
+
+// Owner mode, before inserting a union of n keys (hashes in mhash): grow
+// this rank's buckets so its keys stay at load <= 1/3 (one bucket per key).
+__global__ void own_count(const uint32_t *mhash, uint32_t n, uint32_t own_n,
+                          uint32_t own_r, Ctl *ctl) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += gridDim.x * blockDim.x) {
+    const uint32_t k = wave_append(&ctl->own_new, owner_of(mhash[j], own_n) == own_r);
+    (void)k;
+  }
+}
+
+int tbl_owner_reserve(vp_ctx *c, FlowTable &t, uint32_t n) {
+  if (!t.own_n || !n) return 0;
+  VP_HIP(hipMemsetAsync(&t.ctl->own_new, 0, 4, c->stream));
+  own_count<<<grid_for(n), 256, 0, c->stream>>>(c->ws.mhash, n, t.own_n, t.own_r,
+                                                t.ctl);
+  VP_HIP(hipGetLastError());
+  VP_TRY(read_ctl(c, t));
+  const uint64_t need = (uint64_t)t.h_ctl.sh_live + t.h_ctl.n_tomb + t.h_ctl.own_new;
+  if (need <= (uint64_t)t.bmask + 1) return 0;
+  uint64_t nb = (uint64_t)t.bmask + 1;
+  while (nb < need) nb <<= 1;
+  return tbl_rebuild(c, t, nb);
 }
 
 int tbl_expire(vp_ctx *c, FlowTable &t, int64_t cutoff, uint32_t *n_out) {
@@ -843,14 +912,14 @@ int tbl_expire(vp_ctx *c, FlowTable &t, int64_t cutoff, uint32_t *n_out) {
                                             t.ekey, t.ekey2, t.eidx2, t.eidx,
                                             (int)k, 0, 64, c->stream));
   exp_apply<<<grid_for(k), 256, 0, c->stream>>>(tbl_dev(t), t.eidx, k);
-  exp_commit<<<1, 64, 0, c->stream>>>(t.ctl, k);
+  exp_commit<<<1, 64, 0, c->stream>>>(t.ctl, k, t.h_ctl.n_tomb);
   VP_HIP(hipGetLastError());
   return tbl_check_tombs(c, t);
 }
 
 int tbl_check_tombs(vp_ctx *c, FlowTable &t) {
   VP_TRY(read_ctl(c, t));
-  if ((uint64_t)t.h_ctl.n_tomb + t.h_ctl.n_live > tbl_entries(t) * 85 / 100)
+  if ((uint64_t)t.h_ctl.n_tomb + t.h_ctl.sh_live > tbl_entries(t) * 85 / 100)
     return tbl_rebuild(c, t);
   return 0;
 }

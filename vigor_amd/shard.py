@@ -18,7 +18,10 @@ import traceback
 
 import numpy as np
 
-from . import ALLGATHER_FN, ALLREDUCE_FN, CommOpsC, _check, lib
+from . import (ALLGATHER_FN, ALLREDUCE_FN, ALLTOALLV_FN, SHARD_OWNER,
+               SHARD_REPLICATED, CommOpsC, _check, lib)
+
+MODES = {"replicated": SHARD_REPLICATED, "owner": SHARD_OWNER}
 
 
 def slice_bounds(sizes):
@@ -44,8 +47,9 @@ class TorchComm:
         self.world = dist.get_world_size(group)
         self._ag = ALLGATHER_FN(self._allgather)
         self._ar = ALLREDUCE_FN(self._allreduce)
+        self._a2a = ALLTOALLV_FN(self._alltoallv)
         self.ops = CommOpsC(user=None, allgather=self._ag,
-                            allreduce_max_u64=self._ar)
+                            allreduce_max_u64=self._ar, alltoallv=self._a2a)
 
     def allgather_bytes(self, data: bytes) -> list:
         import torch
@@ -73,6 +77,24 @@ class TorchComm:
             traceback.print_exc(file=sys.stderr)
             return 1
 
+    def _alltoallv(self, user, send, send_bytes, recv, recv_bytes):
+        try:
+            import torch
+            sb = [int(send_bytes[q]) for q in range(self.world)]
+            rb = [int(recv_bytes[q]) for q in range(self.world)]
+
+            def view(addr, n):
+                if n == 0:
+                    return torch.empty(0, dtype=torch.uint8)
+                return torch.from_numpy(np.ctypeslib.as_array(
+                    (C.c_uint8 * n).from_address(addr)))
+            self.dist.all_to_all_single(view(recv, sum(rb)), view(send, sum(sb)),
+                                        rb, sb, group=self.group)
+            return 0
+        except Exception:
+            traceback.print_exc(file=sys.stderr)
+            return 1
+
     def _allreduce(self, user, buf, count):
         try:
             if count == 0:
@@ -93,7 +115,14 @@ def rccl_unique_id() -> bytes:
     return bytes(buf)
 
 
-def attach_rccl(nf, rank: int, world: int, group=None):
+def set_mode(nf, mode: str):
+    """Dictionary placement (vp_shard_mode): "replicated" (every rank holds
+    every key) or "owner" (keys sharded by flow hash, LAN lookups of other
+    ranks' keys through an all-to-all)."""
+    _check(nf.L.vp_shard_mode(nf.h, MODES[mode]), "vp_shard_mode")
+
+
+def attach_rccl(nf, rank: int, world: int, group=None, mode: str = "replicated"):
     """RCCL communicator for `nf` (collective over the torch.distributed
     group): rank 0's id is broadcast with torch.distributed."""
     import torch.distributed as dist
@@ -101,13 +130,16 @@ def attach_rccl(nf, rank: int, world: int, group=None):
     dist.broadcast_object_list(obj, src=0, group=group)
     buf = (C.c_uint8 * 128).from_buffer_copy(obj[0])
     _check(nf.L.vp_attach_rccl(nf.h, buf, world, rank), "vp_attach_rccl")
+    set_mode(nf, mode)
 
 
-def attach_torch(nf, rank: int, world: int, group=None) -> TorchComm:
+def attach_torch(nf, rank: int, world: int, group=None,
+                 mode: str = "replicated") -> TorchComm:
     """Host-callback communicator over torch.distributed; keep the returned
     object alive as long as `nf`."""
     comm = TorchComm(group)
     _check(nf.L.vp_attach_comm(nf.h, C.byref(comm.ops), world, rank),
            "vp_attach_comm")
     nf._comm = comm
+    set_mode(nf, mode)
     return comm
