@@ -13,11 +13,15 @@ rate is reported as new_flow_mpps).
 
 N > 1 (torch.distributed, one rank per GPU; BASELINE configs[4]): ONE vignat
 over all GPUs with 16M flows; every global batch is N x B packets and rank r
-ingests its contiguous slice r (B packets, weak scaling). The ranks keep a
-replicated dictionary; new flows are all-gathered over RCCL so every rank
-allocates identically; results equal one nf.c over the concatenated batch
-(tests/test_shard_gpu.py). value = all ranks' packets /
-max-over-ranks time.
+ingests its contiguous slice r (B packets, weak scaling). By default the
+flow dictionary is sharded by flow hash (--shard-mode owner, north_star):
+LAN packets whose key another GPU owns are looked up there through an RCCL
+all-to-all of 16-byte keys and 4-byte answers over xGMI; new flows are
+all-gathered so every rank allocates identically (--shard-mode replicated
+keeps a whole dictionary per GPU instead). Results equal one nf.c over the
+concatenated batch (tests/test_shard_gpu.py). value = all
+ranks' packets / max-over-ranks time. `--gpus N` without a torch.distributed
+environment starts the N ranks itself.
 
 Also reported:
   roofline      algorithmic HBM-read bytes per packet (92 B)
@@ -168,6 +172,9 @@ def main():
                     help="default: 1M (config 2) on one GPU, 16M (config 5) "
                          "over N > 1 GPUs")
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
+    ap.add_argument("--shard-mode", choices=("owner", "replicated"), default="owner",
+                    help="N > 1: flow dictionary sharded by flow hash (owner) "
+                         "or replicated on every GPU")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -200,9 +207,9 @@ def main():
     if world > 1:  # one vignat over all ranks
         from vigor_amd import shard
         if host_comm:
-            shard.attach_torch(nat, rank, world)
+            shard.attach_torch(nat, rank, world, mode=args.shard_mode)
         else:
-            shard.attach_rccl(nat, rank, world)
+            shard.attach_rccl(nat, rank, world, mode=args.shard_mode)
     bank = FlowBank(args.flows, 0, dev)
     B = args.batch
     lens = torch.full((B,), 60, dtype=torch.int16, device=dev)
@@ -284,10 +291,13 @@ def main():
         workload = ("vignat 64B, 1M flows, 1xMI355X (parse+hash+map-probe "
                     "kernel, checksum rewrite)")
     elif world > 1:
+        how = ("flow-hash sharded dictionary: keys owned by another GPU "
+               "looked up through an all-to-all over %s" if args.shard_mode == "owner"
+               else "replicated dictionary") % ("gloo (host)" if host_comm else
+                                                 "RCCL/xGMI")
         workload = ("vignat 64B, %d flows, %dxMI355X: one NF over all GPUs, "
                     "each ingesting a contiguous 1/%d of every global batch "
-                    "(replicated dictionary, new flows all-gathered over "
-                    "RCCL)" % (args.flows, world, world))
+                    "(%s; new flows all-gathered)" % (args.flows, world, world, how))
     else:
         workload = "vignat 64B, %d flows, 1xMI355X" % args.flows
     if rank == 0:
@@ -314,8 +324,8 @@ def main():
                        "batch_packets_per_gpu": B,
                        "global_batch_packets": B * world,
                        "frame_bytes": 60, "slot_bytes": SLOT,
-                       "parallelism": "shard%d" % world if world > 1
-                       else "single"},
+                       "parallelism": ("%s%d" % (args.shard_mode, world))
+                       if world > 1 else "single"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -324,7 +334,9 @@ def main():
                                            "WRITE_SIZE) per launch / this "
                                            "run's kernel time" % TRAFFIC_PROFILE
                                            if traffic else None,
-                         "kernel": "nat_classify64",
+                         "kernel": "nat_classify64" if world == 1 or
+                                   args.shard_mode == "replicated"
+                                   else "nat_classify64+nat_remote64",
                          "kernel_ms_per_launch": round(per_launch_s * 1e3, 4),
                          "alg_bytes_per_packet": ALG_BYTES,
                          "kernel_mpps": round(pkts_per_launch / per_launch_s
