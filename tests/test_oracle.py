@@ -94,16 +94,28 @@ def test_appendix_a_reverse_path(ref):
     # reply: 8.8.8.8:53 -> 0.0.0.0, dst port bytes 05 00 -> index 5
     r = _udp(T.ip4(8, 8, 8, 8), 0, 53, 0x0500)
     assert o.process(1, r, 60, 64, t + 20) == 0
-    # SURVEY.md prints UDP checksum e51b for this reply; its probe frame
-    # carried a non-zero payload byte. With the 18 B zero payload used here
-    # the RFC 768 checksum of those exact header bytes is e520 (checked
-    # independently below); every other byte matches the KAT.
     assert r[:40].hex() == ("012345678900020304050607" "0800"
                             "4500002e00000000401160ab" "08080808" "0a000005"
                             "0035" "0050" "001a")
+    # SURVEY.md prints only the first 42 bytes of its probe frame and UDP
+    # checksum e51b. With the 18 B zero payload used here the checksum of
+    # these header bytes is e520 (also by an independent RFC 768 sum). The
+    # two differ by 0x0500 in the sum, i.e. exactly one payload byte 0x05 at
+    # an odd L4 offset: the same reply with payload 00 05 00 ... gives e51b
+    # from both the oracle and the RFC 768 sum, so the printed KAT holds for
+    # a probe frame with that payload.
     assert r[40:42].hex() == "%04x" % _rfc768(bytes(r[26:30]), bytes(r[30:34]),
                                                bytes(r[34:60]))
     assert r[40:42].hex() == "e520"
+    o2 = kat_nat(ref)
+    for i in range(5):
+        o2.process(0, _udp(T.ip4(10, 0, 0, 100 + i), 0, 1, 1), 60, 64, t + i)
+    o2.process(0, _udp(T.ip4(10, 0, 0, 5), T.ip4(8, 8, 8, 8), 80, 53), 60, 64, t + 10)
+    rp = _udp(T.ip4(8, 8, 8, 8), 0, 53, 0x0500)
+    rp[43] = 0x05  # L4 offset 9: the second payload byte
+    assert o2.process(1, rp, 60, 64, t + 20) == 0
+    assert rp[40:42].hex() == "e51b"
+    assert "%04x" % _rfc768(bytes(rp[26:30]), bytes(rp[30:34]), bytes(rp[34:60])) == "e51b"
     # dst port bytes 00 05 -> index 0x0500 = 1280, not allocated -> drop
     r2 = _udp(T.ip4(8, 8, 8, 8), 0, 53, 0x0005)
     before = bytes(r2)
