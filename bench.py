@@ -136,6 +136,36 @@ def golden_batch_digest(flows: int, batch: int):
         return int(z["batch_digest"][-1])
 
 
+E2E_BATCH = 1 << 24
+E2E_CHUNK = 1 << 22
+
+
+def end_to_end(nat, bank, dev, start: int, steps: int = 3):
+    """The path's real ends (SURVEY.md §8(d) "End-to-end"; nf.c:153,166):
+    frames start and end in page-locked host memory (a registered mbuf
+    pool), vp_process_host moves them over PCIe in E2E_CHUNK-packet chunks on
+    a copy stream beside the compute stream (double buffered). Every flow is
+    already warm. Returns Mpps over `steps` host batches of E2E_BATCH."""
+    os.environ["VIGPATH_HOST_CHUNK"] = str(E2E_CHUNK)
+    B = E2E_BATCH
+    lens = np.full(B, 60, np.uint16)
+    ind = np.zeros(B, np.uint16)
+    d = torch.empty(B * SLOT, dtype=torch.uint8, device=dev)
+    bufs, nows = [], []
+    for k in range(steps):
+        bank.fill(d, start + k * B)
+        bufs.append(d.cpu().pin_memory().numpy())
+        nows.append(T.NOW0 + start + k * B + np.arange(B, dtype=np.int64))
+    del d
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        out = nat.process_host(bufs[k], lens, ind, nows[k], SLOT)
+    el = time.perf_counter() - t0
+    assert (out == 1).all()
+    return B * steps / el / 1e6
+
+
 def launch_ranks(n: int) -> int:
     """--gpus N > 1 without a torch.distributed environment: start one rank
     per GPU as child processes (torch.distributed.run), before anything here
@@ -176,6 +206,8 @@ def main():
                     help="N > 1: flow dictionary sharded by flow hash (owner) "
                          "or replicated on every GPU")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the host-resident end-to-end rate")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -300,6 +332,15 @@ def main():
                     "(%s; new flows all-gathered)" % (args.flows, world, world, how))
     else:
         workload = "vignat 64B, %d flows, 1xMI355X" % args.flows
+    e2e = None
+    if world == 1 and not args.no_e2e:
+        e2e = {"value": round(end_to_end(nat, bank, dev, gstart(args.warmup + args.steps)), 1),
+               "unit": "Mpps",
+               "path": "page-locked host frames -> hipMemcpyAsync H2D -> process -> "
+                       "D2H, %d-packet chunks double-buffered on a copy stream "
+                       "(vp_process_host)" % E2E_CHUNK,
+               "batch_packets": E2E_BATCH,
+               "pcie_bytes_per_packet": SLOT + 12 + SLOT + 2}
     if rank == 0:
         cpu = None
         if not args.no_cpu and world == 1:
@@ -344,6 +385,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "new_flow_mpps": round(new_flow_mpps, 2) if new_flow_mpps else None,
+            "end_to_end": e2e,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -39,16 +39,16 @@ for step in "$@"; do
     bench) run bench 600 python3 bench.py $BA > $O/${TAG}_bench.log 2>&1 || exit $? ;;
     trace) rm -rf $O/${TAG}_kt
            run trace 400 rocprofv3 --kernel-trace --stats --output-format csv \
-             -d $O/${TAG}_kt -- python3 bench.py --steps 10 --warmup 2 --no-cpu $BA \
+             -d $O/${TAG}_kt -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-e2e $BA \
              > $O/${TAG}_kt.log 2>&1 || exit $? ;;
     pmc) rm -rf $O/${TAG}_fetch $O/${TAG}_write
          run pmc_fetch 180 rocprofv3 --pmc FETCH_SIZE --output-format csv \
-           -d $O/${TAG}_fetch -- python3 bench.py --steps 5 --warmup 2 --no-cpu $BA \
+           -d $O/${TAG}_fetch -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-e2e $BA \
            > $O/${TAG}_fetch.log 2>&1 || exit $?
          run pmc_write 180 rocprofv3 --pmc WRITE_SIZE --output-format csv \
-           -d $O/${TAG}_write -- python3 bench.py --steps 5 --warmup 2 --no-cpu $BA \
+           -d $O/${TAG}_write -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-e2e $BA \
            > $O/${TAG}_write.log 2>&1 || exit $? ;;
-    shard2) VIGPATH_COMM=host run shard2 600 python3 bench.py --gpus 2 --no-cpu $BA \
+    shard2) VIGPATH_COMM=host run shard2 600 python3 bench.py --gpus 2 --no-cpu --no-e2e $BA \
              > $O/${TAG}_shard2.log 2>&1 || exit $? ;;
     e2e) run e2e 600 python3 tools/bench_e2e.py > $O/${TAG}_e2e.log 2>&1 || exit $? ;;
     nf) run nf 900 python3 tools/bench_nf.py > $O/${TAG}_nf.log 2>&1 || exit $? ;;
