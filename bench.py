@@ -323,10 +323,10 @@ def main():
         workload = ("vignat 64B, 1M flows, 1xMI355X (parse+hash+map-probe "
                     "kernel, checksum rewrite)")
     elif world > 1:
-        how = ("flow-hash sharded dictionary: keys owned by another GPU "
-               "looked up through an all-to-all over %s" if args.shard_mode == "owner"
-               else "replicated dictionary") % ("gloo (host)" if host_comm else
-                                                 "RCCL/xGMI")
+        via = "gloo (host)" if host_comm else "RCCL/xGMI"
+        how = ("flow-hash sharded dictionary: keys owned by another GPU looked up "
+               "through an all-to-all over %s" % via if args.shard_mode == "owner"
+               else "replicated dictionary over %s" % via)
         workload = ("vignat 64B, %d flows, %dxMI355X: one NF over all GPUs, "
                     "each ingesting a contiguous 1/%d of every global batch "
                     "(%s; new flows all-gathered)" % (args.flows, world, world, how))

@@ -32,8 +32,9 @@ for step in "$@"; do
   case $step in
     tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 200 \
              --timeout-method thread > $O/${TAG}_pytest.log 2>&1 || exit $? ;;
-    test:*) run "$step" 600 python -u -m pytest tests -m gpu -x -v --timeout 200 \
-             --timeout-method thread -k "${step#test:}" > $O/${TAG}_pytest_k.log 2>&1 || exit $? ;;
+    test:*) k=${step#test:}
+            run "$step" 600 python -u -m pytest tests -m gpu -x -v --timeout 200 \
+             --timeout-method thread -k "$k" > $O/${TAG}_pytest_${k//[^A-Za-z0-9]/_}.log 2>&1 || exit $? ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" \
              > $O/${TAG}_smoke.log 2>&1 || exit $? ;;
     bench) run bench 600 python3 bench.py $BA > $O/${TAG}_bench.log 2>&1 || exit $? ;;
