@@ -234,7 +234,7 @@ static int bridge_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.st = TableDev{};
   a.st.bk = c->st_bk;
   a.st.bmask = c->st_bmask;
-  a.st.mix = 1;
+  a.st.mix = kMixMul;
   a.st_val = c->st_val;
   a.n_static = c->n_static;
   a.crc_tab = c->crc_tab;
@@ -318,7 +318,7 @@ int bridge_static_build(const vp_bridge_config *cfg, std::vector<Bucket> &bk,
     const uint32_t h = S[0 * 256 + (eh & 0xFF)] ^ S[1 * 256 + ((eh >> 8) & 0xFF)] ^
                        S[2 * 256 + ((eh >> 16) & 0xFF)] ^ S[3 * 256 + (eh >> 24)] ^
                        S[4 * 256 + (dev & 0xFF)] ^ S[5 * 256 + (dev >> 8)];
-    uint32_t b = home_bucket(h, *bmask, 1);
+    uint32_t b = home_bucket(h, *bmask, kMixMul);
     bool placed = false;
     while (!placed) {
       for (uint32_t e = 0; e < kBucketEntries && !placed; e++) {

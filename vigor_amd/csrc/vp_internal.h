@@ -63,6 +63,7 @@ struct FlowTable {
   uint32_t cap = 0;
   uint32_t mix = 0;    // home-bucket mode (vp_table.h home_bucket)
   uint64_t ins_since = 0;  // inserts since the last rebuild (mode check)
+  uint32_t layout_tries = 0;  // tbl_choose_layout calls so far
   uint32_t *slot_of = nullptr;
   uint32_t *hash_of = nullptr;
   uint64_t *ts = nullptr;

@@ -61,19 +61,24 @@ struct NowSpec {
   }
 };
 
-// Home bucket of a key hash. Mode 0 masks the CRC like the reference
-// (hash & (cap-1), map-impl-pow2.c:15-27): CRC32C is GF(2)-linear, so keys
-// that differ in a few low bits (sequential ports/addresses, the benchmark's
-// flows) land on a structured, well-spread set of buckets, which the memory
-// system serves faster than random lines. For some key sets the masked bits
-// lose rank and buckets cluster; the table detects long insert probes and
-// rebuilds in mode 1 (multiplicative spread). Only the key -> index mapping
-// is observable, so either layout gives identical results.
+// Home bucket of a key hash. Modes 0-31 take the CRC's bits from bit `mix`
+// on (a rotation, then the reference's mask: mode 0 is hash & (cap-1),
+// map-impl-pow2.c:15-27). CRC32C is GF(2)-linear, so keys that differ in a
+// few low bits (sequential ports/addresses, the benchmark's flows) land on a
+// structured, well-spread set of buckets, which the memory system serves
+// faster than random lines -- when the selected bits have full rank over the
+// key set. For some key sets they lose rank and buckets cluster; the table
+// detects long insert probes, scores every rotation over its live keys and
+// rebuilds with the best one, or with the multiplicative spread (kMixMul)
+// when none is clean (tbl_choose_layout). Only the key -> index mapping is
+// observable, so every layout gives identical results.
+constexpr uint32_t kMixMul = 32;
 __host__ __device__ __forceinline__ uint32_t home_bucket(uint32_t h,
                                                          uint32_t bmask,
                                                          uint32_t mix) {
-  return mix ? (uint32_t)(((uint64_t)(h * 0x9E3779B1u) * (bmask + 1ull)) >> 32)
-             : (h & bmask);
+  if (mix >= kMixMul)
+    return (uint32_t)(((uint64_t)(h * 0x9E3779B1u) * (bmask + 1ull)) >> 32);
+  return ((h >> mix) | (h << ((32 - mix) & 31))) & bmask;
 }
 
 // One bucket (key words k0-k2, entry indices ix) against `key`, entries in

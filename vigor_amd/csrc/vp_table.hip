@@ -127,6 +127,7 @@ static int dalloc(T **p, size_t count) {
 }
 
 static int tbl_rebuild(vp_ctx *c, FlowTable &t, uint64_t nb_new = 0);
+static int tbl_choose_layout(vp_ctx *c, FlowTable &t);
 
 static uint64_t tbl_entries(const FlowTable &t) {
   return (uint64_t)(t.bmask + 1) * kBucketEntries;
@@ -146,8 +147,8 @@ int tbl_alloc(vp_ctx *c, FlowTable &t, uint32_t cap) {
   }
   t.bmask = (uint32_t)(nb - 1);
   t.cap = cap;
-  const char *mix = getenv("VIGPATH_MIX");  // diagnostics: start in mode 1
-  t.mix = mix && atoi(mix) ? 1 : 0;
+  const char *mix = getenv("VIGPATH_MIX");  // diagnostics: start multiplicative
+  t.mix = mix && atoi(mix) ? kMixMul : 0;
   VP_TRY(dalloc(&t.bk, nb));
   VP_TRY(dalloc(&t.slot_of, cap));
   VP_TRY(dalloc(&t.hash_of, cap));
@@ -232,7 +233,7 @@ __global__ void nk_dedup(NkArgs m) {
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m.n;
        j += gridDim.x * blockDim.x) {
     const uint32_t *kj = m.mkey + 4 * (size_t)j;
-    uint32_t s = home_bucket(m.mhash[j], m.smask, 1);
+    uint32_t s = home_bucket(m.mhash[j], m.smask, kMixMul);
     for (;;) {
       uint32_t old = atomicCAS(&m.scratch[s], kEmpty, j);
       if (old == kEmpty) break;
@@ -347,17 +348,68 @@ int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
   VP_HIP(hipGetLastError());
   VP_TRY(read_ctl(c, t));
   if (n_new) *n_new = t.h_ctl.new_count;
-  // The masked layout is exact-structured for GF(2)-linear key sets: either
-  // well spread or clustered (a long probe, or a quarter of the keys past
-  // their home bucket). Clustered: rebuild into the multiplicative layout.
+  // A linear layout is exact-structured for GF(2)-linear key sets: either
+  // well spread or clustered (a long probe, or a tenth of the keys past
+  // their home bucket). Clustered: choose another layout and rebuild.
   t.ins_since += t.h_ctl.new_count;
-  if (!t.mix && (t.h_ctl.max_disp ||
-                 (t.ins_since >= 4096 && 10ull * t.h_ctl.disp_count > t.ins_since))) {
-    t.mix = 1;
+  if (t.mix < kMixMul && (t.h_ctl.max_disp ||
+                          (t.ins_since >= 4096 && 10ull * t.h_ctl.disp_count > t.ins_since))) {
     VP_HIP(hipMemsetAsync(&t.ctl->max_disp, 0, 4, c->stream));
-    VP_TRY(tbl_rebuild(c, t));
+    VP_TRY(tbl_choose_layout(c, t));
   }
   return 0;
+}
+
+// ---------------------------------------------------------------- layout --
+// Score a home-bucket mode over this rank's live keys: the number of keys
+// beyond the 3 entries of their home bucket.
+__global__ void lay_count(TableDev t, uint32_t mix, uint32_t *cnt) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.cap;
+       i += gridDim.x * blockDim.x)
+    if (t.slot_of[i] < kElsewhere) atomicAdd(&cnt[home_bucket(t.hash_of[i], t.bmask, mix)], 1u);
+}
+__global__ void lay_score(const uint32_t *cnt, uint32_t nb, uint32_t *over) {
+  uint32_t o = 0;
+  for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nb;
+       b += gridDim.x * blockDim.x)
+    o += cnt[b] > kBucketEntries ? cnt[b] - kBucketEntries : 0;
+  for (uint32_t s = 32; s > 0; s >>= 1) o += __shfl_xor(o, s);
+  if ((threadIdx.x & 63) == 0 && o) atomicAdd(over, o);
+}
+
+// Every rotation of the CRC bits (modes 0-31) scored over the live keys; the
+// cleanest one if few keys overflow their home bucket, else the
+// multiplicative spread. Then rebuild. A table that keeps clustering after
+// a few choices stays multiplicative.
+static int tbl_choose_layout(vp_ctx *c, FlowTable &t) {
+  const uint64_t nb = (uint64_t)t.bmask + 1;
+  uint32_t best = kMixMul;
+  if (++t.layout_tries <= 4) {
+    uint32_t *cnt = nullptr, *over = nullptr;
+    VP_TRY(dalloc(&cnt, nb));
+    VP_TRY(dalloc(&over, 32));
+    VP_HIP(hipMemsetAsync(over, 0, 4 * 32, c->stream));
+    for (uint32_t m = 0; m < 32; m++) {
+      VP_HIP(hipMemsetAsync(cnt, 0, 4 * nb, c->stream));
+      lay_count<<<grid_for(t.cap), 256, 0, c->stream>>>(tbl_dev(t), m, cnt);
+      lay_score<<<grid_for(nb), 256, 0, c->stream>>>(cnt, (uint32_t)nb, over + m);
+    }
+    VP_HIP(hipGetLastError());
+    uint32_t h_over[32];
+    VP_HIP(hipMemcpyAsync(h_over, over, sizeof h_over, hipMemcpyDeviceToHost, c->stream));
+    VP_HIP(hipStreamSynchronize(c->stream));
+    hipFree(cnt);
+    hipFree(over);
+    VP_TRY(read_ctl(c, t));
+    uint32_t m_best = 0;
+    for (uint32_t m = 1; m < 32; m++)
+      if (h_over[m] < h_over[m_best]) m_best = m;
+    // clean enough (under 1 % of the keys overflow) and not the layout
+    // that just clustered
+    if (m_best != t.mix && 100ull * h_over[m_best] <= t.h_ctl.sh_live) best = m_best;
+  }
+  t.mix = best;
+  return tbl_rebuild(c, t);
 }
 
 // ---------------------------------------------------------- touch log --
