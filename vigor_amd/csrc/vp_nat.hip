@@ -20,6 +20,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -812,9 +814,45 @@ struct PhaseA {
   float ms;
 };
 
+// VIGPATH_PHASES=1: per-segment stage times of the owner-mode phase A on
+// stderr (diagnostics; events on the context's stream).
+struct PhaseMarks {
+  hipEvent_t ev[8] = {};
+  int n = 0;
+  bool on = false;
+  explicit PhaseMarks(hipStream_t s) : stream(s) {
+    const char *e = getenv("VIGPATH_PHASES");
+    on = e && atoi(e);
+    if (on)
+      for (auto &x : ev) (void)hipEventCreate(&x);
+  }
+  ~PhaseMarks() {
+    if (on)
+      for (auto &x : ev) (void)hipEventDestroy(x);
+  }
+  void mark() {
+    if (on && n < 8) (void)hipEventRecord(ev[n++], stream);
+  }
+  void print(int rank, uint32_t np) {
+    if (!on || n < 2) return;
+    (void)hipEventSynchronize(ev[n - 1]);
+    static const char *names[] = {"pass1", "offsets", "a2a_keys", "probe",
+                                  "a2a_answers", "pass2", "fold"};
+    fprintf(stderr, "vigpath owner r%d n=%u:", rank, np);
+    for (int i = 1; i < n; i++) {
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, ev[i - 1], ev[i]);
+      fprintf(stderr, " %s %.3f", names[i - 1], ms);
+    }
+    fprintf(stderr, " ms\n");
+  }
+  hipStream_t stream;
+};
+
 static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
                              const NowSpec &now, uint32_t p0, uint32_t p1,
                              uint64_t seq0, PhaseA *ph) {
+  PhaseMarks pm(c->stream);
   FlowTable &t = c->ft;
   Workspace &w = c->ws;
   Comm &m = *c->comm;
@@ -846,6 +884,7 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
 
   VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
   VP_HIP(hipEventRecord(c->ev0, c->stream));
+  pm.mark();
   if (np) {
     if (ph->tiles64) {
       NatArgs a1 = a;
@@ -861,6 +900,7 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
     VP_HIP(hipMemsetAsync(w.dcnt, 0, sizeof(uint32_t) * slices, c->stream));
   }
   VP_HIP(hipEventRecord(c->ev1, c->stream));
+  pm.mark();
   route_scan<<<n, 256, 0, c->stream>>>(w.dcnt, ph->grid1, n, w.dbase, w.dtot);
   route_base<<<grid_for(slices), 256, 0, c->stream>>>(w.dbase, w.dtot, ph->grid1, n);
   VP_HIP(hipGetLastError());
@@ -887,13 +927,17 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   route_pack<<<ph->grid1, 256, 0, c->stream>>>(w.desc, w.dcnt, w.dbase, n, ph->range1,
                                                w.sendk);
   VP_HIP(hipGetLastError());
+  pm.mark();
   VP_TRY(m.alltoallv_dev(c, w.sendk, sk.data(), w.recvk, rk.data()));
+  pm.mark();
   if (R) {
     nat_own_probe<<<grid_for(R, 256, 4096), 256, 0, c->stream>>>(
         tbl_dev(t), c->crc_tab, w.recvk, (uint32_t)R, w.reply);
     VP_HIP(hipGetLastError());
   }
+  pm.mark();
   VP_TRY(m.alltoallv_dev(c, w.reply, sr.data(), w.rreply, rr.data()));
+  pm.mark();
   VP_HIP(hipEventRecord(c->ev2, c->stream));
   if (np) {
     if (ph->tiles64) {
@@ -912,12 +956,15 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
     VP_HIP(hipGetLastError());
   }
   VP_HIP(hipEventRecord(c->ev3, c->stream));
+  pm.mark();
   VP_TRY(read_ctl_post(c, t));
   if (ph->bp.on)
     VP_TRY(tbl_bins_reduce(c, t, ph->bp, p0, now, seq0));
   else
     VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
+  pm.mark();
   VP_TRY(read_ctl_wait(c, t));
+  pm.print(m.r, np);
   float k1 = 0.f, k2 = 0.f;
   VP_HIP(hipEventElapsedTime(&k1, c->ev0, c->ev1));
   VP_HIP(hipEventElapsedTime(&k2, c->ev2, c->ev3));
