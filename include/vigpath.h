@@ -147,10 +147,14 @@ typedef struct vp_dev_batch {
 
 /* Process one device-resident batch on HIP stream `stream` (a hipStream_t,
  * or NULL for the context's own stream). Returns after the results (frames,
- * out_dev) are in device memory. In steady state the fold of the flow
- * timestamps may still be running on the context's stream when it returns;
- * it is ordered before every later call on this context (dumps, counts,
- * the next batch) and before work enqueued on `stream` afterwards. */
+ * out_dev) are in device memory; from then on no work of the library reads
+ * the caller's buffers, so all of them (the per-packet time array included)
+ * may be refilled or freed at once. With affine time (now == NULL) the fold
+ * of the flow timestamps, which reads only library workspace, may still be
+ * running on the context's stream when it returns; it is ordered before
+ * every later call on this context (dumps, counts, the next batch) and
+ * before work enqueued on `stream` afterwards. A batch with a time array
+ * completes entirely before the call returns. */
 int vp_process_device(vp_ctx *ctx, const vp_dev_batch *batch, void *stream);
 
 /* Host-resident batch shaped like a DPDK rx burst: frames[i] -> mbuf data of

@@ -2,7 +2,18 @@
 produced by the oracle glue over the REFERENCE's own libVig (oracle/_ref,
 compiled from /root/reference/libvig/verified by oracle/Makefile), stored in
 tests/golden/<name>.npz by tests/golden/make_golden.py. The GPU box has no
-reference: these fixtures carry its answers there."""
+reference: these fixtures carry its answers there.
+
+What they pin: the libVig layer (map with chain counters, dchain allocation
+/ LRU / expiry, vector, CHT) is the reference's own code. The NF-level glue
+(header parse, nf_process decision logic of vignat / vigfw / vigbridge /
+viglb / vigpol, the DPDK checksum) is the clean-room restatement in
+oracle/orc.c on both sides, so these fixtures leave NF-level semantics
+parity-unpinned: a misreading shared by the restatement and the GPU path
+would not show here. vignat's NF level is pinned separately by the
+SURVEY.md Appendix-A byte-level KATs (tests/test_oracle.py), recorded from
+the reference's own nat_main.c in the survey probe; the reference NF
+sources cannot be compiled here."""
 import os
 
 import numpy as np

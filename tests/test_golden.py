@@ -2,7 +2,9 @@
 from the oracle glue over the REFERENCE's own libVig, oracle/_ref): the
 restated oracle and the GPU path must both reproduce them bit-exact: out
 ports, every frame byte, and which indices are allocated with their
-timestamps. These run where the reference is absent (the GPU box)."""
+timestamps. These run where the reference is absent (the GPU box). They pin
+the libVig layer; NF-level glue semantics are parity-unpinned by them (the
+restated glue is on both sides; see golden_cases.py and DESIGN.md §7)."""
 import numpy as np
 import pytest
 

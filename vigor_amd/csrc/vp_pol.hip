@@ -125,9 +125,11 @@ __global__ __launch_bounds__(256) void pol_classify(PolArgs a) {
     const uint32_t idx = tbl_probe(a.t, pol_hash(T, dst), key);
     if (idx != kNone) {
       a.pidx[p] = idx;
-      const uint32_t r = atomicAdd(&a.cnt[idx], 1u);
-      a.rnk[p] = r;
-      lmax = max(lmax, r + 1);
+      if (a.cnt) {  // grouping path: this hit's rank in its index's run
+        const uint32_t r = atomicAdd(&a.cnt[idx], 1u);
+        a.rnk[p] = r;
+        lmax = max(lmax, r + 1);
+      }
     } else if (len <= a.burst) {
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
     } else {
@@ -362,19 +364,23 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.thr = c->pol.burst * kNsPerS / c->pol.rate;
   a.lan = c->pol.lan_device;
   a.wan = c->pol.wan_device;
-  a.cnt = c->pol_cnt;
   a.rnk = w.aux;
   a.maxrun = &t.ctl->aux_count;
   const uint32_t n = p1 - p0;
+  // The grouping path costs O(capacity) per segment (clear, scan and one
+  // lane per index); segments much shorter than the table (per-packet
+  // nf_process calls, churn cut into many segments) take the sorting path.
+  const bool grouping = (uint64_t)n * 8 >= t.cap;
+  a.cnt = grouping ? c->pol_cnt : nullptr;
 
   VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
   VP_HIP(hipMemsetAsync(a.maxrun, 0, 4, c->stream));
-  VP_HIP(hipMemsetAsync(c->pol_cnt, 0, 4ull * t.cap, c->stream));
+  if (grouping) VP_HIP(hipMemsetAsync(c->pol_cnt, 0, 4ull * t.cap, c->stream));
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   pol_classify<<<grid_for(n), 256, 0, c->stream>>>(a);
   VP_HIP(hipGetLastError());
   VP_HIP(hipEventRecord(c->ev1, c->stream));
-  {  // phase T, grouping path (speculative: no-ops unless pol_grouping_ok)
+  if (grouping) {  // phase T, grouping path (speculative: no-ops unless pol_grouping_ok)
     size_t need = 0;
     hipcub::DeviceScan::ExclusiveSum(nullptr, need, c->pol_cnt, c->pol_off,
                                      (int)t.cap, c->stream);
@@ -419,7 +425,7 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.t = tbl_dev(t);
   // the grouping path already ran (every policed packet was a counted
   // phase-A hit and runs are short): nothing left
-  if (!nmiss && !ndefer && t.h_ctl.aux_count <= kRunMax) return 0;
+  if (grouping && !nmiss && !ndefer && t.h_ctl.aux_count <= kRunMax) return 0;
   // phase T, sorting path: (index, packet) pairs sorted by index; radix sort
   // is stable, so each index's packets stay in packet order
   uint32_t bits = 1;
