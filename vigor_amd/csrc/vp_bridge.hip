@@ -61,11 +61,11 @@ __device__ __forceinline__ uint32_t static_hash(const uint32_t *T, uint32_t eh,
          S[4 * 256 + (dev & 0xFF)] ^ S[5 * 256 + ((dev >> 8) & 0xFF)];
 }
 
-// map_get on the dynamic table keyed by words 0-1; *port = entry word 2.
-__device__ __forceinline__ uint32_t mac_probe(const TableDev &t, uint32_t h,
-                                              uint32_t m0, uint32_t m1,
-                                              uint32_t *port) {
-  uint32_t b = home_bucket(h, t.bmask, t.mix);
+// map_get on the dynamic table keyed by words 0-1, from bucket b on;
+// *port = entry word 2.
+__device__ __forceinline__ uint32_t mac_probe_from(const TableDev &t, uint32_t b,
+                                                   uint32_t m0, uint32_t m1,
+                                                   uint32_t *port) {
   for (uint32_t i = 0; i <= t.bmask; i++) {
     const uint4 *q = reinterpret_cast<const uint4 *>(t.bk + b);
     const uint4 k0 = q[0], k1 = q[1], k2 = q[2], ix = q[3];
@@ -87,6 +87,11 @@ __device__ __forceinline__ uint32_t mac_probe(const TableDev &t, uint32_t h,
     b = (b + 1) & t.bmask;
   }
   return kNone;
+}
+__device__ __forceinline__ uint32_t mac_probe(const TableDev &t, uint32_t h,
+                                              uint32_t m0, uint32_t m1,
+                                              uint32_t *port) {
+  return mac_probe_from(t, home_bucket(h, t.bmask, t.mix), m0, m1, port);
 }
 
 struct BridgeArgs {
@@ -118,39 +123,127 @@ __device__ __forceinline__ uint4 eth_words(const BridgeArgs &a, uint32_t p) {
   return *reinterpret_cast<const uint4 *>(a.frames + (size_t)p * a.slot);
 }
 
-__global__ __launch_bounds__(256) void bridge_classify(BridgeArgs a) {
+// One dynamic-table bucket against a MAC (words 0-1): the index and *port
+// (entry word 2) on a match; kNone with *done on an empty entry; kNone with
+// !*done when the probe continues in the next bucket.
+__device__ __forceinline__ uint32_t mac_match(const uint4 *row, uint32_t m0, uint32_t m1,
+                                              uint32_t *port, bool *done) {
+  const uint4 ix = row[3];
+  const uint32_t id[3] = {ix.x, ix.y, ix.z};
+  *done = true;
+#pragma unroll
+  for (int e = 0; e < 3; e++) {
+    if (id[e] == kEmpty) return kNone;
+    if (id[e] != kTomb && row[e].x == m0 && row[e].y == m1) {
+      *port = row[e].z;
+      return id[e];
+    }
+  }
+  *done = false;
+  return kNone;
+}
+
+// Phase A. Blocks own contiguous ranges of 64-packet tiles, their four waves
+// interleaved (the frames64_tiles layout, so the launch can bin its touches:
+// tbl_bins_plan); a lane takes one packet of its wave's tile. The src and
+// dst home buckets are fetched together, four lanes per 64-byte row
+// (wave-cooperative, one request per row), then handed to their lanes
+// through LDS; a probe that continues past its home bucket walks on alone.
+__global__ __launch_bounds__(256) void bridge_classify(BridgeArgs a, TouchBins bins) {
   __shared__ uint32_t T[kBridgeTabs * 256];
+  __shared__ uint4 stage[4][256];
+  __shared__ uint32_t cur[kCurs];
+  for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
   for (uint32_t i = threadIdx.x; i < kBridgeTabs * 256; i += blockDim.x)
     T[i] = a.crc_tab[i];
   __syncthreads();
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t p = a.p0 + blockIdx.x * blockDim.x + threadIdx.x; p < a.p1;
-       p += stride) {
-    const uint4 h = eth_words(a, p);
-    const uint32_t in = a.in_dev[p];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint4 *S = stage[wv];
+  const uint32_t first = a.p0 & ~63u;
+  const uint32_t tiles = (a.p1 - first + 63) / 64;
+  const uint32_t rb = blockIdx.x;
+  const uint32_t per_b = (tiles + gridDim.x - 1) / gridDim.x;
+  const uint32_t tend = min(tiles, rb * per_b + per_b);
+  const uint32_t range0 = first + rb * per_b * 64;
+  const uint8_t *bk = reinterpret_cast<const uint8_t *>(a.t.bk);
+  for (uint32_t tile = rb * per_b + wv; tile < tend; tile += 4) {  // wave-uniform
+    const uint32_t p = first + tile * 64 + lane;
+    const bool mine = p >= a.p0 && p < a.p1;
+    uint4 h = make_uint4(0, 0, 0, 0);
+    uint32_t in = 0;
+    if (mine) {
+      h = eth_words(a, p);
+      in = a.in_dev[p];
+    }
     const uint32_t d0 = h.x, d1 = h.y & 0xFFFF;
     const uint32_t s0 = (h.y >> 16) | (h.z << 16), s1 = h.z >> 16;
-    // bridge_put_update_entry
-    uint32_t unused;
-    const uint32_t si = mac_probe(a.t, eth_hash(T, s0, s1), s0, s1, &unused);
-    a.log[p] = si;  // kNone: phase B writes the real entry
-    if (si == kNone) a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
-    // bridge_get_device
-    const uint32_t dh = eth_hash(T, d0, d1);
-    if (a.n_static) {
+    const uint32_t sh = eth_hash(T, s0, s1), dh = eth_hash(T, d0, d1);
+    // bridge_get_device: the static table first (bridge_main.c:38-61)
+    int32_t st_fwd = 0;
+    bool st_hit = false;
+    if (a.n_static && mine) {
       const uint32_t key[4] = {d0, d1 | (in << 16), 0, 0};
       const uint32_t k = tbl_probe(a.st, static_hash(T, dh, in), key);
       if (k != kNone) {
-        a.out[p] = resolve(a.st_val[k], in);
-        continue;
+        st_hit = true;
+        st_fwd = a.st_val[k];
       }
     }
-    uint32_t port = 0;
-    const uint32_t di = mac_probe(a.t, dh, d0, d1, &port);
-    // unknown: flooded unless learned earlier in this segment (phase C
-    // re-examines flooded frames only when phase B learned something)
-    a.out[p] = di != kNone ? (uint16_t)port : VP_FLOOD_FRAME;
+    // both home rows in flight at once
+    uint32_t sb = home_bucket(sh, a.t.bmask, a.t.mix), db = home_bucket(dh, a.t.bmask, a.t.mix);
+    uint4 q[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+      const uint32_t src_l = 16 * j + (lane >> 2);
+      const uint32_t r0 = __shfl(mine ? sb : kNone, src_l);
+      const uint32_t r1 = __shfl(mine && !st_hit ? db : kNone, src_l);
+      q[j] = r0 != kNone ? reinterpret_cast<const uint4 *>(bk + (size_t)r0 * 64)[lane & 3]
+                         : make_uint4(0, 0, 0, 0);
+      q[4 + j] = r1 != kNone ? reinterpret_cast<const uint4 *>(bk + (size_t)r1 * 64)[lane & 3]
+                             : make_uint4(0, 0, 0, 0);
+    }
+    uint4 srow[4], drow[4];
+    wave_lds_sync();
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = q[j];
+    wave_lds_sync();
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) srow[k] = S[chunk_swz(4 * lane + k)];
+    wave_lds_sync();
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = q[4 + j];
+    wave_lds_sync();
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) drow[k] = S[chunk_swz(4 * lane + k)];
+    uint32_t touch = kNone;
+    if (mine) {
+      // bridge_put_update_entry: a known src is rejuvenated, an unknown one
+      // queued for phase B
+      uint32_t unused = 0;
+      bool done;
+      uint32_t si = mac_match(srow, s0, s1, &unused, &done);
+      if (!done) {
+        TableDev t = a.t;
+        si = mac_probe_from(t, (sb + 1) & t.bmask, s0, s1, &unused);
+      }
+      touch = si;
+      log_put(a.log, p, si);  // kNone: phase B writes the real entry
+      if (si == kNone) a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
+      if (st_hit) {
+        a.out[p] = resolve(st_fwd, in);
+      } else {
+        uint32_t port = 0;
+        uint32_t di = mac_match(drow, d0, d1, &port, &done);
+        if (!done) di = mac_probe_from(a.t, (db + 1) & a.t.bmask, d0, d1, &port);
+        // unknown: flooded unless learned earlier in this segment (phase C
+        // re-examines flooded frames only when phase B learned something)
+        a.out[p] = di != kNone ? (uint16_t)port : VP_FLOOD_FRAME;
+      }
+    }
+    bins_put(bins, cur, rb, per_b * 64, range0, p, touch);
   }
+  __syncthreads();
+  bins_publish(bins, cur, rb);
 }
 
 // Keys + hashes of the queued src MACs (packet order).
@@ -241,19 +334,39 @@ static int bridge_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.miss = w.miss;
   a.defer = w.defer;
 
-  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 8, c->stream));  // + defer
+  // the classify launch bins its touches when it can (TouchBins; no touch
+  // log then), else logs them and the log is folded
+  BinsPlan bp{};
+  VP_TRY(tbl_bins_plan(c, t, (const void *)bridge_classify, p0, p1, &bp));
+  const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
+  const uint32_t grid = bp.on ? bp.grid : resident_grid((const void *)bridge_classify,
+                                                        (tiles + 3) / 4);
+  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. touch_ovf
   VP_HIP(hipEventRecord(c->ev0, c->stream));
-  bridge_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
+  BridgeArgs a1 = a;
+  if (bp.on) a1.log = nullptr;
+  bridge_classify<<<grid, 256, 0, c->stream>>>(a1, bp.bins);
   VP_HIP(hipGetLastError());
   VP_HIP(hipEventRecord(c->ev1, c->stream));
-  VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, c->seq));
-  VP_TRY(read_ctl(c, t));
+  VP_TRY(read_ctl_post(c, t));
+  if (bp.on)
+    VP_TRY(tbl_bins_reduce(c, t, bp, p0, now, c->seq));
+  else
+    VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, c->seq));
+  VP_TRY(read_ctl_wait(c, t));
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
   *ms += kms;
   *launches += 1;
+  const bool ovf = bp.on && t.h_ctl.touch_ovf != 0;
+  if (ovf)  // touches that found their bin slice full, logged alone
+    VP_TRY(tbl_late_touches(c, t, bp.bins.oent, bp.bins.ocnt, 0, bp.range, bp.grid,
+                            w.log, now, c->seq));
   const uint32_t nmiss = t.h_ctl.miss_count;
-  if (!nmiss) return 0;  // nothing learned: provisional floods stand
+  // nothing learned: provisional floods stand; only the fold may still run
+  // (not when it reads the caller's time array)
+  c->fold_pending = !nmiss && !ovf && !b->now;
+  if (!nmiss) return 0;
 
   size_t need = 0;
   hipcub::DeviceRadixSort::SortKeys(nullptr, need, w.miss, w.miss_sorted,
@@ -273,7 +386,9 @@ static int bridge_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   bridge_defer_finish<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
   VP_HIP(hipGetLastError());
   *allocated |= 1u;
-  VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, c->seq));
+  // the learning packets' touches on top of the fold (last toucher wins)
+  VP_TRY(tbl_late_touches(c, t, w.miss_sorted, nullptr, nmiss, 256, (nmiss + 255) / 256,
+                          w.log, now, c->seq));
   VP_TRY(read_ctl(c, t));
   return 0;
 }

@@ -290,6 +290,43 @@ __device__ __forceinline__ uint32_t bin_index(uint32_t bin, uint32_t local,
   return ((local >> 4) << (4 + bbits)) | (bin << 4) | (local & 15u);
 }
 
+// Append packet p's touch (kNone: none) to block rb's slice of its bin
+// (wave-uniform call; `range` = packets per block, range0 = the block's first
+// packet). A full slice logs the touch alone on the block's overflow queue.
+__device__ __forceinline__ void bins_put(const TouchBins &bins, uint32_t *cur,
+                                         uint32_t rb, uint32_t range, uint32_t range0,
+                                         uint32_t p, uint32_t touch) {
+  if (!bins.ent) return;
+  const bool v = touch != kNone;
+  const uint32_t b = v ? bin_of(touch, bins.bbits) : 0;
+  const uint32_t k = group_reserve(cur, b, v);
+  const bool fits = k < bins.cap;
+  if (v && fits)
+    bins.ent[(((size_t)rb << bins.bbits) + b) * bins.cap + k] =
+        (bin_local(touch, bins.bbits) << bins.pbits) | (p - range0);
+  const bool spill = v && !fits;
+  const uint32_t o = group_reserve(cur, kCurOverflow, spill);
+  if (spill) {
+    bins.olog[p] = touch;
+    bins.oent[(size_t)rb * range + o] = p;
+  }
+}
+
+// After the block's last bins_put and a barrier: publish its slice sizes.
+__device__ __forceinline__ void bins_publish(const TouchBins &bins, const uint32_t *cur,
+                                             uint32_t rb) {
+  if (!bins.ent) return;
+  for (uint32_t b = threadIdx.x; b < (1u << bins.bbits); b += blockDim.x) {
+    const uint32_t c = cur[b];
+    bins.cnt[((size_t)rb << bins.bbits) + b] = c < bins.cap ? c : bins.cap;
+  }
+  if (threadIdx.x == 0) {
+    const uint32_t o = cur[kCurOverflow];
+    bins.ocnt[rb] = o;
+    if (o) *bins.ovf = 1;
+  }
+}
+
 // Packets [p0, p1) of a batch of n_all 64-byte slots, in tiles of 64
 // consecutive packets per wave (256-thread blocks, 4 waves): every global
 // load/store instruction moves 1 KiB contiguous (lane l <-> bytes
@@ -407,21 +444,7 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
       if (v) rq.ent[(size_t)rb * per_b * 64 + k] = p;
     }
     if (touch == kReprobe) touch = kNone;
-    if (bins.ent) {  // append to this block's slice of the touch's bin
-      const bool v = touch != kNone;
-      const uint32_t b = v ? bin_of(touch, bins.bbits) : 0;
-      const uint32_t k = group_reserve(cur, b, v);
-      const bool fits = k < bins.cap;
-      if (v && fits)
-        bins.ent[(((size_t)rb << bins.bbits) + b) * bins.cap + k] =
-            (bin_local(touch, bins.bbits) << bins.pbits) | (p - range0);
-      const bool spill = v && !fits;  // slice full: log this touch alone
-      const uint32_t o = group_reserve(cur, kCurOverflow, spill);
-      if (spill) {
-        bins.olog[p] = touch;
-        bins.oent[(size_t)rb * per_b * 64 + o] = p;
-      }
-    }
+    bins_put(bins, cur, rb, per_b * 64, range0, p, touch);
     if (mod) {
 #pragma unroll
       for (uint32_t k = 0; k < 4; k++)
@@ -442,17 +465,7 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
     wave_lds_sync();  // the next tile overwrites S
   }
   if (bins.ent || rq.ent) __syncthreads();
-  if (bins.ent) {  // publish this block's slice sizes
-    for (uint32_t b = threadIdx.x; b < (1u << bins.bbits); b += blockDim.x) {
-      const uint32_t c = cur[b];
-      bins.cnt[((size_t)rb << bins.bbits) + b] = c < bins.cap ? c : bins.cap;
-    }
-    if (threadIdx.x == 0) {
-      const uint32_t o = cur[kCurOverflow];
-      bins.ocnt[rb] = o;
-      if (o) *bins.ovf = 1;
-    }
-  }
+  bins_publish(bins, cur, rb);
   if (rq.ent && threadIdx.x == 0) {
     const uint32_t c = cur[kCurReprobe];
     rq.cnt[rb] = c;

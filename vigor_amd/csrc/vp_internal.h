@@ -104,6 +104,7 @@ struct Workspace {
   uint32_t *defer_sorted = nullptr;
   uint32_t *aux = nullptr, *aux_sorted = nullptr;  // third queue (viglb)
   uint32_t *rlist = nullptr;  // re-classification input (viglb rounds)
+  uint32_t *hbl = nullptr;    // viglb: heartbeat positions of a segment
   // multi-GPU: new-flow records exchanged between ranks, union positions/times
   void *sbuf = nullptr, *rbuf = nullptr;
   size_t sbuf_bytes = 0, rbuf_bytes = 0;

@@ -120,6 +120,7 @@ struct LbArgs {
   const uint32_t *crc_tab;
   const uint32_t *dmacw;
   uint32_t *miss, *stale, *hb;  // queues M, S, H
+  uint32_t *hbl;  // phase A: every heartbeat's position (its backend touch)
   uint16_t wan, n_dev;
 };
 
@@ -179,22 +180,24 @@ __device__ __forceinline__ void lb_rewrite_generic(const LbArgs &a, const GFrame
 // Decision for a parsed packet (phase A / re-classification). Heartbeats are
 // logged or queued (H); WAN packets hitting a flow with a live backend are
 // handed to `rw` with the backend record; the rest are queued (M / S).
+// The backend touch log (log2) is written only for heartbeats: phase A lists
+// them (hbl) and the segment applies them as late touches.
 template <class Rw>
 __device__ __forceinline__ bool lb_decide(const LbArgs &a, const uint32_t *T,
                                           uint32_t p, uint32_t in, uint32_t sip,
                                           uint32_t dip, uint32_t sp, uint32_t dp,
-                                          uint32_t proto, Rw rw) {
+                                          uint32_t proto, Rw rw, uint32_t *touch = nullptr) {
   if (in != a.wan) {  // lb_process_heartbit; the packet itself is dropped
     const uint32_t key[4] = {sip, 0, 0, 0};
     const uint32_t bi = tbl_probe(a.bt, ip_hash(T, sip), key);
     a.out[p] = (uint16_t)in;
     a.log[p] = kNone;
     a.log2[p] = bi;  // kNone: queued, the round writes the real entry
-    wave_append(&a.bt.ctl->defer_count, true);  // heartbeats seen
+    const uint32_t k = wave_append(&a.bt.ctl->defer_count, true);  // heartbeats seen
+    if (a.hbl) a.hbl[k] = p;
     if (bi == kNone) a.hb[wave_append(&a.bt.ctl->miss_count, true)] = p;
     return false;
   }
-  a.log2[p] = kNone;
   uint32_t w3 = 0;
   const uint32_t fi =
       flow_probe(a.ft, lbflow_hash(T, sip, dip, sp, dp, proto), sip, dip,
@@ -211,6 +214,7 @@ __device__ __forceinline__ bool lb_decide(const LbArgs &a, const uint32_t *T,
     return false;
   }
   a.log[p] = fi;
+  if (touch) *touch = fi;
   return rw(a.be_rec[bi]);
 }
 
@@ -227,7 +231,6 @@ VP_LB_GENERIC_FN void lb_generic_a(const LbArgs &a, const uint32_t *T,
   if (!h.ok) {
     a.out[p] = (uint16_t)in;
     a.log[p] = kNone;
-    a.log2[p] = kNone;
     return;
   }
   const uint32_t proto = f.r8(h.ip + 9);
@@ -241,7 +244,7 @@ VP_LB_GENERIC_FN void lb_generic_a(const LbArgs &a, const uint32_t *T,
 
 __device__ __forceinline__ bool lb_fast(const LbArgs &a, const uint32_t *T,
                                         uint32_t p, RFrame &f, uint32_t in,
-                                        uint32_t len) {
+                                        uint32_t len, uint32_t &touch) {
   const uint32_t et = f.w[3] & 0xFFFF;
   const uint32_t ihl = (f.w[3] >> 16) & 0x0F;
   const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
@@ -256,14 +259,13 @@ __device__ __forceinline__ bool lb_fast(const LbArgs &a, const uint32_t *T,
   if (!ok) {
     a.out[p] = (uint16_t)in;
     a.log[p] = kNone;
-    a.log2[p] = kNone;
     return false;
   }
   const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
   const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
   return lb_decide(a, T, p, in, sip, dip, sp, dp, proto, [&](uint4 rec) {
     return lb_rewrite_fast(a, f, rec, proto, tl, p);
-  });
+  }, &touch);
 }
 
 __device__ __forceinline__ void lb_load_tables(uint32_t *T, const uint32_t *g) {
@@ -271,10 +273,13 @@ __device__ __forceinline__ void lb_load_tables(uint32_t *T, const uint32_t *g) {
   __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void lb_classify64(LbArgs a, uint32_t n_all) {
+__global__ __launch_bounds__(256) void lb_classify64(LbArgs a, uint32_t n_all,
+                                                    TouchBins bins) {
   __shared__ uint32_t T[kLbTabs * 256];
   __shared__ uint4 stage[4][256];
-  lb_load_tables(T, a.crc_tab);
+  __shared__ uint32_t cur[kCurs];
+  for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
+  lb_load_tables(T, a.crc_tab);  // (its barrier also covers cur)
   struct NoPend {
     uint32_t row;
   };
@@ -285,12 +290,12 @@ __global__ __launch_bounds__(256) void lb_classify64(LbArgs a, uint32_t n_all) {
         return NoPend{kNone};
       },
       [&](NoPend, const uint4 *, uint32_t p, RFrame &f, uint32_t in, uint32_t len,
-          uint32_t &) -> uint32_t {
+          uint32_t &touch) -> uint32_t {
         // dst address, MACs and checksums: bytes 0-47, and the TCP checksum
-        if (!lb_fast(a, T, p, f, in, len)) return 0u;
+        if (!lb_fast(a, T, p, f, in, len, touch)) return 0u;
         return (f.w[5] >> 24) == 6 ? 0xFu : 0x7u;
       },
-      TouchBins{}, TileQueue{}, nullptr);
+      bins, TileQueue{}, cur);
 }
 
 __global__ __launch_bounds__(256) void lb_classify(LbArgs a) {
@@ -547,22 +552,34 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.miss = w.miss;
   a.stale = w.defer;
   a.hb = w.aux;
+  a.hbl = w.hbl;
   a.wan = c->lb.wan_device;
   a.n_dev = c->lb.n_devices;
 
   VP_TRY(zero_queues(c));
   VP_HIP(hipMemsetAsync(&c->ft2.ctl->defer_count, 0, 4, c->stream));  // heartbeats
+  VP_HIP(hipMemsetAsync(&c->ft.ctl->touch_ovf, 0, 4, c->stream));
+  BinsPlan bp{};
+  const bool tiles64 = b->slot == 64 && c->coalesced_io;
   VP_HIP(hipEventRecord(c->ev0, c->stream));
-  if (b->slot == 64 && c->coalesced_io) {
+  if (tiles64) {
+    // the flow touches also go to the touch bins (the log stays complete:
+    // the rounds below refold it whenever a queue is non-empty)
+    VP_TRY(tbl_bins_plan(c, c->ft, (const void *)lb_classify64, p0, p1, &bp));
     const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
-    lb_classify64<<<resident_grid((const void *)lb_classify64, (tiles + 3) / 4), 256,
-                    0, c->stream>>>(a, b->n);
+    const uint32_t grid =
+        bp.on ? bp.grid : resident_grid((const void *)lb_classify64, (tiles + 3) / 4);
+    lb_classify64<<<grid, 256, 0, c->stream>>>(a, b->n, bp.bins);
   } else {
     lb_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
   }
   VP_HIP(hipGetLastError());
   VP_HIP(hipEventRecord(c->ev1, c->stream));
-  VP_TRY(tbl_touch_reduce(c, c->ft, w.log, p0, p1, now, c->seq));  // optimistic
+  a.hbl = nullptr;  // re-classification rounds list no heartbeat twice
+  if (bp.on)  // optimistic fold
+    VP_TRY(tbl_bins_reduce(c, c->ft, bp, p0, now, c->seq));
+  else
+    VP_TRY(tbl_touch_reduce(c, c->ft, w.log, p0, p1, now, c->seq));
   VP_TRY(read_ctl2(c, c->ft2, c->ft));
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
@@ -570,6 +587,7 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   *launches += 1;
   const uint32_t nm = c->ft.h_ctl.miss_count, ns = c->ft.h_ctl.defer_count;
   const uint32_t nh = c->ft2.h_ctl.miss_count, nhb = c->ft2.h_ctl.defer_count;
+  const bool ovf = bp.on && c->ft.h_ctl.touch_ovf != 0;
 
   if (nm || ns || nh) {
     VP_TRY(sort_list(c, w.miss, w.miss_sorted, nm));
@@ -639,9 +657,12 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
         ih = jh;
       }
     }
-    VP_TRY(tbl_touch_reduce(c, c->ft, w.log, p0, p1, now, c->seq));
   }
-  if (nhb) VP_TRY(tbl_touch_reduce(c, c->ft2, w.log2, p0, p1, now, c->seq));
+  // the rounds completed the log (or a bin slice overflowed): refold it
+  if (nm || ns || nh || ovf) VP_TRY(tbl_touch_reduce(c, c->ft, w.log, p0, p1, now, c->seq));
+  if (nhb)  // the heartbeats' backend touches (log2 holds only theirs)
+    VP_TRY(tbl_late_touches(c, c->ft2, w.hbl, nullptr, nhb, 256, (nhb + 255) / 256,
+                            w.log2, now, c->seq));
   return 0;
 }
 

@@ -67,12 +67,12 @@ static void ws_release(Workspace &w) {
   void *ptrs[] = {w.miss,  w.miss_sorted, w.defer, w.mkey, w.mhash,
                   w.first, w.rank,        w.rep,   w.assign, w.scratch,
                   w.log,   w.iota,        w.skey,  w.sval,
-                  w.log2,  w.defer_sorted, w.aux,  w.aux_sorted, w.rlist,
+                  w.log2,  w.defer_sorted, w.aux,  w.aux_sorted, w.rlist, w.hbl,
                   w.unow,  w.reprobe,     w.reprobe_cnt, w.ovf_q, w.ovf_cnt};
   for (void *p : ptrs) hipFree(p);
   w.miss = w.miss_sorted = w.defer = w.mkey = w.mhash = w.first = w.rank =
       w.rep = w.assign = w.scratch = w.log = w.iota = w.skey = w.sval = nullptr;
-  w.log2 = w.defer_sorted = w.aux = w.aux_sorted = w.rlist = nullptr;
+  w.log2 = w.defer_sorted = w.aux = w.aux_sorted = w.rlist = w.hbl = nullptr;
   w.unow = nullptr;
   w.reprobe = w.reprobe_cnt = nullptr;
   w.ovf_q = w.ovf_cnt = nullptr;
@@ -109,6 +109,7 @@ int ws_reserve(vp_ctx *c, uint32_t n) {
     VP_TRY(dalloc(&w.aux, cap));
     VP_TRY(dalloc(&w.aux_sorted, cap));
     VP_TRY(dalloc(&w.rlist, cap));
+    VP_TRY(dalloc(&w.hbl, cap));
   }
   if (c->kind == KIND_POL) VP_TRY(dalloc(&w.aux, cap));  // hit ranks (vp_pol.hip)
   VP_TRY(dalloc(&w.iota, cap));
