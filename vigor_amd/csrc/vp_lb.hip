@@ -576,11 +576,13 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   VP_HIP(hipGetLastError());
   VP_HIP(hipEventRecord(c->ev1, c->stream));
   a.hbl = nullptr;  // re-classification rounds list no heartbeat twice
+  // phase A's counts are copied out before the fold and waited for alone
+  VP_TRY(read_ctl2_post(c, c->ft2, c->ft));
   if (bp.on)  // optimistic fold
     VP_TRY(tbl_bins_reduce(c, c->ft, bp, p0, now, c->seq));
   else
     VP_TRY(tbl_touch_reduce(c, c->ft, w.log, p0, p1, now, c->seq));
-  VP_TRY(read_ctl2(c, c->ft2, c->ft));
+  VP_TRY(read_ctl2_wait(c, c->ft2, c->ft));
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
   *ms += kms;
@@ -663,6 +665,9 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   if (nhb)  // the heartbeats' backend touches (log2 holds only theirs)
     VP_TRY(tbl_late_touches(c, c->ft2, w.hbl, nullptr, nhb, 256, (nhb + 255) / 256,
                             w.log2, now, c->seq));
+  // steady state: frames and ports complete, only the flow fold may still
+  // run (not when it reads the caller's time array)
+  c->fold_pending = !(nm || ns || nh || ovf || nhb) && !b->now;
   return 0;
 }
 

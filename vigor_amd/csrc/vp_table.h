@@ -234,6 +234,8 @@ int read_ctl(vp_ctx *c, FlowTable &t);
 int read_ctl2(vp_ctx *c, FlowTable &a, FlowTable &b);
 int read_ctl_post(vp_ctx *c, FlowTable &t);
 int read_ctl_wait(vp_ctx *c, FlowTable &t);
+int read_ctl2_post(vp_ctx *c, FlowTable &a, FlowTable &b);
+int read_ctl2_wait(vp_ctx *c, FlowTable &a, FlowTable &b);
 
 // ---------------------------------------------------------- batch driver --
 // A table whose entries expire, and the cutoff for a packet at time t (the

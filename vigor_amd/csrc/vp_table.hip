@@ -102,6 +102,27 @@ int read_ctl_wait(vp_ctx *c, FlowTable &t) {
   return 0;
 }
 
+// Both tables' control blocks copied behind the work enqueued so far; wait
+// with read_ctl2_wait (viglb: the fold runs in between).
+int read_ctl2_post(vp_ctx *c, FlowTable &a, FlowTable &b) {
+  VP_HIP(hipMemcpyAsync(a.h_pin, a.ctl, sizeof(Ctl), hipMemcpyDeviceToHost,
+                        c->stream));
+  VP_HIP(hipMemcpyAsync(b.h_pin, b.ctl, sizeof(Ctl), hipMemcpyDeviceToHost,
+                        c->stream));
+  VP_HIP(hipEventRecord(c->evc, c->stream));
+  return 0;
+}
+
+int read_ctl2_wait(vp_ctx *c, FlowTable &a, FlowTable &b) {
+  hipError_t e;
+  while ((e = hipEventQuery(c->evc)) == hipErrorNotReady) {
+  }
+  VP_HIP(e);
+  a.h_ctl = *a.h_pin;
+  b.h_ctl = *b.h_pin;
+  return 0;
+}
+
 // Both tables' control blocks with one wait (viglb reads its two together).
 int read_ctl2(vp_ctx *c, FlowTable &a, FlowTable &b) {
   VP_HIP(hipMemcpyAsync(a.h_pin, a.ctl, sizeof(Ctl), hipMemcpyDeviceToHost,
