@@ -9,6 +9,7 @@
 #                                                 -> gpurun_out/TAG_kt/
 #   pmc      two --pmc passes (FETCH_SIZE, WRITE_SIZE) of bench.py --no-cpu
 #                                                 -> gpurun_out/TAG_fetch/, TAG_write/
+#   pmcnf:NF the two --pmc passes over tools/bench_nf.py --only NF
 #   shard2   bench.py --gpus 2 with VIGPATH_COMM=host (ranks share GPU 0)
 #   e2e      tools/bench_e2e.py                   -> gpurun_out/TAG_e2e.log
 #   nf       tools/bench_nf.py                    -> gpurun_out/TAG_nf.log
@@ -49,6 +50,14 @@ for step in "$@"; do
          run pmc_write 180 rocprofv3 --pmc WRITE_SIZE --output-format csv \
            -d $O/${TAG}_write -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-e2e $BA \
            > $O/${TAG}_write.log 2>&1 || exit $? ;;
+    pmcnf:*) nf=${step#pmcnf:}
+         rm -rf $O/${TAG}_${nf}_fetch $O/${TAG}_${nf}_write
+         run pmcnf_fetch 240 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+           -d $O/${TAG}_${nf}_fetch -- python3 tools/bench_nf.py --only $nf --no-cpu --steps 3 \
+           > $O/${TAG}_${nf}_fetch.log 2>&1 || exit $?
+         run pmcnf_write 240 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+           -d $O/${TAG}_${nf}_write -- python3 tools/bench_nf.py --only $nf --no-cpu --steps 3 \
+           > $O/${TAG}_${nf}_write.log 2>&1 || exit $? ;;
     shard2) VIGPATH_COMM=host run shard2 600 python3 bench.py --gpus 2 --no-cpu --no-e2e $BA \
              > $O/${TAG}_shard2.log 2>&1 || exit $? ;;
     e2e) run e2e 600 python3 tools/bench_e2e.py > $O/${TAG}_e2e.log 2>&1 || exit $? ;;

@@ -21,7 +21,7 @@ import os
 import statistics
 import sys
 
-KERNEL = "nat_classify64"
+KERNEL = os.environ.get("PROF_KERNEL", "nat_classify64")
 
 
 def _rows(d, suffix):
