@@ -26,11 +26,14 @@ def main():
     variants["bpc3"] = (None, {"VIGPATH_BLOCKS_PER_CU": "3"})
     variants["bpc2"] = (None, {"VIGPATH_BLOCKS_PER_CU": "2"})
     only = os.environ.get("ABLATE_ONLY")  # comma-separated variant names
-    for v in ("NOPROBE", "NOINLINE", "NT", "NOFRAME", "NTLD", "SC1ST", "NTSC"):
-        p = os.path.join(ROOT, "vigor_amd", "abl", "libvigpath_%s.so" % v)
-        if os.path.exists(p):  # NOFRAME lives in the per-lane kernel
-            variants[v] = (p, {"VIGPATH_COALESCED": "0"} if v == "NOFRAME"
-                           else {})
+    abl = os.path.join(ROOT, "vigor_amd", "abl")
+    names = sorted(f[len("libvigpath_"):-3] for f in os.listdir(abl)
+                   if f.startswith("libvigpath_") and f.endswith(".so")) \
+        if os.path.isdir(abl) else []
+    for v in names:  # ablation builds, or any other build to compare (A/B)
+        p = os.path.join(abl, "libvigpath_%s.so" % v)
+        # NOFRAME lives in the per-lane kernel
+        variants[v] = (p, {"VIGPATH_COALESCED": "0"} if v == "NOFRAME" else {})
     if only:
         keep = set(only.split(",")) | {"full"}
         variants = {k: v for k, v in variants.items() if k in keep}

@@ -242,10 +242,14 @@ __device__ __forceinline__ uint32_t group_reserve(uint32_t *ctr, uint32_t ch,
 // to kMaxBins, chosen per table so that a bin's indices fit one LDS tile)
 // while classifying, so the timestamp fold needs a single pass
 // (touch_bins_reduce, vp_table.hip) instead of count + scan + scatter +
-// reduce. Index i belongs to bin (i >> 4) & (2^bbits - 1), at in-bin position
-// ((i >> (4 + bbits)) << 4) | (i & 15): runs of 16 consecutive indices per
-// bin, so sequential flow sets spread over all bins and the fold writes whole
-// 128-byte runs of ts. Each block appends to
+// reduce. Index i belongs to bin (i >> 6) & (2^bbits - 1), at in-bin position
+// ((i >> (6 + bbits)) << 6) | (i & 63): runs of 64 consecutive indices per
+// bin, so sequential flow sets spread over all bins, the fold writes whole
+// 512-byte runs of ts, and a wave whose 64 packets touch consecutive indices
+// appends them as one 256-byte run (whole lines; with runs of 16 a wave wrote
+// four 64-byte pieces into four bins whose lines stayed partial in L2 for
+// dozens of tiles: 11 % of the classify kernel, tools/ablate.py NOBINS).
+// Each block appends to
 // its own fixed-size slice of every bin (LDS cursors). With bins on, the
 // classify kernels write no per-packet touch log: a touch that finds its
 // slice full is logged alone (olog[p] = index) and queued on the block's
@@ -279,15 +283,18 @@ struct TouchBins {
 __device__ __forceinline__ void log_put(uint32_t *log, uint32_t p, uint32_t v) {
   if (log) log[p] = v;
 }
+constexpr uint32_t kBinRunBits = 6;  // runs of 64 consecutive indices per bin
+constexpr uint32_t kBinRun = 1u << kBinRunBits;
 __device__ __forceinline__ uint32_t bin_of(uint32_t i, uint32_t bbits) {
-  return (i >> 4) & ((1u << bbits) - 1);
+  return (i >> kBinRunBits) & ((1u << bbits) - 1);
 }
 __device__ __forceinline__ uint32_t bin_local(uint32_t i, uint32_t bbits) {
-  return ((i >> (4 + bbits)) << 4) | (i & 15u);
+  return ((i >> (kBinRunBits + bbits)) << kBinRunBits) | (i & (kBinRun - 1));
 }
 __device__ __forceinline__ uint32_t bin_index(uint32_t bin, uint32_t local,
                                               uint32_t bbits) {
-  return ((local >> 4) << (4 + bbits)) | (bin << 4) | (local & 15u);
+  return ((local >> kBinRunBits) << (kBinRunBits + bbits)) | (bin << kBinRunBits) |
+         (local & (kBinRun - 1));
 }
 
 // Append packet p's touch (kNone: none) to block rb's slice of its bin

@@ -52,6 +52,47 @@ __device__ __forceinline__ uint32_t flowid_hash(const uint32_t *T, uint32_t sp,
          T[14 * 256 + (proto & 0xFF)];
 }
 
+// flowid_hash for the lean classify tile: the 15 table reads are issued back
+// to back and waited for once (compiled from the expression above, every read
+// waits for the one before it: 15 LDS round trips per packet). The tables
+// must be the kernel's LDS array T (15 x 256 words).
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+#define VP_TAB_RD(t, a, off) \
+  asm volatile("ds_read_b32 %0, %1 offset:" #off : "=v"(t) : "v"(a))
+__device__ __forceinline__ uint32_t flowid_hash_batched(const uint32_t *T, uint32_t sp,
+                                                        uint32_t dp, uint32_t sip,
+                                                        uint32_t dip, uint32_t dev,
+                                                        uint32_t proto) {
+  const uint32_t base = lds_addr(T);
+  auto at = [&](uint32_t byte) { return base + (byte << 2); };
+  uint32_t t0, t1, t2, t3, t4, t5, t6, t7, t8, t9, t10, t11, t12, t13, t14;
+  VP_TAB_RD(t0, at(sp & 0xFF), 0);
+  VP_TAB_RD(t1, at((sp >> 8) & 0xFF), 1024);
+  VP_TAB_RD(t2, at(dp & 0xFF), 2048);
+  VP_TAB_RD(t3, at((dp >> 8) & 0xFF), 3072);
+  VP_TAB_RD(t4, at(sip & 0xFF), 4096);
+  VP_TAB_RD(t5, at((sip >> 8) & 0xFF), 5120);
+  VP_TAB_RD(t6, at((sip >> 16) & 0xFF), 6144);
+  VP_TAB_RD(t7, at(sip >> 24), 7168);
+  VP_TAB_RD(t8, at(dip & 0xFF), 8192);
+  VP_TAB_RD(t9, at((dip >> 8) & 0xFF), 9216);
+  VP_TAB_RD(t10, at((dip >> 16) & 0xFF), 10240);
+  VP_TAB_RD(t11, at(dip >> 24), 11264);
+  VP_TAB_RD(t12, at(dev & 0xFF), 12288);
+  VP_TAB_RD(t13, at((dev >> 8) & 0xFF), 13312);
+  VP_TAB_RD(t14, at(proto & 0xFF), 14336);
+  // (the results as operands: nothing reads them before this wait)
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(t0), "+v"(t1), "+v"(t2), "+v"(t3), "+v"(t4), "+v"(t5), "+v"(t6),
+                 "+v"(t7), "+v"(t8), "+v"(t9), "+v"(t10), "+v"(t11), "+v"(t12),
+                 "+v"(t13), "+v"(t14));
+  return (t0 ^ t1 ^ t2) ^ (t3 ^ t4 ^ t5) ^ (t6 ^ t7 ^ t8) ^ (t9 ^ t10 ^ t11) ^
+         (t12 ^ t13 ^ t14);
+}
+#undef VP_TAB_RD
+
 // Owner mode (vp_shard_mode): a LAN packet whose FlowId is
 // owned by another rank leaves phase A as a 16-byte key in this block's
 // slice for that owner (desc), and route[p] says where its answer will be:
@@ -441,8 +482,48 @@ __global__ __launch_bounds__(256) void nat_classify(NatArgs a) {
     nat_lane(a, T, p);
 }
 
-// Phase A for 64-byte slots: LDS-staged 1 KiB-contiguous frame I/O
-// (frames64_tiles, vp_device.h); each wave owns 64 consecutive packets.
+// The fast-path predicate of nat_issue for a LAN packet: IPv4, IHL 5,
+// total_length <= 50 (every L4 byte in the slot), and the parse accepts it
+// (nf_then_get_rte_ipv4_header / nf_then_get_tcpudp_header, nf-util.h:116-162).
+__device__ __forceinline__ bool nat_lan_fast_ok(const NatArgs &a, const RFrame &f,
+                                                uint32_t in, uint32_t len) {
+  const uint32_t et = f.w[3] & 0xFFFF;
+  const uint32_t ihl = (f.w[3] >> 16) & 0x0F;
+  const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
+  const uint32_t proto = f.w[5] >> 24;
+  const uint16_t unread = (uint16_t)(len - 14);
+  return (in != a.wan) & (et == 0x0008) & (ihl == 5) & (tl <= 50) & (unread >= 20) &
+         (unread >= tl) & ((proto == 6) | (proto == 17)) & ((uint32_t)(len - 34) >= 4u);
+}
+
+// bucket_match without branches (the same answer): entries in order, the
+// first empty entry ends the probe, a tombstone never matches.
+__device__ __forceinline__ uint32_t bucket_match_sel(const uint4 *row,
+                                                    const uint32_t key[4], bool *done) {
+  const uint4 ix = row[3];
+  const bool e0 = ix.x == kEmpty, e1 = ix.y == kEmpty, e2 = ix.z == kEmpty;
+  const bool m0 = (ix.x != kTomb) & !e0 &
+                  (((row[0].x ^ key[0]) | (row[0].y ^ key[1]) | (row[0].z ^ key[2]) |
+                    (row[0].w ^ key[3])) == 0);
+  const bool m1 = (ix.y != kTomb) & !e1 &
+                  (((row[1].x ^ key[0]) | (row[1].y ^ key[1]) | (row[1].z ^ key[2]) |
+                    (row[1].w ^ key[3])) == 0);
+  const bool m2 = (ix.z != kTomb) & !e2 &
+                  (((row[2].x ^ key[0]) | (row[2].y ^ key[1]) | (row[2].z ^ key[2]) |
+                    (row[2].w ^ key[3])) == 0);
+  *done = m0 | e0 | m1 | e1 | m2 | e2;
+  return m0 ? ix.x : e0 ? kNone : m1 ? ix.y : e1 ? kNone : m2 ? ix.z : kNone;
+}
+
+// Phase A for 64-byte slots: LDS-staged 1 KiB-contiguous frame I/O, each wave
+// owns 64 consecutive packets (the loop of frames64_tiles, vp_device.h, whose
+// comments describe the layout and the order of the memory operations). A
+// wave whose 64 packets are all fast-path LAN packets (the steady state of a
+// LAN->WAN stream, BASELINE config 2) takes a straight-line tile: hash, one
+// cooperative bucket-row gather, branch-free match, rewrite and checksums in
+// registers, the whole tile stored back (packets left for phase B or the
+// reprobe walk are stored unchanged). Any other tile runs nat_issue /
+// nat_finish per lane. Owner mode always takes the per-lane path.
 __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_all,
                                                         TouchBins bins, TileQueue rq) {
   __shared__ uint32_t T[15 * 256];
@@ -451,22 +532,195 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
   for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
   a.own.cur = cur + kCurDest;
   load_crc_tables(T, a.crc_tab);  // (its barrier also covers cur)
-  frames64_tiles(
-      a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
-      reinterpret_cast<const uint4 *>(a.t.bk),
-      [&](uint32_t p, const RFrame &f, uint32_t in, uint32_t len, bool mine) {
-        return nat_issue(a, T, p, f, in, len, mine);
-      },
-      [&](const NatPend &P, const uint4 *row, uint32_t p, RFrame &f, uint32_t in,
-          uint32_t len, uint32_t &touch) -> uint32_t {
-        // a rewrite touches bytes 0-47; the TCP checksum (bytes 50-51) also
-        // dirties chunk 3 (the protocol byte is never rewritten)
-        const bool m = nat_finish(a, T, P, row, p, f, in, len, touch);
+  uint4 *S = stage[threadIdx.x >> 6];
+  const uint4 *rows = reinterpret_cast<const uint4 *>(a.t.bk);
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t first = a.p0 & ~63u;
+  const uint32_t tiles = (a.p1 - first + 63) / 64;
+  const bool lean_ok = a.own.n == 0 && rq.ent != nullptr;
+  uint4 r[4];
+  uint32_t m_in = 0, m_len = 0;
+  auto fetch = [&](uint32_t tile) {
+    const uint32_t tb = first + tile * 64;
+    const uint4 *g = reinterpret_cast<const uint4 *>(a.frames + (size_t)tb * 64);
+    const uint32_t p = tb + lane;
+    if (tb + 64 <= n_all) {  // (wave-uniform) a whole tile: no per-lane guards
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) r[j] = tile_ld(g + 64 * j + lane);
+      m_in = a.in_dev[p];
+      m_len = a.len[p];
+      return;
+    }
+    const uint32_t avail = n_all - tb;  // in the batch
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+      const uint32_t c = 64 * j + lane;
+      r[j] = (c >> 2) < avail ? tile_ld(g + c) : make_uint4(0, 0, 0, 0);
+    }
+    m_in = p < n_all ? a.in_dev[p] : 0u;
+    m_len = p < n_all ? a.len[p] : 0u;
+  };
+  const uint32_t rb = blockIdx.x;
+  const uint32_t per_b = (tiles + gridDim.x - 1) / gridDim.x;
+  uint32_t tile = rb * per_b + wv;
+  const uint32_t tend = min(tiles, rb * per_b + per_b), tstep = 4;
+  const uint32_t range0 = first + rb * per_b * 64;  // this block's first packet
+  if (tile < tend) fetch(tile);
+  for (; tile < tend; tile += tstep) {
+    const uint32_t tb = first + tile * 64;
+    uint4 *g = reinterpret_cast<uint4 *>(a.frames + (size_t)tb * 64);
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = r[j];
+    wave_lds_sync();
+    const uint32_t p = tb + lane;
+    const bool mine = p >= a.p0 && p < a.p1;
+    RFrame f;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint4 v = S[chunk_swz(4 * lane + k)];
+      f.w[4 * k] = v.x;
+      f.w[4 * k + 1] = v.y;
+      f.w[4 * k + 2] = v.z;
+      f.w[4 * k + 3] = v.w;
+    }
+    const uint32_t in = m_in, ln = m_len;
+    uint4 row[4];
+    uint32_t touch = kNone;
+    bool store_all;
+    if (lean_ok && __ballot(mine && nat_lan_fast_ok(a, f, in, ln)) == ~0ull) {
+      // ---- lean tile: every lane a fast-path LAN packet
+      const uint32_t proto = f.w[5] >> 24;
+      const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
+      const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
+      const uint32_t b = home_bucket(flowid_hash_batched(T, sp, dp, sip, dip, in, proto),
+                                     a.t.bmask, a.t.mix);
+      // lane L fetches part L % 4 of the row of packet 16 j + L / 4: the four
+      // row numbers come in by ds_bpermute, issued together and waited for
+      // once; named registers (an array here stays in scratch memory)
+      uint32_t b0, b1, b2, b3;
+      const uint32_t src = lane & ~3u;  // byte address of lane L / 4
+      asm volatile("ds_bpermute_b32 %0, %1, %2" : "=v"(b0) : "v"(src), "v"(b));
+      asm volatile("ds_bpermute_b32 %0, %1, %2 offset:64" : "=v"(b1) : "v"(src), "v"(b));
+      asm volatile("ds_bpermute_b32 %0, %1, %2 offset:128" : "=v"(b2) : "v"(src), "v"(b));
+      asm volatile("ds_bpermute_b32 %0, %1, %2 offset:192" : "=v"(b3) : "v"(src), "v"(b));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
+      const uint32_t part = lane & 3;
+#ifdef VP_ABL_L2ROW  // diagnostic: every row from 64 fixed buckets (L2 hits)
+      b0 = 0 * 16 + (lane >> 2); b1 = 16 + (lane >> 2); b2 = 32 + (lane >> 2); b3 = 48 + (lane >> 2);
+#endif
+      const uint4 q0 = rows[4 * (size_t)b0 + part];
+      const uint4 q1 = rows[4 * (size_t)b1 + part];
+      const uint4 q2 = rows[4 * (size_t)b2 + part];
+      const uint4 q3 = rows[4 * (size_t)b3 + part];
+      if (tile + tstep < tend) fetch(tile + tstep);
+      wave_lds_sync();
+      S[chunk_swz(lane)] = q0;
+      S[chunk_swz(64 + lane)] = q1;
+      S[chunk_swz(128 + lane)] = q2;
+      S[chunk_swz(192 + lane)] = q3;
+      wave_lds_sync();
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) row[k] = S[chunk_swz(4 * lane + k)];
+      const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
+      bool done;
+#ifdef VP_ABL_L2ROW
+      asm volatile("" ::"v"(row[0].x), "v"(row[1].y), "v"(row[2].z), "v"(row[3].w));
+      done = true;
+      const uint32_t idx = p & (a.t.cap - 1);
+#else
+      const uint32_t idx = bucket_match_sel(row, key, &done);
+#endif
+      const bool hit = done & (idx != kNone);
+      if (__ballot(!hit)) {  // misses (phase B) and full home buckets (reprobes)
+        const bool miss = done & !hit;
+        if (miss) a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
+        const uint32_t k = group_reserve(cur, kCurReprobe, !done);
+        if (!done) rq.ent[(size_t)rb * per_b * 64 + k] = p;
+        if (!hit) log_put(a.log, p, kNone);
+      }
+      if (hit) {
+        log_put(a.log, p, idx);
+        touch = idx;
+        f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
+        f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
+#ifndef VP_ABL_NOCSUM  // diagnostic builds skip the checksums (tools/ablate.py)
+        fast_checksums(f, proto, bswap16((uint16_t)(f.w[4] & 0xFFFF)));
+#endif
+        f.w[0] = a.wan_macw0;
+        f.w[1] = a.wan_macw1;
+        f.w[2] = a.wan_macw2;
+#ifndef VP_ABL_NOOUT  // diagnostic builds skip the out-port store
+        a.out[p] = a.wan;
+#endif
+      }
+#ifdef VP_ABL_NOBINS  // diagnostic builds skip the touch bins
+      touch = kNone;
+#endif
+      store_all = true;
+    } else {
+      // ---- per-lane tile (nat_issue / nat_finish)
+      const NatPend pend = nat_issue(a, T, p, f, in, ln, mine);
+      uint4 q[4];
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t rw = __shfl(pend.row, 16 * j + (lane >> 2));
+        q[j] = rw != kNone ? rows[4 * (size_t)rw + (lane & 3)] : make_uint4(0, 0, 0, 0);
+      }
+      if (tile + tstep < tend) fetch(tile + tstep);
+      wave_lds_sync();
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = q[j];
+      wave_lds_sync();
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) row[k] = S[chunk_swz(4 * lane + k)];
+      bool m = false;
+      if (mine) {
+        m = nat_finish(a, T, pend, row, p, f, in, ln, touch);
         touch = route_note(a, p, touch);
-        if (!m) return 0u;
-        return (f.w[5] >> 24) == 6 ? 0xFu : 0x7u;
-      },
-      bins, rq, cur);
+      }
+      {  // queue on this block's reprobe slice
+        const bool v = touch == kReprobe;
+        const uint32_t k = group_reserve(cur, kCurReprobe, v);
+        if (v) rq.ent[(size_t)rb * per_b * 64 + k] = p;
+      }
+      if (touch == kReprobe) touch = kNone;
+      // a rewrite touches bytes 0-47; the TCP checksum (bytes 50-51) also
+      // dirties chunk 3: whole tiles are stored only when every lane rewrote
+      store_all = __ballot(m) == ~0ull;
+      if (!store_all) {
+        const uint64_t mm = __ballot(m);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+          S[chunk_swz(4 * lane + k)] =
+              make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
+        wave_lds_sync();
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+          const uint32_t c = 64 * j + lane;
+          if ((mm >> (c >> 2)) & 1ull) tile_st(g, c, S[chunk_swz(c)]);
+        }
+        wave_lds_sync();  // the next tile overwrites S
+      }
+    }
+    bins_put(bins, cur, rb, per_b * 64, range0, p, touch);
+    if (store_all) {
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++)
+        S[chunk_swz(4 * lane + k)] =
+            make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
+      wave_lds_sync();
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) tile_st(g, 64 * j + lane, S[chunk_swz(64 * j + lane)]);
+      wave_lds_sync();  // the next tile overwrites S
+    }
+  }
+  __syncthreads();
+  bins_publish(bins, cur, rb);
+  if (rq.ent && threadIdx.x == 0) {
+    const uint32_t c = cur[kCurReprobe];
+    rq.cnt[rb] = c;
+    if (c) atomicAdd(rq.total, c);
+  }
   route_publish(a, cur + kCurDest);
 }
 

@@ -638,7 +638,7 @@ int tbl_touch_reduce(vp_ctx *c, FlowTable &t, const uint32_t *log, uint32_t p0,
 // Single-pass fold of the touch bins a 64-byte classify launch filled
 // (TouchBins, vp_device.h): one block per bin keeps the largest position per
 // in-bin index in LDS, reading every source block's slice of its bin, then
-// writes ts/tseq in runs of 16 consecutive indices. About 8 B of traffic per
+// writes ts/tseq in runs of 64 consecutive indices. About 8 B of traffic per
 // packet (one write while classifying, one read here).
 constexpr uint32_t kBinLocalMax = 16384;  // in-bin indices held in LDS
 
@@ -709,11 +709,13 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   const uint32_t range = per_b * 64;
   // the fewest bins (>= 256) whose in-bin index range fits the fold's LDS
   uint32_t bbits = 8;
-  while (bbits < 10 && (((uint64_t)t.cap + (16ull << bbits) - 1) >> (4 + bbits)) << 4 >
-                           kBinLocalMax)
-    bbits++;
+  auto in_bin = [&](uint32_t bb) {  // in-bin index range for 2^bb bins
+    return (((uint64_t)t.cap + ((uint64_t)kBinRun << bb) - 1) >> (kBinRunBits + bb))
+           << kBinRunBits;
+  };
+  while (bbits < 10 && in_bin(bbits) > kBinLocalMax) bbits++;
   const uint32_t nbins = 1u << bbits;
-  const uint32_t L = (uint32_t)((((uint64_t)t.cap + (16ull << bbits) - 1) >> (4 + bbits)) << 4);
+  const uint32_t L = (uint32_t)in_bin(bbits);
   const uint32_t pbits = std::max<uint32_t>(1, ceil_log2(range));
   if (L > kBinLocalMax || ceil_log2(L) + pbits > 32) return 0;
   // twice a uniform share of a block's packets per bin, in 64-entry lines
