@@ -348,12 +348,7 @@ static int bridge_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   bridge_classify<<<grid, 256, 0, c->stream>>>(a1, bp.bins);
   VP_HIP(hipGetLastError());
   VP_HIP(hipEventRecord(c->ev1, c->stream));
-  VP_TRY(read_ctl_post(c, t));
-  if (bp.on)
-    VP_TRY(tbl_bins_reduce(c, t, bp, p0, now, c->seq));
-  else
-    VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, c->seq));
-  VP_TRY(read_ctl_wait(c, t));
+  VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, c->seq));
   float kms = 0.f;
   VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
   *ms += kms;

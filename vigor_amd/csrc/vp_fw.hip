@@ -414,13 +414,9 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     VP_HIP(hipGetLastError());
   }
   VP_HIP(hipEventRecord(c->ev1, c->stream));
-  VP_TRY(read_ctl_post(c, t));  // phase A's counts, waited for alone
-  // fold phase A's touches; queued packets follow as late touches
-  if (bp.on)
-    VP_TRY(tbl_bins_reduce(c, t, bp, p0, now, seq0));
-  else
-    VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
-  VP_TRY(read_ctl_wait(c, t));
+  // phase A's counts, and the fold of its touches behind them; queued
+  // packets follow as late touches
+  VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, seq0));
   // reprobes come only from the 64-byte tiles (fw_generic_a walks in place)
   const uint32_t nre = t.h_ctl.reprobe_count;
   if (nre) {  // probes past a full home bucket: finish them, patch the fold

@@ -56,6 +56,13 @@ struct Ctl {
   uint32_t own_new;     // owner mode: union keys this rank will insert (upper bound)
 };
 
+// The control block as a fold kernel publishes it into page-locked host
+// memory (tbl_fold_read_ctl, vp_table.hip); the host polls `epoch`.
+struct CtlPub {
+  Ctl ctl;
+  uint32_t epoch;
+};
+
 // One device table (see vp_table.h).
 struct FlowTable {
   Bucket *bk = nullptr;
@@ -74,8 +81,13 @@ struct FlowTable {
   Ctl *ctl = nullptr;
   Ctl h_ctl{};                     // last copy read back
   Ctl *h_pin = nullptr;            // page-locked landing buffer for h_ctl
+  CtlPub *h_pub = nullptr;         // host-coherent page, written by the fold
+  uint32_t pub_epoch = 0;          // last epoch asked of the fold
   uint32_t *ttotal = nullptr;  // touch-reduce entry count (device)
   uint64_t ts_floor = UINT64_MAX;  // lower bound of min ts over live indices
+  // the segment counters (miss_count .. reprobe_count) are known to be zero on
+  // the device: the next segment needs no reset (vignat steady state)
+  bool ctl_clean = false;
   // expiry workspace (sized cap)
   uint64_t *ekey = nullptr, *ekey2 = nullptr;
   uint32_t *eidx = nullptr, *eidx2 = nullptr;

@@ -1211,13 +1211,8 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   }
   VP_HIP(hipEventRecord(c->ev3, c->stream));
   pm.mark();
-  VP_TRY(read_ctl_post(c, t));
-  if (ph->bp.on)
-    VP_TRY(tbl_bins_reduce(c, t, ph->bp, p0, now, seq0));
-  else
-    VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
+  VP_TRY(tbl_fold_read_ctl(c, t, ph->bp, w.log, p0, p1, now, seq0));
   pm.mark();
-  VP_TRY(read_ctl_wait(c, t));
   pm.print(m.r, np);
   float k1 = 0.f, k2 = 0.f;
   VP_HIP(hipEventElapsedTime(&k1, c->ev0, c->ev1));
@@ -1275,7 +1270,9 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     a.tileq = 1;
   }
   if (!owner) {
-  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
+  if (!t.ctl_clean)
+    VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
+  t.ctl_clean = false;
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   if (p1 > p0) {
     if (tiles64) {
@@ -1288,16 +1285,11 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     VP_HIP(hipGetLastError());
   }
   VP_HIP(hipEventRecord(c->ev1, c->stream));
-  // phase A's counts are copied out before the fold and waited for alone
-  VP_TRY(read_ctl_post(c, t));
-  // Fold phase A's touches right away; the packets it queued (reprobes,
-  // overflowed bin entries, phase B/C) are applied on top of it afterwards
-  // as late touches (tbl_late_touches: last toucher still wins).
-  if (bp.on)
-    VP_TRY(tbl_bins_reduce(c, t, bp, p0, now, seq0));
-  else
-    VP_TRY(tbl_touch_reduce(c, t, w.log, p0, p1, now, seq0));
-  VP_TRY(read_ctl_wait(c, t));
+  // Phase A's counts for the host, and the fold of its touches right away;
+  // the packets it queued (reprobes, overflowed bin entries, phase B/C) are
+  // applied on top of it afterwards as late touches (tbl_late_touches: last
+  // toucher still wins).
+  VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, seq0));
   VP_HIP(hipEventElapsedTime(&ph.ms, c->ev0, c->ev1));
   }  // !owner
   a.own.n = 0;  // below: this rank's own table only
@@ -1369,6 +1361,9 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // the caller may reuse as soon as the call returns
   c->fold_pending = !c->comm && !b->now && !nre && !nmiss && !ndefer && !union_n &&
                     !ovf;
+  // phase A appended nothing and nothing ran after its counts were read:
+  // the counters are still zero for the next segment
+  t.ctl_clean = !owner && !c->comm && !nre && !nmiss && !ndefer && !union_n && !ovf;
   return 0;
 }
 

@@ -53,6 +53,25 @@ __host__ __device__ __forceinline__ uint32_t owner_of(uint32_t h, uint32_t n) {
   return (uint32_t)(((uint64_t)h * n) >> 32);
 }
 
+// A fold kernel's publication of the control block into host-coherent
+// memory (tbl_fold_read_ctl): pub == null means off. One thread calls
+// ctl_publish after the launch that filled `ctl` has completed: device-scope
+// loads of the block, system-scope stores, the epoch last (release).
+struct PubArgs {
+  CtlPub *pub;
+  const Ctl *ctl;
+  uint32_t epoch;
+};
+__device__ __forceinline__ void ctl_publish(const PubArgs &a) {
+  if (!a.pub) return;
+  const uint32_t *s = reinterpret_cast<const uint32_t *>(a.ctl);
+  uint32_t *d = reinterpret_cast<uint32_t *>(&a.pub->ctl);
+  for (uint32_t i = 0; i < sizeof(Ctl) / 4; i++)
+    __hip_atomic_store(d + i, __hip_atomic_load(s + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&a.pub->epoch, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct NowSpec {
   const int64_t *arr;
   int64_t now0, step;
@@ -208,6 +227,8 @@ int tbl_late_touches(vp_ctx *c, FlowTable &t, const uint32_t *list,
 // instead (t.ctl->touch_ovf set; apply plan.bins.oent with tbl_late_touches).
 int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
                     const NowSpec &now, uint64_t seq_base);
+int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_t *log,
+                      uint32_t p0, uint32_t p1, const NowSpec &now, uint64_t seq_base);
 
 // Exact min ts over allocated indices -> t.ts_floor (~0 if none).
 int tbl_exact_floor(vp_ctx *c, FlowTable &t);

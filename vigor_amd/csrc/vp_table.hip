@@ -180,6 +180,9 @@ int tbl_alloc(vp_ctx *c, FlowTable &t, uint32_t cap) {
   VP_TRY(dalloc(&t.lastg, cap));
   VP_TRY(dalloc(&t.ctl, 1));
   VP_HIP(hipHostMalloc((void **)&t.h_pin, sizeof(Ctl), hipHostMallocDefault));
+  VP_HIP(hipHostMalloc((void **)&t.h_pub, sizeof(CtlPub),
+                       hipHostMallocMapped | hipHostMallocCoherent));
+  memset(t.h_pub, 0, sizeof(CtlPub));
   VP_TRY(dalloc(&t.ttotal, 1));
   VP_TRY(dalloc(&t.ekey, cap));
   VP_TRY(dalloc(&t.ekey2, cap));
@@ -203,6 +206,7 @@ void tbl_free(FlowTable &t) {
   hipFree(t.ttotal);
   hipFree(t.kv);
   if (t.h_pin) hipHostFree(t.h_pin);
+  if (t.h_pub) hipHostFree(t.h_pub);
   t = FlowTable{};
 }
 
@@ -645,9 +649,11 @@ constexpr uint32_t kBinLocalMax = 16384;  // in-bin indices held in LDS
 __global__ __launch_bounds__(1024) void touch_bins_reduce(
     const uint32_t *ent, const uint32_t *cnt, uint32_t nsrc, uint32_t cap,
     uint32_t pbits, uint32_t bbits, uint32_t range, uint32_t L, uint32_t tcap,
-    uint32_t p0, NowSpec now, uint64_t seq_base, uint64_t *ts, uint64_t *tseq) {
+    uint32_t p0, NowSpec now, uint64_t seq_base, uint64_t *ts, uint64_t *tseq,
+    PubArgs pub) {
   __shared__ uint32_t last[kBinLocalMax];  // 1 + position in the launch, 0 = none
   const uint32_t bin = blockIdx.x;
+  if (bin == 0 && threadIdx.x == 0) ctl_publish(pub);
   for (uint32_t i = threadIdx.x; i < L; i += blockDim.x) last[i] = 0;
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
@@ -746,12 +752,50 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   return 0;
 }
 
-int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
-                    const NowSpec &now, uint64_t seq_base) {
+static int bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
+                       const NowSpec &now, uint64_t seq_base, PubArgs pub) {
   touch_bins_reduce<<<1u << plan.bins.bbits, 1024, 0, c->stream>>>(
       plan.bins.ent, plan.bins.cnt, plan.grid, plan.bins.cap, plan.bins.pbits,
-      plan.bins.bbits, plan.range, plan.L, t.cap, p0, now, seq_base, t.ts, t.tseq);
+      plan.bins.bbits, plan.range, plan.L, t.cap, p0, now, seq_base, t.ts, t.tseq,
+      pub);
   VP_HIP(hipGetLastError());
+  return 0;
+}
+
+int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
+                    const NowSpec &now, uint64_t seq_base) {
+  return bins_reduce(c, t, plan, p0, now, seq_base, PubArgs{});
+}
+
+// Phase A's control block for the host, and the fold of phase A's touches
+// behind it. With touch bins the fold kernel's first thread reads the block
+// (the classify launch has completed: kernel boundary) and publishes it into
+// host-coherent memory, so no copy launch and its kernel boundary sit between
+// the classify and the fold; the host polls for it while the fold runs.
+// Without bins: a copy behind phase A, then the log fold. On return h_ctl
+// holds phase A's counts; the fold may still be running.
+int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_t *log,
+                      uint32_t p0, uint32_t p1, const NowSpec &now, uint64_t seq_base) {
+  if (!bp.on) {
+    VP_TRY(read_ctl_post(c, t));
+    VP_TRY(tbl_touch_reduce(c, t, log, p0, p1, now, seq_base));
+    return read_ctl_wait(c, t);
+  }
+  CtlPub *dpub = nullptr;
+  VP_HIP(hipHostGetDevicePointer((void **)&dpub, t.h_pub, 0));
+  const uint32_t epoch = ++t.pub_epoch;
+  VP_TRY(bins_reduce(c, t, bp, p0, now, seq_base, PubArgs{dpub, t.ctl, epoch}));
+  // poll the epoch; a stream that ends (or fails) without it is an error
+  for (uint32_t spin = 1;; spin++) {
+    if (__atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE) == epoch) break;
+    if ((spin & 1023) == 0) {
+      const hipError_t e = hipStreamQuery(c->stream);
+      if (e == hipSuccess && __atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE) != epoch)
+        return VP_EIO;
+      if (e != hipSuccess && e != hipErrorNotReady) VP_HIP(e);
+    }
+  }
+  memcpy(&t.h_ctl, (const void *)&t.h_pub->ctl, sizeof(Ctl));
   return 0;
 }
 
