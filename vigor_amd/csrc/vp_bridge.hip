@@ -350,7 +350,7 @@ static int bridge_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   VP_HIP(hipEventRecord(c->ev1, c->stream));
   VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, c->seq));
   float kms = 0.f;
-  VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
+  VP_HIP(event_ms(c->ev0, c->ev1, &kms));
   *ms += kms;
   *launches += 1;
   const bool ovf = bp.on && t.h_ctl.touch_ovf != 0;

@@ -156,10 +156,13 @@ __device__ __forceinline__ void st_stream(uint4 *p, uint4 v) {
 #endif
 }
 
-// Tile frame loads / stores of frames64_tiles. Ablation builds (tools/
-// ablate.py) change their cache policy: VP_ABL_NTLD loads non-temporal
-// (evict-first in L2), VP_ABL_SC1ST stores write-through (sc1: the line
-// leaves the XCD's L2), so the frame stream displaces fewer table rows.
+// Tile frame loads / stores of frames64_tiles and the vignat classify loop.
+// Stores are write-through (sc1: the written line leaves the XCD's L2 at
+// once, so the frame stream leaves fewer dirty lines between the table rows
+// and at the kernel boundary): 3.5 % faster nat_classify64 than write-back
+// stores (tools/ablate.py, VP_ABL_WBST builds keep plain stores). Ablation
+// builds also change the loads: VP_ABL_NTLD non-temporal (evict-first in L2;
+// measured 30 % slower).
 __device__ __forceinline__ uint4 tile_ld(const uint4 *p) {
 #if defined(VP_ABL_NTLD) || defined(VP_ABL_NTSC)
   typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -170,7 +173,7 @@ __device__ __forceinline__ uint4 tile_ld(const uint4 *p) {
 #endif
 }
 __device__ __forceinline__ void tile_st(uint4 *g, uint32_t c, uint4 v) {
-#if defined(VP_ABL_SC1ST) || defined(VP_ABL_NTSC)
+#ifndef VP_ABL_WBST
   typedef unsigned v4u __attribute__((ext_vector_type(4)));
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(g, 0, 4096, 0x00020000);
   const v4u x = {v.x, v.y, v.z, v.w};

@@ -432,7 +432,7 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     VP_TRY(tbl_late_touches(c, t, bp.bins.oent, bp.bins.ocnt, 0, range64, grid64,
                             w.log, now, seq0));
   float kms = 0.f;
-  VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
+  VP_HIP(event_ms(c->ev0, c->ev1, &kms));
   *ms += kms;
   *launches += 1;
   const uint32_t nmiss = t.h_ctl.miss_count, ndefer = t.h_ctl.defer_count;

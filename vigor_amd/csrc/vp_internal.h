@@ -29,6 +29,7 @@ int hip_fail(hipError_t e, const char *what, const char *file, int line);
 // as DPDK's lcores do): a blocking wait adds tens of microseconds of wake-up
 // latency to every batch's control-block read-back.
 hipError_t stream_wait(hipStream_t s);
+hipError_t event_ms(hipEvent_t a, hipEvent_t b, float *ms);
 
 struct Comm;  // vp_comm.hip: collectives between the ranks of one NF
 constexpr int kMaxRanks = 64;
@@ -82,6 +83,7 @@ struct FlowTable {
   Ctl h_ctl{};                     // last copy read back
   Ctl *h_pin = nullptr;            // page-locked landing buffer for h_ctl
   CtlPub *h_pub = nullptr;         // host-coherent page, written by the fold
+  CtlPub *d_pub = nullptr;         // (its device address)
   uint32_t pub_epoch = 0;          // last epoch asked of the fold
   uint32_t *ttotal = nullptr;  // touch-reduce entry count (device)
   uint64_t ts_floor = UINT64_MAX;  // lower bound of min ts over live indices
@@ -153,7 +155,8 @@ struct Workspace {
   uint32_t d_meta_n = 0;
   // pipelined host batches (vp_process_host): copy stream, per-buffer
   // events, pinned staging of the small per-packet arrays
-  hipStream_t cstream = nullptr;
+  hipStream_t cstream = nullptr;  // host -> device copies
+  hipStream_t dstream = nullptr;  // device -> host copies (PCIe is full duplex)
   hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr},
              ev_out[2] = {nullptr, nullptr};
   uint8_t *h_meta = nullptr;
@@ -168,6 +171,10 @@ struct vp_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t evc = nullptr;  // control-block copy (read_ctl_post / _wait)
+  // host copy of the current device batch's time array (host_pipeline sets it
+  // for the chunk it hands to vp_process_device): the batch driver reads its
+  // expiry cuts from it instead of copying the array back
+  const int64_t *host_now = nullptr;
   hipEvent_t ev2 = nullptr, ev3 = nullptr;  // owner mode: pass 2 timing
   // The last segment left only its timestamp fold running on `stream`
   // (results complete): run_batch returns without waiting for it.

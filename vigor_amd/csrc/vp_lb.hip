@@ -584,7 +584,7 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     VP_TRY(tbl_touch_reduce(c, c->ft, w.log, p0, p1, now, c->seq));
   VP_TRY(read_ctl2_wait(c, c->ft2, c->ft));
   float kms = 0.f;
-  VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
+  VP_HIP(event_ms(c->ev0, c->ev1, &kms));
   *ms += kms;
   *launches += 1;
   const uint32_t nm = c->ft.h_ctl.miss_count, ns = c->ft.h_ctl.defer_count;

@@ -1215,8 +1215,8 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   pm.mark();
   pm.print(m.r, np);
   float k1 = 0.f, k2 = 0.f;
-  VP_HIP(hipEventElapsedTime(&k1, c->ev0, c->ev1));
-  VP_HIP(hipEventElapsedTime(&k2, c->ev2, c->ev3));
+  VP_HIP(event_ms(c->ev0, c->ev1, &k1));
+  VP_HIP(event_ms(c->ev2, c->ev3, &k2));
   ph->ms = k1 + k2;
   return 0;
 }
@@ -1290,7 +1290,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // applied on top of it afterwards as late touches (tbl_late_touches: last
   // toucher still wins).
   VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, seq0));
-  VP_HIP(hipEventElapsedTime(&ph.ms, c->ev0, c->ev1));
+  VP_HIP(event_ms(c->ev0, c->ev1, &ph.ms));
   }  // !owner
   a.own.n = 0;  // below: this rank's own table only
   const uint32_t nre = t.h_ctl.reprobe_count;

@@ -396,7 +396,7 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   }
   VP_TRY(read_ctl(c, t));
   float kms = 0.f;
-  VP_HIP(hipEventElapsedTime(&kms, c->ev0, c->ev1));
+  VP_HIP(event_ms(c->ev0, c->ev1, &kms));
   *ms += kms;
   *launches += 1;
   const uint32_t nmiss = t.h_ctl.miss_count, ndefer = t.h_ctl.defer_count;

@@ -48,6 +48,14 @@ hipError_t stream_wait(hipStream_t s) {
   return e;
 }
 
+// Kernel time between two events of the context's stream. The host may learn
+// that the work behind `b` ran (a published control block) before the
+// runtime has marked `b` complete, so wait for `b` first.
+hipError_t event_ms(hipEvent_t a, hipEvent_t b, float *ms) {
+  const hipError_t e = hipEventSynchronize(b);
+  return e != hipSuccess ? e : hipEventElapsedTime(ms, a, b);
+}
+
 static bool is_pow2(uint32_t v) { return v && !(v & (v - 1)); }
 
 template <class T>
@@ -169,6 +177,7 @@ static void free_all(vp_ctx *c) {
     if (w.ev_out[i]) hipEventDestroy(w.ev_out[i]);
   }
   if (w.cstream) hipStreamDestroy(w.cstream);
+  if (w.dstream) hipStreamDestroy(w.dstream);
   delete c->comm;
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
@@ -331,11 +340,15 @@ static bool is_pinned(const void *p) {
   return a.type == hipMemoryTypeHost;
 }
 
-// Host batch in chunks of `ch` packets, double-buffered in HBM: a copy
-// stream moves chunk k+1 in and chunk k-1 out while chunk k is processed
-// (chunks are processed in order, so results equal one call on the batch).
-// Pinned frames are DMA'd in place; pageable ones through pinned staging.
-// The small per-packet arrays always go through pinned staging.
+// Host batch in chunks of `ch` packets, double-buffered in HBM: one copy
+// stream moves chunk k+1 in while another moves chunk k-1 out (PCIe carries
+// both directions at once) and chunk k is processed (chunks are processed in
+// order, so results equal one call on the batch). Chunk k's work is enqueued
+// before the host waits for chunk k-1's results, so the GPU never idles on
+// the host. Pinned frames are DMA'd in place; pageable ones through pinned
+// staging. The small per-packet arrays always go through pinned staging; the
+// host's copy of the time array serves the batch driver's expiry cuts
+// (vp_ctx::host_now), so it is not read back.
 static int host_pipeline(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
                          uint8_t *frames, uint32_t slot, const uint16_t *len,
                          const int64_t *now, uint16_t *out_dev) {
@@ -374,6 +387,7 @@ static int host_pipeline(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
   }
   if (!w.cstream) {
     VP_HIP(hipStreamCreateWithFlags(&w.cstream, hipStreamNonBlocking));
+    VP_HIP(hipStreamCreateWithFlags(&w.dstream, hipStreamNonBlocking));
     for (int i = 0; i < 2; i++) {
       VP_HIP(hipEventCreateWithFlags(&w.ev_in[i], hipEventDisableTiming));
       VP_HIP(hipEventCreateWithFlags(&w.ev_done[i], hipEventDisableTiming));
@@ -417,7 +431,6 @@ static int host_pipeline(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
   VP_TRY(issue_in(0));
   for (uint32_t k = 0; k < K; k++) {
     const uint32_t i = k & 1, m = cnt(k);
-    if (k + 1 < K) VP_TRY(issue_in(k + 1));
     VP_HIP(hipStreamWaitEvent(c->stream, w.ev_in[i], 0));
     vp_dev_batch b{};
     b.frames = dfr(k);
@@ -427,14 +440,18 @@ static int host_pipeline(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
     b.in_dev = w.d_in + i * ch;
     b.now = w.d_now + i * ch;
     b.out_dev = w.d_out + i * ch;
-    VP_TRY(vp_process_device(c, &b, nullptr));
+    c->host_now = now + (size_t)k * ch;
+    const int rc = vp_process_device(c, &b, nullptr);
+    c->host_now = nullptr;
+    VP_TRY(rc);
     VP_HIP(hipEventRecord(w.ev_done[i], c->stream));
-    VP_HIP(hipStreamWaitEvent(w.cstream, w.ev_done[i], 0));
+    VP_HIP(hipStreamWaitEvent(w.dstream, w.ev_done[i], 0));
     VP_HIP(hipMemcpyAsync(hfr(k), dfr(k), (size_t)m * slot, hipMemcpyDeviceToHost,
-                          w.cstream));
+                          w.dstream));
     VP_HIP(hipMemcpyAsync(hm(k) + 12ull * ch, w.d_out + i * ch, 2ull * m,
-                          hipMemcpyDeviceToHost, w.cstream));
-    VP_HIP(hipEventRecord(w.ev_out[i], w.cstream));
+                          hipMemcpyDeviceToHost, w.dstream));
+    VP_HIP(hipEventRecord(w.ev_out[i], w.dstream));
+    if (k + 1 < K) VP_TRY(issue_in(k + 1));  // (waits for chunk k-1's results)
   }
   for (uint32_t k = K >= 2 ? K - 2 : 0; k < K; k++) VP_TRY(retire(k));
   return 0;

@@ -62,13 +62,19 @@ struct PubArgs {
   const Ctl *ctl;
   uint32_t epoch;
 };
+static_assert(sizeof(Ctl) % 8 == 0, "Ctl is published as 8-byte words");
 __device__ __forceinline__ void ctl_publish(const PubArgs &a) {
   if (!a.pub) return;
-  const uint32_t *s = reinterpret_cast<const uint32_t *>(a.ctl);
-  uint32_t *d = reinterpret_cast<uint32_t *>(&a.pub->ctl);
-  for (uint32_t i = 0; i < sizeof(Ctl) / 4; i++)
-    __hip_atomic_store(d + i, __hip_atomic_load(s + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  constexpr uint32_t kW = sizeof(Ctl) / 8;
+  const uint64_t *s = reinterpret_cast<const uint64_t *>(a.ctl);
+  uint64_t *d = reinterpret_cast<uint64_t *>(&a.pub->ctl);
+  uint64_t v[kW];  // all loads issued before the first store waits
+#pragma unroll
+  for (uint32_t i = 0; i < kW; i++)
+    v[i] = __hip_atomic_load(s + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (uint32_t i = 0; i < kW; i++)
+    __hip_atomic_store(d + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&a.pub->epoch, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 

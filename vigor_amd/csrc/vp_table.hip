@@ -9,6 +9,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -183,6 +184,7 @@ int tbl_alloc(vp_ctx *c, FlowTable &t, uint32_t cap) {
   VP_HIP(hipHostMalloc((void **)&t.h_pub, sizeof(CtlPub),
                        hipHostMallocMapped | hipHostMallocCoherent));
   memset(t.h_pub, 0, sizeof(CtlPub));
+  VP_HIP(hipHostGetDevicePointer((void **)&t.d_pub, t.h_pub, 0));
   VP_TRY(dalloc(&t.ttotal, 1));
   VP_TRY(dalloc(&t.ekey, cap));
   VP_TRY(dalloc(&t.ekey2, cap));
@@ -781,17 +783,19 @@ int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_
     VP_TRY(tbl_touch_reduce(c, t, log, p0, p1, now, seq_base));
     return read_ctl_wait(c, t);
   }
-  CtlPub *dpub = nullptr;
-  VP_HIP(hipHostGetDevicePointer((void **)&dpub, t.h_pub, 0));
   const uint32_t epoch = ++t.pub_epoch;
-  VP_TRY(bins_reduce(c, t, bp, p0, now, seq_base, PubArgs{dpub, t.ctl, epoch}));
+  VP_TRY(bins_reduce(c, t, bp, p0, now, seq_base, PubArgs{t.d_pub, t.ctl, epoch}));
   // poll the epoch; a stream that ends (or fails) without it is an error
   for (uint32_t spin = 1;; spin++) {
     if (__atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE) == epoch) break;
     if ((spin & 1023) == 0) {
       const hipError_t e = hipStreamQuery(c->stream);
-      if (e == hipSuccess && __atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE) != epoch)
+      if (e == hipSuccess && __atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE) != epoch) {
+        if (getenv("VIGPATH_DEBUG"))
+          fprintf(stderr, "vigpath: fold ended without publishing epoch %u (seen %u)\n",
+                  epoch, __atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE));
         return VP_EIO;
+      }
       if (e != hipSuccess && e != hipErrorNotReady) VP_HIP(e);
     }
   }
@@ -1068,13 +1072,17 @@ int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
     return VP_EINVAL;
   VP_TRY(ws_reserve(c, n));
 
-  std::vector<int64_t> h_now;
+  std::vector<int64_t> h_copy;
+  const int64_t *h_now = c->host_now;  // the caller's host copy, if any
   int64_t t_first, t_last;
   if (b->now) {
-    h_now.resize(n);
-    VP_HIP(hipMemcpyAsync(h_now.data(), b->now, sizeof(int64_t) * (size_t)n,
-                          hipMemcpyDeviceToHost, c->stream));
-    VP_HIP(hipStreamSynchronize(c->stream));
+    if (!h_now) {
+      h_copy.resize(n);
+      VP_HIP(hipMemcpyAsync(h_copy.data(), b->now, sizeof(int64_t) * (size_t)n,
+                            hipMemcpyDeviceToHost, c->stream));
+      VP_HIP(hipStreamSynchronize(c->stream));
+      h_now = h_copy.data();
+    }
     for (uint32_t i = 1; i < n; i++)
       if (h_now[i] < h_now[i - 1]) return VP_ENOTSUP;
     t_first = h_now[0];
