@@ -169,6 +169,15 @@ int vp_process_host(vp_ctx *ctx, uint32_t n, const uint16_t *in_dev,
                     uint8_t *frames, uint32_t slot, const uint16_t *len,
                     const int64_t *now, uint16_t *out_dev);
 
+/* The same with every field of vp_dev_batch, as host pointers: time is
+ * now[i], or now0 + i * now_step when now is NULL (nf.c stamps every packet
+ * of one polling sweep with one current_time(), nf.c:56: now_step 0). Arrays
+ * in page-locked memory (hipHostMalloc / hipHostRegister, e.g. a DPDK
+ * hugepage pool) are DMA'd in place, others staged through pinned memory.
+ * Frames and out_dev hold the results when the call returns. */
+typedef vp_dev_batch vp_host_batch;
+int vp_process_host_batch(vp_ctx *ctx, const vp_host_batch *batch);
+
 /* -------------------------------------------------------- multi-GPU -- *
  * One vignat instance over N GPUs (one process and one context per GPU),
  * identical to a single nf.c processing the concatenation of the ranks'

@@ -179,6 +179,40 @@ def test_host_pipeline_chunks(pinned, monkeypatch):
     check_state(nat, o, 256)
 
 
+@pytest.mark.parametrize("pinned,affine", [(False, False), (True, False),
+                                           (True, True), (False, True)])
+def test_host_batch_entry(pinned, affine, monkeypatch):
+    """vp_process_host_batch: every per-packet array page-locked (DMA'd in
+    place) or pageable (staged), time per packet or affine (nf.c's one
+    current_time() per sweep is now_step 0), several chunks."""
+    import torch
+    monkeypatch.setenv("VIGPATH_HOST_CHUNK", "700")
+    rng = np.random.default_rng(23)
+    fr, ln, dv, now = mixed_nat_trace(rng, 5000, 200, max_idx=256)
+    if affine:  # churn with one stamp per 64-packet sweep
+        now = (now[0] + (np.arange(len(now)) // 64) * 3000).astype(np.int64)
+    nat, o = make_pair(max_flows=256, expire_us=3)
+    exp = fr.copy()
+    exp_out = o.run(exp, ln, dv, now, 64)
+
+    def host(a):
+        if not pinned:
+            return a.copy()
+        return torch.from_numpy(a.copy()).pin_memory().numpy()
+    got, lens, ind = host(fr), host(ln), host(dv)
+    out = host(np.zeros(len(ln), np.uint16))
+    if affine:  # one call per 64-packet sweep, its packets stamped alike
+        for s in range(0, len(ln), 64):
+            e = min(len(ln), s + 64)
+            nat.process_host_batch(got[s * 64:e * 64], lens[s:e], ind[s:e], out[s:e],
+                                   64, now0=int(now[s]), now_step=0)
+    else:
+        nat.process_host_batch(got, lens, ind, out, 64, now=host(now))
+    np.testing.assert_array_equal(out, exp_out)
+    np.testing.assert_array_equal(got, exp)
+    check_state(nat, o, 256)
+
+
 @pytest.mark.parametrize("n_flows,order", [(4096, "uniform"), (3, "rr"),
                                           (1 << 16, "rr")])
 def test_touch_bins_steady_state(n_flows, order):

@@ -102,7 +102,7 @@ class DevBatchC(C.Structure):
 # every symbol include/vigpath.h declares
 EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_fw_create",
            "vp_pol_create", "vp_pol_dump", "vp_destroy", "vp_process_device", "vp_process_batch",
-           "vp_process_host", "vp_nat_dump", "vp_bridge_dump", "vp_lb_dump",
+           "vp_process_host", "vp_process_host_batch", "vp_nat_dump", "vp_bridge_dump", "vp_lb_dump",
            "vp_fw_dump", "vp_comm_unique_id", "vp_attach_rccl",
            "vp_attach_comm", "vp_shard_mode", "vp_sync_state", "vp_live_count",
            "vp_last_kernel_ms", "vp_version"]
@@ -147,6 +147,8 @@ def lib(path: str | None = None):
                                   C.c_void_p, C.c_uint32, C.c_void_p,
                                   C.c_void_p, C.c_void_p]
     L.vp_process_host.restype = C.c_int
+    L.vp_process_host_batch.argtypes = [C.c_void_p, C.POINTER(DevBatchC)]
+    L.vp_process_host_batch.restype = C.c_int
     L.vp_process_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p,
                                    C.POINTER(C.c_void_p), C.c_void_p,
                                    C.c_void_p, C.c_void_p]

@@ -157,8 +157,7 @@ struct Workspace {
   // events, pinned staging of the small per-packet arrays
   hipStream_t cstream = nullptr;  // host -> device copies
   hipStream_t dstream = nullptr;  // device -> host copies (PCIe is full duplex)
-  hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr},
-             ev_out[2] = {nullptr, nullptr};
+  hipEvent_t ev_in[3] = {}, ev_done[3] = {}, ev_out[3] = {};  // per buffer set
   uint8_t *h_meta = nullptr;
   size_t h_meta_bytes = 0;
 };

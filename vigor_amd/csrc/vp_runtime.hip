@@ -171,7 +171,7 @@ static void free_all(vp_ctx *c) {
   if (w.h_tot) hipHostFree(w.h_tot);
   if (w.h_frames) hipHostFree(w.h_frames);
   if (w.h_meta) hipHostFree(w.h_meta);
-  for (int i = 0; i < 2; i++) {
+  for (int i = 0; i < 3; i++) {
     if (w.ev_in[i]) hipEventDestroy(w.ev_in[i]);
     if (w.ev_done[i]) hipEventDestroy(w.ev_done[i]);
     if (w.ev_out[i]) hipEventDestroy(w.ev_out[i]);
@@ -340,28 +340,33 @@ static bool is_pinned(const void *p) {
   return a.type == hipMemoryTypeHost;
 }
 
-// Host batch in chunks of `ch` packets, double-buffered in HBM: one copy
-// stream moves chunk k+1 in while another moves chunk k-1 out (PCIe carries
-// both directions at once) and chunk k is processed (chunks are processed in
-// order, so results equal one call on the batch). Chunk k's work is enqueued
-// before the host waits for chunk k-1's results, so the GPU never idles on
-// the host. Pinned frames are DMA'd in place; pageable ones through pinned
-// staging. The small per-packet arrays always go through pinned staging; the
-// host's copy of the time array serves the batch driver's expiry cuts
-// (vp_ctx::host_now), so it is not read back.
-static int host_pipeline(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
-                         uint8_t *frames, uint32_t slot, const uint16_t *len,
-                         const int64_t *now, uint16_t *out_dev) {
+// Host batch in chunks of `ch` packets, three buffer sets in HBM: one copy
+// stream moves chunks k+1 and k+2 in while another moves chunk k-1 out (PCIe
+// carries both directions at once: 48.6 GB/s each way together, 57 GB/s
+// alone, tools/pcie_probe.hip) and chunk k is processed (chunks are processed
+// in order, so results equal one call on the batch). Chunk k+2's copy is
+// enqueued while chunk k is processed, so the host->device engine never
+// waits for the host (vp_process_device returns only once phase A's counts
+// are known). Page-locked arrays (hipHostMalloc'd or hipHostRegister'ed, e.g. a
+// DPDK hugepage mbuf pool) are DMA'd in place; pageable ones go through
+// pinned staging. With a time array, the host's copy serves the batch
+// driver's expiry cuts (vp_ctx::host_now), so it is not read back; with
+// affine time (now == NULL) no time crosses PCIe at all.
+static int host_pipeline(vp_ctx *c, const vp_host_batch *hb) {
   Workspace &w = c->ws;
+  const uint32_t n = hb->n, slot = hb->slot;
   const char *env = getenv("VIGPATH_HOST_CHUNK");
   uint32_t ch = env ? (uint32_t)atoi(env) : (1u << 20);
   if (ch == 0) ch = 1u << 20;
   ch = std::min(ch, n);
   const uint32_t K = (n + ch - 1) / ch;
-  const bool pinned = is_pinned(frames);
-  VP_TRY(stage_meta(c, 2 * ch));
-  {  // device frames (2 chunks); pinned staging only for pageable frames
-    const size_t bytes = 2ull * ch * slot;
+  const bool pin_fr = is_pinned(hb->frames), pin_len = is_pinned(hb->len),
+             pin_in = is_pinned(hb->in_dev), pin_out = is_pinned(hb->out_dev),
+             pin_now = hb->now && is_pinned(hb->now);
+  constexpr uint32_t S = 3;  // buffer sets
+  VP_TRY(stage_meta(c, S * ch));
+  {  // device frames (S chunks); pinned staging only for pageable frames
+    const size_t bytes = (size_t)S * ch * slot;
     if (bytes > w.d_frames_bytes) {
       hipFree(w.d_frames);
       w.d_frames = nullptr;
@@ -369,7 +374,7 @@ static int host_pipeline(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
       VP_HIP(hipMalloc((void **)&w.d_frames, bytes));
       w.d_frames_bytes = bytes;
     }
-    if (!pinned && bytes > w.h_frames_bytes) {
+    if (!pin_fr && bytes > w.h_frames_bytes) {
       if (w.h_frames) hipHostFree(w.h_frames);
       w.h_frames = nullptr;
       w.h_frames_bytes = 0;
@@ -378,59 +383,69 @@ static int host_pipeline(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
     }
   }
   const size_t meta = 14ull * ch;  // len 2 + in 2 + now 8 + out 2 per packet
-  if (2 * meta > w.h_meta_bytes) {
+  if (S * meta > w.h_meta_bytes) {
     if (w.h_meta) hipHostFree(w.h_meta);
     w.h_meta = nullptr;
     w.h_meta_bytes = 0;
-    VP_HIP(hipHostMalloc((void **)&w.h_meta, 2 * meta, hipHostMallocDefault));
-    w.h_meta_bytes = 2 * meta;
+    VP_HIP(hipHostMalloc((void **)&w.h_meta, S * meta, hipHostMallocDefault));
+    w.h_meta_bytes = S * meta;
   }
   if (!w.cstream) {
     VP_HIP(hipStreamCreateWithFlags(&w.cstream, hipStreamNonBlocking));
     VP_HIP(hipStreamCreateWithFlags(&w.dstream, hipStreamNonBlocking));
-    for (int i = 0; i < 2; i++) {
+    for (uint32_t i = 0; i < S; i++) {
       VP_HIP(hipEventCreateWithFlags(&w.ev_in[i], hipEventDisableTiming));
       VP_HIP(hipEventCreateWithFlags(&w.ev_done[i], hipEventDisableTiming));
       VP_HIP(hipEventCreateWithFlags(&w.ev_out[i], hipEventDisableTiming));
     }
   }
   auto cnt = [&](uint32_t k) { return std::min(ch, n - k * ch); };
-  auto hm = [&](uint32_t k) { return w.h_meta + (k & 1) * meta; };
-  auto dfr = [&](uint32_t k) { return w.d_frames + (size_t)(k & 1) * ch * slot; };
+  auto hm = [&](uint32_t k) { return w.h_meta + (k % S) * meta; };
+  auto dfr = [&](uint32_t k) { return w.d_frames + (size_t)(k % S) * ch * slot; };
   auto hfr = [&](uint32_t k) {
-    return pinned ? frames + (size_t)k * ch * slot
-                  : w.h_frames + (size_t)(k & 1) * ch * slot;
+    return pin_fr ? hb->frames + (size_t)k * ch * slot
+                  : w.h_frames + (size_t)(k % S) * ch * slot;
+  };
+  // where chunk k's out ports land on the host
+  auto hout = [&](uint32_t k) {
+    return pin_out ? hb->out_dev + (size_t)k * ch
+                   : reinterpret_cast<uint16_t *>(hm(k) + 12ull * ch);
+  };
+  // a per-packet array's chunk k: the caller's page-locked memory itself, or
+  // a staged copy at offset `at` of the chunk's meta block
+  auto src = [&](const void *arr, bool pinned, size_t esz, size_t at, uint32_t k) {
+    const uint8_t *a = static_cast<const uint8_t *>(arr) + (size_t)k * ch * esz;
+    if (pinned) return a;
+    memcpy(hm(k) + at, a, esz * cnt(k));
+    return static_cast<const uint8_t *>(hm(k) + at);
   };
   // chunk k's results back to the caller (after its D2H completed)
   auto retire = [&](uint32_t k) -> int {
-    VP_HIP(hipEventSynchronize(w.ev_out[k & 1]));
+    VP_HIP(hipEventSynchronize(w.ev_out[k % S]));
     const uint32_t m = cnt(k);
-    if (!pinned) memcpy(frames + (size_t)k * ch * slot, hfr(k), (size_t)m * slot);
-    memcpy(out_dev + (size_t)k * ch, hm(k) + 12ull * ch, 2ull * m);
+    if (!pin_fr) memcpy(hb->frames + (size_t)k * ch * slot, hfr(k), (size_t)m * slot);
+    if (!pin_out) memcpy(hb->out_dev + (size_t)k * ch, hout(k), 2ull * m);
     return 0;
   };
   auto issue_in = [&](uint32_t k) -> int {
-    const uint32_t m = cnt(k), o = k * ch, i = k & 1;
-    if (k >= 2) VP_TRY(retire(k - 2));  // frees buffer set k & 1
-    uint8_t *h = hm(k);
-    memcpy(h, len + o, 2ull * m);
-    memcpy(h + 2ull * ch, in_dev + o, 2ull * m);
-    memcpy(h + 4ull * ch, now + o, 8ull * m);
-    if (!pinned) memcpy(hfr(k), frames + (size_t)o * slot, (size_t)m * slot);
+    const uint32_t m = cnt(k), o = k * ch, i = k % S;
+    if (k >= S) VP_TRY(retire(k - S));  // frees buffer set k % S
+    if (!pin_fr) memcpy(hfr(k), hb->frames + (size_t)o * slot, (size_t)m * slot);
     VP_HIP(hipMemcpyAsync(dfr(k), hfr(k), (size_t)m * slot, hipMemcpyHostToDevice,
                           w.cstream));
-    VP_HIP(hipMemcpyAsync(w.d_len + i * ch, h, 2ull * m, hipMemcpyHostToDevice,
-                          w.cstream));
-    VP_HIP(hipMemcpyAsync(w.d_in + i * ch, h + 2ull * ch, 2ull * m,
+    VP_HIP(hipMemcpyAsync(w.d_len + i * ch, src(hb->len, pin_len, 2, 0, k), 2ull * m,
                           hipMemcpyHostToDevice, w.cstream));
-    VP_HIP(hipMemcpyAsync(w.d_now + i * ch, h + 4ull * ch, 8ull * m,
-                          hipMemcpyHostToDevice, w.cstream));
+    VP_HIP(hipMemcpyAsync(w.d_in + i * ch, src(hb->in_dev, pin_in, 2, 2ull * ch, k),
+                          2ull * m, hipMemcpyHostToDevice, w.cstream));
+    if (hb->now)
+      VP_HIP(hipMemcpyAsync(w.d_now + i * ch, src(hb->now, pin_now, 8, 4ull * ch, k),
+                            8ull * m, hipMemcpyHostToDevice, w.cstream));
     VP_HIP(hipEventRecord(w.ev_in[i], w.cstream));
     return 0;
   };
-  VP_TRY(issue_in(0));
+  for (uint32_t k = 0; k < std::min(K, S - 1); k++) VP_TRY(issue_in(k));
   for (uint32_t k = 0; k < K; k++) {
-    const uint32_t i = k & 1, m = cnt(k);
+    const uint32_t i = k % S, m = cnt(k);
     VP_HIP(hipStreamWaitEvent(c->stream, w.ev_in[i], 0));
     vp_dev_batch b{};
     b.frames = dfr(k);
@@ -438,9 +453,11 @@ static int host_pipeline(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
     b.n = m;
     b.len = w.d_len + i * ch;
     b.in_dev = w.d_in + i * ch;
-    b.now = w.d_now + i * ch;
+    b.now = hb->now ? w.d_now + i * ch : nullptr;
+    b.now0 = hb->now0 + (int64_t)k * ch * hb->now_step;
+    b.now_step = hb->now_step;
     b.out_dev = w.d_out + i * ch;
-    c->host_now = now + (size_t)k * ch;
+    c->host_now = hb->now ? hb->now + (size_t)k * ch : nullptr;
     const int rc = vp_process_device(c, &b, nullptr);
     c->host_now = nullptr;
     VP_TRY(rc);
@@ -448,12 +465,12 @@ static int host_pipeline(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
     VP_HIP(hipStreamWaitEvent(w.dstream, w.ev_done[i], 0));
     VP_HIP(hipMemcpyAsync(hfr(k), dfr(k), (size_t)m * slot, hipMemcpyDeviceToHost,
                           w.dstream));
-    VP_HIP(hipMemcpyAsync(hm(k) + 12ull * ch, w.d_out + i * ch, 2ull * m,
-                          hipMemcpyDeviceToHost, w.dstream));
+    VP_HIP(hipMemcpyAsync(hout(k), w.d_out + i * ch, 2ull * m, hipMemcpyDeviceToHost,
+                          w.dstream));
     VP_HIP(hipEventRecord(w.ev_out[i], w.dstream));
-    if (k + 1 < K) VP_TRY(issue_in(k + 1));  // (waits for chunk k-1's results)
+    if (k + S - 1 < K) VP_TRY(issue_in(k + S - 1));  // (waits for chunk k-1's results)
   }
-  for (uint32_t k = K >= 2 ? K - 2 : 0; k < K; k++) VP_TRY(retire(k));
+  for (uint32_t k = K >= S ? K - S : 0; k < K; k++) VP_TRY(retire(k));
   return 0;
 }
 
@@ -624,15 +641,29 @@ static int run_staged(vp_ctx *c, uint32_t n, uint32_t slot, const uint16_t *in_d
   return 0;
 }
 
+int vp_process_host_batch(vp_ctx *c, const vp_host_batch *b) {
+  if (!c || !b) return VP_EINVAL;
+  if (b->n && (!b->in_dev || !b->frames || !b->len || !b->out_dev)) return VP_EINVAL;
+  if (b->n == 0) return 0;
+  if (b->slot < 64 || (b->slot & 15)) return VP_EINVAL;
+  if (!b->now && (b->now_step < 0 || b->now0 < 0)) return VP_ENOTSUP;
+  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  return host_pipeline(c, b);
+}
+
 int vp_process_host(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
                     uint8_t *frames, uint32_t slot, const uint16_t *len,
                     const int64_t *now, uint16_t *out_dev) {
-  if (!c || (n && (!in_dev || !frames || !len || !now || !out_dev)))
-    return VP_EINVAL;
-  if (n == 0) return 0;
-  if (slot < 64 || (slot & 15)) return VP_EINVAL;
-  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
-  return host_pipeline(c, n, in_dev, frames, slot, len, now, out_dev);
+  if (!c || (n && !now)) return VP_EINVAL;
+  vp_host_batch b{};
+  b.frames = frames;
+  b.slot = slot;
+  b.n = n;
+  b.len = len;
+  b.in_dev = in_dev;
+  b.now = now;
+  b.out_dev = out_dev;
+  return vp_process_host_batch(c, &b);
 }
 
 int vp_process_batch(vp_ctx *c, uint32_t n, const uint16_t *in_dev,

@@ -726,8 +726,10 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   const uint32_t L = (uint32_t)in_bin(bbits);
   const uint32_t pbits = std::max<uint32_t>(1, ceil_log2(range));
   if (L > kBinLocalMax || ceil_log2(L) + pbits > 32) return 0;
-  // twice a uniform share of a block's packets per bin, in 64-entry lines
-  const uint32_t cap = ((2 * range / nbins + 32) + 15) & ~15u;
+  // twice a uniform share of a block's packets per bin, and at least two
+  // waves' worth (a wave touching 64 consecutive indices fills one bin)
+  const uint32_t cap =
+      std::max<uint32_t>(((2 * range / nbins + 32) + 15) & ~15u, 2 * kBinRun);
   const size_t ne = (size_t)grid * nbins * cap, nc = (size_t)grid * nbins;
   if (ne > w.bins_ent_n) {
     VP_HIP(hipStreamSynchronize(c->stream));

@@ -87,6 +87,25 @@ class NfBase:
                "vp_process_host")
         return out
 
+    def process_host_batch(self, frames: np.ndarray, lens, in_dev, out, slot: int,
+                           now=None, now0: int = 0, now_step: int = 0):
+        """vp_process_host_batch: host numpy arrays (page-locked ones, e.g.
+        torch.pin_memory() views, are DMA'd in place), rewritten in place;
+        out (u16/i16, n) receives the out ports. now: int64 array, or None
+        for now0 + i * now_step."""
+        n = int(lens.shape[0])
+        assert frames.dtype == np.uint8 and frames.flags.c_contiguous
+        assert frames.size == n * slot and out.shape[0] == n
+        for a in (lens, in_dev, out):
+            assert a.flags.c_contiguous and a.itemsize == 2
+        if now is not None:
+            assert now.dtype == np.int64 and now.flags.c_contiguous
+        b = DevBatchC(frames=frames.ctypes.data, slot=slot, n=n, len=lens.ctypes.data,
+                      in_dev=in_dev.ctypes.data,
+                      now=now.ctypes.data if now is not None else None,
+                      now0=now0, now_step=now_step, out_dev=out.ctypes.data)
+        _check(self.L.vp_process_host_batch(self.h, C.byref(b)), "vp_process_host_batch")
+
     def process_mbufs(self, bufs, in_dev, now):
         """Per-frame host buffers (bytearray each, mbuf-like), rewritten in
         place. Returns out_dev."""
