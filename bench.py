@@ -13,15 +13,18 @@ rate is reported as new_flow_mpps).
 
 N > 1 (torch.distributed, one rank per GPU; BASELINE configs[4]): ONE vignat
 over all GPUs with 16M flows; every global batch is N x B packets and rank r
-ingests its contiguous slice r (B packets, weak scaling). By default the
-flow dictionary is sharded by flow hash (--shard-mode owner, north_star):
-LAN packets whose key another GPU owns are looked up there through an RCCL
-all-to-all of 16-byte keys and 4-byte answers over xGMI; new flows are
-all-gathered so every rank allocates identically (--shard-mode replicated
-keeps a whole dictionary per GPU instead). Results equal one nf.c over the
-concatenated batch (tests/test_shard_gpu.py). value = all
-ranks' packets / max-over-ranks time. `--gpus N` without a torch.distributed
-environment starts the N ranks itself.
+ingests its contiguous slice r (B packets, weak scaling). By default every
+GPU holds the whole flow dictionary (--shard-mode replicated): steady-state
+packets need no data-path collective, only small all-gathers per batch, and
+new flows are all-gathered so every rank allocates identically.
+--shard-mode owner shards the dictionary by flow hash (north_star): LAN
+packets whose key another GPU owns are looked up there through an RCCL
+all-to-all of 16-byte keys and 4-byte answers over xGMI, at the price of a
+second pass over the frames (DESIGN.md §6.1 measures both). Results equal
+one nf.c over the concatenated batch in both modes (DESIGN.md §6,
+tests/test_shard_gpu.py). value = all ranks' packets / max-over-ranks time.
+`--gpus N` without a torch.distributed environment starts the N ranks
+itself.
 
 Also reported:
   roofline      algorithmic HBM-read bytes per packet (92 B)
@@ -212,9 +215,11 @@ def main():
                     help="default: 1M (config 2) on one GPU, 16M (config 5) "
                          "over N > 1 GPUs")
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
-    ap.add_argument("--shard-mode", choices=("owner", "replicated"), default="owner",
-                    help="N > 1: flow dictionary sharded by flow hash (owner) "
-                         "or replicated on every GPU")
+    ap.add_argument("--shard-mode", choices=("owner", "replicated"), default="replicated",
+                    help="N > 1: flow dictionary replicated on every GPU (no "
+                         "data-path collective; the faster one, DESIGN.md §6.1) "
+                         "or sharded by flow hash with an all-to-all of keys "
+                         "and answers (owner)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the host-resident end-to-end rate")
