@@ -8,7 +8,7 @@ import pytest
 import orc
 import vigor_amd
 from gpuh import check_batches, run_gpu
-from tracegen import edge_nat_trace, mixed_nat_trace
+from tracegen import edge_nat_trace, lan_tile_trace, mixed_nat_trace
 from vigor_amd import traces as T
 
 pytestmark = pytest.mark.gpu
@@ -282,3 +282,22 @@ def test_now_buffer_reusable_after_return():
     del nt
     torch.cuda.synchronize()
     check_state(nat, o, 1 << 16)
+
+
+@pytest.mark.parametrize("max_flows,n_flows,expire_us,mix", [
+    (4096, 3000, 60_000_000, "0"),   # misses in lean tiles, then hits
+    (256, 400, 60_000_000, "0"),     # table full inside lean tiles
+    (1024, 900, 2, "0"),             # expiry between lean tiles
+    (4096, 3000, 60_000_000, "1"),   # multiplicative home buckets: reprobes
+])
+def test_lean_tiles(max_flows, n_flows, expire_us, mix, monkeypatch):
+    """The classify kernel's lean tile (every lane a fast-path LAN packet:
+    batched CRC reads, branch-free bucket match, whole-tile store) beside
+    per-lane tiles (one malformed packet each), TCP and UDP, with new flows,
+    a full table, expiry and reprobes; several batches."""
+    monkeypatch.setenv("VIGPATH_MIX", mix)
+    rng = np.random.default_rng(max_flows + n_flows)
+    fr, ln, dv, now = lan_tile_trace(rng, 40_000, n_flows)
+    nat, o = make_pair(max_flows=max_flows, expire_us=expire_us)
+    check_batches(nat, o, fr, ln, dv, now, 64, [4096, 4100, 20_000])
+    check_state(nat, o, max_flows)

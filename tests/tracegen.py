@@ -208,3 +208,36 @@ def mixed_pol_trace(rng, n, n_dsts, n_dev=3, lan=1, wan=0, slot=64,
     frames[(bad >= 0.04) & (bad < 0.06), 14] = 0x46        # IP options
     now = T.NOW0 + np.cumsum(rng.integers(0, gap_ns, n))
     return frames.reshape(-1), lens, in_dev, now.astype(np.int64)
+
+
+def lan_tile_trace(rng, n, n_flows, bad_tiles=0.1, slot=64):
+    """LAN-only traffic (TCP and UDP, several devices below the WAN port) in
+    which most 64-packet tiles are entirely fast-path packets (the classify
+    kernel's lean tile) and a fraction `bad_tiles` of the tiles carry one
+    malformed packet each (those tiles take the per-lane path)."""
+    fl = rng.integers(0, n_flows, n)
+    sip = T.ip4(10, 1, 0, 0) + fl
+    dip = T.ip4(9, 9, 0, 0) + (fl % 11)
+    sp = 2000 + fl % 17
+    dp = 80 + fl % 3
+    proto = np.where(fl % 3 == 0, 6, 17)
+    frames = np.zeros((n, slot), np.uint8)
+    lens = np.zeros(n, np.uint16)
+    for p_ in (6, 17):
+        m = proto == p_
+        f, ln = T.udp_frames(sip[m], dip[m], sp[m], dp[m], slot=slot, proto=p_)
+        frames[m] = f.reshape(-1, slot)
+        lens[m] = ln
+    tiles = (n + 63) // 64
+    for t in np.nonzero(rng.random(tiles) < bad_tiles)[0]:
+        p = min(n - 1, int(t) * 64 + int(rng.integers(0, 64)))
+        kind = int(rng.integers(0, 3))
+        if kind == 0:
+            frames[p, 12] = 0x86  # not IPv4
+        elif kind == 1:
+            frames[p, 14] = 0x46  # IHL 6: the byte-addressed path
+        else:
+            frames[p, 23] = 1  # ICMP: dropped
+    in_dev = np.zeros(n, np.uint16)
+    now = T.NOW0 + np.cumsum(rng.integers(0, 4, n))
+    return frames.reshape(-1), lens, in_dev, now.astype(np.int64)
