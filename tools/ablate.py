@@ -25,6 +25,8 @@ def main():
     variants = {"full": (None, {}), "perlane": (None, {"VIGPATH_COALESCED": "0"})}
     variants["bpc3"] = (None, {"VIGPATH_BLOCKS_PER_CU": "3"})
     variants["bpc2"] = (None, {"VIGPATH_BLOCKS_PER_CU": "2"})
+    variants["nolin"] = (None, {"VIGPATH_LIN": "0"})  # CRC-bit home buckets
+    variants["lin1"] = (None, {"VIGPATH_LIN": "1"})  # one index per bucket
     only = os.environ.get("ABLATE_ONLY")  # comma-separated variant names
     abl = os.path.join(ROOT, "vigor_amd", "abl")
     names = sorted(f[len("libvigpath_"):-3] for f in os.listdir(abl)
@@ -44,7 +46,7 @@ def main():
     buf = torch.empty(B * 64, dtype=torch.uint8, device=dev)
     nfs = {}
     def use_env(env):  # read at context creation and at every launch
-        for k in ("VIGPATH_COALESCED", "VIGPATH_BLOCKS_PER_CU"):
+        for k in ("VIGPATH_COALESCED", "VIGPATH_BLOCKS_PER_CU", "VIGPATH_LIN"):
             os.environ.pop(k, None)
         os.environ.update(env)
 

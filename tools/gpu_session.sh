@@ -14,6 +14,9 @@
 #   e2e      tools/bench_e2e.py                   -> gpurun_out/TAG_e2e.log
 #   nf       tools/bench_nf.py                    -> gpurun_out/TAG_nf.log
 #   test:EXPR  pytest -m gpu -k EXPR
+#   probe[:ARG] tools/stream_probe [ARG]          -> gpurun_out/TAG_probe.log
+#   ablate:V,..  tools/ablate.py over the listed ablation builds
+#                                                 -> gpurun_out/TAG_ablate.log
 # Extra bench.py arguments for bench/trace/pmc: BENCH_ARGS env.
 set -o pipefail
 TAG=$1; shift
@@ -61,6 +64,10 @@ for step in "$@"; do
     shard2) VIGPATH_COMM=host run shard2 600 python3 bench.py --gpus 2 --no-cpu --no-e2e $BA \
              > $O/${TAG}_shard2.log 2>&1 || exit $? ;;
     e2e) run e2e 600 python3 tools/bench_e2e.py > $O/${TAG}_e2e.log 2>&1 || exit $? ;;
+    probe|probe:*) a=${step#probe}; a=${a#:}
+           run probe 300 tools/stream_probe $a > $O/${TAG}_probe.log 2>&1 || exit $? ;;
+    ablate:*) ABLATE_ONLY=${step#ablate:} run ablate 600 python3 tools/ablate.py 5 \
+             > $O/${TAG}_ablate.log 2>&1 || exit $? ;;
     nf) run nf 900 python3 tools/bench_nf.py > $O/${TAG}_nf.log 2>&1 || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -1,9 +1,11 @@
 // Host-side context shared by the runtime translation units.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <tuple>
 #include <vector>
 
 #include "../../include/vigpath.h"
@@ -30,6 +32,22 @@ int hip_fail(hipError_t e, const char *what, const char *file, int line);
 // latency to every batch's control-block read-back.
 hipError_t stream_wait(hipStream_t s);
 hipError_t event_ms(hipEvent_t a, hipEvent_t b, float *ms);
+// Launch k with its dispatch's own start and end timestamps in e0 / e1
+// (hipExtLaunchKernel: the kernel's AQL packet is timed, as rocprofv3's
+// kernel trace times it, not the marker packets around it). e1 completes
+// with the kernel.
+template <class... P, class... A>
+hipError_t launch_timed(void (*k)(P...), dim3 grid, dim3 block, hipStream_t s,
+                        hipEvent_t e0, hipEvent_t e1, A... args) {
+  static_assert(sizeof...(P) == sizeof...(A), "kernel argument count");
+  std::tuple<P...> t{args...};
+  void *ptrs[sizeof...(P)];
+  std::apply([&](auto &...x) {
+    size_t i = 0;
+    ((ptrs[i++] = (void *)&x), ...);
+  }, t);
+  return hipExtLaunchKernel((const void *)k, grid, block, ptrs, 0, s, e0, e1, 0);
+}
 
 struct Comm;  // vp_comm.hip: collectives between the ranks of one NF
 constexpr int kMaxRanks = 64;
@@ -72,6 +90,14 @@ struct FlowTable {
   uint32_t mix = 0;    // home-bucket mode (vp_table.h home_bucket)
   uint64_t ins_since = 0;  // inserts since the last rebuild (mode check)
   uint32_t layout_tries = 0;  // tbl_choose_layout calls so far
+  // allocation-order layout (mix == kMixLin, vp_table.hip tbl_try_linear):
+  // the linear map's four byte tables on the device; lin_ok: the NF's
+  // classify kernels stage them (vignat); lin_tried: fitted once already
+  // (lin_ok 2: two consecutive indices per bucket, half the buckets)
+  uint32_t *lin = nullptr;
+  uint32_t lin_ok = 0;
+  bool lin_tried = false;
+  uint64_t nb_nominal = 0;  // buckets of the CRC-bit layouts
   uint32_t *slot_of = nullptr;
   uint32_t *hash_of = nullptr;
   uint64_t *ts = nullptr;

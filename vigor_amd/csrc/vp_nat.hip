@@ -52,6 +52,12 @@ __device__ __forceinline__ uint32_t flowid_hash(const uint32_t *T, uint32_t sp,
          T[14 * 256 + (proto & 0xFF)];
 }
 
+// The CRC position tables and, for the linear home-bucket layout, its four
+// byte tables behind them (T[kCrcWords ..], see nat_lin).
+constexpr uint32_t kCrcWords = 15 * 256;
+constexpr uint32_t kNatTabWords = kCrcWords + 1024;
+__device__ __forceinline__ const uint32_t *nat_lin(const uint32_t *T) { return T + kCrcWords; }
+
 // flowid_hash for the lean classify tile: the 15 table reads are issued back
 // to back and waited for once (compiled from the expression above, every read
 // waits for the one before it: 15 LDS round trips per packet). The tables
@@ -297,7 +303,7 @@ __device__ __forceinline__ NatPend nat_issue(const NatArgs &a, const uint32_t *T
       return P;
     }
     P.kind = kPendLan;
-    P.b = home_bucket(hh, a.t.bmask, a.t.mix);
+    P.b = home_bucket(hh, a.t.bmask, a.t.mix, nat_lin(T));
 #ifndef VP_ABL_NOPROBE  // diagnostic builds skip the read (tools/ablate.py)
     P.row = P.b;
 #endif
@@ -391,6 +397,12 @@ __device__ __forceinline__ void load_crc_tables(uint32_t *T, const uint32_t *g) 
   for (uint32_t i = threadIdx.x; i < 15 * 256; i += blockDim.x) T[i] = g[i];
   __syncthreads();
 }
+__device__ __forceinline__ void load_nat_tables(uint32_t *T, const NatArgs &a) {
+  if (a.t.mix == kMixLin)
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) T[kCrcWords + i] = a.t.lin[i];
+  load_crc_tables(T, a.crc_tab);
+}
+
 
 // Owner mode: the route of a packet phase A did not hand to another rank
 // (its touch, or nothing); returns the touch for this launch's bins.
@@ -462,13 +474,13 @@ __device__ __forceinline__ uint32_t nat_lane(const NatArgs &a, const uint32_t *T
 // Phase A, any slot size: one packet per lane, grid-stride, the first 64
 // bytes of the slot as four 16-byte loads per lane.
 __global__ __launch_bounds__(256) void nat_classify(NatArgs a) {
-  __shared__ uint32_t T[15 * 256];
+  __shared__ uint32_t T[kNatTabWords];
   __shared__ uint32_t dcur[kMaxDest];
   if (a.own.n) {  // owner mode: block b takes packets [first + b * range, +range)
     for (uint32_t o = threadIdx.x; o < kMaxDest; o += blockDim.x) dcur[o] = 0;
     a.own.cur = dcur;
   }
-  load_crc_tables(T, a.crc_tab);  // (its barrier also covers dcur)
+  load_nat_tables(T, a);  // (its barrier also covers dcur)
   if (a.own.n) {
     const uint32_t b0 = a.own.first + blockIdx.x * a.own.range;
     const uint32_t b1 = min(a.p1, b0 + a.own.range);
@@ -526,12 +538,12 @@ __device__ __forceinline__ uint32_t bucket_match_sel(const uint4 *row,
 // nat_finish per lane. Owner mode always takes the per-lane path.
 __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_all,
                                                         TouchBins bins, TileQueue rq) {
-  __shared__ uint32_t T[15 * 256];
+  __shared__ uint32_t T[kNatTabWords];
   __shared__ uint4 stage[4][256];
   __shared__ uint32_t cur[kCurs];
   for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
   a.own.cur = cur + kCurDest;
-  load_crc_tables(T, a.crc_tab);  // (its barrier also covers cur)
+  load_nat_tables(T, a);  // (its barrier also covers cur)
   uint4 *S = stage[threadIdx.x >> 6];
   const uint4 *rows = reinterpret_cast<const uint4 *>(a.t.bk);
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -547,8 +559,13 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
     if (tb + 64 <= n_all) {  // (wave-uniform) a whole tile: no per-lane guards
 #pragma unroll
       for (uint32_t j = 0; j < 4; j++) r[j] = tile_ld(g + 64 * j + lane);
+#ifdef VP_ABL_NOSIDE  // diagnostic: no len / in_dev loads (the bench's values)
+      m_in = 0;
+      m_len = 60;
+#else
       m_in = a.in_dev[p];
       m_len = a.len[p];
+#endif
       return;
     }
     const uint32_t avail = n_all - tb;  // in the batch
@@ -592,8 +609,13 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
       const uint32_t proto = f.w[5] >> 24;
       const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
       const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
+#ifdef VP_ABL_SEQROW  // diagnostic: consecutive packets -> consecutive rows (two per row)
+      const uint32_t b = ((p >> 1) ^ (flowid_hash_batched(T, sp, dp, sip, dip, in, proto) & 0)) &
+                         a.t.bmask;
+#else
       const uint32_t b = home_bucket(flowid_hash_batched(T, sp, dp, sip, dip, in, proto),
-                                     a.t.bmask, a.t.mix);
+                                     a.t.bmask, a.t.mix, nat_lin(T));
+#endif
       // lane L fetches part L % 4 of the row of packet 16 j + L / 4: the four
       // row numbers come in by ds_bpermute, issued together and waited for
       // once; named registers (an array here stays in scratch memory)
@@ -623,7 +645,7 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
       for (uint32_t k = 0; k < 4; k++) row[k] = S[chunk_swz(4 * lane + k)];
       const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
       bool done;
-#ifdef VP_ABL_L2ROW
+#if defined(VP_ABL_L2ROW) || defined(VP_ABL_SEQROW)
       asm volatile("" ::"v"(row[0].x), "v"(row[1].y), "v"(row[2].z), "v"(row[3].w));
       done = true;
       const uint32_t idx = p & (a.t.cap - 1);
@@ -649,7 +671,7 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
         f.w[0] = a.wan_macw0;
         f.w[1] = a.wan_macw1;
         f.w[2] = a.wan_macw2;
-#ifndef VP_ABL_NOOUT  // diagnostic builds skip the out-port store
+#if !defined(VP_ABL_NOOUT) && !defined(VP_ABL_NOSIDE)  // diagnostic builds skip the out-port store
         a.out[p] = a.wan;
 #endif
       }
@@ -784,9 +806,9 @@ __global__ __launch_bounds__(256) void nat_reprobe(NatArgs a, const uint32_t *li
                                                    const uint32_t *cnt, uint32_t n,
                                                    uint32_t range, uint32_t nblk,
                                                    uint64_t seq_base) {
-  __shared__ uint32_t T[15 * 256];
+  __shared__ uint32_t T[kNatTabWords];
   __shared__ uint4 stage[4][256];
-  load_crc_tables(T, a.crc_tab);
+  load_nat_tables(T, a);
   a.tileq = 1;  // a full bucket answers kReprobe: reprobe_wave walks on
   uint4 *S = stage[threadIdx.x >> 6];
   reprobe_slices(list, cnt, n, range, nblk, a.t.tseq, seq_base, [&](uint32_t p, bool act) {
@@ -885,7 +907,7 @@ __global__ __launch_bounds__(256) void nat_own_probe(TableDev t, const uint32_t 
     const uint32_t key[4] = {k.x, k.y, k.z, k.w};
     const uint32_t h = flowid_hash(T, k.x & 0xFFFF, k.x >> 16, k.y, k.z, k.w & 0xFFFF,
                                    (k.w >> 16) & 0xFF);
-    uint32_t b = home_bucket(h, t.bmask, t.mix), res = kNone;
+    uint32_t b = home_bucket(h, t.bmask, t.mix, t.lin), res = kNone;
     bool live = act;
     for (uint32_t step = 0;; step++) {
       uint4 row[4];
@@ -1273,18 +1295,20 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   if (!t.ctl_clean)
     VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
   t.ctl_clean = false;
-  VP_HIP(hipEventRecord(c->ev0, c->stream));
-  if (p1 > p0) {
+  if (p1 > p0) {  // (the launch's own timestamps in ev0 / ev1)
     if (tiles64) {
       NatArgs a64 = a;
       if (bp.on) a64.log = nullptr;  // touches go to the bins only
-      nat_classify64<<<grid64, 256, 0, c->stream>>>(a64, b->n, bp.bins, rq);
+      VP_HIP(launch_timed(nat_classify64, grid64, 256, c->stream, c->ev0, c->ev1, a64,
+                          (uint32_t)b->n, bp.bins, rq));
     } else {
-      nat_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
+      VP_HIP(launch_timed(nat_classify, grid_for(p1 - p0), 256, c->stream, c->ev0,
+                          c->ev1, a));
     }
-    VP_HIP(hipGetLastError());
+  } else {
+    VP_HIP(hipEventRecord(c->ev0, c->stream));
+    VP_HIP(hipEventRecord(c->ev1, c->stream));
   }
-  VP_HIP(hipEventRecord(c->ev1, c->stream));
   // Phase A's counts for the host, and the fold of its touches right away;
   // the packets it queued (reprobes, overflowed bin entries, phase B/C) are
   // applied on top of it afterwards as late touches (tbl_late_touches: last

@@ -198,6 +198,11 @@ static int nat_init(vp_ctx *c, const vp_nat_config *cfg) {
   c->kind = KIND_NAT;
   c->nat = *cfg;
   VP_TRY(tbl_alloc(c, c->ft, cfg->max_flows));
+  {  // the nat kernels stage the linear layout's tables (VIGPATH_LIN: 0 off,
+     // 1 one index per bucket, 2 two per bucket, the default)
+    const char *lin = getenv("VIGPATH_LIN");
+    c->ft.lin_ok = lin ? (uint32_t)atoi(lin) : 2u;
+  }
   std::vector<uint32_t> tab;
   build_flowid_tables(tab);
   VP_TRY(upload(&c->crc_tab, tab));

@@ -41,6 +41,7 @@ struct TableDev {
   Ctl *ctl;
   uint4 *kv;               // owner mode: key by index (replicated); else null
   uint32_t own_n, own_r;   // owner mode: ranks and this rank; own_n == 0 off
+  const uint32_t *lin;     // mix == kMixLin: the map's byte tables (4 x 256)
 };
 
 // slot_of[] in owner mode: allocated, but its key lives in another rank's
@@ -98,9 +99,20 @@ struct NowSpec {
 // when none is clean (tbl_choose_layout). Only the key -> index mapping is
 // observable, so every layout gives identical results.
 constexpr uint32_t kMixMul = 32;
+// kMixLin: bucket = L(h) & bmask for a GF(2)-linear map L of the hash bits
+// fitted to the live keys so that indices allocated one after another sit in
+// consecutive buckets (tbl_try_linear, vp_table.hip); L is given by four
+// 256-entry tables, one per hash byte (`lin`, in LDS or global memory).
+constexpr uint32_t kMixLin = 33;
+__host__ __device__ __forceinline__ uint32_t lin_map(const uint32_t *L, uint32_t h) {
+  return L[h & 255] ^ L[256 + ((h >> 8) & 255)] ^ L[512 + ((h >> 16) & 255)] ^
+         L[768 + (h >> 24)];
+}
 __host__ __device__ __forceinline__ uint32_t home_bucket(uint32_t h,
                                                          uint32_t bmask,
-                                                         uint32_t mix) {
+                                                         uint32_t mix,
+                                                         const uint32_t *lin = nullptr) {
+  if (mix == kMixLin) return lin_map(lin, h) & bmask;
   if (mix >= kMixMul)
     return (uint32_t)(((uint64_t)(h * 0x9E3779B1u) * (bmask + 1ull)) >> 32);
   return ((h >> mix) | (h << ((32 - mix) & 31))) & bmask;
@@ -161,7 +173,7 @@ template <uint32_t M3 = 0xFFFFFFFFu>
 __device__ __forceinline__ uint32_t tbl_probe(const TableDev &t, uint32_t h,
                                               const uint32_t key[4],
                                               uint32_t *w3 = nullptr) {
-  return tbl_probe_from<M3>(t, home_bucket(h, t.bmask, t.mix), key, t.bmask + 1,
+  return tbl_probe_from<M3>(t, home_bucket(h, t.bmask, t.mix, t.lin), key, t.bmask + 1,
                             w3);
 }
 

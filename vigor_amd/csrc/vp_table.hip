@@ -138,7 +138,8 @@ int read_ctl2(vp_ctx *c, FlowTable &a, FlowTable &b) {
 
 TableDev tbl_dev(const FlowTable &t) {
   return TableDev{t.bk,  t.bmask, t.cap,   t.mix, t.slot_of, t.hash_of, t.ts,
-                  t.tseq, t.birth, t.stack, t.ctl, t.kv,      t.own_n,   t.own_r};
+                  t.tseq, t.birth, t.stack, t.ctl, t.kv,      t.own_n,   t.own_r,
+                  t.lin};
 }
 
 template <class T>
@@ -150,6 +151,9 @@ static int dalloc(T **p, size_t count) {
 
 static int tbl_rebuild(vp_ctx *c, FlowTable &t, uint64_t nb_new = 0);
 static int tbl_choose_layout(vp_ctx *c, FlowTable &t);
+static int tbl_try_linear(vp_ctx *c, FlowTable &t);
+__global__ void lay_count(TableDev t, uint32_t mix, uint32_t *cnt);
+__global__ void lay_score(const uint32_t *cnt, uint32_t nb, uint32_t *over);
 
 static uint64_t tbl_entries(const FlowTable &t) {
   return (uint64_t)(t.bmask + 1) * kBucketEntries;
@@ -168,6 +172,7 @@ int tbl_alloc(vp_ctx *c, FlowTable &t, uint32_t cap) {
     if (k < 0) nb = std::max<uint64_t>(64, nb >> std::min(-k, 3));
   }
   t.bmask = (uint32_t)(nb - 1);
+  t.nb_nominal = nb;
   t.cap = cap;
   const char *mix = getenv("VIGPATH_MIX");  // diagnostics: start multiplicative
   t.mix = mix && atoi(mix) ? kMixMul : 0;
@@ -206,6 +211,7 @@ void tbl_free(FlowTable &t) {
                   t.ekey2, t.eidx,    t.eidx2};
   for (void *p : ptrs) hipFree(p);
   hipFree(t.ttotal);
+  hipFree(t.lin);
   hipFree(t.kv);
   if (t.h_pin) hipHostFree(t.h_pin);
   if (t.h_pub) hipHostFree(t.h_pub);
@@ -217,7 +223,7 @@ void tbl_free(FlowTable &t) {
 // Returns the entry id. Concurrent claimers race on the index word only.
 __device__ uint32_t tbl_insert(const TableDev &t, uint32_t h, const uint32_t *k,
                                uint32_t idx, bool *reused_tomb, uint32_t *disp) {
-  uint32_t b = home_bucket(h, t.bmask, t.mix);
+  uint32_t b = home_bucket(h, t.bmask, t.mix, t.lin);
   for (uint32_t d = 0;; d++) {
     if (d == 1) *disp += 1;  // past the home bucket
     if (d == 8) atomicMax(&t.ctl->max_disp, d);  // clustering signal
@@ -379,12 +385,148 @@ int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
   // well spread or clustered (a long probe, or a tenth of the keys past
   // their home bucket). Clustered: choose another layout and rebuild.
   t.ins_since += t.h_ctl.new_count;
-  if (t.mix < kMixMul && (t.h_ctl.max_disp ||
-                          (t.ins_since >= 4096 && 10ull * t.h_ctl.disp_count > t.ins_since))) {
+  if ((t.mix < kMixMul || t.mix == kMixLin) &&
+      (t.h_ctl.max_disp ||
+       (t.ins_since >= 4096 && 10ull * t.h_ctl.disp_count > t.ins_since))) {
     VP_HIP(hipMemsetAsync(&t.ctl->max_disp, 0, 4, c->stream));
     VP_TRY(tbl_choose_layout(c, t));
+  } else if (t.lin_ok && !t.lin_tried && !t.own_n && t.mix != kMixLin &&
+             2ull * t.h_ctl.n_live > (uint64_t)t.bmask + 1) {
+    VP_TRY(tbl_try_linear(c, t));
   }
   return 0;
+}
+
+// ------------------------------------------------------ linear layout --
+// vignat allocates indices in arrival order (dchain_allocate_new_index), so
+// flows that arrive together get consecutive indices; when their keys differ
+// in a GF(2)-linear way (a counter in a key field: the reference's MoonGen
+// traffic, bench.lua:54,125, sets udp.src = counter) the CRC hashes of index
+// pairs 2^k apart differ by fixed vectors a_k = h(2^k) ^ h(0). A linear map L
+// with L(a_k) = e_k sends index i's hash to bucket i ^ L(h(0)) (in the low
+// bits), so packets that touch neighbouring flows read neighbouring buckets:
+// a tile's 64 rows are one 4 KB run instead of 64 scattered lines
+// (DESIGN.md §5). L is fitted once, from the hashes of indices 0 and 2^k,
+// kept only if at least 90 % of a sample of live indices land exactly in
+// index order and under 1 % of the keys overflow their home bucket, and
+// dropped by the clustering check like any other layout. For keys without
+// that structure any full-rank L spreads like the CRC bits themselves.
+static bool gf2_inverse(const uint32_t cols[32], uint32_t inv_rows[32]) {
+  uint32_t row[32], aug[32];
+  for (int r = 0; r < 32; r++) {
+    row[r] = 0;
+    for (int cc = 0; cc < 32; cc++) row[r] |= ((cols[cc] >> r) & 1u) << cc;
+    aug[r] = 1u << r;
+  }
+  for (int cc = 0; cc < 32; cc++) {
+    int piv = -1;
+    for (int r = cc; r < 32; r++)
+      if ((row[r] >> cc) & 1u) {
+        piv = r;
+        break;
+      }
+    if (piv < 0) return false;
+    std::swap(row[cc], row[piv]);
+    std::swap(aug[cc], aug[piv]);
+    for (int r = 0; r < 32; r++)
+      if (r != cc && ((row[r] >> cc) & 1u)) {
+        row[r] ^= row[cc];
+        aug[r] ^= aug[cc];
+      }
+  }
+  for (int r = 0; r < 32; r++) inv_rows[r] = aug[r];
+  return true;
+}
+static uint32_t gf2_apply(const uint32_t rows[32], uint32_t h) {
+  uint32_t o = 0;
+  for (int r = 0; r < 32; r++) o |= (uint32_t)(__builtin_popcount(rows[r] & h) & 1) << r;
+  return o;
+}
+
+static int tbl_try_linear(vp_ctx *c, FlowTable &t) {
+  t.lin_tried = true;
+  const uint32_t nbits = (uint32_t)__builtin_ctz(t.bmask + 1);
+  const uint32_t S = std::min<uint32_t>(t.cap, std::min<uint32_t>(t.bmask + 1, 1u << 16));
+  if (nbits > 31 || (1u << (nbits - 1)) >= t.cap) return 0;
+  // hashes and entries of indices 0 .. S-1 and 2^k (k < nbits)
+  std::vector<uint32_t> h(S), e(S), hk(nbits), ek(nbits);
+  VP_HIP(hipMemcpyAsync(h.data(), t.hash_of, 4ull * S, hipMemcpyDeviceToHost, c->stream));
+  VP_HIP(hipMemcpyAsync(e.data(), t.slot_of, 4ull * S, hipMemcpyDeviceToHost, c->stream));
+  for (uint32_t k = 0; k < nbits; k++) {
+    VP_HIP(hipMemcpyAsync(&hk[k], t.hash_of + (1u << k), 4, hipMemcpyDeviceToHost, c->stream));
+    VP_HIP(hipMemcpyAsync(&ek[k], t.slot_of + (1u << k), 4, hipMemcpyDeviceToHost, c->stream));
+  }
+  VP_HIP(hipStreamSynchronize(c->stream));
+  const uint32_t kFree = 0xFFFFFFFFu;  // slot_of of an index never allocated
+  if (e[0] == kFree) return 0;
+  for (uint32_t k = 0; k < nbits; k++)
+    if (ek[k] == kFree) return 0;
+  // basis: a_0 .. a_{nbits-1}, completed with unit vectors
+  uint32_t cols[32], echelon[32] = {};
+  uint32_t n = 0;
+  auto add = [&](uint32_t v) {  // independent of the columns so far?
+    uint32_t x = v;
+    for (int b = 31; b >= 0; b--)
+      if ((x >> b) & 1u) {
+        if (!echelon[b]) {
+          echelon[b] = x;
+          cols[n++] = v;
+          return true;
+        }
+        x ^= echelon[b];
+      }
+    return false;
+  };
+  for (uint32_t k = 0; k < nbits; k++)
+    if (!add(hk[k] ^ h[0])) return 0;  // rank-deficient: no such layout
+  for (uint32_t b = 0; b < 32 && n < 32; b++) add(1u << b);
+  uint32_t inv[32];
+  if (n != 32 || !gf2_inverse(cols, inv)) return 0;
+  const uint32_t base = gf2_apply(inv, h[0]) & t.bmask;
+  uint64_t live = 0, exact = 0;
+  for (uint32_t i = 0; i < S; i++) {
+    if (e[i] == kFree || e[i] >= kElsewhere) continue;
+    live++;
+    exact += ((gf2_apply(inv, h[i]) & t.bmask) ^ base) == i;
+  }
+  if (!live || 10 * exact < 9 * live) return 0;
+  // pairs: rotate the map right by one bit, so indices 2m and 2m + 1 share a
+  // bucket of half as many (load 2/3 of the 3 entries, every key in its
+  // home bucket): a tile's 64 rows are 2 KB, half the row bytes per packet
+  const bool pairs = t.lin_ok >= 2 && t.bmask >= 127;
+  const uint64_t nb = pairs ? ((uint64_t)t.bmask + 1) / 2 : (uint64_t)t.bmask + 1;
+  std::vector<uint32_t> tab(1024);
+  for (uint32_t j = 0; j < 4; j++)
+    for (uint32_t v = 0; v < 256; v++) {
+      const uint32_t x = gf2_apply(inv, v << (8 * j));
+      tab[256 * j + v] = pairs ? (x >> 1) | (x << 31) : x;
+    }
+  if (!t.lin) VP_TRY(dalloc(&t.lin, 1024));
+  VP_HIP(hipMemcpyAsync(t.lin, tab.data(), 4096, hipMemcpyHostToDevice, c->stream));
+  // spread check over every live key, then rebuild in the new layout
+  uint32_t *cnt = nullptr, *over = nullptr;
+  VP_TRY(dalloc(&cnt, nb));
+  VP_TRY(dalloc(&over, 1));
+  VP_HIP(hipMemsetAsync(over, 0, 4, c->stream));
+  VP_HIP(hipMemsetAsync(cnt, 0, 4 * nb, c->stream));
+  TableDev d = tbl_dev(t);
+  d.bmask = (uint32_t)(nb - 1);
+  lay_count<<<grid_for(t.cap), 256, 0, c->stream>>>(d, kMixLin, cnt);
+  lay_score<<<grid_for(nb), 256, 0, c->stream>>>(cnt, (uint32_t)nb, over);
+  VP_HIP(hipGetLastError());
+  uint32_t h_over = 0;
+  VP_HIP(hipMemcpyAsync(&h_over, over, 4, hipMemcpyDeviceToHost, c->stream));
+  VP_HIP(hipStreamSynchronize(c->stream));
+  hipFree(cnt);
+  hipFree(over);
+  VP_TRY(read_ctl(c, t));
+  if (100ull * h_over > t.h_ctl.sh_live) return 0;
+  if (getenv("VIGPATH_DEBUG"))
+    fprintf(stderr, "vigpath: linear layout: %llu of %llu sampled indices in order, "
+            "%u keys past home\n", (unsigned long long)exact, (unsigned long long)live,
+            h_over);
+  t.mix = kMixLin;
+  return tbl_rebuild(c, t, nb);
 }
 
 // ---------------------------------------------------------------- layout --
@@ -393,7 +535,8 @@ int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
 __global__ void lay_count(TableDev t, uint32_t mix, uint32_t *cnt) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.cap;
        i += gridDim.x * blockDim.x)
-    if (t.slot_of[i] < kElsewhere) atomicAdd(&cnt[home_bucket(t.hash_of[i], t.bmask, mix)], 1u);
+    if (t.slot_of[i] < kElsewhere)
+      atomicAdd(&cnt[home_bucket(t.hash_of[i], t.bmask, mix, t.lin)], 1u);
 }
 __global__ void lay_score(const uint32_t *cnt, uint32_t nb, uint32_t *over) {
   uint32_t o = 0;
@@ -409,6 +552,10 @@ __global__ void lay_score(const uint32_t *cnt, uint32_t nb, uint32_t *over) {
 // multiplicative spread. Then rebuild. A table that keeps clustering after
 // a few choices stays multiplicative.
 static int tbl_choose_layout(vp_ctx *c, FlowTable &t) {
+  if (t.mix == kMixLin) {  // the keys lost their structure: back to the CRC bits
+    t.mix = 0;
+    return tbl_rebuild(c, t, t.nb_nominal);
+  }
   const uint64_t nb = (uint64_t)t.bmask + 1;
   uint32_t best = kMixMul;
   if (++t.layout_tries <= 4) {
