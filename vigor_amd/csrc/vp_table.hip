@@ -553,6 +553,7 @@ __global__ void lay_score(const uint32_t *cnt, uint32_t nb, uint32_t *over) {
 // a few choices stays multiplicative.
 static int tbl_choose_layout(vp_ctx *c, FlowTable &t) {
   if (t.mix == kMixLin) {  // the keys lost their structure: back to the CRC bits
+    if (getenv("VIGPATH_DEBUG")) fprintf(stderr, "vigpath: linear layout dropped\n");
     t.mix = 0;
     return tbl_rebuild(c, t, t.nb_nominal);
   }
