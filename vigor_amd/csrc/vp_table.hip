@@ -385,14 +385,21 @@ int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
   // well spread or clustered (a long probe, or a tenth of the keys past
   // their home bucket). Clustered: choose another layout and rebuild.
   t.ins_since += t.h_ctl.new_count;
+  // first chance for the allocation-order layout (below), whatever the
+  // current layout's clustering: it replaces it
+  if (t.lin_ok && !t.lin_tried && !t.own_n && t.mix != kMixLin &&
+      2ull * t.h_ctl.n_live > (uint64_t)t.bmask + 1) {
+    VP_TRY(tbl_try_linear(c, t));
+    if (t.mix == kMixLin) {
+      VP_HIP(hipMemsetAsync(&t.ctl->max_disp, 0, 4, c->stream));
+      return 0;
+    }
+  }
   if ((t.mix < kMixMul || t.mix == kMixLin) &&
       (t.h_ctl.max_disp ||
        (t.ins_since >= 4096 && 10ull * t.h_ctl.disp_count > t.ins_since))) {
     VP_HIP(hipMemsetAsync(&t.ctl->max_disp, 0, 4, c->stream));
     VP_TRY(tbl_choose_layout(c, t));
-  } else if (t.lin_ok && !t.lin_tried && !t.own_n && t.mix != kMixLin &&
-             2ull * t.h_ctl.n_live > (uint64_t)t.bmask + 1) {
-    VP_TRY(tbl_try_linear(c, t));
   }
   return 0;
 }
