@@ -160,6 +160,7 @@ def test_multiplicative_home_buckets_reprobe(monkeypatch):
     (LAN hits, WAN replies and new flows alike)."""
     monkeypatch.setenv("VIGPATH_MIX", "1")
     monkeypatch.setenv("VIGPATH_SPARSE", "-1")  # load 2/3: many reprobes
+    monkeypatch.setenv("VIGPATH_LIN", "0")  # (no allocation-order layout)
     fw, o = make_pair(max_flows=4096)
     fr, ln, dv, now = T.fw_trace(4000, 4000)
     check_batches(fw, o, fr, ln, dv, now, 64, [1500])

@@ -240,6 +240,7 @@ def test_multiplicative_home_buckets_reprobe(order, slot, monkeypatch):
     per-lane path of wider slots). Outputs and state equal the oracle's."""
     monkeypatch.setenv("VIGPATH_MIX", "1")
     monkeypatch.setenv("VIGPATH_SPARSE", "-1")  # load 2/3: many reprobes
+    monkeypatch.setenv("VIGPATH_LIN", "0")  # (no allocation-order layout)
     def wide(fr):  # 64-byte slots -> `slot`-byte slots, zero padded
         w = np.zeros((fr.size // 64, slot), np.uint8)
         w[:, :64] = fr.reshape(-1, 64)
@@ -296,6 +297,8 @@ def test_lean_tiles(max_flows, n_flows, expire_us, mix, monkeypatch):
     per-lane tiles (one malformed packet each), TCP and UDP, with new flows,
     a full table, expiry and reprobes; several batches."""
     monkeypatch.setenv("VIGPATH_MIX", mix)
+    if mix == "1":  # (keep the spread: no allocation-order layout)
+        monkeypatch.setenv("VIGPATH_LIN", "0")
     rng = np.random.default_rng(max_flows + n_flows)
     fr, ln, dv, now = lan_tile_trace(rng, 40_000, n_flows)
     nat, o = make_pair(max_flows=max_flows, expire_us=expire_us)

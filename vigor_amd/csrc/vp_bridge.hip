@@ -91,7 +91,7 @@ __device__ __forceinline__ uint32_t mac_probe_from(const TableDev &t, uint32_t b
 __device__ __forceinline__ uint32_t mac_probe(const TableDev &t, uint32_t h,
                                               uint32_t m0, uint32_t m1,
                                               uint32_t *port) {
-  return mac_probe_from(t, home_bucket(h, t.bmask, t.mix), m0, m1, port);
+  return mac_probe_from(t, home_bucket(h, t.bmask, t.mix, t.lin), m0, m1, port);
 }
 
 struct BridgeArgs {
@@ -190,7 +190,8 @@ __global__ __launch_bounds__(256) void bridge_classify(BridgeArgs a, TouchBins b
       }
     }
     // both home rows in flight at once
-    uint32_t sb = home_bucket(sh, a.t.bmask, a.t.mix), db = home_bucket(dh, a.t.bmask, a.t.mix);
+    uint32_t sb = home_bucket(sh, a.t.bmask, a.t.mix, a.t.lin),
+             db = home_bucket(dh, a.t.bmask, a.t.mix, a.t.lin);
     uint4 q[8];
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) {

@@ -167,7 +167,7 @@ __device__ __forceinline__ FwPend fw_issue(const FwArgs &a, const uint32_t *T,
   const uint32_t hh = in == a.wan ? fw_hash(T, dp, sp, dip, sip, proto)
                                   : fw_hash(T, sp, dp, sip, dip, proto);
   P.kind = kFwProbe;
-  P.row = home_bucket(hh, a.t.bmask, a.t.mix);
+  P.row = home_bucket(hh, a.t.bmask, a.t.mix, a.t.lin);
   return P;
 }
 
@@ -448,6 +448,7 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
                                                          w.mkey, w.mhash);
     VP_HIP(hipGetLastError());
     VP_TRY(tbl_new_keys(c, t, NewKeys{nmiss, w.miss_sorted}, c->seq, nullptr));
+    a.t = tbl_dev(t);  // a rebuild may have moved the buckets
     fw_miss_finish<<<grid_for(nmiss), 256, 0, c->stream>>>(
         a, w.miss_sorted, nmiss, w.mkey, w.scratch, w.rep, w.assign);
     VP_HIP(hipGetLastError());

@@ -79,7 +79,7 @@ __device__ __forceinline__ uint32_t flow_probe(const TableDev &t, uint32_t h,
                                                uint32_t k0, uint32_t k1,
                                                uint32_t k2, uint32_t proto,
                                                uint32_t *w3) {
-  uint32_t b = home_bucket(h, t.bmask, t.mix);
+  uint32_t b = home_bucket(h, t.bmask, t.mix, t.lin);
   for (uint32_t i = 0; i <= t.bmask; i++) {
     const uint4 *q = reinterpret_cast<const uint4 *>(t.bk + b);
     const uint4 e0 = q[0], e1 = q[1], e2 = q[2], ix = q[3];

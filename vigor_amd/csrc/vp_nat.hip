@@ -1362,6 +1362,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
       VP_HIP(hipGetLastError());
     } else {
       VP_TRY(tbl_new_keys(c, t, NewKeys{nmiss, w.miss_sorted}, c->seq, nullptr));
+      a.t = tbl_dev(t);  // a rebuild may have moved the buckets
     }
     if (nmiss) {
       nat_miss_finish<<<grid_for(nmiss), 256, 0, c->stream>>>(

@@ -412,6 +412,7 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
                                                           w.mkey, w.mhash);
     VP_HIP(hipGetLastError());
     VP_TRY(tbl_new_keys(c, t, NewKeys{nmiss, w.miss_sorted}, c->seq, nullptr));
+    a.t = tbl_dev(t);  // a rebuild may have moved the buckets
     pol_miss_finish<<<grid_for(nmiss), 256, 0, c->stream>>>(
         a, w.miss_sorted, nmiss, w.scratch, w.rep, w.assign);
     VP_HIP(hipGetLastError());

@@ -194,15 +194,19 @@ static int upload(uint32_t **dst, const std::vector<uint32_t> &v) {
   return 0;
 }
 
+// The allocation-order home-bucket layout (vp_table.hip tbl_try_linear) for
+// a table whose indices the dchain hands out in arrival order: VIGPATH_LIN 0
+// off, 1 one index per bucket, 2 two per bucket (the default).
+static void lin_enable(FlowTable &t) {
+  const char *lin = getenv("VIGPATH_LIN");
+  t.lin_ok = lin ? (uint32_t)atoi(lin) : 2u;
+}
+
 static int nat_init(vp_ctx *c, const vp_nat_config *cfg) {
   c->kind = KIND_NAT;
   c->nat = *cfg;
   VP_TRY(tbl_alloc(c, c->ft, cfg->max_flows));
-  {  // the nat kernels stage the linear layout's tables (VIGPATH_LIN: 0 off,
-     // 1 one index per bucket, 2 two per bucket, the default)
-    const char *lin = getenv("VIGPATH_LIN");
-    c->ft.lin_ok = lin ? (uint32_t)atoi(lin) : 2u;
-  }
+  lin_enable(c->ft);
   std::vector<uint32_t> tab;
   build_flowid_tables(tab);
   VP_TRY(upload(&c->crc_tab, tab));
@@ -219,6 +223,7 @@ static int bridge_init(vp_ctx *c, const vp_bridge_config *cfg) {
   c->brg = *cfg;
   c->brg.static_rules = nullptr;
   VP_TRY(tbl_alloc(c, c->ft, cfg->dyn_capacity));
+  lin_enable(c->ft);
   std::vector<uint32_t> tab;
   build_bridge_tables(tab);
   VP_TRY(upload(&c->crc_tab, tab));
@@ -240,6 +245,7 @@ static int lb_init(vp_ctx *c, const vp_lb_config *cfg) {
   c->kind = KIND_LB;
   c->lb = *cfg;
   VP_TRY(tbl_alloc(c, c->ft, cfg->flow_capacity));
+  lin_enable(c->ft);
   VP_TRY(tbl_alloc(c, c->ft2, cfg->backend_capacity));
   std::vector<uint32_t> tab;
   build_lb_tables(tab);
@@ -263,6 +269,7 @@ static int fw_init(vp_ctx *c, const vp_fw_config *cfg) {
   c->kind = KIND_FW;
   c->fw = *cfg;
   VP_TRY(tbl_alloc(c, c->ft, cfg->max_flows));
+  lin_enable(c->ft);
   std::vector<uint32_t> tab;
   build_fw_tables(tab);
   VP_TRY(upload(&c->crc_tab, tab));
@@ -277,6 +284,7 @@ static int pol_init(vp_ctx *c, const vp_pol_config *cfg) {
   c->kind = KIND_POL;
   c->pol = *cfg;
   VP_TRY(tbl_alloc(c, c->ft, cfg->dyn_capacity));
+  lin_enable(c->ft);
   std::vector<uint32_t> tab;
   build_pol_tables(tab);
   VP_TRY(upload(&c->crc_tab, tab));

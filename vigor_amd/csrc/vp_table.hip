@@ -452,9 +452,12 @@ static uint32_t gf2_apply(const uint32_t rows[32], uint32_t h) {
 
 static int tbl_try_linear(vp_ctx *c, FlowTable &t) {
   t.lin_tried = true;
-  const uint32_t nbits = (uint32_t)__builtin_ctz(t.bmask + 1);
-  const uint32_t S = std::min<uint32_t>(t.cap, std::min<uint32_t>(t.bmask + 1, 1u << 16));
-  if (nbits > 31 || (1u << (nbits - 1)) >= t.cap) return 0;
+  // index bits: indices live below cap <= 2^nbits (the nominal bucket count)
+  uint32_t nbits = 0;
+  while ((1ull << nbits) < t.cap) nbits++;
+  if (nbits < 7 || nbits > 31) return 0;
+  const uint32_t imask = (1u << nbits) - 1;
+  const uint32_t S = std::min<uint32_t>(t.cap, 1u << 16);
   // hashes and entries of indices 0 .. S-1 and 2^k (k < nbits)
   std::vector<uint32_t> h(S), e(S), hk(nbits), ek(nbits);
   VP_HIP(hipMemcpyAsync(h.data(), t.hash_of, 4ull * S, hipMemcpyDeviceToHost, c->stream));
@@ -465,9 +468,9 @@ static int tbl_try_linear(vp_ctx *c, FlowTable &t) {
   }
   VP_HIP(hipStreamSynchronize(c->stream));
   const uint32_t kFree = 0xFFFFFFFFu;  // slot_of of an index never allocated
-  if (e[0] == kFree) return 0;
+  if (e[0] == kFree || e[0] >= kElsewhere) return 0;
   for (uint32_t k = 0; k < nbits; k++)
-    if (ek[k] == kFree) return 0;
+    if (ek[k] == kFree || ek[k] >= kElsewhere) return 0;
   // basis: a_0 .. a_{nbits-1}, completed with unit vectors
   uint32_t cols[32], echelon[32] = {};
   uint32_t n = 0;
@@ -489,19 +492,20 @@ static int tbl_try_linear(vp_ctx *c, FlowTable &t) {
   for (uint32_t b = 0; b < 32 && n < 32; b++) add(1u << b);
   uint32_t inv[32];
   if (n != 32 || !gf2_inverse(cols, inv)) return 0;
-  const uint32_t base = gf2_apply(inv, h[0]) & t.bmask;
+  const uint32_t base = gf2_apply(inv, h[0]) & imask;
   uint64_t live = 0, exact = 0;
   for (uint32_t i = 0; i < S; i++) {
     if (e[i] == kFree || e[i] >= kElsewhere) continue;
     live++;
-    exact += ((gf2_apply(inv, h[i]) & t.bmask) ^ base) == i;
+    exact += ((gf2_apply(inv, h[i]) & imask) ^ base) == i;
   }
   if (!live || 10 * exact < 9 * live) return 0;
-  // pairs: rotate the map right by one bit, so indices 2m and 2m + 1 share a
-  // bucket of half as many (load 2/3 of the 3 entries, every key in its
-  // home bucket): a tile's 64 rows are 2 KB, half the row bytes per packet
-  const bool pairs = t.lin_ok >= 2 && t.bmask >= 127;
-  const uint64_t nb = pairs ? ((uint64_t)t.bmask + 1) / 2 : (uint64_t)t.bmask + 1;
+  // 2^nbits buckets, one index each; pairs: rotate the map right by one bit,
+  // so indices 2m and 2m + 1 share a bucket of half as many (2^nbits / 2
+  // buckets x 3 entries >= cap; every key in its home bucket): a tile's 64
+  // rows are 2 KB, half the row bytes per packet
+  const bool pairs = t.lin_ok >= 2;
+  const uint64_t nb = pairs ? 1ull << (nbits - 1) : 1ull << nbits;
   std::vector<uint32_t> tab(1024);
   for (uint32_t j = 0; j < 4; j++)
     for (uint32_t v = 0; v < 256; v++) {
