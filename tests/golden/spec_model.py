@@ -1,0 +1,184 @@
+"""Executable model of the reference's NF specifications (test
+infrastructure: fixture generation only, in the container that holds the
+reference).
+
+vignat, vigfw and vigbridge each ship a behavioural specification
+(`vignat/spec.py`, `vigfw/spec.py`, `vigbridge/spec.py`) that the reference's
+validator translates into VeriFast contracts (`validator/translate-spec.py`).
+They are Python syntax over a small vocabulary: `pop_header`, header
+constructors with `...` for unspecified fields, and the abstract state
+objects (`emap`, `vector`). This module gives that vocabulary the meaning the
+reference's own models give it, and runs a spec text once per packet:
+
+  emap (libvig/verified/emap.h:10-69): a map key -> index, a vector
+  index -> key and a dchain of (index, time) cells;
+  expire_all(t) drops every index whose time is < t (is_cell_expired,
+  double-chain.h:127-129), refresh_idx re-stamps, add allocates
+  `the_index_allocated` (the spec leaves the choice to the implementation:
+  the caller supplies the implementation's index), full() is
+  dchain_out_of_space_fp (double-chain.h:35-39: size <= live count).
+
+  Header fields (translate-spec.py:6-9) are read from the frame the way the
+  NF's C structs read them (little-endian loads of network-order bytes;
+  ether.type 0x0800 reads as 8, the value the specs assert). pop_header
+  fails (on_mismatch: drop) when the frame is too short for the header or
+  the outer header announces another protocol; the specs' asserts (IPv4
+  ethertype, TCP/UDP protocol) are enforced the same way. The NF's finer
+  parse predicates (IHL, total_length) are not part of the specs, so the
+  traces that use this model keep to IHL 5 and consistent lengths.
+
+The spec text is read from the reference at generation time only; what the
+model derives is committed as fixtures (tests/golden/spec_*.npz).
+"""
+from __future__ import annotations
+
+import collections
+import textwrap
+
+
+class Emap:
+    def __init__(self, size: int):
+        self.size = size
+        self.m = {}    # key -> index
+        self.v = {}    # index -> key
+        self.ch = {}   # index -> time (allocated indices)
+
+    def expire_all(self, t):
+        for i in [i for i, ts in self.ch.items() if ts < t]:
+            del self.ch[i]
+            k = self.v.pop(i)
+            if self.m.get(k) == i:
+                del self.m[k]
+
+    def has(self, k):
+        return k in self.m
+
+    def get(self, k):
+        return self.m[k]
+
+    def has_idx(self, i):
+        return i in self.ch
+
+    def get_key(self, i):
+        return self.v[i]
+
+    def refresh_idx(self, i, t):
+        self.ch[i] = t
+
+    def add(self, k, i, t):
+        assert i not in self.ch, "index %d allocated twice" % i
+        self.m[k] = i
+        self.v[i] = k
+        self.ch[i] = t
+
+    def erase(self, k):
+        i = self.m.pop(k)
+        del self.ch[i]
+
+    def full(self):
+        return self.size <= len(self.ch)
+
+
+class Vector(dict):
+    def set(self, i, val):
+        self[i] = val
+
+
+class Hdr:
+    """A header value: named fields; Ellipsis = left unspecified."""
+
+    def __init__(self, kind, fields):
+        self.kind = kind
+        self.f = dict(fields)
+
+    def __getattr__(self, name):
+        try:
+            return self.__dict__["f"][name]
+        except KeyError as e:
+            raise AttributeError(name) from e
+
+
+def _le16(b, o):
+    return b[o] | (b[o + 1] << 8)
+
+
+def _le32(b, o):
+    return b[o] | (b[o + 1] << 8) | (b[o + 2] << 16) | (b[o + 3] << 24)
+
+
+def parse(frame: bytes):
+    """{header kind: Hdr} of the headers a frame carries (model above)."""
+    out = {}
+    if len(frame) < 14:
+        return out
+    out["ether"] = Hdr("ether", {"daddr": bytes(frame[0:6]),
+                                 "saddr": bytes(frame[6:12]),
+                                 "type": _le16(frame, 12)})
+    if out["ether"].type != 8 or len(frame) < 34:
+        return out
+    ip = {"vihl": frame[14], "tos": frame[15], "len": _le16(frame, 16),
+          "pid": _le16(frame, 18), "foff": _le16(frame, 20), "ttl": frame[22],
+          "npid": frame[23], "cksum": _le16(frame, 24),
+          "saddr": _le32(frame, 26), "daddr": _le32(frame, 30)}
+    out["ipv4"] = Hdr("ipv4", ip)
+    if ip["npid"] not in (6, 17) or len(frame) < 38:
+        return out
+    out["tcpudp"] = Hdr("tcpudp", {"src_port": _le16(frame, 34),
+                                   "dst_port": _le16(frame, 36)})
+    return out
+
+
+class _Drop(Exception):
+    pass
+
+
+def _header_ctor(kind):
+    def make(base=None, **kw):
+        f = dict(base.f) if base is not None else {}
+        f.update(kw)
+        return Hdr(kind, f)
+    return make
+
+
+def _record(*names):
+    """A spec value constructor (FlowIdc, ...): hashable, fields by name."""
+    return collections.namedtuple("Rec", names)
+
+
+def compile_spec(text: str):
+    """The spec text as a function of one packet's environment (the
+    `from state import ...` line's objects come from the caller's env)."""
+    body = "\n".join(l for l in text.splitlines()
+                     if not l.startswith("from state import"))
+    src = "def __spec__():\n" + textwrap.indent(body, "    ") + "\n"
+    code = compile(src, "<spec>", "exec")
+    return code
+
+
+_CTORS = {"ether": _header_ctor("ether"), "ipv4": _header_ctor("ipv4"),
+          "tcpudp": _header_ctor("tcpudp")}
+_KIND = {v: k for k, v in _CTORS.items()}
+
+
+def run_packet(code, env: dict, headers: dict):
+    """Evaluate the compiled spec for one packet: (ports, headers).
+    `pop_header(ipv4, ...)` names the header by its constructor."""
+    def pop_header(ctor, on_mismatch):
+        k = _KIND[ctor]
+        if k not in headers:
+            raise _Drop()
+        return headers[k]
+    g = dict(env, pop_header=pop_header, **_CTORS)
+    ns = {}
+    exec(code, g, ns)
+    try:
+        return ns["__spec__"]()
+    except _Drop:  # on_mismatch=([],[]) in every spec: dropped
+        return ([], [])
+
+
+def base_env():
+    return {"FlowIdc": _record("sp", "dp", "sip", "dip", "idev", "prot"),
+            "a_packet_received": True,
+            "vector_get": lambda vec, i: vec[i],
+            "vector_set": lambda vec, i, val: vec.set(i, val)}

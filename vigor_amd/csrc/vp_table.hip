@@ -819,6 +819,13 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const uint32_t pmask = (1u << pbits) - 1;
+#if defined(VP_ABL_FOLDKU16)  // diagnostic builds (tools/ablate.py)
+#define VP_FOLD_KU 16
+#elif defined(VP_ABL_FOLDKU32)
+#define VP_FOLD_KU 32
+#elif defined(VP_ABL_FOLDKU64)
+#define VP_FOLD_KU 64
+#endif
 #ifndef VP_FOLD_KU
 #define VP_FOLD_KU 8
 #endif
