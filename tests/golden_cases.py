@@ -10,10 +10,11 @@ What they pin: the libVig layer (map with chain counters, dchain allocation
 viglb / vigpol, the DPDK checksum) is the clean-room restatement in
 oracle/orc.c on both sides, so these fixtures leave NF-level semantics
 parity-unpinned: a misreading shared by the restatement and the GPU path
-would not show here. vignat's NF level is pinned separately by the
-SURVEY.md Appendix-A byte-level KATs (tests/test_oracle.py), recorded from
-the reference's own nat_main.c in the survey probe; the reference NF
-sources cannot be compiled here."""
+would not show here. The NF level is pinned separately: by the reference's
+own specifications (vignat/vigfw/vigbridge spec.py, executed over a model of
+libvig's VeriFast definitions: tests/spec_cases.py, tests/test_spec.py) and
+by the SURVEY.md Appendix-A byte-level KATs (tests/test_oracle.py); the
+reference NF sources cannot be compiled here."""
 import os
 
 import numpy as np
