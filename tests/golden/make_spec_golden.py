@@ -1,5 +1,5 @@
 """Fixtures from the reference's own NF specifications (this container only:
-reads /root/reference/{vignat,vigfw,vigbridge}/spec.py).
+reads /root/reference/{vignat,vigfw,vigbridge,vigpol}/spec.py).
 
 For each NF a seeded churn trace (new flows, hits, WAN replies right and
 wrong, non-IPv4 and non-TCP/UDP frames, a full table, expiry) is run through
@@ -17,7 +17,7 @@ The spec leaves the allocated index to the implementation
 (`the_index_allocated`): vignat's is observable (the external port), so the
 generator takes it from the restated oracle's output for that packet and the
 spec then pins everything else; vigfw's and vigbridge's are not observable,
-so the model allocates the lowest free index. The restated oracle must agree
+so the model allocates the lowest free index at the spec's `add`. The restated oracle must agree
 with the spec on every packet here (asserted), and tests/test_spec.py /
 tests/test_spec_gpu.py check the oracle and the GPU path against the stored
 fixtures (where the reference is absent).
@@ -73,7 +73,7 @@ def spec_nat(fr, ln, dv, now, out_fr, out):
 def spec_fw(fr, ln, dv, now):
     code = S.compile_spec(open(os.path.join(REF, "vigfw", "spec.py")).read())
     em = S.Emap(C.FW_CAP)
-    vec = S.Vector()
+    vec = S.AutoVector(em)
     env = S.base_env()
     env.update(flow_emap=em, int_devices=vec,
                FlowIdc=S._record("sp", "dp", "sip", "dip", "prot"))
@@ -81,9 +81,8 @@ def spec_fw(fr, ln, dv, now):
     exp_out = np.full(n, -1, np.int32)
     for p in range(n):
         f = fr[p * 64:p * 64 + int(ln[p])].tobytes()
-        free = min(set(range(C.FW_CAP)) - set(em.ch)) if not em.full() else -1
         e = dict(env, now=int(now[p]), received_on_port=int(dv[p]),
-                 the_index_allocated=free)
+                 the_index_allocated=S.Emap.AUTO)
         ports, _ = S.run_packet(code, e, S.parse(f))
         if ports:
             exp_out[p] = ports[0]
@@ -94,7 +93,7 @@ def spec_bridge(fr, ln, dv, now):
     code = S.compile_spec(open(os.path.join(REF, "vigbridge", "spec.py")).read())
     dyn = S.Emap(C.BRIDGE_CAP)
     stat = S.Emap(1 << 30)  # no static rules in these traces
-    vals = S.Vector()
+    vals = S.AutoVector(dyn)
     env = S.base_env()
     env.update(dyn_emap=dyn, stat_emap=stat, dyn_vals=vals,
                DynamicValuec=lambda port: type("DV", (), {"output_port": port})(),
@@ -103,9 +102,28 @@ def spec_bridge(fr, ln, dv, now):
     exp_out = np.full(n, -1, np.int32)
     for p in range(n):
         f = fr[p * 64:p * 64 + int(ln[p])].tobytes()
-        free = min(set(range(C.BRIDGE_CAP)) - set(dyn.ch)) if not dyn.full() else -1
         e = dict(env, now=int(now[p]), received_on_port=int(dv[p]),
-                 the_index_allocated=free)
+                 the_index_allocated=S.Emap.AUTO)
+        ports, _ = S.run_packet(code, e, S.parse(f))
+        if ports:
+            exp_out[p] = ports[0]
+    return exp_out
+
+
+def spec_pol(fr, ln, dv, now):
+    code = S.compile_spec(open(os.path.join(REF, "vigpol", "spec.py")).read())
+    em = S.Emap(C.POL_CAP)
+    vals = S.AutoVector(em)
+    env = S.base_env()
+    env.update(flow_emap=em, dyn_vals=vals, ip_addrc=S._record("addr"),
+               DynamicValuec=S._record("bucket_size", "bucket_time"))
+    n = ln.shape[0]
+    exp_out = np.full(n, -1, np.int32)
+    for p in range(n):
+        f = fr[p * 64:(p + 1) * 64].tobytes()  # (sizes past the slot read as 0)
+        f = f + bytes(max(0, int(ln[p]) - 64))
+        e = dict(env, now=int(now[p]), received_on_port=int(dv[p]),
+                 packet_size=int(ln[p]), the_index_allocated=S.Emap.AUTO)
         ports, _ = S.run_packet(code, e, S.parse(f))
         if ports:
             exp_out[p] = ports[0]
@@ -161,6 +179,19 @@ def main():
                         in_dev=dv, now=now, out=exp_out,
                         spec=np.array("vigbridge/spec.py"))
     print("spec_bridge: %d packets, %d forwarded" % (ln.shape[0], int((exp_out >= 0).sum())))
+    # vigpol
+    fr, ln, dv, now = C.pol_trace()
+    o = C.pol_oracle()
+    out_fr = fr.copy()
+    out = o.run(out_fr, ln, dv, now, 64).astype(np.int32)
+    exp_out = spec_pol(fr, ln, dv, now)
+    got = np.where(out == dv, -1, out)
+    bad = np.nonzero(got != exp_out)[0]
+    assert bad.size == 0, ("pol out", bad[:10], got[bad[:10]], exp_out[bad[:10]])
+    assert np.array_equal(out_fr, fr), "vigpol forwards frames unchanged"
+    np.savez_compressed(os.path.join(HERE, "spec_pol.npz"), frames=fr, lens=ln,
+                        in_dev=dv, now=now, out=exp_out, spec=np.array("vigpol/spec.py"))
+    print("spec_pol: %d packets, %d forwarded" % (ln.shape[0], int((exp_out >= 0).sum())))
 
 
 if __name__ == "__main__":

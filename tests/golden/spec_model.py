@@ -32,6 +32,7 @@ model derives is committed as fixtures (tests/golden/spec_*.npz).
 """
 from __future__ import annotations
 
+import ast
 import collections
 import textwrap
 
@@ -65,8 +66,13 @@ class Emap:
     def refresh_idx(self, i, t):
         self.ch[i] = t
 
+    AUTO = "lowest free index"  # the_index_allocated where unobservable
+
     def add(self, k, i, t):
+        if i is Emap.AUTO:
+            i = min(set(range(self.size)) - set(self.ch))
         assert i not in self.ch, "index %d allocated twice" % i
+        self.last = i
         self.m[k] = i
         self.v[i] = k
         self.ch[i] = t
@@ -82,6 +88,21 @@ class Emap:
 class Vector(dict):
     def set(self, i, val):
         self[i] = val
+
+
+class AutoVector(Vector):
+    """A vector indexed by the emap's AUTO indices: `set(the_index_allocated,
+    v)` right after `add` refers to the index add just chose."""
+
+    def __init__(self, emap):
+        super().__init__()
+        self.emap = emap
+
+    def _ix(self, i):
+        return self.emap.last if i is Emap.AUTO else i
+
+    def set(self, i, val):
+        self[self._ix(i)] = val
 
 
 class Hdr:
@@ -145,14 +166,25 @@ def _record(*names):
     return collections.namedtuple("Rec", names)
 
 
+class _IntDiv(ast.NodeTransformer):
+    """`/` is integer division in the specs (translate-spec.py renders it as
+    VeriFast's `/` over integers); their operands are non-negative here."""
+
+    def visit_BinOp(self, node):
+        self.generic_visit(node)
+        if isinstance(node.op, ast.Div):
+            node.op = ast.FloorDiv()
+        return node
+
+
 def compile_spec(text: str):
     """The spec text as a function of one packet's environment (the
     `from state import ...` line's objects come from the caller's env)."""
     body = "\n".join(l for l in text.splitlines()
                      if not l.startswith("from state import"))
     src = "def __spec__():\n" + textwrap.indent(body, "    ") + "\n"
-    code = compile(src, "<spec>", "exec")
-    return code
+    tree = ast.fix_missing_locations(_IntDiv().visit(ast.parse(src)))
+    return compile(tree, "<spec>", "exec")
 
 
 _CTORS = {"ether": _header_ctor("ether"), "ipv4": _header_ctor("ipv4"),
@@ -172,9 +204,12 @@ def run_packet(code, env: dict, headers: dict):
     ns = {}
     exec(code, g, ns)
     try:
-        return ns["__spec__"]()
+        r = ns["__spec__"]()
     except _Drop:  # on_mismatch=([],[]) in every spec: dropped
         return ([], [])
+    # a path without a return (vigpol: a new address with the table full)
+    # sends nothing
+    return ([], []) if r is None else r
 
 
 def base_env():

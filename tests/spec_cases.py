@@ -8,10 +8,11 @@ broadcast at the other of two ports, so the configurations here do too:
 import numpy as np
 
 import orc
+from tracegen import mixed_pol_trace
 from vigor_amd import traces as T
 
 N = 3000
-NAT_CAP, FW_CAP, BRIDGE_CAP = 64, 64, 64
+NAT_CAP, FW_CAP, BRIDGE_CAP, POL_CAP = 64, 64, 64, 64
 NAT_START_PORT = 1000
 NAT_EXT_IP = T.ip4(192, 168, 4, 2)
 EXPIRE = 10
@@ -178,3 +179,25 @@ def bridge_oracle():
 
 def bridge_gpu_args():
     return ["--expire", str(EXPIRE), "--capacity", str(BRIDGE_CAP)]
+
+
+# vigpol/spec.py:2-6 fixes LAN 1, WAN 0, the bucket (burst 3.75e9 B, rate
+# 3.75e8 B/s: the Makefile defaults) and EXP_TIME = 10 s in ns.
+def pol_trace(seed=204, n=N):
+    """WAN packets to 100 destinations (the table holds 64), LAN packets,
+    a third device, non-IPv4, IHL < 5, total_length > size, IP options;
+    gaps of 0-0.1 s in steps of 10 ms (entries expire after 10 s idle,
+    stamps sit at the cutoff)."""
+    rng = np.random.default_rng(seed)
+    fr, ln, dv, _ = mixed_pol_trace(rng, n, 100)
+    step = rng.choice([0, 10_000_000, 50_000_000, 100_000_000], n)
+    return fr, ln, dv, T.NOW0 + np.cumsum(step).astype(np.int64)
+
+
+def pol_oracle():
+    return orc.Oracle("pol", orc.pol_cfg(lan=1, wan=0, capacity=POL_CAP, n_devices=3))
+
+
+def pol_gpu_args():
+    return ["--lan", "1", "--wan", "0", "--rate", "375000000", "--burst",
+            "3750000000", "--capacity", str(POL_CAP)]

@@ -1,11 +1,11 @@
 """The restated oracle against fixtures derived from the reference's own NF
-specifications (vignat/spec.py, vigfw/spec.py, vigbridge/spec.py) by
-tests/golden/make_spec_golden.py: out device or drop per packet, and
-vignat's rewritten addresses and ports. These pin the NF-level decision
-logic (WAN/LAN dispatch, the reply check, table full, expiry before every
-packet, the rewrite) with the reference's semantics instead of the
-restatement's; the parse predicates beyond the specs' headers and the
-checksums stay pinned as DESIGN.md §7 says."""
+specifications (vignat/spec.py, vigfw/spec.py, vigbridge/spec.py,
+vigpol/spec.py) by tests/golden/make_spec_golden.py: out device or drop per
+packet, and vignat's rewritten addresses and ports. These pin the NF-level
+decision logic (WAN/LAN dispatch, the reply check, table full, expiry before
+every packet, the rewrite, vigpol's malformed-IPv4 predicate) with the
+reference's semantics instead of the restatement's; the other parse
+predicates and the checksums stay pinned as DESIGN.md §7 says."""
 import os
 
 import numpy as np
@@ -52,7 +52,7 @@ def check(nf, out, frames, g):
         np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("nf", ["nat", "fw", "bridge"])
+@pytest.mark.parametrize("nf", ["nat", "fw", "bridge", "pol"])
 def test_oracle_matches_reference_spec(nf):
     g = load(nf)
     o = getattr(C, nf + "_oracle")()
@@ -61,7 +61,7 @@ def test_oracle_matches_reference_spec(nf):
     check(nf, out, fr, g)
 
 
-@pytest.mark.parametrize("nf", ["nat", "fw", "bridge"])
+@pytest.mark.parametrize("nf", ["nat", "fw", "bridge", "pol"])
 def test_spec_fixture_trace_is_reproducible(nf):
     """The committed trace is spec_cases' seeded trace (regenerable)."""
     g = load(nf)
