@@ -32,6 +32,9 @@ int hip_fail(hipError_t e, const char *what, const char *file, int line);
 // latency to every batch's control-block read-back.
 hipError_t stream_wait(hipStream_t s);
 hipError_t event_ms(hipEvent_t a, hipEvent_t b, float *ms);
+// Host-side stage clock (VIGPATH_HOSTPROF=1, diagnostics): hostprof(k)
+// stamps stage k of the current call; the call's stamps go to stderr.
+void hostprof(int k);
 // Launch k with its dispatch's own start and end timestamps in e0 / e1
 // (hipExtLaunchKernel: the kernel's AQL packet is timed, as rocprofv3's
 // kernel trace times it, not the marker packets around it). e1 completes

@@ -1295,6 +1295,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   if (!t.ctl_clean)
     VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
   t.ctl_clean = false;
+  hostprof(1);
   if (p1 > p0) {  // (the launch's own timestamps in ev0 / ev1)
     if (tiles64) {
       NatArgs a64 = a;
@@ -1313,8 +1314,11 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // the packets it queued (reprobes, overflowed bin entries, phase B/C) are
   // applied on top of it afterwards as late touches (tbl_late_touches: last
   // toucher still wins).
+  hostprof(2);
   VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, seq0));
+  hostprof(4);
   VP_HIP(event_ms(c->ev0, c->ev1, &ph.ms));
+  hostprof(5);
   }  // !owner
   a.own.n = 0;  // below: this rank's own table only
   const uint32_t nre = t.h_ctl.reprobe_count;

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -591,8 +592,27 @@ int vp_pol_create(const vp_pol_config *cfg, int gpu, vp_ctx **out) {
 
 void vp_destroy(vp_ctx *ctx) { free_all(ctx); }
 
+extern "C++" {
+namespace vp {
+static const bool g_hostprof = [] {
+  const char *e = getenv("VIGPATH_HOSTPROF");
+  return e && atoi(e);
+}();
+static double g_hp[8];
+void hostprof(int k) {
+  if (g_hostprof && k >= 0 && k < 8)
+    g_hp[k] = std::chrono::duration<double, std::micro>(
+                  std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace vp
+}
+
 int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
   if (!c || !b) return VP_EINVAL;
+  if (vp::g_hostprof) {
+    for (double &x : vp::g_hp) x = 0;
+    vp::hostprof(0);
+  }
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
   hipStream_t user = (hipStream_t)stream;
   hipEvent_t dep = nullptr;
@@ -625,6 +645,13 @@ int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
     hipEventRecord(dep, c->stream);
     hipStreamWaitEvent(user, dep, 0);
     hipEventDestroy(dep);
+  }
+  if (vp::g_hostprof) {  // entry -> classify issued -> fold issued -> ctl seen -> exit
+    vp::hostprof(7);
+    fprintf(stderr, "vigpath hostprof:");
+    for (int k = 1; k < 8; k++)
+      if (vp::g_hp[k] > 0) fprintf(stderr, " s%d %.1f", k, vp::g_hp[k] - vp::g_hp[0]);
+    fprintf(stderr, " us\n");
   }
   return rc;
 }

@@ -956,6 +956,7 @@ int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_
   }
   const uint32_t epoch = ++t.pub_epoch;
   VP_TRY(bins_reduce(c, t, bp, p0, now, seq_base, PubArgs{t.d_pub, t.ctl, epoch}));
+  hostprof(3);
   // poll the epoch; a stream that ends (or fails) without it is an error
   for (uint32_t spin = 1;; spin++) {
     if (__atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE) == epoch) break;

@@ -54,6 +54,25 @@ class NfBase:
         _check(self.L.vp_process_device(self.h, C.byref(b), s),
                "vp_process_device")
 
+    def device_step(self, frames, lens, in_dev, out, slot: int):
+        """A prepared vp_process_device call over fixed device buffers with
+        affine time: returns f(now0, now_step). The batch descriptor and its
+        pointers are built once (a C caller's per-burst cost), so a loop of
+        calls pays only the C-ABI call itself."""
+        n = lens.numel()
+        assert frames.numel() == n * slot and frames.is_cuda
+        b = DevBatchC(frames=frames.data_ptr(), slot=slot, n=n,
+                      len=lens.data_ptr(), in_dev=in_dev.data_ptr(), now=None,
+                      now0=0, now_step=0, out_dev=out.data_ptr())
+        ref, fn, h = C.byref(b), self.L.vp_process_device, self.h
+
+        def step(now0: int, now_step: int):
+            b.now0, b.now_step = now0, now_step
+            rc = fn(h, ref, None)
+            if rc:
+                _check(rc, "vp_process_device")
+        return step
+
     def sync_state(self):
         """Multi-GPU: merge the ranks' timestamps (collective)."""
         _check(self.L.vp_sync_state(self.h), "vp_sync_state")
