@@ -78,9 +78,11 @@ class NfBase:
         _check(self.L.vp_sync_state(self.h), "vp_sync_state")
 
     def last_kernel_ms(self):
-        ms, k = C.c_float(), C.c_int()
-        _check(self.L.vp_last_kernel_ms(self.h, C.byref(ms), C.byref(k)),
-               "vp_last_kernel_ms")
+        if not hasattr(self, "_kms"):  # (built once: called every batch)
+            ms, k = C.c_float(), C.c_int()
+            self._kms = (ms, k, C.byref(ms), C.byref(k))
+        ms, k, rms, rk = self._kms
+        _check(self.L.vp_last_kernel_ms(self.h, rms, rk), "vp_last_kernel_ms")
         return ms.value, k.value
 
     def live_count(self) -> int:
