@@ -1,5 +1,6 @@
 """Fixtures from the reference's own NF specifications (this container only:
-reads /root/reference/{vignat,vigfw,vigbridge,vigpol}/spec.py).
+reads /root/reference/{vignat,vigfw,vigbridge,vigpol,viglb}/spec.py; viglb's
+CHT comes from the reference's own cht_fill_cht in oracle/_ref).
 
 For each NF a seeded churn trace (new flows, hits, WAN replies right and
 wrong, non-IPv4 and non-TCP/UDP frames, a full table, expiry) is run through
@@ -17,7 +18,8 @@ The spec leaves the allocated index to the implementation
 (`the_index_allocated`): vignat's is observable (the external port), so the
 generator takes it from the restated oracle's output for that packet and the
 spec then pins everything else; vigfw's and vigbridge's are not observable,
-so the model allocates the lowest free index at the spec's `add`. The restated oracle must agree
+so the model follows libVig's dchain order at the spec's `add` (which
+viglb's CHT choice does observe for backends). The restated oracle must agree
 with the spec on every packet here (asserted), and tests/test_spec.py /
 tests/test_spec_gpu.py check the oracle and the GPU path against the stored
 fixtures (where the reference is absent).
@@ -130,6 +132,49 @@ def spec_pol(fr, ln, dv, now):
     return exp_out
 
 
+def reference_cht():
+    """The CHT the reference's own cht_fill_cht builds (oracle/_ref)."""
+    import orc
+    tab = np.zeros(C.LB_HEIGHT * C.LB_BACKENDS, np.uint32)
+    mask = np.zeros(C.LB_BACKENDS, np.uint8)
+    hs = np.zeros(1, np.uint64)
+    ch = np.zeros(1, np.int32)
+    P = lambda a: a.ctypes.data  # noqa: E731
+    L = orc.lib(ref=True)
+    assert L.orc_impl_name().decode() == "reference"
+    assert L.orc_test_cht(C.LB_HEIGHT, C.LB_BACKENDS, P(tab), P(mask), 0, P(hs), P(ch))
+    return [int(x) for x in tab]
+
+
+def spec_lb(fr, ln, dv, now):
+    code = S.compile_spec(open(os.path.join(REF, "viglb", "spec.py")).read())
+    flows = S.Emap(C.LB_CAP)
+    bips = S.Emap(C.LB_BACKENDS)
+    env = S.base_env()
+    env.update(flow_emap=flows, backend_ip_emap=bips, cht=reference_cht(),
+               flow_id_to_backend_id=S.AutoVector(flows),
+               backends=S.AutoVector(bips),
+               LoadBalancedFlowc=S._record("src_ip", "dst_ip", "src_port", "dst_port",
+                                           "protocol"),
+               LoadBalancedBackendc=S._record("nic", "mac", "ip"),
+               ip_addrc=S._record("addr"),
+               _LoadBalancedFlow_hash=lambda f: S.struct_hash(*f))
+    n = ln.shape[0]
+    exp_out = np.full(n, -1, np.int32)
+    fields = np.zeros((n, 2), np.int64)  # dst MAC (48 bits), IPv4 dst
+    for p in range(n):
+        f = fr[p * 64:p * 64 + int(ln[p])].tobytes()
+        e = dict(env, now=int(now[p]), received_on_port=int(dv[p]),
+                 the_index_allocated=S.Emap.AUTO)
+        ports, hdrs = S.run_packet(code, e, S.parse(f))
+        if ports:
+            exp_out[p] = ports[0]
+            eth = [h for h in hdrs if h.kind == "ether"][0]
+            ip = [h for h in hdrs if h.kind == "ipv4"][0]
+            fields[p] = (int.from_bytes(eth.daddr, "little"), ip.daddr)
+    return exp_out, fields
+
+
 def main():
     # vignat
     fr, ln, dv, now = C.nat_trace()
@@ -192,6 +237,23 @@ def main():
     np.savez_compressed(os.path.join(HERE, "spec_pol.npz"), frames=fr, lens=ln,
                         in_dev=dv, now=now, out=exp_out, spec=np.array("vigpol/spec.py"))
     print("spec_pol: %d packets, %d forwarded" % (ln.shape[0], int((exp_out >= 0).sum())))
+    # viglb
+    fr, ln, dv, now = C.lb_trace()
+    o = C.lb_oracle()
+    out_fr = fr.copy()
+    out = o.run(out_fr, ln, dv, now, 64).astype(np.int32)
+    exp_out, fields = spec_lb(fr, ln, dv, now)
+    got = np.where(out == dv, -1, out)
+    bad = np.nonzero(got != exp_out)[0]
+    assert bad.size == 0, ("lb out", bad[:10], got[bad[:10]], exp_out[bad[:10]])
+    fwd = exp_out >= 0
+    have = np.array([(int.from_bytes(out_fr[p * 64:p * 64 + 6].tobytes(), "little"),
+                      _le32(out_fr, p * 64 + 30)) for p in range(ln.shape[0])], np.int64)
+    assert np.array_equal(have[fwd], fields[fwd]), "lb fields"
+    np.savez_compressed(os.path.join(HERE, "spec_lb.npz"), frames=fr, lens=ln,
+                        in_dev=dv, now=now, out=exp_out, fields=fields,
+                        spec=np.array("viglb/spec.py"))
+    print("spec_lb: %d packets, %d forwarded" % (ln.shape[0], int(fwd.sum())))
 
 
 if __name__ == "__main__":

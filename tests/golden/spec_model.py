@@ -15,7 +15,8 @@ reference's own models give it, and runs a spec text once per packet:
   expire_all(t) drops every index whose time is < t (is_cell_expired,
   double-chain.h:127-129), refresh_idx re-stamps, add allocates
   `the_index_allocated` (the spec leaves the choice to the implementation:
-  the caller supplies the implementation's index), full() is
+  the caller supplies the implementation's index, or Emap.AUTO for libVig's
+  dchain order), full() is
   dchain_out_of_space_fp (double-chain.h:35-39: size <= live count).
 
   Header fields (translate-spec.py:6-9) are read from the frame the way the
@@ -42,11 +43,21 @@ class Emap:
         self.size = size
         self.m = {}    # key -> index
         self.v = {}    # index -> key
-        self.ch = {}   # index -> time (allocated indices)
+        self.ch = {}   # index -> time, in LRU order (the dchain's alist)
+        # the implementation's choice of `the_index_allocated` where the spec
+        # leaves it open (Emap.AUTO): libVig's dchain hands out freed indices
+        # last-freed first, then never-used ones in order
+        # (double-chain-impl.c, pinned against oracle/_ref)
+        self.freed = []
+        self.fresh = 0
+
+    def _free(self, i):
+        del self.ch[i]
+        self.freed.append(i)
 
     def expire_all(self, t):
-        for i in [i for i, ts in self.ch.items() if ts < t]:
-            del self.ch[i]
+        for i in [i for i, ts in self.ch.items() if ts < t]:  # LRU first
+            self._free(i)
             k = self.v.pop(i)
             if self.m.get(k) == i:
                 del self.m[k]
@@ -64,13 +75,19 @@ class Emap:
         return self.v[i]
 
     def refresh_idx(self, i, t):
+        del self.ch[i]  # (to the MRU end: dchain_rejuvenate_fp)
         self.ch[i] = t
 
     AUTO = "lowest free index"  # the_index_allocated where unobservable
 
     def add(self, k, i, t):
         if i is Emap.AUTO:
-            i = min(set(range(self.size)) - set(self.ch))
+            if self.freed:
+                i = self.freed.pop()
+            else:
+                i, self.fresh = self.fresh, self.fresh + 1
+        elif i in self.freed:
+            self.freed.remove(i)
         assert i not in self.ch, "index %d allocated twice" % i
         self.last = i
         self.m[k] = i
@@ -79,10 +96,25 @@ class Emap:
 
     def erase(self, k):
         i = self.m.pop(k)
-        del self.ch[i]
+        self._free(i)
+        self.v.pop(i, None)
 
     def full(self):
         return self.size <= len(self.ch)
+
+    # emap_exists_with_cht / emap_choose_with_cht (emap.h:73-83): row
+    # hash % height of the CHT (cht.h:26-34, height = length / index range),
+    # the first of its backends allocated in this emap's dchain
+    def _row(self, cht, h):
+        height = len(cht) // self.size
+        r = h % height
+        return cht[r * self.size:(r + 1) * self.size]
+
+    def exists_with_cht(self, cht, h):
+        return any(b in self.ch for b in self._row(cht, h))
+
+    def choose_with_cht(self, cht, h):
+        return next(b for b in self._row(cht, h) if b in self.ch)
 
 
 class Vector(dict):
@@ -210,6 +242,24 @@ def run_packet(code, env: dict, headers: dict):
     # a path without a return (vigpol: a new address with the table full)
     # sends nothing
     return ([], []) if r is None else r
+
+
+def crc32c_u32(h: int, v: int) -> int:
+    """One SSE4.2 crc32 step over a zero-extended u32 (reflected 0x82F63B78,
+    no final xor): the generated hashes' step (boilerplate-util.h:9)."""
+    h ^= v & 0xFFFFFFFF
+    for _ in range(32):
+        h = (h >> 1) ^ (0x82F63B78 if h & 1 else 0)
+    return h
+
+
+def struct_hash(*fields) -> int:
+    """A generated `<Struct>_hash`: one crc step per field in declaration
+    order (codegen/main.ml:328-401)."""
+    h = 0
+    for f in fields:
+        h = crc32c_u32(h, f)
+    return h
 
 
 def base_env():

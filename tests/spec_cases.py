@@ -8,11 +8,14 @@ broadcast at the other of two ports, so the configurations here do too:
 import numpy as np
 
 import orc
-from tracegen import mixed_pol_trace
+from tracegen import mixed_lb_trace, mixed_pol_trace
 from vigor_amd import traces as T
 
 N = 3000
-NAT_CAP, FW_CAP, BRIDGE_CAP, POL_CAP = 64, 64, 64, 64
+NAT_CAP, FW_CAP, BRIDGE_CAP, POL_CAP, LB_CAP = 64, 64, 64, 64, 64
+LB_BACKENDS, LB_HEIGHT = 32, 97  # cht height: a prime above the backends
+LB_BACKEND_EXPIRE = 3_600_000_000  # viglb/spec.py:3 (x 1000 in the NF)
+LB_MACS = [bytes([0x10 * d + i for i in range(6)]) for d in range(3)]
 NAT_START_PORT = 1000
 NAT_EXT_IP = T.ip4(192, 168, 4, 2)
 EXPIRE = 10
@@ -201,3 +204,43 @@ def pol_oracle():
 def pol_gpu_args():
     return ["--lan", "1", "--wan", "0", "--rate", "375000000", "--burst",
             "3750000000", "--capacity", str(POL_CAP)]
+
+
+# viglb/spec.py:2-4 fixes EXP_TIME = 10 * 1000, the backends' expiry
+# (3,600,000,000 x 1000) and the client port 2.
+def lb_trace(seed=205, n=N):
+    """Client flows (port 2) over 150 5-tuples, heartbeats from 24 backends
+    on ports 0/1, non-IPv4 and ICMP frames; a time jump past the backends'
+    expiry at packet 1500 with no heartbeat for the next 300 packets (flows
+    whose backend died are erased and re-balanced, or dropped)."""
+    rng = np.random.default_rng(seed)
+    fr, ln, dv, _ = mixed_lb_trace(rng, n, 150, 24, hb_frac=0.08, quiet=(1500, 1800),
+                                   bad_frac=0.0)
+    f = fr.reshape(n, 64)
+    bad = rng.random(n)
+    f[bad < 0.03, 12] = 0x86                      # not IPv4
+    f[(bad >= 0.03) & (bad < 0.06), 23] = 1       # not TCP/UDP
+    fast = (np.arange(n) // 500) % 2 == 0
+    step = np.where(fast, rng.choice([0, 10], n), rng.choice([0, 100, 200, 300, 500], n))
+    step[1500] = 3_600_000_000 * 1000 + 5_000     # every backend expires
+    return fr, ln, dv, T.NOW0 + np.cumsum(step).astype(np.int64)
+
+
+def lb_cfg():
+    c = orc.LbCfg(flow_capacity=LB_CAP, flow_expiration_time=EXPIRE,
+                  backend_capacity=LB_BACKENDS, cht_height=LB_HEIGHT,
+                  backend_expiration_time=LB_BACKEND_EXPIRE, wan_device=2,
+                  n_devices=3)
+    for d in range(3):
+        c.device_macs[d][:] = list(LB_MACS[d])
+    return c
+
+
+def lb_oracle(ref=False):
+    return orc.Oracle("lb", lb_cfg(), ref=ref)
+
+
+def lb_gpu_args():
+    return ["--flow-capacity", str(LB_CAP), "--backend-capacity", str(LB_BACKENDS),
+            "--cht-height", str(LB_HEIGHT), "--flow-expiration", str(EXPIRE),
+            "--backend-expiration", str(LB_BACKEND_EXPIRE), "--wan", "2"]

@@ -1,7 +1,8 @@
 """The restated oracle against fixtures derived from the reference's own NF
 specifications (vignat/spec.py, vigfw/spec.py, vigbridge/spec.py,
-vigpol/spec.py) by tests/golden/make_spec_golden.py: out device or drop per
-packet, and vignat's rewritten addresses and ports. These pin the NF-level
+vigpol/spec.py, viglb/spec.py) by tests/golden/make_spec_golden.py: out
+device or drop per packet, vignat's rewritten addresses and ports, viglb's
+backend MAC and address. These pin the NF-level
 decision logic (WAN/LAN dispatch, the reply check, table full, expiry before
 every packet, the rewrite, vigpol's malformed-IPv4 predicate) with the
 reference's semantics instead of the restatement's; the other parse
@@ -46,13 +47,18 @@ def check(nf, out, frames, g):
     fwd = exp >= 0
     if nf == "nat":
         np.testing.assert_array_equal(nat_fields(frames, n)[fwd], g["fields"][fwd])
+    elif nf == "lb":  # the backend's MAC and address
+        f = frames.reshape(n, -1).astype(np.int64)
+        mac = sum(f[:, i] << (8 * i) for i in range(6))
+        dip = sum(f[:, 30 + i] << (8 * i) for i in range(4))
+        np.testing.assert_array_equal(np.stack([mac, dip], 1)[fwd], g["fields"][fwd])
     else:  # the IPv4 + L4 headers go out as they came in
         a = frames.reshape(n, -1)[fwd, 14:38]
         b = g["frames"].reshape(n, -1)[fwd, 14:38]
         np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("nf", ["nat", "fw", "bridge", "pol"])
+@pytest.mark.parametrize("nf", ["nat", "fw", "bridge", "pol", "lb"])
 def test_oracle_matches_reference_spec(nf):
     g = load(nf)
     o = getattr(C, nf + "_oracle")()
@@ -61,7 +67,7 @@ def test_oracle_matches_reference_spec(nf):
     check(nf, out, fr, g)
 
 
-@pytest.mark.parametrize("nf", ["nat", "fw", "bridge", "pol"])
+@pytest.mark.parametrize("nf", ["nat", "fw", "bridge", "pol", "lb"])
 def test_spec_fixture_trace_is_reproducible(nf):
     """The committed trace is spec_cases' seeded trace (regenerable)."""
     g = load(nf)

@@ -18,13 +18,16 @@ def make(nf):
     if nf == "fw":
         return vigor_amd.Fw(vigor_amd.fw_config_from_args(C.fw_gpu_args(), 3, C.DEV3),
                             gpu=0)
+    if nf == "lb":
+        return vigor_amd.Lb(vigor_amd.lb_config_from_args(C.lb_gpu_args(), 3, C.LB_MACS),
+                            gpu=0)
     if nf == "pol":
         return vigor_amd.Pol(vigor_amd.pol_config_from_args(C.pol_gpu_args(), 3), gpu=0)
     return vigor_amd.Bridge(vigor_amd.bridge_config_from_args(C.bridge_gpu_args(), 2,
                                                               []), gpu=0)
 
 
-@pytest.mark.parametrize("nf", ["nat", "fw", "bridge", "pol"])
+@pytest.mark.parametrize("nf", ["nat", "fw", "bridge", "pol", "lb"])
 def test_gpu_matches_reference_spec(nf):
     g = load(nf)
     dev = make(nf)
