@@ -281,6 +281,21 @@ struct TouchBins {
   uint32_t *olog;  // olog[p] = index of an overflowed touch
   uint32_t cap, pbits, bbits;
 };
+// Per-packet side stores of the classify tiles (touch-bin entry, out port):
+// ablation builds make them write-through (`sc1`, relaxed agent-scope
+// atomic stores: the written lines leave the XCD's L2 at once, as the frame
+// stores do): VP_ABL_BINWT, VP_ABL_OUTWT.
+#if defined(VP_ABL_BINWT) || defined(VP_ABL_SIDEWT)
+#define VP_BIN_ST(p, v) __hip_atomic_store((p), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+#else
+#define VP_BIN_ST(p, v) (*(p) = (v))
+#endif
+#if defined(VP_ABL_OUTWT) || defined(VP_ABL_SIDEWT)
+#define VP_OUT_ST(p, v) __hip_atomic_store((p), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+#else
+#define VP_OUT_ST(p, v) (*(p) = (v))
+#endif
+
 // Touch-log entry of packet p; `log` is null in the classify kernels that
 // bin their touches.
 __device__ __forceinline__ void log_put(uint32_t *log, uint32_t p, uint32_t v) {
@@ -312,8 +327,8 @@ __device__ __forceinline__ void bins_put(const TouchBins &bins, uint32_t *cur,
   const uint32_t k = group_reserve(cur, b, v);
   const bool fits = k < bins.cap;
   if (v && fits)
-    bins.ent[(((size_t)rb << bins.bbits) + b) * bins.cap + k] =
-        (bin_local(touch, bins.bbits) << bins.pbits) | (p - range0);
+    VP_BIN_ST(bins.ent + (((size_t)rb << bins.bbits) + b) * bins.cap + k,
+              (bin_local(touch, bins.bbits) << bins.pbits) | (p - range0));
   const bool spill = v && !fits;
   const uint32_t o = group_reserve(cur, kCurOverflow, spill);
   if (spill) {

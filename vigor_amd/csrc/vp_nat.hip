@@ -672,7 +672,7 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
         f.w[1] = a.wan_macw1;
         f.w[2] = a.wan_macw2;
 #if !defined(VP_ABL_NOOUT) && !defined(VP_ABL_NOSIDE)  // diagnostic builds skip the out-port store
-        a.out[p] = a.wan;
+        VP_OUT_ST(a.out + p, (uint16_t)a.wan);
 #endif
       }
 #ifdef VP_ABL_NOBINS  // diagnostic builds skip the touch bins
