@@ -150,12 +150,15 @@ __device__ __forceinline__ uint32_t mac_match(const uint4 *row, uint32_t m0, uin
 // (wave-cooperative, one request per row), then handed to their lanes
 // through LDS; a probe that continues past its home bucket walks on alone.
 __global__ __launch_bounds__(256) void bridge_classify(BridgeArgs a, TouchBins bins) {
-  __shared__ uint32_t T[kBridgeTabs * 256];
+  __shared__ uint32_t T[kBridgeTabs * 256 + 1024];  // + the layout's tables
   __shared__ uint4 stage[4][256];
   __shared__ uint32_t cur[kCurs];
   for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
   for (uint32_t i = threadIdx.x; i < kBridgeTabs * 256; i += blockDim.x)
     T[i] = a.crc_tab[i];
+  const uint32_t *lin = T + kBridgeTabs * 256;
+  if (a.t.mix == kMixLin)
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) T[kBridgeTabs * 256 + i] = a.t.lin[i];
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint4 *S = stage[wv];
@@ -190,8 +193,8 @@ __global__ __launch_bounds__(256) void bridge_classify(BridgeArgs a, TouchBins b
       }
     }
     // both home rows in flight at once
-    uint32_t sb = home_bucket(sh, a.t.bmask, a.t.mix, a.t.lin),
-             db = home_bucket(dh, a.t.bmask, a.t.mix, a.t.lin);
+    uint32_t sb = home_bucket(sh, a.t.bmask, a.t.mix, lin),
+             db = home_bucket(dh, a.t.bmask, a.t.mix, lin);
     uint4 q[8];
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) {

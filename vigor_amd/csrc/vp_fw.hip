@@ -140,6 +140,12 @@ struct FwPend {
   uint32_t row;  // home bucket (gathered by frames64_tiles) or kNone
 };
 
+// T holds the CRC tables, then the layout's byte tables (fw_load_tables).
+constexpr uint32_t kFwTabWords = kFwTabs * 256 + 1024;
+__device__ __forceinline__ const uint32_t *fw_lin(const uint32_t *T) {
+  return T + kFwTabs * 256;
+}
+
 __device__ __forceinline__ FwPend fw_issue(const FwArgs &a, const uint32_t *T,
                                            uint32_t p, const RFrame &f,
                                            uint32_t in, uint32_t len, bool mine) {
@@ -167,7 +173,7 @@ __device__ __forceinline__ FwPend fw_issue(const FwArgs &a, const uint32_t *T,
   const uint32_t hh = in == a.wan ? fw_hash(T, dp, sp, dip, sip, proto)
                                   : fw_hash(T, sp, dp, sip, dip, proto);
   P.kind = kFwProbe;
-  P.row = home_bucket(hh, a.t.bmask, a.t.mix, a.t.lin);
+  P.row = home_bucket(hh, a.t.bmask, a.t.mix, fw_lin(T));
   return P;
 }
 
@@ -218,15 +224,19 @@ __device__ __forceinline__ bool fw_finish(const FwArgs &a, const uint32_t *T,
   return true;
 }
 
-__device__ __forceinline__ void fw_load_tables(uint32_t *T, const uint32_t *g) {
-  for (uint32_t i = threadIdx.x; i < kFwTabs * 256; i += blockDim.x) T[i] = g[i];
+// The CRC tables, and behind them the allocation-order layout's byte tables
+// when the table uses it (fw_lin(T), vp_table.h kMixLin).
+__device__ __forceinline__ void fw_load_tables(uint32_t *T, const FwArgs &a) {
+  for (uint32_t i = threadIdx.x; i < kFwTabs * 256; i += blockDim.x) T[i] = a.crc_tab[i];
+  if (a.t.mix == kMixLin)
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) T[kFwTabs * 256 + i] = a.t.lin[i];
   __syncthreads();
 }
 
 // Phase A, any slot size: one packet per lane (byte path; no checksum work).
 __global__ __launch_bounds__(256) void fw_classify(FwArgs a) {
-  __shared__ uint32_t T[kFwTabs * 256];
-  fw_load_tables(T, a.crc_tab);
+  __shared__ uint32_t T[kFwTabWords];
+  fw_load_tables(T, a);
   for (uint32_t p = a.p0 + blockIdx.x * blockDim.x + threadIdx.x; p < a.p1;
        p += gridDim.x * blockDim.x)
     fw_generic_a(a, T, p, a.in_dev[p], a.len[p]);
@@ -235,11 +245,11 @@ __global__ __launch_bounds__(256) void fw_classify(FwArgs a) {
 // Phase A for 64-byte slots: LDS-staged coalesced frame I/O.
 __global__ __launch_bounds__(256, 4) void fw_classify64(FwArgs a, uint32_t n_all,
                                                        TouchBins bins, TileQueue rq) {
-  __shared__ uint32_t T[kFwTabs * 256];
+  __shared__ uint32_t T[kFwTabWords];
   __shared__ uint4 stage[4][256];
   __shared__ uint32_t cur[kCurs];
   for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
-  fw_load_tables(T, a.crc_tab);  // (its barrier also covers cur)
+  fw_load_tables(T, a);  // (its barrier also covers cur)
   frames64_tiles(
       a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
       reinterpret_cast<const uint4 *>(a.t.bk),
@@ -260,9 +270,9 @@ __global__ __launch_bounds__(256) void fw_reprobe(FwArgs a, const uint32_t *list
                                                   const uint32_t *cnt, uint32_t n,
                                                   uint32_t range, uint32_t nblk,
                                                   uint64_t seq_base) {
-  __shared__ uint32_t T[kFwTabs * 256];
+  __shared__ uint32_t T[kFwTabWords];
   __shared__ uint4 stage[4][256];
-  fw_load_tables(T, a.crc_tab);
+  fw_load_tables(T, a);
   a.tileq = 1;  // a full bucket answers kReprobe: reprobe_wave walks on
   uint4 *S = stage[threadIdx.x >> 6];
   reprobe_slices(list, cnt, n, range, nblk, a.t.tseq, seq_base, [&](uint32_t p, bool act) {
