@@ -304,3 +304,30 @@ def test_lean_tiles(max_flows, n_flows, expire_us, mix, monkeypatch):
     nat, o = make_pair(max_flows=max_flows, expire_us=expire_us)
     check_batches(nat, o, fr, ln, dv, now, 64, [4096, 4100, 20_000])
     check_state(nat, o, max_flows)
+
+
+def test_prepared_device_step():
+    """Nat.device_step (the bench's prepared C-ABI call over fixed buffers,
+    affine time) gives what the oracle gives, batch after batch."""
+    import torch
+    nf = 1 << 12
+    nat, o = make_pair(max_flows=nf)
+    B = 1 << 14
+    d = torch.device("cuda:0")
+    f_t = torch.empty(B * 64, dtype=torch.uint8, device=d)
+    l_t = torch.empty(B, dtype=torch.int16, device=d)
+    i_t = torch.empty(B, dtype=torch.int16, device=d)
+    o_t = torch.zeros(B, dtype=torch.int16, device=d)
+    step = nat.device_step(f_t, l_t, i_t, o_t, 64)
+    for j in range(3):
+        fr, ln, dv, now = T.nat_lan_trace(B, nf + 100, start=j * B)
+        f_t.copy_(torch.from_numpy(fr))
+        l_t.copy_(torch.from_numpy(ln.view(np.int16)))
+        i_t.copy_(torch.from_numpy(dv.view(np.int16)))
+        exp = fr.copy()
+        exp_out = o.run(exp, ln, dv, now, 64)
+        step(int(now[0]), 1)
+        torch.cuda.synchronize()
+        assert np.array_equal(o_t.cpu().numpy().view(np.uint16), exp_out)
+        assert np.array_equal(f_t.cpu().numpy(), exp)
+    check_state(nat, o, nf)
