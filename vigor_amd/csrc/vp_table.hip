@@ -405,15 +405,17 @@ int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
 }
 
 // ------------------------------------------------------ linear layout --
-// vignat allocates indices in arrival order (dchain_allocate_new_index), so
+// The NFs allocate indices in arrival order (dchain_allocate_new_index), so
 // flows that arrive together get consecutive indices; when their keys differ
 // in a GF(2)-linear way (a counter in a key field: the reference's MoonGen
 // traffic, bench.lua:54,125, sets udp.src = counter) the CRC hashes of index
 // pairs 2^k apart differ by fixed vectors a_k = h(2^k) ^ h(0). A linear map L
 // with L(a_k) = e_k sends index i's hash to bucket i ^ L(h(0)) (in the low
-// bits), so packets that touch neighbouring flows read neighbouring buckets:
-// a tile's 64 rows are one 4 KB run instead of 64 scattered lines
-// (DESIGN.md §5). L is fitted once, from the hashes of indices 0 and 2^k,
+// bits), so packets that touch neighbouring flows read neighbouring buckets;
+// rotated right by one bit (the default, VIGPATH_LIN=2) it puts indices 2m
+// and 2m + 1 in one bucket of half as many: a tile's 64 rows are one 2 KB
+// run instead of 64 scattered lines. Every NF's flow table
+// allocates this way. L is fitted once, from the hashes of indices 0 and 2^k,
 // kept only if at least 90 % of a sample of live indices land exactly in
 // index order and under 1 % of the keys overflow their home bucket, and
 // dropped by the clustering check like any other layout. For keys without
