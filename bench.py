@@ -62,29 +62,101 @@ NAT_ARGS = ["--expire", "60000000", "--starting-port", "0", "--wan", "1",
             "--eth-dest", "1,90:e2:ba:55:12:21"]
 
 
-class FlowBank:
-    """Per-flow header bytes of the synthetic trace, on the device."""
+def _s64(c: int) -> int:
+    return c - (1 << 64) if c >= 1 << 63 else c
 
-    def __init__(self, n_flows: int, flow_base: int, dev):
+
+def _shr(z, k: int):  # logical shift right of int64 lanes holding u64 bits
+    return (z >> k) & ((1 << (64 - k)) - 1)
+
+
+def uniform_flows(p, n_flows: int, seed: int = 0x5EED):
+    """SURVEY.md §8(d) secondary order on the device: flow =
+    splitmix64(seed, p) mod N (traces.flow_order "uniform"), u64 arithmetic
+    in int64 lanes; N a power of two."""
+    assert n_flows & (n_flows - 1) == 0
+    z = (p + 1) * _s64(0x9E3779B97F4A7C15) + seed
+    z = (z ^ _shr(z, 30)) * _s64(0xBF58476D1CE4E5B9)
+    z = (z ^ _shr(z, 27)) * _s64(0x94D049BB133111EB)
+    return (z ^ _shr(z, 31)) & (n_flows - 1)
+
+
+def frame_len_for(slot: int) -> int:
+    """The bench's frame in a `slot`-byte slot: 60 B in 64 (a 64 B wire
+    frame less its FCS), up to 1514 B (1518 B on the wire)."""
+    return min(slot, 1518) - 4
+
+
+class FlowBank:
+    """Per-flow header bytes of the synthetic trace, on the device. Wider
+    slots carry a fixed payload pattern (the L4 checksum sums it); 64-byte
+    slots the reference's zero payload."""
+
+    def __init__(self, n_flows: int, flow_base: int, dev, slot: int = 64):
         fl = np.arange(flow_base, flow_base + n_flows, dtype=np.int64)
         src = T.ip4(10, 0, 0, 0) + (fl >> 16)
         sp = fl & 0xFFFF
         z = np.zeros_like(fl)
-        f, _ = T.udp_frames(src, z, sp, z, slot=SLOT)
-        f = f.reshape(n_flows, SLOT)
-        self.template = torch.from_numpy(f[0].copy()).to(dev)
+        flen = frame_len_for(slot)
+        f, _ = T.udp_frames(src, z, sp, z, slot=slot, frame_len=flen)
+        f = f.reshape(n_flows, slot)
+        tmpl = f[0].copy()
+        if slot > 64:  # (64 B: the reference's zero payload, bench.lua:61-71)
+            tmpl[42:flen] = (np.arange(42, flen) * 7 % 251).astype(np.uint8)
+        self.template = torch.from_numpy(tmpl).to(dev)
         self.var = torch.from_numpy(np.ascontiguousarray(
             np.concatenate([f[:, 24:30], f[:, 34:36]], axis=1))).to(dev)
         self.n = n_flows
+        self.slot = slot
+        self.frame_len = flen
 
-    def fill(self, frames: torch.Tensor, start: int):
-        B = frames.shape[0] // SLOT
-        fv = frames.view(B, SLOT)
-        fv.copy_(self.template.expand(B, SLOT))
-        fl = torch.arange(start, start + B, device=frames.device) % self.n
+    def fill(self, frames: torch.Tensor, start: int, order: str = "rr"):
+        S = self.slot
+        B = frames.shape[0] // S
+        fv = frames.view(B, S)
+        fv.copy_(self.template.expand(B, S))
+        p = torch.arange(start, start + B, device=frames.device)
+        fl = uniform_flows(p, self.n) if order == "uniform" else p % self.n
         v = self.var.index_select(0, fl)
         fv[:, 24:30] = v[:, 0:6]
         fv[:, 34:36] = v[:, 6:8]
+
+
+def verify_sample(frames: torch.Tensor, slot: int, ext_ip: int, k: int = 4096):
+    """Size-independent check of a processed wide-slot batch (no oracle on
+    the timed path): k frames spread over the batch carry the external
+    source address, and their IPv4 header and UDP checksums verify (RFC 791
+    / 768 ones-complement sums over the rewritten bytes = 0xFFFF)."""
+    B = frames.numel() // slot
+    idx = torch.linspace(0, B - 1, steps=min(k, B), device=frames.device).long()
+    f = frames.view(B, slot).index_select(0, idx).cpu().numpy().astype(np.uint32)
+    w = lambda a, o: (a[:, o] << 8) | a[:, o + 1]  # noqa: E731 (big-endian word)
+
+    def fold(s):
+        s = (s & 0xFFFF) + (s >> 16)
+        return (s & 0xFFFF) + (s >> 16)
+    ip_sum = fold(sum(w(f, o) for o in range(14, 34, 2)))
+    tl = w(f, 16)
+    ok_ip = bool((ip_sum == 0xFFFF).all())
+    # nat_main.c stores the host-order config value raw (little-endian bytes)
+    src = (f[:, 29] << 24) | (f[:, 28] << 16) | (f[:, 27] << 8) | f[:, 26]
+    ok_src = bool((src == ext_ip).all())
+    l4 = tl - 20
+    ok_l4 = True
+    for r in range(f.shape[0]):
+        n = int(l4[r])
+        seg = f[r, 34:34 + n]
+        if n & 1:
+            seg = np.append(seg, 0)
+        s = int((seg[0::2] << 8 | seg[1::2]).sum())
+        s += int(w(f[r:r + 1], 26)[0] + w(f[r:r + 1], 28)[0] + w(f[r:r + 1], 30)[0] +
+                 w(f[r:r + 1], 32)[0] + 17 + n)
+        if fold(np.uint32(s % (1 << 32))) != 0xFFFF:
+            ok_l4 = False
+            break
+    return {"frames_checked": int(f.shape[0]), "ip_checksum_ok": ok_ip,
+            "udp_checksum_ok": ok_l4, "src_is_external": ok_src,
+            "match": ok_ip and ok_l4 and ok_src}
 
 
 CPU_SAMPLES = 5
@@ -149,7 +221,7 @@ def end_to_end(nat, bank, dev, start: int, steps: int = 3):
     (a registered mbuf pool: DPDK keeps mbufs in hugepages);
     vp_process_host_batch moves them over PCIe in E2E_CHUNK-packet chunks,
     host->device and device->host on two copy streams beside the compute
-    stream (double buffered). Time is the bench's affine now_p = NOW0 + p
+    stream, three buffer sets in HBM (the H2D copy runs two chunks ahead). Time is the bench's affine now_p = NOW0 + p
     (SURVEY.md §8(d)), so no time array crosses PCIe. Every flow is already
     warm; one untimed batch allocates the staging buffers. Returns Mpps over
     `steps` host batches of E2E_BATCH."""
@@ -205,25 +277,90 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank, first, steps,
+                order="rr", host_comm=False):
+    """Fill one buffer per step (batches first .. first + steps - 1 of this
+    rank's slices, `order`), then time exactly `steps` prepared
+    vp_process_device calls between barriers + synchronisations. Returns
+    (elapsed s, max over ranks; [(kernel ms, launches)] per step; buffers)."""
+    def gstart(k):  # global position of this rank's slice of global batch k
+        return (k * world + rank) * B
+    bufs = []
+    for k in range(steps):
+        b = torch.empty(B * slot, dtype=torch.uint8, device=dev)
+        bank.fill(b, gstart(first + k), order)
+        bufs.append(b)
+    calls = [nat.device_step(b, lens, in_dev, out, slot) for b in bufs]
+    torch.cuda.synchronize()
+    kms = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        calls[k](T.NOW0 + gstart(first + k), 1)
+        kms.append(nat.last_kernel_ms())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cpu" if host_comm else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # every packet hit (steady state) and went out on the WAN port
+    assert int((out != 1).sum().item()) == 0
+    return elapsed, kms, bufs
+
+
+def kernel_rate(kms, B, steps, alg_bytes):
+    """(per-launch s, packets per launch, achieved algorithmic GB/s)."""
+    launches = sum(k for _, k in kms)
+    per_launch_s = sum(m for m, _ in kms) / 1e3 / max(1, launches)
+    pkts = B * steps / max(1, launches)
+    return per_launch_s, pkts, alg_bytes * pkts / per_launch_s / 1e9
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=1 << 24)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="packets per GPU and step (default 2^24 x 64 / slot)")
+    ap.add_argument("--slot", type=int, default=SLOT,
+                    help="slot bytes (frames of min(slot, 1518) - 4 bytes): "
+                         "64 is BASELINE's config; wider slots measure the "
+                         "65-1518 B frames of north_star (R = slot + 28)")
+    ap.add_argument("--order", choices=("rr", "uniform"), default="rr",
+                    help="packet order (SURVEY.md §8(d)): round robin over "
+                         "the flows (bench.lua:125, the headline) or uniform")
     ap.add_argument("--flows", type=int, default=None,
                     help="default: 1M (config 2) on one GPU, 16M (config 5) "
                          "over N > 1 GPUs")
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
-    ap.add_argument("--shard-mode", choices=("owner", "replicated"), default="replicated",
-                    help="N > 1: flow dictionary replicated on every GPU (no "
-                         "data-path collective; the faster one, DESIGN.md §6.1) "
-                         "or sharded by flow hash with an all-to-all of keys "
-                         "and answers (owner)")
+    ap.add_argument("--shard-mode", choices=("owner", "replicated"), default="owner",
+                    help="N > 1: flow dictionary sharded by flow hash with an "
+                         "all-to-all of keys and answers (owner, north_star's "
+                         "design: the headline value) or replicated on every "
+                         "GPU; the other mode is measured too (extra key "
+                         "other_shard_mode) unless --no-extra")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the host-resident end-to-end rate")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the secondary measurements (uniform order; "
+                         "N > 1: the other dictionary placement)")
     args = ap.parse_args()
+    slot = args.slot
+    if slot < 64 or slot % 16:
+        raise SystemExit("bench.py: --slot must be a multiple of 16, >= 64")
+    B = args.batch
+    if B is None:
+        B = 1 << 24
+        while B * slot > (1 << 30):
+            B >>= 1
+    alg_bytes = slot + 28  # SURVEY.md §8(d): R = slot(len) + 28 (92 at 64 B)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -247,74 +384,51 @@ def main():
                                     device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-
-    cfg = vigor_amd.nat_config_from_args(
-        NAT_ARGS + ["--max-flows", str(args.flows)], 2, DEV_MACS)
-    nat = vigor_amd.Nat(cfg, gpu=local)
-    if world > 1:  # one vignat over all ranks
-        from vigor_amd import shard
-        if host_comm:
-            shard.attach_torch(nat, rank, world, mode=args.shard_mode)
-        else:
-            shard.attach_rccl(nat, rank, world, mode=args.shard_mode)
-    bank = FlowBank(args.flows, 0, dev)
-    B = args.batch
-    lens = torch.full((B,), 60, dtype=torch.int16, device=dev)
+    bank = FlowBank(args.flows, 0, dev, slot)
+    lens = torch.full((B,), bank.frame_len, dtype=torch.int16, device=dev)
     in_dev = torch.zeros(B, dtype=torch.int16, device=dev)
     out = torch.zeros(B, dtype=torch.int16, device=dev)
 
-    def gstart(k):  # global position of this rank's slice of global batch k
-        return (k * world + rank) * B
+    def make_nat(mode):
+        cfg = vigor_amd.nat_config_from_args(
+            NAT_ARGS + ["--max-flows", str(args.flows)], 2, DEV_MACS)
+        nat = vigor_amd.Nat(cfg, gpu=local)
+        if world > 1:  # one vignat over all ranks
+            from vigor_amd import shard
+            if host_comm:
+                shard.attach_torch(nat, rank, world, mode=mode)
+            else:
+                shard.attach_rccl(nat, rank, world, mode=mode)
+        return nat
 
-    def step(frames, k):
-        nat.process_device(frames, lens, in_dev, out, SLOT,
-                           now0=T.NOW0 + gstart(k), now_step=1)
+    def warm(nat):
+        """The first global batch allocates every flow (round robin: the
+        allocation order of the reference's own traffic); returns the new-
+        flow rate of batch 0 in Mpps."""
+        wbuf = torch.empty(B * slot, dtype=torch.uint8, device=dev)
+        rate = None
+        for w in range(args.warmup):
+            bank.fill(wbuf, (w * world + rank) * B)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            nat.process_device(wbuf, lens, in_dev, out, slot,
+                               now0=T.NOW0 + (w * world + rank) * B, now_step=1)
+            torch.cuda.synchronize()
+            if w == 0:
+                rate = B * world / (time.perf_counter() - t0) / 1e6
+        assert nat.live_count() == min(args.flows, B * world * max(1, args.warmup))
+        return rate
 
-    def timed_step(call, k):  # a prepared call (Nat.device_step)
-        call(T.NOW0 + gstart(k), 1)
-
-    # warm-up: the first global batch allocates every flow
-    wbuf = torch.empty(B * SLOT, dtype=torch.uint8, device=dev)
-    new_flow_mpps = None
-    for w in range(args.warmup):
-        bank.fill(wbuf, gstart(w))
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        step(wbuf, w)
-        torch.cuda.synchronize()
-        if w == 0:
-            new_flow_mpps = B * world / (time.perf_counter() - t0) / 1e6
-    assert nat.live_count() == min(args.flows, B * world * max(1, args.warmup))
-    del wbuf
-    bufs = []
-    for k in range(args.steps):
-        b = torch.empty(B * SLOT, dtype=torch.uint8, device=dev)
-        bank.fill(b, gstart(args.warmup + k))
-        bufs.append(b)
-    calls = [nat.device_step(b, lens, in_dev, out, SLOT) for b in bufs]
-    torch.cuda.synchronize()
-
-    kms = []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        timed_step(calls[k], args.warmup + k)
-        kms.append(nat.last_kernel_ms())
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device="cpu" if host_comm else dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    # every packet hit (steady state) and went out on the WAN port
-    assert int((out != 1).sum().item()) == 0
+    mode = args.shard_mode
+    nat = make_nat(mode)
+    new_flow_mpps = warm(nat)
+    elapsed, kms, bufs = timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world,
+                                     rank, args.warmup, args.steps, args.order, host_comm)
     # the last timed batch, byte for byte, against the reference's output of
-    # the same batch (after timing; the golden exists for the default shape)
-    want = golden_batch_digest(args.flows, B) if world == 1 else None
+    # the same batch (after timing; the golden exists for the default shape);
+    # wider slots: a size-independent check of a sample (checksums verify)
+    want = (golden_batch_digest(args.flows, B)
+            if world == 1 and slot == SLOT and args.order == "rr" else None)
     parity = None
     if want is not None:
         got = T.batch_digest(bufs[-1].cpu().numpy(), out.cpu().numpy().view(np.uint16),
@@ -323,47 +437,80 @@ def main():
                   "match": got == want,
                   "source": "tests/golden/nat_bench_shape.npz (reference libVig)"}
         assert got == want, "timed batch differs from the reference: %s" % parity
-
-    total_pkts = B * args.steps * world
-    mpps = total_pkts / elapsed / 1e6
-    launches = sum(k for _, k in kms)
-    kernel_s = sum(m for m, _ in kms) / 1e3
-    per_launch_s = kernel_s / max(1, launches)
-    pkts_per_launch = B * args.steps / max(1, launches)
-    achieved = ALG_BYTES * pkts_per_launch / per_launch_s / 1e9
+    elif slot != SLOT:
+        parity = verify_sample(bufs[-1], slot, T.ip4(192, 168, 4, 2))
+        parity["source"] = "RFC 791/768 checksum verification of a sample (property)"
+        assert parity["match"], parity
+    del bufs
+    mpps = B * args.steps * world / elapsed / 1e6
+    per_launch_s, pkts_per_launch, achieved = kernel_rate(kms, B, args.steps, alg_bytes)
     traffic = None  # PMC bytes of the same kernel (profiles/, per launch)
     tpath = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE)
     if (os.path.exists(tpath) and B == 1 << 24 and args.flows == 1 << 20
-            and world == 1):
+            and world == 1 and slot == SLOT and args.order == "rr"):
         with open(tpath) as fh:
             tb = json.load(fh)["traffic_bytes_per_launch"]
         traffic = round(tb * pkts_per_launch / (1 << 24) / per_launch_s / 1e9, 1)
-    if world == 1 and args.flows == 1 << 20:
+    flen = bank.frame_len
+    if world == 1 and args.flows == 1 << 20 and slot == SLOT and args.order == "rr":
         workload = ("vignat 64B, 1M flows, 1xMI355X (parse+hash+map-probe "
                     "kernel, checksum rewrite)")
     elif world > 1:
         via = "gloo (host)" if host_comm else "RCCL/xGMI"
         how = ("flow-hash sharded dictionary: keys owned by another GPU looked up "
-               "through an all-to-all over %s" % via if args.shard_mode == "owner"
+               "through an all-to-all over %s" % via if mode == "owner"
                else "replicated dictionary over %s" % via)
-        workload = ("vignat 64B, %d flows, %dxMI355X: one NF over all GPUs, "
+        workload = ("vignat %dB, %d flows, %dxMI355X: one NF over all GPUs, "
                     "each ingesting a contiguous 1/%d of every global batch "
-                    "(%s; new flows all-gathered)" % (args.flows, world, world, how))
+                    "(%s; new flows all-gathered)" % (flen, args.flows, world, world, how))
     else:
-        workload = "vignat 64B, %d flows, 1xMI355X" % args.flows
+        workload = "vignat %dB frames in %dB slots, %d flows, %s order, 1xMI355X" % (
+            flen, slot, args.flows, args.order)
+    kname = ("nat_classify64" if slot == SLOT else "nat_classify_wide")
+    if world > 1 and mode == "owner":
+        kname += "+nat_remote64"
+    extra = {}
+    if not args.no_extra and world == 1 and args.order == "rr":
+        # SURVEY.md §8(d) secondary order on the same warm table
+        el2, kms2, bufs2 = timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world,
+                                       rank, args.warmup + args.steps, args.steps,
+                                       "uniform", host_comm)
+        del bufs2
+        pl2, pk2, ach2 = kernel_rate(kms2, B, args.steps, alg_bytes)
+        extra["secondary_order"] = {
+            "order": "uniform (flow = splitmix64(0x5EED, p) mod N)",
+            "value": round(B * args.steps / el2 / 1e6, 2), "unit": "Mpps",
+            "ms_per_step": round(el2 / args.steps * 1e3, 4),
+            "kernel_ms_per_launch": round(pl2 * 1e3, 4),
+            "kernel_mpps": round(pk2 / pl2 / 1e6, 1),
+            "frac": round(ach2 / HBM_PEAK_GBS, 4)}
     e2e = None
-    if world == 1 and not args.no_e2e:
-        e2e = {"value": round(end_to_end(nat, bank, dev, gstart(args.warmup + args.steps)), 1),
+    if world == 1 and not args.no_e2e and slot == SLOT and args.order == "rr":
+        e2e = {"value": round(end_to_end(nat, bank, dev, (args.warmup + 2 * args.steps) * B), 1),
                "unit": "Mpps",
                "path": "page-locked host frames and per-packet arrays -> "
                        "hipMemcpyAsync H2D -> process -> D2H, %d-packet chunks "
-                       "double-buffered, H2D and D2H on two copy streams "
+                       "over three buffer sets (H2D two chunks ahead), H2D and "
+                       "D2H on two copy streams "
                        "(vp_process_host_batch, affine time)" % E2E_CHUNK,
                "batch_packets": E2E_BATCH,
                "pcie_bytes_per_packet": SLOT + 4 + SLOT + 2}
+    if world > 1 and not args.no_extra:
+        # the other dictionary placement, same workload
+        other = "replicated" if mode == "owner" else "owner"
+        nat.close()
+        nat2 = make_nat(other)
+        warm(nat2)
+        el3, kms3, bufs3 = timed_steps(nat2, bank, dev, lens, in_dev, out, B, slot, world,
+                                       rank, args.warmup, args.steps, "rr", host_comm)
+        del bufs3
+        extra["other_shard_mode"] = {
+            "mode": other, "value": round(B * args.steps * world / el3 / 1e6, 2),
+            "unit": "Mpps", "ms_per_step": round(el3 / args.steps * 1e3, 4)}
+        nat2.close()
     if rank == 0:
         cpu = None
-        if not args.no_cpu and world == 1:
+        if not args.no_cpu and world == 1 and slot == SLOT:
             cmpps, rates, sample, core = cpu_baseline(args.flows, args.cpu_sample)
             cpu = {"value": round(cmpps, 3), "unit": "Mpps", "cores": 1,
                    "kind": "port",
@@ -384,22 +531,23 @@ def main():
             "config": {"workload": workload, "flows": args.flows,
                        "batch_packets_per_gpu": B,
                        "global_batch_packets": B * world,
-                       "frame_bytes": 60, "slot_bytes": SLOT,
-                       "parallelism": ("%s%d" % (args.shard_mode, world))
+                       "frame_bytes": flen, "slot_bytes": slot,
+                       "order": args.order,
+                       "parallelism": ("%s%d" % (mode, world))
                        if world > 1 else "single"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "frac_step": round(mpps / world * 1e6 * alg_bytes / 1e9
+                                            / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "traffic_source": "profiles/%s: (2 x FETCH_SIZE + "
                                            "WRITE_SIZE) per launch / this "
                                            "run's kernel time" % TRAFFIC_PROFILE
                                            if traffic else None,
-                         "kernel": "nat_classify64" if world == 1 or
-                                   args.shard_mode == "replicated"
-                                   else "nat_classify64+nat_remote64",
+                         "kernel": kname,
                          "kernel_ms_per_launch": round(per_launch_s * 1e3, 4),
-                         "alg_bytes_per_packet": ALG_BYTES,
+                         "alg_bytes_per_packet": alg_bytes,
                          "kernel_mpps": round(pkts_per_launch / per_launch_s
                                               / 1e6, 1)},
             "cpu_baseline": cpu,
@@ -407,6 +555,7 @@ def main():
             "new_flow_mpps": round(new_flow_mpps, 2) if new_flow_mpps else None,
             "end_to_end": e2e,
         }
+        line.update(extra)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

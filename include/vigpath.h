@@ -46,6 +46,9 @@ extern "C" {
 #define VP_ENOMEM (-12)
 #define VP_EIO (-5)       /* HIP runtime failure */
 #define VP_ENOTSUP (-95)  /* outside the supported domain */
+#define VP_ESTATE (-71)   /* EPROTO: a device-side protocol of the library broke
+                           * (e.g. the fold kernel ended without publishing its
+                           * control block); distinct from a HIP failure */
 
 typedef struct vp_ctx vp_ctx;
 
@@ -127,9 +130,10 @@ void vp_destroy(vp_ctx *ctx);
 /* ------------------------------------------------------------ batches -- */
 
 /* A batch already resident in device memory (all pointers are device
- * pointers). Frames sit `slot` bytes apart and are rewritten in place, like
- * the mbuf data nf_process mutates (nf.c:154-156). `slot` must be a multiple
- * of 16 and >= 64. Bytes past a frame's slot read as 0.
+ * pointers). Frames sit `slot` bytes apart from a 16-byte aligned start and
+ * are rewritten in place, like the mbuf data nf_process mutates
+ * (nf.c:154-156). `slot` must be a multiple of 16 and >= 64 (wider slots:
+ * frames up to the slot, e.g. 1518 B in 1536 or mbuf-sized 2048). Bytes past a frame's slot read as 0.
  * Time: if `now` is NULL, packet i has now0 + i * now_step (ns); otherwise
  * now[i]. Times must be non-decreasing (nf.c takes them from
  * CLOCK_MONOTONIC, vigor-time.c:56-66) and >= 0 (nat_flowmanager.c:58). */
@@ -262,6 +266,26 @@ int vp_pol_dump(vp_ctx *ctx, uint8_t *alloc, int64_t *ts, uint32_t *keys,
 
 /* Number of live flows / learned MACs / flows+backends. */
 int64_t vp_live_count(vp_ctx *ctx);
+
+/* Bookkeeping of one device table: table 0 = the NF's flow table (vignat /
+ * vigfw flows, vigbridge dynamic MACs, viglb flows, vigpol destinations),
+ * table 1 = viglb's backend table. */
+typedef struct vp_table_stats {
+  uint64_t live;        /* allocated indices (dchain) */
+  uint64_t shard_live;  /* entries in this rank's buckets (= live unless
+                         * VP_SHARD_OWNER) */
+  uint64_t tombstones;  /* erased entries not yet rebuilt away */
+  uint64_t buckets;     /* 64-byte buckets (3 entries each) */
+  uint64_t rebuilds;    /* bucket-array rebuilds since creation */
+  uint32_t layout;      /* home-bucket mode (vp_table.h kMix*) */
+  uint32_t pad;
+} vp_table_stats;
+int vp_table_stats_get(vp_ctx *ctx, int table, vp_table_stats *out);
+
+/* Why the calling thread's last failing vp_* call failed: the HIP error and
+ * the call site for VP_EIO / VP_ENOMEM, the broken invariant for VP_ESTATE
+ * ("" if none was recorded). The text stays until the thread's next failure. */
+const char *vp_last_error(void);
 
 /* Per-context kernel timing of the last vp_process_device call: time of the
  * dominant classification kernel in ms (HIP events on the stream it ran on),

@@ -2,7 +2,8 @@
 for oracle/_ref). Inputs are the seeded traces of tests/golden_cases.py;
 expected outputs come from the oracle glue over the reference's own libVig.
 
-  python3 tests/golden/make_golden.py
+  python3 tests/golden/make_golden.py          (all)
+  python3 tests/golden/make_golden.py --wide   (nat_wide.npz only)
 """
 import os
 import sys
@@ -17,7 +18,27 @@ import golden_cases as G  # noqa: E402
 from vigor_amd import traces as T  # noqa: E402
 
 
+def wide():
+    """nat_wide.npz: 1518-byte frames in 2048-byte slots (golden_cases)."""
+    fr, ln, dv, now = G.wide_trace()
+    o = G.wide_oracle(ref=True)
+    assert o.L.orc_impl_name().decode() == "reference", o.L.orc_impl_name()
+    out_fr = fr.copy()
+    out = o.run(out_fr, ln, dv, now, G.WIDE_SLOT)
+    alloc, ts, _ = o.nat_dump(G.WIDE_CAP)
+    np.savez_compressed(os.path.join(HERE, "nat_wide.npz"),
+                        in_hash=G.slot_hashes(fr, G.WIDE_SLOT), out_dev=out,
+                        out_hash=G.slot_hashes(out_fr, G.WIDE_SLOT), alloc=alloc,
+                        ts=np.where(alloc == 1, ts, 0),
+                        impl=np.array(o.L.orc_impl_name().decode()))
+    print("nat_wide packets", ln.shape[0], "max len", int(ln.max()), "dropped",
+          int((out == dv).sum()), "live", int(alloc.sum()))
+
+
 def main():
+    if sys.argv[1:] == ["--wide"]:
+        return wide()
+    wide()
     for name, (kind, cap, trace) in G.CASES.items():
         fr, ln, dv, now = trace()
         o = G.oracle(name, ref=True)

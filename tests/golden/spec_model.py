@@ -209,13 +209,56 @@ class _IntDiv(ast.NodeTransformer):
         return node
 
 
+# The spec files are public, untrusted text: before anything runs, their AST
+# must stay inside the vocabulary the reference's specs use (assertions,
+# assignments, conditionals, arithmetic, calls of the model's constructors
+# and of emap/vector methods). No imports, loops, lambdas, comprehensions,
+# f-strings or dunder names; no attribute beginning with "_". They run with
+# no builtins, over the model objects the caller passes in.
+_SPEC_NODES = {
+    "Module", "FunctionDef", "arguments", "Assert", "Assign", "AugAssign", "Expr",
+    "If", "Return", "Pass", "BinOp", "BoolOp", "UnaryOp", "Compare", "Call",
+    "keyword", "Attribute", "Name", "Load", "Store", "Constant", "List", "Tuple",
+    "Subscript", "IfExp",
+    "Add", "Sub", "Mult", "Div", "FloorDiv", "Mod", "BitAnd", "BitOr", "BitXor",
+    "LShift", "RShift", "And", "Or", "Not", "USub", "UAdd", "Invert",
+    "Eq", "NotEq", "Lt", "LtE", "Gt", "GtE", "Is", "IsNot", "In", "NotIn"}
+
+
+class SpecRejected(ValueError):
+    pass
+
+
+def check_spec_ast(tree: ast.AST) -> None:
+    """Raise SpecRejected unless every node is in the spec vocabulary."""
+    for node in ast.walk(tree):
+        kind = type(node).__name__
+        if kind not in _SPEC_NODES:
+            raise SpecRejected("spec uses %s (line %s)" % (kind, getattr(node, "lineno", "?")))
+        if isinstance(node, ast.Name) and node.id.startswith("__"):
+            raise SpecRejected("spec names %r" % node.id)
+        if isinstance(node, ast.Attribute) and node.attr.startswith("_"):
+            raise SpecRejected("spec reads attribute %r" % node.attr)
+        if isinstance(node, ast.FunctionDef) and node.name.startswith("__") \
+                and node.name != "__spec__":
+            raise SpecRejected("spec defines %r" % node.name)
+        if isinstance(node, ast.Call) and not isinstance(node.func, (ast.Name, ast.Attribute)):
+            raise SpecRejected("spec calls a computed callee (line %s)" % node.lineno)
+        if isinstance(node, ast.Constant) and not (isinstance(node.value, (int, bool))
+                                                    or node.value in (None, Ellipsis)):
+            raise SpecRejected("spec constant %r" % (node.value,))
+
+
 def compile_spec(text: str):
     """The spec text as a function of one packet's environment (the
-    `from state import ...` line's objects come from the caller's env)."""
+    `from state import ...` line's objects come from the caller's env),
+    after check_spec_ast has accepted it."""
     body = "\n".join(l for l in text.splitlines()
                      if not l.startswith("from state import"))
     src = "def __spec__():\n" + textwrap.indent(body, "    ") + "\n"
-    tree = ast.fix_missing_locations(_IntDiv().visit(ast.parse(src)))
+    tree = ast.parse(src)
+    check_spec_ast(tree)
+    tree = ast.fix_missing_locations(_IntDiv().visit(tree))
     return compile(tree, "<spec>", "exec")
 
 
@@ -233,6 +276,7 @@ def run_packet(code, env: dict, headers: dict):
             raise _Drop()
         return headers[k]
     g = dict(env, pop_header=pop_header, **_CTORS)
+    g["__builtins__"] = {}  # the spec sees the model's objects only
     ns = {}
     exec(code, g, ns)
     try:

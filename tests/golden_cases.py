@@ -21,7 +21,7 @@ import numpy as np
 
 import orc
 from tracegen import (mixed_bridge_trace, mixed_fw_trace, mixed_lb_trace,
-                      mixed_nat_trace, mixed_pol_trace)
+                      mixed_nat_trace, mixed_pol_trace, wide_nat_trace)
 from vigor_amd import traces as T
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -196,3 +196,45 @@ def run_oracle_chunks(o, n_packets, n_flows, start=0, on_chunk=None):
         if on_chunk:
             on_chunk(p, fr, out)
         p += m
+
+
+# Wide slots (north_star: 64-1518 B frames): vignat churn over frames of
+# 60..1518 bytes with random payloads in 2048-byte (mbuf-sized) slots, table
+# of 256 flows with expiry, WAN replies, padded / odd / malformed frames. The
+# trace is regenerated from its seed (a fixture of 8 MB of random payload
+# would be copied data, not a vector); stored: a digest of the input slots
+# (generator drift), out ports, a per-packet FNV-1a-64 of each output slot
+# (orc.slot_hashes), and the final allocated indices with their stamps.
+WIDE_N, WIDE_SLOT, WIDE_CAP = 4096, 2048, 256
+
+
+def wide_trace():
+    return wide_nat_trace(np.random.default_rng(106), WIDE_N, 300, WIDE_SLOT,
+                          max_len=1518)
+
+
+def wide_oracle(ref=False):
+    cfg = orc.nat_cfg(wan=1, start_port=0, ext_ip=T.ip4(192, 168, 4, 2),
+                      expire_us=2, max_flows=WIDE_CAP, device_macs=DEV3[:2],
+                      endpoint_macs=END3[:2], n_devices=2)
+    return orc.Oracle("nat", cfg, ref=ref)
+
+
+def wide_gpu():
+    import vigor_amd
+    args = ["--wan", "1", "--expire", "2", "--starting-port", "0",
+            "--max-flows", str(WIDE_CAP), "--extip", "192.168.4.2"]
+    for d in range(2):
+        args += ["--eth-dest", "%d,%s" % (d, END3[d].hex(":"))]
+    return vigor_amd.Nat(vigor_amd.nat_config_from_args(args, 2, DEV3[:2]))
+
+
+def slot_hashes(frames, slot):
+    """FNV-1a-64 over each slot's 8-byte LE words (per packet)."""
+    w = np.ascontiguousarray(frames.reshape(-1, slot)).view("<u8")
+    h = np.full(w.shape[0], T.FNV64_BASIS, np.uint64)
+    with np.errstate(over="ignore"):
+        for j in range(w.shape[1]):
+            np.bitwise_xor(h, w[:, j], out=h)
+            np.multiply(h, np.uint64(T.FNV64_PRIME), out=h)
+    return h

@@ -167,3 +167,56 @@ def test_restated_oracle_reproduces_16m_digest():
     assert acc[0] % (1 << 64) == int(g["digest"])
     alloc, ts, _ = o.nat_dump(G.F16M_FLOWS)
     assert T.state_digest(alloc, ts) == int(g["state_digest"])
+
+
+# ---- wide slots: 60..1518-byte frames in 2048-byte slots ------------------
+
+def _wide_golden():
+    g = G.load("nat_wide")
+    assert str(g["impl"]) == "reference"
+    fr, ln, dv, now = G.wide_trace()
+    # the trace regenerates bit-identically from its seed (no generator drift)
+    np.testing.assert_array_equal(G.slot_hashes(fr, G.WIDE_SLOT), g["in_hash"])
+    assert int(ln.max()) == 1518
+    return g, (fr, ln, dv, now)
+
+
+def _wide_check(g, out, frames, alloc, ts):
+    bad = np.nonzero(out != g["out_dev"])[0]
+    assert bad.size == 0, "out port mismatch at %s" % bad[:10]
+    badf = np.nonzero(G.slot_hashes(frames, G.WIDE_SLOT) != g["out_hash"])[0]
+    assert badf.size == 0, "frame mismatch at %s" % badf[:10]
+    np.testing.assert_array_equal(alloc, g["alloc"])
+    np.testing.assert_array_equal(np.where(alloc == 1, ts, 0), g["ts"])
+
+
+def test_restated_oracle_reproduces_wide():
+    g, (fr, ln, dv, now) = _wide_golden()
+    o = G.wide_oracle()
+    f = fr.copy()
+    out = o.run(f, ln, dv, now, G.WIDE_SLOT)
+    alloc, ts, _ = o.nat_dump(G.WIDE_CAP)
+    _wide_check(g, out, f, alloc, ts)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("slot", [2048, 1536])
+def test_gpu_reproduces_wide(slot):
+    """The reference's answers for 1518-byte frames through the wide-slot
+    kernels, in the fixture's 2048-byte slots and re-packed into 1536-byte
+    slots (every frame fits; the bytes past 1536 are not the NF's), two
+    batches."""
+    g, (fr, ln, dv, now) = _wide_golden()
+    S = G.WIDE_SLOT
+    src = fr.reshape(-1, S)[:, :slot].copy().reshape(-1)
+    nat = G.wide_gpu()
+    outs, frames = [], []
+    for a, b in ((0, 1500), (1500, G.WIDE_N)):
+        f, o = run_gpu(nat, src[a * slot:b * slot], ln[a:b], dv[a:b], now[a:b], slot)
+        frames.append(f)
+        outs.append(o)
+    got = np.concatenate(frames).reshape(-1, slot)
+    full = fr.reshape(-1, S).copy()
+    full[:, :slot] = got  # the tail past `slot` is the unmodified input
+    alloc, ts, _ = nat.dump()
+    _wide_check(g, np.concatenate(outs), full.reshape(-1), alloc, ts)

@@ -109,3 +109,26 @@ def test_rejects_bad_config():
         make_pair(bcap=128, height=97)  # backends >= height
     with pytest.raises(vigor_amd.VigpathError):
         make_pair(flow_cap=1000)
+
+
+def test_stale_frees_keep_shard_count():
+    """Flows whose backend died while no backend is alive are erased and
+    their indices freed (lb_stale_free_seq) — cycle after cycle. The bucket
+    bookkeeping must follow (shard_live == live: the layout and rebuild
+    checks count it), so the table does not rebuild on every check; outputs
+    and state equal the oracle's throughout."""
+    nb, nfl = 20, 200
+    lb, o = make_pair(flow_cap=256, bexp=5_000)  # backends expire after 5 ms
+    for c in range(12):
+        t = T.NOW0 + c * 10_000_000
+        stale = T.lb_traffic(nfl, nfl)            # backends expired: stale frees
+        hb = T.lb_heartbeats(nb, t0=t + 1_000)
+        fresh = T.lb_traffic(2 * nfl, nfl)        # re-balanced, new indices
+        stale = stale[:3] + (t + np.arange(nfl, dtype=np.int64),)
+        fresh = fresh[:3] + (t + 2_000 + np.arange(2 * nfl, dtype=np.int64),)
+        fr, ln, dv, now = concat(stale, hb, fresh)
+        check_batches(lb, o, fr, ln, dv, now, 64, [nfl + 7])
+        st = lb.table_stats(0)
+        assert st["shard_live"] == st["live"], (c, st)
+    check_state(lb, o)
+    assert lb.table_stats(0)["rebuilds"] <= 4, lb.table_stats(0)

@@ -8,7 +8,7 @@ import pytest
 import orc
 import vigor_amd
 from gpuh import check_batches, run_gpu
-from tracegen import edge_nat_trace, lan_tile_trace, mixed_nat_trace
+from tracegen import edge_nat_trace, lan_tile_trace, mixed_nat_trace, wide_nat_trace
 from vigor_amd import traces as T
 
 pytestmark = pytest.mark.gpu
@@ -67,8 +67,8 @@ def test_mixed_traces(seed, max_flows, expire_us, n_flows, cuts):
     check_state(nat, o, max_flows)
 
 
-@pytest.mark.parametrize("slot,long_frames", [(64, False), (128, False),
-                                              (2048, True)])
+@pytest.mark.parametrize("slot,long_frames", [(64, False), (128, False), (256, True),
+                                              (1536, True), (2048, True)])
 def test_header_edge_cases(slot, long_frames):
     rng = np.random.default_rng(slot)
     n = 3000
@@ -330,4 +330,71 @@ def test_prepared_device_step():
         torch.cuda.synchronize()
         assert np.array_equal(o_t.cpu().numpy().view(np.uint16), exp_out)
         assert np.array_equal(f_t.cpu().numpy(), exp)
+    check_state(nat, o, nf)
+
+
+def test_rebuild_inside_phase_b_then_phase_c():
+    """One vp_process_device call whose phase B allocates enough flows to
+    switch the table to the allocation-order layout (tbl_try_linear rebuilds
+    the buckets at half the count, freeing the old array), followed in the
+    same segment by WAN replies to those flows (phase C reads the buckets).
+    Round 2's nat_churn EIO was a stale bucket pointer in exactly this spot;
+    the layout switch must happen here and the results equal the oracle's."""
+    cap, n_new = 1024, 600  # > cap / 2 live: the linear layout is tried
+    nat, o = make_pair(max_flows=cap)
+    fr, ln, dv, now = T.nat_lan_trace(n_new, n_new)
+    rep = fr.reshape(n_new, 64).copy()  # WAN replies to flows 0..n_new-1
+    rep[:, 26:34] = 0                                  # src 0.0.0.0, dst (unchecked)
+    rep[:, 34:36] = 0                                  # src_port = flow dst_port 0
+    idx = np.arange(n_new)
+    rep[:, 36], rep[:, 37] = idx & 0xFF, idx >> 8      # dst_port = external port (raw)
+    fr2 = np.concatenate([fr, rep.reshape(-1)])
+    ln2 = np.concatenate([ln, ln])
+    dv2 = np.concatenate([dv, np.ones(n_new, np.uint16)])
+    now2 = T.NOW0 + np.arange(2 * n_new, dtype=np.int64)
+    before = nat.table_stats()
+    check_batches(nat, o, fr2, ln2, dv2, now2, 64, [])
+    after = nat.table_stats()
+    assert after["rebuilds"] > before["rebuilds"], (before, after)
+    assert after["buckets"] < before["buckets"], (before, after)  # the array moved
+    fr3, ln3, dv3, now3 = T.nat_lan_trace(3 * n_new, n_new, start=2 * n_new)
+    check_batches(nat, o, fr3, ln3, dv3, now3, 64, [1000])
+    check_state(nat, o, cap)
+
+
+@pytest.mark.parametrize("slot,max_len", [(80, 80), (96, 96), (128, 128), (192, 192),
+                                          (256, 256), (512, 512), (1536, 1518),
+                                          (2048, 1518)])
+def test_wide_slots(slot, max_len):
+    """Frames of 60..1518 bytes in wide slots through nat_classify_wide<G>
+    (tile_tail_sums: the L4 sum's bytes past the first 64, G lanes per
+    frame): new flows, hits, WAN replies, padded frames, odd lengths and
+    malformed frames, several batches; out ports, every slot byte and the
+    table state equal the oracle's."""
+    rng = np.random.default_rng(slot)
+    fr, ln, dv, now = wide_nat_trace(rng, 6000, 400, slot, max_len=max_len)
+    nat, o = make_pair(max_flows=1024)
+    check_batches(nat, o, fr, ln, dv, now, slot, [700, 700 + 64 * 5, 4100])
+    check_state(nat, o, 1024)
+
+
+@pytest.mark.parametrize("slot", [128, 1536])
+def test_wide_steady_state(slot):
+    """Bench-shaped wide traffic (every packet a hit after the warm-up, the
+    lean tile with the touch bins) in 1518-byte or 124-byte frames with a
+    payload pattern."""
+    nf = 1 << 12
+    nat, o = make_pair(max_flows=nf)
+    flen = min(slot - 4, 1514)
+    for j, B in enumerate((nf, 1 << 15, 1 << 15)):
+        start = 0 if j == 0 else nf + (j - 1) * (1 << 15)
+        fl = T.flow_order(B, nf, start=start)
+        z = np.zeros_like(fl)
+        fr, ln = T.udp_frames(T.ip4(10, 0, 0, 0) + (fl >> 16), z, fl & 0xFFFF, z,
+                              slot=slot, frame_len=flen)
+        f2 = fr.reshape(B, slot)
+        f2[:, 42:flen] = (np.arange(42, flen) * 7 % 251).astype(np.uint8)
+        dv = np.zeros(B, np.uint16)
+        now = T.NOW0 + np.arange(start, start + B, dtype=np.int64)
+        check_batches(nat, o, fr, ln, dv, now, slot, [], affine=True)
     check_state(nat, o, nf)

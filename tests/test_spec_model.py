@@ -71,3 +71,27 @@ def test_spec_fixtures_regenerate(tmp_path, monkeypatch):
         old = np.load(os.path.join(HERE, "golden", "spec_%s.npz" % nf))
         for k in old.files:
             assert np.array_equal(new[k], old[k]), (nf, k)
+
+
+@pytest.mark.parametrize("text", [
+    "import os\nreturn ([], [])\n",
+    "from os import system\n",
+    "x = ether.__class__\n",
+    "__import__('os')\n",
+    "f = lambda: 1\n",
+    "for i in [1]:\n    pass\n",
+    "return ([open], [])\n" + "x = 'text'\n",
+    "return [y for y in [1]]\n",
+    "(pop_header)(ether, on_mismatch=([], []))\n" + "x = [1][0]()\n",
+])
+def test_spec_sandbox_rejects(text):
+    """The spec files are untrusted text: anything outside the specs'
+    vocabulary is refused before it is compiled, let alone run."""
+    with pytest.raises(S.SpecRejected):
+        S.compile_spec(text)
+
+
+def test_spec_runs_without_builtins():
+    code = S.compile_spec("return ([open], [])\n")
+    with pytest.raises(NameError):
+        S.run_packet(code, {}, {})

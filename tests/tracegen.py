@@ -241,3 +241,57 @@ def lan_tile_trace(rng, n, n_flows, bad_tiles=0.1, slot=64):
     in_dev = np.zeros(n, np.uint16)
     now = T.NOW0 + np.cumsum(rng.integers(0, 4, n))
     return frames.reshape(-1), lens, in_dev, now.astype(np.int64)
+
+
+def wide_nat_trace(rng, n, n_flows, slot, max_len=1518, wan_frac=0.25,
+                   bad_frac=0.03, pad_frac=0.1):
+    """vignat traffic in wide slots (65-1518 B frames, SURVEY.md §8(d) "R =
+    slot(len) + 28"): frame lengths uniform in [60, min(slot, max_len)],
+    random payload bytes (so the L4 checksum covers real data), TCP and UDP,
+    LAN packets over n_flows and WAN replies to indices 0..2 n_flows (known,
+    unknown, wrong protocol), some frames padded past total_length (the L4 sum ends at
+    14 + total_length, not at the frame's end), odd lengths, and a few
+    malformed frames (not IPv4, IHL 6, total_length past the frame) that
+    take the byte-addressed path. Monotone time with ties."""
+    top = min(slot, max_len)
+    fl = rng.integers(0, n_flows, n)
+    sip = T.ip4(10, 2, 0, 0) + fl
+    dip = np.full(n, T.ip4(9, 9, 0, 1))
+    sp = 3000 + fl % 19
+    dp = np.full(n, 443)
+    proto = np.where(fl % 3 == 0, 6, 17)
+    lens = rng.integers(60, top + 1, n).astype(np.uint16)
+    frames = rng.integers(0, 256, (n, slot), dtype=np.uint8)
+    for p_ in (6, 17):
+        m = proto == p_
+        f, _ = T.udp_frames(sip[m], dip[m], sp[m], dp[m], slot=slot, proto=p_)
+        f = f.reshape(-1, slot)
+        frames[m, :38] = f[:, :38]
+        if p_ == 17:  # UDP length; checksum field left random (recomputed)
+            frames[m, 38:40] = 0
+    tl = lens.astype(np.int64) - 14
+    pad = rng.random(n) < pad_frac  # total_length short of the frame
+    tl[pad] = np.maximum(20, tl[pad] - rng.integers(1, 40, int(pad.sum())))
+    frames[:, 16] = (tl >> 8).astype(np.uint8)
+    frames[:, 17] = (tl & 0xFF).astype(np.uint8)
+    udp = proto == 17
+    ul = tl[udp] - 20
+    frames[udp, 38] = (ul >> 8).astype(np.uint8)
+    frames[udp, 39] = (ul & 0xFF).astype(np.uint8)
+    in_dev = np.zeros(n, np.uint16)
+    wan = rng.random(n) < wan_frac
+    in_dev[wan] = 1
+    w = frames[wan]
+    w[:, 26:30], w[:, 30:34] = frames[wan][:, 30:34], frames[wan][:, 26:30]
+    w[:, 34:36] = frames[wan][:, 36:38]
+    idx = rng.integers(0, n_flows + n_flows // 4, int(wan.sum())).astype(np.uint16)
+    w[:, 36] = (idx & 0xFF).astype(np.uint8)
+    w[:, 37] = (idx >> 8).astype(np.uint8)
+    frames[wan] = w
+    bad = rng.random(n)
+    frames[bad < bad_frac / 3, 12] = 0x86
+    frames[(bad >= bad_frac / 3) & (bad < 2 * bad_frac / 3), 14] = 0x46
+    big = (bad >= 2 * bad_frac / 3) & (bad < bad_frac)
+    frames[big, 16] = 0xFF  # total_length past the packet: dropped
+    now = T.NOW0 + np.cumsum(rng.integers(0, 3, n))
+    return frames.reshape(-1), lens, in_dev, now.astype(np.int64)

@@ -12,6 +12,7 @@
 #   pmcnf:NF the two --pmc passes over tools/bench_nf.py --only NF
 #   shard2   bench.py --gpus 2 with VIGPATH_COMM=host (ranks share GPU 0)
 #   e2e      tools/bench_e2e.py                   -> gpurun_out/TAG_e2e.log
+#   slots:S,S,..  bench.py --slot S (wide frames) per slot -> gpurun_out/TAG_slots.log
 #   nf       tools/bench_nf.py                    -> gpurun_out/TAG_nf.log
 #   test:EXPR  pytest -m gpu -k EXPR
 #   probe[:ARG] tools/stream_probe [ARG]          -> gpurun_out/TAG_probe.log
@@ -64,6 +65,10 @@ for step in "$@"; do
     shard2) VIGPATH_COMM=host run shard2 600 python3 bench.py --gpus 2 --no-cpu --no-e2e $BA \
              > $O/${TAG}_shard2.log 2>&1 || exit $? ;;
     e2e) run e2e 600 python3 tools/bench_e2e.py > $O/${TAG}_e2e.log 2>&1 || exit $? ;;
+    slots:*) for sl in $(echo ${step#slots:} | tr , ' '); do
+               run "slot$sl" 300 python3 bench.py --slot $sl --no-cpu --no-e2e --no-extra $BA \
+                 >> $O/${TAG}_slots.log 2>&1 || exit $?
+             done ;;
     probe|probe:*) a=${step#probe}; a=${a#:}
            run probe 300 tools/stream_probe $a > $O/${TAG}_probe.log 2>&1 || exit $? ;;
     ablate:*) ABLATE_ONLY=${step#ablate:} run ablate 600 python3 tools/ablate.py 5 \

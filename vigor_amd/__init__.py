@@ -17,14 +17,25 @@ MAX_DEV = 32
 FLOOD_FRAME = 0xFFFF
 
 VP_OK, VP_EINVAL, VP_ENOMEM, VP_EIO, VP_ENOTSUP = 0, -22, -12, -5, -95
+VP_ESTATE = -71
 _ERR = {VP_EINVAL: "EINVAL", VP_ENOMEM: "ENOMEM", VP_EIO: "EIO (HIP)",
+        VP_ESTATE: "ESTATE (device protocol)",
         VP_ENOTSUP: "ENOTSUP"}
 
 
 class VigpathError(RuntimeError):
-    def __init__(self, rc: int, what: str):
-        super().__init__(f"{what}: {_ERR.get(rc, rc)}")
+    def __init__(self, rc: int, what: str, detail: str = ""):
+        super().__init__(f"{what}: {_ERR.get(rc, rc)}" + (f" [{detail}]" if detail else ""))
         self.rc = rc
+        self.detail = detail
+
+
+class TableStatsC(C.Structure):
+    """vp_table_stats (include/vigpath.h)."""
+    _fields_ = [("live", C.c_uint64), ("shard_live", C.c_uint64),
+                ("tombstones", C.c_uint64), ("buckets", C.c_uint64),
+                ("rebuilds", C.c_uint64), ("layout", C.c_uint32),
+                ("pad", C.c_uint32)]
 
 
 MacTable = (C.c_uint8 * 6) * MAX_DEV
@@ -105,7 +116,8 @@ EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_fw_create",
            "vp_process_host", "vp_process_host_batch", "vp_nat_dump", "vp_bridge_dump", "vp_lb_dump",
            "vp_fw_dump", "vp_comm_unique_id", "vp_attach_rccl",
            "vp_attach_comm", "vp_shard_mode", "vp_sync_state", "vp_live_count",
-           "vp_last_kernel_ms", "vp_version"]
+           "vp_last_kernel_ms", "vp_version", "vp_table_stats_get",
+           "vp_last_error"]
 
 _libs = {}
 
@@ -175,13 +187,21 @@ def lib(path: str | None = None):
     L.vp_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float),
                                     C.POINTER(C.c_int)]
     L.vp_last_kernel_ms.restype = C.c_int
+    L.vp_table_stats_get.argtypes = [C.c_void_p, C.c_int, C.POINTER(TableStatsC)]
+    L.vp_table_stats_get.restype = C.c_int
+    L.vp_last_error.argtypes = []
+    L.vp_last_error.restype = C.c_char_p
     _libs[path] = L
     return L
 
 
 def _check(rc: int, what: str):
     if rc != 0:
-        raise VigpathError(rc, what)
+        detail = ""
+        L = next(iter(_libs.values()), None)
+        if L is not None:
+            detail = (L.vp_last_error() or b"").decode(errors="replace")
+        raise VigpathError(rc, what, detail)
 
 
 from .nf import Bridge, Fw, Lb, Nat, NfBase, Pol  # noqa: E402,F401

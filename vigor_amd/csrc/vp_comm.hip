@@ -13,8 +13,7 @@
 namespace vp {
 
 static int nccl_fail(ncclResult_t e, const char *what) {
-  if (getenv("VIGPATH_DEBUG"))
-    fprintf(stderr, "vigpath: %s failed: %s\n", what, ncclGetErrorString(e));
+  state_fail("RCCL %s failed: %s", what, ncclGetErrorString(e));  // (the message)
   return VP_EIO;
 }
 #define VP_NCCL(call)                                  \
@@ -100,6 +99,11 @@ struct RcclComm : Comm {
   }
 };
 
+static int comm_fail(const char *what) {
+  state_fail("caller-supplied %s callback failed", what);  // (the message)
+  return VP_EIO;
+}
+
 // Caller-supplied host-memory collectives; device variants stage through
 // host memory.
 struct HostComm : Comm {
@@ -107,14 +111,14 @@ struct HostComm : Comm {
   std::vector<uint8_t> hs, hr;
   int allgather_host(vp_ctx *c, const void *send, void *recv, size_t bytes) override {
     (void)c;
-    return ops.allgather(ops.user, send, recv, bytes) ? VP_EIO : 0;
+    return ops.allgather(ops.user, send, recv, bytes) ? comm_fail("allgather") : 0;
   }
   int allgather_dev(vp_ctx *c, const void *send, void *recv, size_t bytes) override {
     hs.resize(bytes ? bytes : 1);
     hr.resize(bytes * n ? bytes * n : 1);
     VP_HIP(hipMemcpyAsync(hs.data(), send, bytes, hipMemcpyDeviceToHost, c->stream));
     VP_HIP(hipStreamSynchronize(c->stream));
-    if (ops.allgather(ops.user, hs.data(), hr.data(), bytes)) return VP_EIO;
+    if (ops.allgather(ops.user, hs.data(), hr.data(), bytes)) return comm_fail("allgather");
     VP_HIP(hipMemcpyAsync(recv, hr.data(), bytes * n, hipMemcpyHostToDevice,
                           c->stream));
     VP_HIP(hipStreamSynchronize(c->stream));
@@ -127,7 +131,7 @@ struct HostComm : Comm {
     VP_HIP(hipStreamSynchronize(c->stream));
     if (ops.allreduce_max_u64(ops.user, reinterpret_cast<uint64_t *>(hs.data()),
                               count))
-      return VP_EIO;
+      return comm_fail("allreduce_max_u64");
     VP_HIP(hipMemcpyAsync(buf, hs.data(), count * 8, hipMemcpyHostToDevice,
                           c->stream));
     VP_HIP(hipStreamSynchronize(c->stream));
@@ -145,7 +149,8 @@ struct HostComm : Comm {
     hr.resize(rt ? rt : 1);
     if (st) VP_HIP(hipMemcpyAsync(hs.data(), send, st, hipMemcpyDeviceToHost, c->stream));
     VP_HIP(hipStreamSynchronize(c->stream));
-    if (ops.alltoallv(ops.user, hs.data(), sbytes, hr.data(), rbytes)) return VP_EIO;
+    if (ops.alltoallv(ops.user, hs.data(), sbytes, hr.data(), rbytes))
+      return comm_fail("alltoallv");
     if (rt) {
       VP_HIP(hipMemcpyAsync(recv, hr.data(), rt, hipMemcpyHostToDevice, c->stream));
       VP_HIP(hipStreamSynchronize(c->stream));

@@ -85,12 +85,46 @@ __device__ inline uint32_t fold16(uint32_t s) {
   s = (s >> 16) + (s & 0xFFFF);
   return s;
 }
+
+// The raw sum's inner step over 16 bytes at an even offset: the four LE words'
+// 16-bit halves added to s (v_sad_u16 against zero adds both halves at once).
+__device__ __forceinline__ uint32_t sum16x4(const uint4 v, uint32_t s) {
+  s = __builtin_amdgcn_sad_u16(v.x, 0u, s);
+  s = __builtin_amdgcn_sad_u16(v.y, 0u, s);
+  s = __builtin_amdgcn_sad_u16(v.z, 0u, s);
+  return __builtin_amdgcn_sad_u16(v.w, 0u, s);
+}
+// Bytes [lo, hi) of a 16-byte chunk kept, the others zeroed (0 <= lo, hi <= 16).
+__device__ __forceinline__ uint32_t bytes_mask(int lo, int hi) {
+  lo = lo < 0 ? 0 : lo > 4 ? 4 : lo;
+  hi = hi < 0 ? 0 : hi > 4 ? 4 : hi;
+  return (uint32_t)(((1ull << (8 * hi)) - 1) & ~((1ull << (8 * lo)) - 1));
+}
+__device__ __forceinline__ uint4 chunk_keep(uint4 v, int lo, int hi) {
+  v.x &= bytes_mask(lo, hi);
+  v.y &= bytes_mask(lo - 4, hi - 4);
+  v.z &= bytes_mask(lo - 8, hi - 8);
+  v.w &= bytes_mask(lo - 12, hi - 12);
+  return v;
+}
+
+// __rte_raw_cksum over bytes [off, off + len) of a frame (off even): the sum
+// of the LE 16-bit words, an odd last byte as a word's low byte; bytes past
+// the slot count as 0. Aligned 16-byte loads (slots are multiples of 16 and
+// start 16-byte aligned), the chunks at either end masked.
+__device__ inline uint32_t raw_sum(const GFrame &f, uint32_t off, uint32_t len) {
+  const uint32_t hi = min(off + len, f.cap);
+  uint32_t s = 0;
+  for (uint32_t c = off & ~15u; c < hi; c += 16) {
+    uint4 v = *reinterpret_cast<const uint4 *>(f.b + c);
+    if (c < off || c + 16 > hi) v = chunk_keep(v, (int)off - (int)c, (int)hi - (int)c);
+    s = sum16x4(v, s);
+  }
+  return s;
+}
 __device__ inline uint32_t raw_cksum(const GFrame &f, uint32_t off,
                                      uint32_t len) {
-  uint32_t sum = 0, i = 0;
-  for (; i + 1 < len; i += 2) sum += f.r16(off + i);
-  if (len & 1) sum += f.r8(off + i);
-  return fold16(sum);
+  return fold16(raw_sum(f, off, len));
 }
 // rte_ipv4_phdr_cksum: {src, dst, 0, proto, be16(l4_len)} as 6 LE words.
 __device__ inline uint32_t phdr_cksum(uint32_t src, uint32_t dst, uint8_t proto,
@@ -183,6 +217,16 @@ __device__ __forceinline__ void tile_st(uint4 *g, uint32_t c, uint4 v) {
 #endif
 }
 
+// Stores of the wide-slot classify tiles: 16 bytes at byte `off` of the tile
+// at g (64 slots, `bytes` in all), write-through like tile_st.
+__device__ __forceinline__ void tile_st_at(uint8_t *g, uint32_t bytes, uint32_t off,
+                                           uint4 v) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(g, 0, (int)bytes, 0x00020000);
+  const v4u x = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)off, 0, 16);
+}
+
 // ------------------------------------------------------------ fast frames --
 // The 64-byte slot held in 16 registers (LE words). Only compile-time word
 // indices are used so nothing spills to scratch.
@@ -253,7 +297,8 @@ __device__ __forceinline__ uint32_t group_reserve(uint32_t *ctr, uint32_t ch,
 // four 64-byte pieces into four bins whose lines stayed partial in L2 for
 // dozens of tiles: 11 % of the classify kernel, tools/ablate.py NOBINS).
 // Each block appends to
-// its own fixed-size slice of every bin (LDS cursors). With bins on, the
+// its own fixed-size slice of every bin (LDS cursors); a bin's slices are
+// adjacent (bin-major), so the fold reads each bin as one region. With bins on, the
 // classify kernels write no per-packet touch log: a touch that finds its
 // slice full is logged alone (olog[p] = index) and queued on the block's
 // overflow slice (oent/ocnt), and *ovf tells the host to apply the queued
@@ -273,13 +318,15 @@ struct TileQueue {
   uint32_t *total;  // += every block's count (one atomic per block)
 };
 struct TouchBins {
-  uint32_t *ent;  // [block][bin][cap] entries (in-bin << pbits | position); null = off
-  uint32_t *cnt;  // [block][bin] entries written
+  // bin-major: the fold's block for bin b reads one contiguous region
+  uint32_t *ent;  // [bin][block][cap] entries (in-bin << pbits | position); null = off
+  uint32_t *cnt;  // [bin][block] entries written
   uint32_t *ovf;  // set when a slice overflowed
   uint32_t *oent;  // [block][range] positions of overflowed touches
   uint32_t *ocnt;  // [block] overflowed touches queued
   uint32_t *olog;  // olog[p] = index of an overflowed touch
   uint32_t cap, pbits, bbits;
+  uint32_t nsrc;  // classify blocks (the launch's grid)
 };
 // Per-packet side stores of the classify tiles (touch-bin entry, out port):
 // ablation builds make them write-through (`sc1`, relaxed agent-scope
@@ -327,7 +374,7 @@ __device__ __forceinline__ void bins_put(const TouchBins &bins, uint32_t *cur,
   const uint32_t k = group_reserve(cur, b, v);
   const bool fits = k < bins.cap;
   if (v && fits)
-    VP_BIN_ST(bins.ent + (((size_t)rb << bins.bbits) + b) * bins.cap + k,
+    VP_BIN_ST(bins.ent + ((size_t)b * bins.nsrc + rb) * bins.cap + k,
               (bin_local(touch, bins.bbits) << bins.pbits) | (p - range0));
   const bool spill = v && !fits;
   const uint32_t o = group_reserve(cur, kCurOverflow, spill);
@@ -343,7 +390,7 @@ __device__ __forceinline__ void bins_publish(const TouchBins &bins, const uint32
   if (!bins.ent) return;
   for (uint32_t b = threadIdx.x; b < (1u << bins.bbits); b += blockDim.x) {
     const uint32_t c = cur[b];
-    bins.cnt[((size_t)rb << bins.bbits) + b] = c < bins.cap ? c : bins.cap;
+    bins.cnt[(size_t)b * bins.nsrc + rb] = c < bins.cap ? c : bins.cap;
   }
   if (threadIdx.x == 0) {
     const uint32_t o = cur[kCurOverflow];
@@ -623,9 +670,80 @@ __device__ __forceinline__ void reprobe_slices(const uint32_t *list, const uint3
   }
 }
 
-// Checksums of a 64-byte IHL=5 frame with total_length <= 50 (so every byte
-// the L4 sum covers lies in the slot). Same arithmetic as set_checksums.
-__device__ inline void fast_checksums(RFrame &f, uint32_t proto, uint32_t tl) {
+// ------------------------------------------------------------ wide slots --
+// Slots wider than 64 bytes (frames of 65-1518 B and mbuf-sized slots,
+// DESIGN.md §5.4): the classify kernels keep each frame's first 64 bytes in
+// registers, as for 64-byte slots, and take the rest of the L4 checksum's
+// sum (nf-util.c:45-64: the L4 sum covers bytes [34, 14 + total_length) of an
+// IHL-5 frame) from here: the raw sum of bytes [64, end) of every frame of
+// the wave's tile (`end` = the lane's own frame's end, 64 = nothing). G
+// lanes per frame, 64 / G frames per load instruction, each lane 16
+// contiguous bytes: a group reads 16 G contiguous bytes of one frame per
+// instruction (256 B at G = 16), eight instructions in flight per wave. The
+// steps are the wave's (frame batch, iteration) pairs flattened, the
+// iterations per frame batch a power of two covering the tile's longest
+// frame (loads past a frame's end are masked off, so they cost issue slots,
+// not bytes). Each lane keeps one running sum per frame batch and leaves it
+// in P[frame][group lane]; lane f adds up its frame's G partial sums. P is
+// the wave's 4 KiB LDS tile (1024 words), free while the frames sit in
+// registers. Returns the lane's own frame's sum (< 2^27, unfolded).
+template <uint32_t G>
+__device__ __forceinline__ uint32_t tile_tail_sums(const uint8_t *tile, uint32_t slot,
+                                                   uint32_t end, uint32_t *P) {
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "lanes per frame");
+  constexpr uint32_t FPI = 64 / G;
+  const uint32_t lane = threadIdx.x & 63, gl = lane % G, gi = lane / G;
+  uint32_t mx = end;
+#pragma unroll
+  for (uint32_t m = 1; m < 64; m <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, m));
+  const uint32_t nch = mx > 64 ? (mx - 64 + 15) >> 4 : 0;  // chunks of the longest tail
+  if (nch == 0) return 0;  // (wave-uniform)
+  uint32_t itb = 0;
+  while ((G << itb) < nch) itb++;
+  const uint32_t K = G << itb, itm = (1u << itb) - 1;
+  wave_lds_sync();  // earlier readers of P (the frame image) are done
+  uint32_t acc = 0;
+  constexpr uint32_t U = 8;  // loads in flight
+  for (uint32_t k0 = 0; k0 < K; k0 += U) {
+    uint4 v[U];
+    uint32_t rem[U];  // bytes of the frame from this lane's chunk on
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t k = k0 + u;
+      const uint32_t fr = (k >> itb) * FPI + gi;
+      const uint32_t o = 64 + 16 * ((k & itm) * G + gl);
+      const uint32_t e = (uint32_t)__shfl((int)end, (int)fr);
+      rem[u] = k < K && o < e ? e - o : 0u;
+      v[u] = rem[u] ? *reinterpret_cast<const uint4 *>(tile + (size_t)fr * slot + o)
+                    : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t k = k0 + u;
+      if (k >= K) break;  // (wave-uniform)
+      uint4 x = v[u];
+      if (rem[u] < 16) x = chunk_keep(x, 0, (int)rem[u]);
+      acc = sum16x4(x, acc);
+      if ((k & itm) == itm) {  // this frame batch's last step
+        P[((k >> itb) * FPI + gi) * G + gl] = acc;
+        acc = 0;
+      }
+    }
+  }
+  wave_lds_sync();
+  uint32_t t = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < G; j++) t += P[lane * G + j];
+  wave_lds_sync();  // P is the next tile's frame image
+  return t;
+}
+
+// Checksums of an IHL=5 frame whose first 64 bytes are in registers. With
+// total_length <= 50 every byte the L4 sum covers lies in them; a longer
+// frame (wide slots) brings the raw sum of its bytes [64, 14 + total_length)
+// as `tail` (tile_tail_sums). Same arithmetic as set_checksums.
+__device__ inline void fast_checksums(RFrame &f, uint32_t proto, uint32_t tl,
+                                      uint32_t tail = 0) {
   f.set16(24, 0);
   if (proto == 6 || proto == 17) {
     const bool tcp = proto == 6;
@@ -642,6 +760,7 @@ __device__ inline void fast_checksums(RFrame &f, uint32_t proto, uint32_t tl) {
                      : (((uint32_t)o + 1 == end) ? 0xFFu : 0u);
         s += word & m;
       }
+      s += tail;
       c = finish_l4(fold16(s), phdr_cksum(f.u32at2(26), f.u32at2(30),
                                           (uint8_t)proto, L));
     }

@@ -26,6 +26,8 @@
 namespace vp {
 
 int hip_fail(hipError_t e, const char *what, const char *file, int line);
+// Record a VP_ESTATE failure (vp_last_error) and return VP_ESTATE.
+int state_fail(const char *fmt, ...);
 
 // Wait for `s` to drain by polling (a packet-processing host thread polls,
 // as DPDK's lcores do): a blocking wait adds tens of microseconds of wake-up
@@ -93,6 +95,7 @@ struct FlowTable {
   uint32_t mix = 0;    // home-bucket mode (vp_table.h home_bucket)
   uint64_t ins_since = 0;  // inserts since the last rebuild (mode check)
   uint32_t layout_tries = 0;  // tbl_choose_layout calls so far
+  uint64_t rebuilds = 0;      // tbl_rebuild calls so far (vp_table_stats_get)
   // allocation-order layout (mix == kMixLin, vp_table.hip tbl_try_linear):
   // the linear map's four byte tables on the device; lin_ok: the NF's
   // classify kernels stage them (vignat); lin_tried: fitted once already

@@ -371,6 +371,7 @@ __global__ void lb_stale_free_seq(LbArgs a, const uint32_t *list, uint32_t n) {
     a.ft.slot_of[fi] = kNone;
     a.ft.stack[ctl->stack_top++] = fi;
     ctl->n_live--;
+    ctl->sh_live--;  // (the layout and rebuild checks count this rank's entries)
     ctl->n_tomb++;
   }
 }

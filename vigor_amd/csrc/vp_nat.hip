@@ -256,10 +256,13 @@ struct NatPend {
   uint32_t s;    // WAN: slot_of[index]
 };
 
+// `lim`: the longest total_length the register path takes (50: the L4 bytes
+// all lie in the 64 registers; slot - 14 in the wide-slot kernels, whose
+// nat_finish gets the rest of the sum as `tail`).
 __device__ __forceinline__ NatPend nat_issue(const NatArgs &a, const uint32_t *T,
                                              uint32_t p, const RFrame &f,
                                              uint32_t in, uint32_t len,
-                                             bool mine) {
+                                             bool mine, uint32_t lim = 50) {
   NatPend P;
   P.kind = kPendDone;
   P.row = kNone;
@@ -267,7 +270,7 @@ __device__ __forceinline__ NatPend nat_issue(const NatArgs &a, const uint32_t *T
   const uint32_t et = f.w[3] & 0xFFFF;
   const uint32_t ihl = (f.w[3] >> 16) & 0x0F;
   const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
-  if (!(et == 0x0008 && ihl == 5 && tl <= 50)) {
+  if (!(et == 0x0008 && ihl == 5 && tl <= lim)) {
     P.kind = kPendGeneric;  // byte-addressed path (nat_generic_a)
     return P;
   }
@@ -314,7 +317,8 @@ __device__ __forceinline__ NatPend nat_issue(const NatArgs &a, const uint32_t *T
 __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
                                            const NatPend &P, const uint4 *row,
                                            uint32_t p, RFrame &f, uint32_t in,
-                                           uint32_t len, uint32_t &touch) {
+                                           uint32_t len, uint32_t &touch,
+                                           uint32_t tail = 0) {
   if (P.kind == kPendDone) return false;
   if (P.kind == kPendGeneric) {
     touch = nat_generic_a(a, T, p, in, len);  // writes global memory itself
@@ -385,7 +389,7 @@ __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
     mw[1] = a.wan_macw1;
     mw[2] = a.wan_macw2;
   }
-  fast_checksums(f, proto, tl);
+  fast_checksums(f, proto, tl, tail);
   f.w[0] = mw[0];
   f.w[1] = mw[1];
   f.w[2] = mw[2];
@@ -497,15 +501,21 @@ __global__ __launch_bounds__(256) void nat_classify(NatArgs a) {
 // The fast-path predicate of nat_issue for a LAN packet: IPv4, IHL 5,
 // total_length <= 50 (every L4 byte in the slot), and the parse accepts it
 // (nf_then_get_rte_ipv4_header / nf_then_get_tcpudp_header, nf-util.h:116-162).
-__device__ __forceinline__ bool nat_lan_fast_ok(const NatArgs &a, const RFrame &f,
-                                                uint32_t in, uint32_t len) {
+// The register path's parse (any direction): IPv4, IHL 5, total_length <=
+// lim (nat_issue), and nf_then_get_* accept it (nf-util.h:116-162).
+__device__ __forceinline__ bool nat_reg_ok(const RFrame &f, uint32_t len, uint32_t lim) {
   const uint32_t et = f.w[3] & 0xFFFF;
   const uint32_t ihl = (f.w[3] >> 16) & 0x0F;
   const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
   const uint32_t proto = f.w[5] >> 24;
   const uint16_t unread = (uint16_t)(len - 14);
-  return (in != a.wan) & (et == 0x0008) & (ihl == 5) & (tl <= 50) & (unread >= 20) &
-         (unread >= tl) & ((proto == 6) | (proto == 17)) & ((uint32_t)(len - 34) >= 4u);
+  return (et == 0x0008) & (ihl == 5) & (tl <= lim) & (unread >= 20) & (unread >= tl) &
+         ((proto == 6) | (proto == 17)) & ((uint32_t)(len - 34) >= 4u);
+}
+__device__ __forceinline__ bool nat_lan_fast_ok(const NatArgs &a, const RFrame &f,
+                                                uint32_t in, uint32_t len,
+                                                uint32_t lim = 50) {
+  return (in != a.wan) & nat_reg_ok(f, len, lim);
 }
 
 // bucket_match without branches (the same answer): entries in order, the
@@ -527,17 +537,24 @@ __device__ __forceinline__ uint32_t bucket_match_sel(const uint4 *row,
   return m0 ? ix.x : e0 ? kNone : m1 ? ix.y : e1 ? kNone : m2 ? ix.z : kNone;
 }
 
-// Phase A for 64-byte slots: LDS-staged 1 KiB-contiguous frame I/O, each wave
-// owns 64 consecutive packets (the loop of frames64_tiles, vp_device.h, whose
-// comments describe the layout and the order of the memory operations). A
-// wave whose 64 packets are all fast-path LAN packets (the steady state of a
+// Phase A over tiles of 64 consecutive packets per wave, the frames staged
+// through the wave's LDS tile. G = 0: 64-byte slots (nat_classify64), every
+// global load/store instruction 1 KiB contiguous (the loop of frames64_tiles,
+// vp_device.h, whose comments describe the layout and the order of the
+// memory operations). G > 0: wider slots (nat_classify_wide<G>, DESIGN.md
+// §5.4): the same tile with each frame's first 64 bytes gathered four lanes
+// per frame (16 frames per instruction, 64 contiguous bytes each), the L4
+// sum's remainder from tile_tail_sums (G lanes per frame, contiguous 16 G-byte
+// runs), and only the header chunks a rewrite changed stored back. A wave
+// whose 64 packets are all register-path LAN packets (the steady state of a
 // LAN->WAN stream, BASELINE config 2) takes a straight-line tile: hash, one
 // cooperative bucket-row gather, branch-free match, rewrite and checksums in
-// registers, the whole tile stored back (packets left for phase B or the
-// reprobe walk are stored unchanged). Any other tile runs nat_issue /
-// nat_finish per lane. Owner mode always takes the per-lane path.
-__global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_all,
-                                                        TouchBins bins, TileQueue rq) {
+// registers, (64-byte slots) the whole tile stored back (packets left for
+// phase B or the reprobe walk are stored unchanged). Any other tile runs
+// nat_issue / nat_finish per lane. Owner mode always takes the per-lane path.
+template <uint32_t G>
+__device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins bins,
+                                          TileQueue rq) {
   __shared__ uint32_t T[kNatTabWords];
   __shared__ uint4 stage[4][256];
   __shared__ uint32_t cur[kCurs];
@@ -550,15 +567,22 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
   const uint32_t first = a.p0 & ~63u;
   const uint32_t tiles = (a.p1 - first + 63) / 64;
   const bool lean_ok = a.own.n == 0 && rq.ent != nullptr;
+  const uint32_t slot = G ? a.slot : 64u;
+  const uint32_t lim = slot - 14;  // total_length bound of the register path
+  // byte offset in the tile of chunk c (packet c / 4, part c % 4)
+  auto chunk_at = [&](uint32_t c) -> uint32_t {
+    return G ? (c >> 2) * slot + (c & 3) * 16 : c * 16;
+  };
   uint4 r[4];
   uint32_t m_in = 0, m_len = 0;
   auto fetch = [&](uint32_t tile) {
     const uint32_t tb = first + tile * 64;
-    const uint4 *g = reinterpret_cast<const uint4 *>(a.frames + (size_t)tb * 64);
+    const uint8_t *g8 = a.frames + (size_t)tb * slot;
     const uint32_t p = tb + lane;
     if (tb + 64 <= n_all) {  // (wave-uniform) a whole tile: no per-lane guards
 #pragma unroll
-      for (uint32_t j = 0; j < 4; j++) r[j] = tile_ld(g + 64 * j + lane);
+      for (uint32_t j = 0; j < 4; j++)
+        r[j] = tile_ld(reinterpret_cast<const uint4 *>(g8 + chunk_at(64 * j + lane)));
 #ifdef VP_ABL_NOSIDE  // diagnostic: no len / in_dev loads (the bench's values)
       m_in = 0;
       m_len = 60;
@@ -572,7 +596,8 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) {
       const uint32_t c = 64 * j + lane;
-      r[j] = (c >> 2) < avail ? tile_ld(g + c) : make_uint4(0, 0, 0, 0);
+      r[j] = (c >> 2) < avail ? tile_ld(reinterpret_cast<const uint4 *>(g8 + chunk_at(c)))
+                              : make_uint4(0, 0, 0, 0);
     }
     m_in = p < n_all ? a.in_dev[p] : 0u;
     m_len = p < n_all ? a.len[p] : 0u;
@@ -585,7 +610,8 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
   if (tile < tend) fetch(tile);
   for (; tile < tend; tile += tstep) {
     const uint32_t tb = first + tile * 64;
-    uint4 *g = reinterpret_cast<uint4 *>(a.frames + (size_t)tb * 64);
+    uint8_t *g8 = a.frames + (size_t)tb * slot;
+    uint4 *g = reinterpret_cast<uint4 *>(g8);
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = r[j];
     wave_lds_sync();
@@ -601,11 +627,18 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
       f.w[4 * k + 3] = v.w;
     }
     const uint32_t in = m_in, ln = m_len;
+    // wide slots: where this frame's L4 sum ends (64: nothing past the
+    // registers, or not a register-path frame)
+    uint32_t end = 64;
+    if constexpr (G > 0) {
+      if (mine && nat_reg_ok(f, ln, lim)) end = 14 + bswap16((uint16_t)(f.w[4] & 0xFFFF));
+    }
     uint4 row[4];
     uint32_t touch = kNone;
-    bool store_all;
-    if (lean_ok && __ballot(mine && nat_lan_fast_ok(a, f, in, ln)) == ~0ull) {
-      // ---- lean tile: every lane a fast-path LAN packet
+    bool store_all = false;
+    uint32_t smask = 0;  // wide slots: header chunks to store back (bit k = bytes 16k..)
+    if (lean_ok && __ballot(mine && nat_lan_fast_ok(a, f, in, ln, lim)) == ~0ull) {
+      // ---- lean tile: every lane a register-path LAN packet
       const uint32_t proto = f.w[5] >> 24;
       const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
       const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
@@ -630,11 +663,21 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
 #ifdef VP_ABL_L2ROW  // diagnostic: every row from 64 fixed buckets (L2 hits)
       b0 = 0 * 16 + (lane >> 2); b1 = 16 + (lane >> 2); b2 = 32 + (lane >> 2); b3 = 48 + (lane >> 2);
 #endif
+      // 64-byte slots: the rows before the next tile's prefetch (vmcnt
+      // drains in order); wide slots: the prefetch, then the tail sums, then
+      // the rows (registers: the tail's loads in flight need them)
+      uint32_t tail = 0;
+      if constexpr (G > 0) {
+        if (tile + tstep < tend) fetch(tile + tstep);
+        tail = tile_tail_sums<G>(g8, slot, end, reinterpret_cast<uint32_t *>(S));
+      }
       const uint4 q0 = rows[4 * (size_t)b0 + part];
       const uint4 q1 = rows[4 * (size_t)b1 + part];
       const uint4 q2 = rows[4 * (size_t)b2 + part];
       const uint4 q3 = rows[4 * (size_t)b3 + part];
-      if (tile + tstep < tend) fetch(tile + tstep);
+      if constexpr (G == 0) {
+        if (tile + tstep < tend) fetch(tile + tstep);
+      }
       wave_lds_sync();
       S[chunk_swz(lane)] = q0;
       S[chunk_swz(64 + lane)] = q1;
@@ -666,7 +709,7 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
         f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
         f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
 #ifndef VP_ABL_NOCSUM  // diagnostic builds skip the checksums (tools/ablate.py)
-        fast_checksums(f, proto, bswap16((uint16_t)(f.w[4] & 0xFFFF)));
+        fast_checksums(f, proto, bswap16((uint16_t)(f.w[4] & 0xFFFF)), tail);
 #endif
         f.w[0] = a.wan_macw0;
         f.w[1] = a.wan_macw1;
@@ -674,6 +717,7 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
 #if !defined(VP_ABL_NOOUT) && !defined(VP_ABL_NOSIDE)  // diagnostic builds skip the out-port store
         VP_OUT_ST(a.out + p, (uint16_t)a.wan);
 #endif
+        smask = proto == 6 ? 0xFu : 0x7u;  // the TCP checksum (bytes 50-51) is in chunk 3
       }
 #ifdef VP_ABL_NOBINS  // diagnostic builds skip the touch bins
       touch = kNone;
@@ -681,14 +725,21 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
       store_all = true;
     } else {
       // ---- per-lane tile (nat_issue / nat_finish)
-      const NatPend pend = nat_issue(a, T, p, f, in, ln, mine);
+      const NatPend pend = nat_issue(a, T, p, f, in, ln, mine, lim);
+      uint32_t tail = 0;
+      if constexpr (G > 0) {  // (the order of the lean tile)
+        if (tile + tstep < tend) fetch(tile + tstep);
+        tail = tile_tail_sums<G>(g8, slot, end, reinterpret_cast<uint32_t *>(S));
+      }
       uint4 q[4];
 #pragma unroll
       for (uint32_t j = 0; j < 4; j++) {
         const uint32_t rw = __shfl(pend.row, 16 * j + (lane >> 2));
         q[j] = rw != kNone ? rows[4 * (size_t)rw + (lane & 3)] : make_uint4(0, 0, 0, 0);
       }
-      if (tile + tstep < tend) fetch(tile + tstep);
+      if constexpr (G == 0) {
+        if (tile + tstep < tend) fetch(tile + tstep);
+      }
       wave_lds_sync();
 #pragma unroll
       for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = q[j];
@@ -697,7 +748,7 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
       for (uint32_t k = 0; k < 4; k++) row[k] = S[chunk_swz(4 * lane + k)];
       bool m = false;
       if (mine) {
-        m = nat_finish(a, T, pend, row, p, f, in, ln, touch);
+        m = nat_finish(a, T, pend, row, p, f, in, ln, touch, tail);
         touch = route_note(a, p, touch);
       }
       {  // queue on this block's reprobe slice
@@ -706,34 +757,60 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
         if (v) rq.ent[(size_t)rb * per_b * 64 + k] = p;
       }
       if (touch == kReprobe) touch = kNone;
-      // a rewrite touches bytes 0-47; the TCP checksum (bytes 50-51) also
-      // dirties chunk 3: whole tiles are stored only when every lane rewrote
-      store_all = __ballot(m) == ~0ull;
-      if (!store_all) {
-        const uint64_t mm = __ballot(m);
+      if constexpr (G > 0) {
+        smask = m ? ((f.w[5] >> 24) == 6 ? 0xFu : 0x7u) : 0u;
+      } else {
+        // a rewrite touches bytes 0-47; the TCP checksum (bytes 50-51) also
+        // dirties chunk 3: whole tiles are stored only when every lane rewrote
+        store_all = __ballot(m) == ~0ull;
+        if (!store_all) {
+          const uint64_t mm = __ballot(m);
+#pragma unroll
+          for (uint32_t k = 0; k < 4; k++)
+            S[chunk_swz(4 * lane + k)] =
+                make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
+          wave_lds_sync();
+#pragma unroll
+          for (uint32_t j = 0; j < 4; j++) {
+            const uint32_t c = 64 * j + lane;
+            if ((mm >> (c >> 2)) & 1ull) tile_st(g, c, S[chunk_swz(c)]);
+          }
+          wave_lds_sync();  // the next tile overwrites S
+        }
+      }
+    }
+    bins_put(bins, cur, rb, per_b * 64, range0, p, touch);
+    if constexpr (G == 0) {
+      if (store_all) {
 #pragma unroll
         for (uint32_t k = 0; k < 4; k++)
           S[chunk_swz(4 * lane + k)] =
               make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
         wave_lds_sync();
 #pragma unroll
+        for (uint32_t j = 0; j < 4; j++) tile_st(g, 64 * j + lane, S[chunk_swz(64 * j + lane)]);
+        wave_lds_sync();  // the next tile overwrites S
+      }
+    } else {
+      // the changed header chunks of the rewritten frames, four lanes per
+      // frame (64 contiguous bytes), through the LDS tile
+      const uint64_t m0 = __ballot(smask & 1u), m1 = __ballot(smask & 2u),
+                     m2 = __ballot(smask & 4u), m3 = __ballot(smask & 8u);
+      if (m0) {  // (every stored frame stores chunk 0)
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+          S[chunk_swz(4 * lane + k)] =
+              make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
+        wave_lds_sync();
+        const uint32_t part = lane & 3;
+        const uint64_t pm = part == 0 ? m0 : part == 1 ? m1 : part == 2 ? m2 : m3;
+#pragma unroll
         for (uint32_t j = 0; j < 4; j++) {
           const uint32_t c = 64 * j + lane;
-          if ((mm >> (c >> 2)) & 1ull) tile_st(g, c, S[chunk_swz(c)]);
+          if ((pm >> (c >> 2)) & 1ull) tile_st_at(g8, 64 * slot, chunk_at(c), S[chunk_swz(c)]);
         }
         wave_lds_sync();  // the next tile overwrites S
       }
-    }
-    bins_put(bins, cur, rb, per_b * 64, range0, p, touch);
-    if (store_all) {
-#pragma unroll
-      for (uint32_t k = 0; k < 4; k++)
-        S[chunk_swz(4 * lane + k)] =
-            make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
-      wave_lds_sync();
-#pragma unroll
-      for (uint32_t j = 0; j < 4; j++) tile_st(g, 64 * j + lane, S[chunk_swz(64 * j + lane)]);
-      wave_lds_sync();  // the next tile overwrites S
     }
   }
   __syncthreads();
@@ -744,6 +821,31 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
     if (c) atomicAdd(rq.total, c);
   }
   route_publish(a, cur + kCurDest);
+}
+
+__global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_all,
+                                                        TouchBins bins, TileQueue rq) {
+  nat_tiles<0>(a, n_all, bins, rq);
+}
+
+// Wide slots (slot > 64): G lanes per frame in the tail sums.
+template <uint32_t G>
+__global__ __launch_bounds__(256, 4) void nat_classify_wide(NatArgs a, uint32_t n_all,
+                                                           TouchBins bins, TileQueue rq) {
+  nat_tiles<G>(a, n_all, bins, rq);
+}
+
+// The classify kernel for a slot: 64 bytes, or the wide kernel whose G is the
+// tail's 16-byte chunks (slot - 64) / 16 rounded up to a power of two, at most 16.
+typedef void (*NatTileKernel)(NatArgs, uint32_t, TouchBins, TileQueue);
+static NatTileKernel nat_tile_kernel(uint32_t slot) {
+  if (slot == 64) return nat_classify64;
+  const uint32_t nch = (slot - 64) / 16;
+  if (nch <= 1) return nat_classify_wide<1>;
+  if (nch <= 2) return nat_classify_wide<2>;
+  if (nch <= 4) return nat_classify_wide<4>;
+  if (nch <= 8) return nat_classify_wide<8>;
+  return nat_classify_wide<16>;
 }
 
 // ------------------------------------------------------------- phase B --
@@ -1277,16 +1379,18 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   const bool owner = c->shard_mode == VP_SHARD_OWNER && c->comm;
   PhaseA ph{};
   if (owner) VP_TRY(nat_phase_a_owner(c, b, a, now, p0, p1, seq0, &ph));
-  // 64-byte slots: the classify launch also bins its touches (TouchBins)
-  // and queues reprobes per block (TileQueue)
-  const bool tiles64 = owner ? ph.tiles64 : p1 > p0 && b->slot == 64 && c->coalesced_io;
+  // tiles of 64 packets (64-byte slots, or wider ones: nat_tiles): the
+  // classify launch also bins its touches (TouchBins) and queues reprobes
+  // per block (TileQueue)
+  const bool tiles64 = owner ? ph.tiles64 : p1 > p0 && c->coalesced_io;
+  const NatTileKernel tk = nat_tile_kernel(b->slot);
   BinsPlan bp = ph.bp;
   uint32_t grid64 = ph.grid1, range64 = ph.range1;
   TileQueue rq{};
   if (tiles64 && !owner) {
-    VP_TRY(tbl_bins_plan(c, t, (const void *)nat_classify64, p0, p1, &bp));
+    VP_TRY(tbl_bins_plan(c, t, (const void *)tk, p0, p1, &bp));
     const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
-    grid64 = resident_grid((const void *)nat_classify64, (tiles + 3) / 4);
+    grid64 = resident_grid((const void *)tk, (tiles + 3) / 4);
     range64 = (tiles + grid64 - 1) / grid64 * 64;
     rq = TileQueue{w.reprobe, w.reprobe_cnt, &t.ctl->reprobe_count};
     a.tileq = 1;
@@ -1300,7 +1404,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     if (tiles64) {
       NatArgs a64 = a;
       if (bp.on) a64.log = nullptr;  // touches go to the bins only
-      VP_HIP(launch_timed(nat_classify64, grid64, 256, c->stream, c->ev0, c->ev1, a64,
+      VP_HIP(launch_timed(tk, grid64, 256, c->stream, c->ev0, c->ev1, a64,
                           (uint32_t)b->n, bp.bins, rq));
     } else {
       VP_HIP(launch_timed(nat_classify, grid_for(p1 - p0), 256, c->stream, c->ev0,

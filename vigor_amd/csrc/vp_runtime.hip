@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdarg>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -14,11 +15,24 @@
 
 namespace vp {
 
+// vp_last_error(): the calling thread's last failure
+static thread_local char g_last_error[256];
+
 int hip_fail(hipError_t e, const char *what, const char *file, int line) {
-  if (getenv("VIGPATH_DEBUG"))
-    fprintf(stderr, "vigpath: %s failed: %s (%s:%d)\n", what,
-            hipGetErrorString(e), file, line);
+  const char *base = strrchr(file, '/');
+  snprintf(g_last_error, sizeof g_last_error, "HIP %s (%s) in %s at %s:%d",
+           hipGetErrorName(e), hipGetErrorString(e), what, base ? base + 1 : file, line);
+  if (getenv("VIGPATH_DEBUG")) fprintf(stderr, "vigpath: %s\n", g_last_error);
   return e == hipErrorOutOfMemory ? VP_ENOMEM : VP_EIO;
+}
+
+int state_fail(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_last_error, sizeof g_last_error, fmt, ap);
+  va_end(ap);
+  if (getenv("VIGPATH_DEBUG")) fprintf(stderr, "vigpath: %s\n", g_last_error);
+  return VP_ESTATE;
 }
 
 int nat_process_device(vp_ctx *c, const vp_dev_batch *b);
@@ -794,6 +808,26 @@ int vp_lb_dump(vp_ctx *c, uint8_t *f_alloc, int64_t *f_ts, uint8_t *f_keys,
   return lb_dump(c, f_alloc, f_ts, f_keys, f_backend, b_alloc, b_ts, b_ip, b_mac,
                  b_nic);
 }
+
+int vp_table_stats_get(vp_ctx *c, int table, vp_table_stats *out) {
+  if (!c || !out || table < 0 || table > 1 || (table == 1 && c->kind != KIND_LB))
+    return VP_EINVAL;
+  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  const vp::FlowTable &t = table ? c->ft2 : c->ft;
+  VP_HIP(hipStreamSynchronize(c->stream));
+  Ctl h{};
+  VP_HIP(hipMemcpy(&h, t.ctl, sizeof h, hipMemcpyDeviceToHost));
+  *out = vp_table_stats{};
+  out->live = h.n_live;
+  out->shard_live = h.sh_live;
+  out->tombstones = h.n_tomb;
+  out->buckets = (uint64_t)t.bmask + 1;
+  out->rebuilds = t.rebuilds;
+  out->layout = t.mix;
+  return 0;
+}
+
+const char *vp_last_error(void) { return vp::g_last_error; }
 
 int vp_last_kernel_ms(vp_ctx *c, float *ms, int *launches) {
   if (!c || !ms || !launches) return VP_EINVAL;

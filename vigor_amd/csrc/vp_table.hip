@@ -804,7 +804,8 @@ int tbl_touch_reduce(vp_ctx *c, FlowTable &t, const uint32_t *log, uint32_t p0,
 // ---------------------------------------------------------- touch bins --
 // Single-pass fold of the touch bins a 64-byte classify launch filled
 // (TouchBins, vp_device.h): one block per bin keeps the largest position per
-// in-bin index in LDS, reading every source block's slice of its bin, then
+// in-bin index in LDS, reading every source block's slice of its bin (one
+// contiguous region: the slices are bin-major), then
 // writes ts/tseq in runs of 64 consecutive indices. About 8 B of traffic per
 // packet (one write while classifying, one read here).
 constexpr uint32_t kBinLocalMax = 16384;  // in-bin indices held in LDS
@@ -836,14 +837,14 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
   // loaded by one instruction (lane l <-> slice w + l * nw)
   for (uint32_t r0 = threadIdx.x >> 6; r0 < nsrc; r0 += 64 * nw) {
     const uint32_t my = r0 + lane * nw;
-    const uint32_t nv = my < nsrc ? cnt[((size_t)my << bbits) + bin] : 0;
+    const uint32_t nv = my < nsrc ? cnt[(size_t)bin * nsrc + my] : 0;
     for (uint32_t i = 0; i < 64; i += kU) {
       uint32_t n[kU], e[kU];
 #pragma unroll
       for (uint32_t u = 0; u < kU; u++) {
         n[u] = __shfl(nv, i + u);
         const uint32_t sb = r0 + (i + u) * nw;
-        e[u] = lane < n[u] ? ent[(((size_t)sb << bbits) + bin) * cap + lane] : 0;
+        e[u] = lane < n[u] ? ent[((size_t)bin * nsrc + sb) * cap + lane] : 0;
       }
 #pragma unroll
       for (uint32_t u = 0; u < kU; u++) {
@@ -852,7 +853,7 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
           atomicMax(&last[e[u] >> pbits], sb * range + (e[u] & pmask) + 1);
         for (uint32_t k = 64; k < n[u]; k += 64) {  // slices longer than 64
           if (k + lane < n[u]) {
-            const uint32_t x = ent[(((size_t)sb << bbits) + bin) * cap + k + lane];
+            const uint32_t x = ent[((size_t)bin * nsrc + sb) * cap + k + lane];
             atomicMax(&last[x >> pbits], sb * range + (x & pmask) + 1);
           }
         }
@@ -923,7 +924,7 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   plan->range = range;
   plan->L = L;
   plan->bins = TouchBins{w.bins_ent, w.bins_cnt, &t.ctl->touch_ovf, w.ovf_q,
-                         w.ovf_cnt, w.log, cap, pbits, bbits};
+                         w.ovf_cnt, w.log, cap, pbits, bbits, grid};
   return 0;
 }
 
@@ -964,12 +965,9 @@ int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_
     if (__atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE) == epoch) break;
     if ((spin & 1023) == 0) {
       const hipError_t e = hipStreamQuery(c->stream);
-      if (e == hipSuccess && __atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE) != epoch) {
-        if (getenv("VIGPATH_DEBUG"))
-          fprintf(stderr, "vigpath: fold ended without publishing epoch %u (seen %u)\n",
-                  epoch, __atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE));
-        return VP_EIO;
-      }
+      if (e == hipSuccess && __atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE) != epoch)
+        return state_fail("fold ended without publishing epoch %u (seen %u)", epoch,
+                          __atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE));
       if (e != hipSuccess && e != hipErrorNotReady) VP_HIP(e);
     }
   }
@@ -1128,6 +1126,7 @@ __global__ void rb_insert(TableDev t, const uint32_t *keys) {
 
 // nb_new: bucket count afterwards (0 = unchanged).
 static int tbl_rebuild(vp_ctx *c, FlowTable &t, uint64_t nb_new) {
+  t.rebuilds++;
   uint32_t *keys = reinterpret_cast<uint32_t *>(t.kv);  // owner mode: kv has them
   if (!keys) {
     VP_TRY(dalloc(&keys, 4ull * t.cap));
@@ -1241,9 +1240,9 @@ int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
   c->last_ms = 0.f;
   c->last_launches = 0;
   if (n == 0) return 0;
-  if (b->slot < 64 || (b->slot & 15) || !b->frames || !b->len || !b->in_dev ||
-      !b->out_dev)
-    return VP_EINVAL;
+  if (b->slot < 64 || (b->slot & 15) || !b->frames || ((uintptr_t)b->frames & 15) ||
+      !b->len || !b->in_dev || !b->out_dev)
+    return VP_EINVAL;  // (frames are read as aligned 16-byte chunks)
   VP_TRY(ws_reserve(c, n));
 
   std::vector<int64_t> h_copy;
@@ -1471,8 +1470,8 @@ static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
   //    errors are decided from the gathered data so all ranks agree
   RankInfo me{};
   me.n = n;
-  if (n && (b->slot < 64 || (b->slot & 15) || !b->frames || !b->len ||
-            !b->in_dev || !b->out_dev))
+  if (n && (b->slot < 64 || (b->slot & 15) || !b->frames ||
+            ((uintptr_t)b->frames & 15) || !b->len || !b->in_dev || !b->out_dev))
     me.bad = 1;
   std::vector<int64_t> h_now;
   if (!me.bad && n) {

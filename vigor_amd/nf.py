@@ -13,7 +13,7 @@ import ctypes as C
 import numpy as np
 
 from . import (BridgeConfigC, DevBatchC, FwConfigC, LbConfigC, NatConfigC,
-               PolConfigC, _check, lib)
+               PolConfigC, TableStatsC, _check, lib)
 
 
 def _dptr(t):
@@ -58,19 +58,22 @@ class NfBase:
         """A prepared vp_process_device call over fixed device buffers with
         affine time: returns f(now0, now_step). The batch descriptor and its
         pointers are built once (a C caller's per-burst cost), so a loop of
-        calls pays only the C-ABI call itself."""
+        calls pays only the C-ABI call itself. The callable keeps the tensors
+        alive: the descriptor holds their raw device pointers."""
         n = lens.numel()
         assert frames.numel() == n * slot and frames.is_cuda
         b = DevBatchC(frames=frames.data_ptr(), slot=slot, n=n,
                       len=lens.data_ptr(), in_dev=in_dev.data_ptr(), now=None,
                       now0=0, now_step=0, out_dev=out.data_ptr())
         ref, fn, h = C.byref(b), self.L.vp_process_device, self.h
+        keep = (frames, lens, in_dev, out)
 
         def step(now0: int, now_step: int):
             b.now0, b.now_step = now0, now_step
             rc = fn(h, ref, None)
             if rc:
                 _check(rc, "vp_process_device")
+        step.tensors = keep
         return step
 
     def sync_state(self):
@@ -84,6 +87,13 @@ class NfBase:
         ms, k, rms, rk = self._kms
         _check(self.L.vp_last_kernel_ms(self.h, rms, rk), "vp_last_kernel_ms")
         return ms.value, k.value
+
+    def table_stats(self, table: int = 0) -> dict:
+        """vp_table_stats_get: live / shard_live / tombstones / buckets /
+        rebuilds / layout of table 0 (flows) or 1 (viglb backends)."""
+        st = TableStatsC()
+        _check(self.L.vp_table_stats_get(self.h, table, C.byref(st)), "vp_table_stats_get")
+        return {k: int(getattr(st, k)) for k, _ in TableStatsC._fields_ if k != "pad"}
 
     def live_count(self) -> int:
         v = self.L.vp_live_count(self.h)
