@@ -327,7 +327,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=None,
-                    help="packets per GPU and step (default 2^24 x 64 / slot)")
+                    help="packets per GPU and step (default 2^24, at most "
+                         "2 GiB of slots)")
     ap.add_argument("--slot", type=int, default=SLOT,
                     help="slot bytes (frames of min(slot, 1518) - 4 bytes): "
                          "64 is BASELINE's config; wider slots measure the "
@@ -356,9 +357,9 @@ def main():
     if slot < 64 or slot % 16:
         raise SystemExit("bench.py: --slot must be a multiple of 16, >= 64")
     B = args.batch
-    if B is None:
+    if B is None:  # 2^24 packets of 64 B; wider slots up to 2 GiB per batch
         B = 1 << 24
-        while B * slot > (1 << 30):
+        while B * slot > (1 << 31):
             B >>= 1
     alg_bytes = slot + 28  # R = slot(len) + 28 (92 at 64 B)
 

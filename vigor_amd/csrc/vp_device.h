@@ -98,7 +98,9 @@ __device__ __forceinline__ uint32_t sum16x4(const uint4 v, uint32_t s) {
 __device__ __forceinline__ uint32_t bytes_mask(int lo, int hi) {
   lo = lo < 0 ? 0 : lo > 4 ? 4 : lo;
   hi = hi < 0 ? 0 : hi > 4 ? 4 : hi;
-  return (uint32_t)(((1ull << (8 * hi)) - 1) & ~((1ull << (8 * lo)) - 1));
+  const uint32_t below_hi = hi >= 4 ? 0xFFFFFFFFu : (1u << (8 * hi)) - 1;
+  const uint32_t below_lo = lo >= 4 ? 0xFFFFFFFFu : (1u << (8 * lo)) - 1;
+  return below_hi & ~below_lo;
 }
 __device__ __forceinline__ uint4 chunk_keep(uint4 v, int lo, int hi) {
   v.x &= bytes_mask(lo, hi);
@@ -676,66 +678,96 @@ __device__ __forceinline__ void reprobe_slices(const uint32_t *list, const uint3
 // registers, as for 64-byte slots, and take the rest of the L4 checksum's
 // sum (nf-util.c:45-64: the L4 sum covers bytes [34, 14 + total_length) of an
 // IHL-5 frame) from here: the raw sum of bytes [64, end) of every frame of
-// the wave's tile (`end` = the lane's own frame's end, 64 = nothing). G
-// lanes per frame, 64 / G frames per load instruction, each lane 16
+// the wave's tile (`end` = the lane's own frame's end, 64 = nothing).
+//   G lanes per frame, 64 / G frames per load instruction, each lane 16
 // contiguous bytes: a group reads 16 G contiguous bytes of one frame per
-// instruction (256 B at G = 16), eight instructions in flight per wave. The
-// steps are the wave's (frame batch, iteration) pairs flattened, the
-// iterations per frame batch a power of two covering the tile's longest
-// frame (loads past a frame's end are masked off, so they cost issue slots,
-// not bytes). Each lane keeps one running sum per frame batch and leaves it
-// in P[frame][group lane]; lane f adds up its frame's G partial sums. P is
-// the wave's 4 KiB LDS tile (1024 words), free while the frames sit in
-// registers. Returns the lane's own frame's sum (< 2^27, unfolded).
-template <uint32_t G>
+// instruction (256 B at G = 16). The steps are the wave's (frame batch,
+// iteration) pairs flattened, U loads in flight; a frame batch's iterations
+// cover the tile's longest tail, and loads past a frame's end go to an
+// offset beyond the buffer resource (they return zeros and touch no memory).
+// Loads use one buffer resource per tile (base in scalar registers) and
+// 32-bit offsets, so no per-lane 64-bit addresses stay live. At a batch's
+// last step the group's partial sums are added by xor shuffles and the
+// frame's sum handed to its own lane. Returns that sum (< 2^27, unfolded).
+__device__ __forceinline__ uint4 buf_ld16(const void *base, uint32_t bytes, uint32_t off) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes,
+                                                    0x00020000);
+  const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+constexpr uint32_t kBufOff = 0x80000000u;  // an offset past every tile's resource
+
+// One round's U loads of tile_tail_sums: the steps' frame ends (U
+// bpermutes, one wait), then the loads (past a frame's end: kBufOff).
+template <uint32_t G, uint32_t U>
+struct TailRound {
+  uint4 v[U];
+  uint32_t rem[U];  // bytes of the frame from the lane's chunk on (0: none)
+  __device__ __forceinline__ void issue(const uint8_t *tile, uint32_t slot, uint32_t bytes,
+                                        uint32_t end, uint32_t k0, uint32_t K, uint32_t n_it,
+                                        uint32_t &qq, uint32_t &ii, uint32_t gi, uint32_t gl) {
+    constexpr uint32_t FPI = 64 / G;
+    uint32_t off[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t fr = qq * FPI + gi;
+      const uint32_t o = 64 + 16 * (ii * G + gl);
+      const uint32_t e = (uint32_t)__shfl((int)end, (int)fr);
+      off[u] = fr * slot + o;
+      rem[u] = (k0 + u < K) & (o < e) ? e - o : 0u;
+      if (++ii == n_it) {
+        ii = 0;
+        qq++;
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) v[u] = buf_ld16(tile, bytes, rem[u] ? off[u] : kBufOff);
+  }
+};
+
+template <uint32_t G, uint32_t H = 1>  // H rounds of 8 loads in flight
 __device__ __forceinline__ uint32_t tile_tail_sums(const uint8_t *tile, uint32_t slot,
-                                                   uint32_t end, uint32_t *P) {
+                                                   uint32_t bytes, uint32_t end) {
   static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "lanes per frame");
-  constexpr uint32_t FPI = 64 / G;
+  constexpr uint32_t FPI = 64 / G, U = 8;
   const uint32_t lane = threadIdx.x & 63, gl = lane % G, gi = lane / G;
   uint32_t mx = end;
 #pragma unroll
   for (uint32_t m = 1; m < 64; m <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, m));
-  const uint32_t nch = mx > 64 ? (mx - 64 + 15) >> 4 : 0;  // chunks of the longest tail
-  if (nch == 0) return 0;  // (wave-uniform)
-  uint32_t itb = 0;
-  while ((G << itb) < nch) itb++;
-  const uint32_t K = G << itb, itm = (1u << itb) - 1;
-  wave_lds_sync();  // earlier readers of P (the frame image) are done
-  uint32_t acc = 0;
-  constexpr uint32_t U = 8;  // loads in flight
-  for (uint32_t k0 = 0; k0 < K; k0 += U) {
-    uint4 v[U];
-    uint32_t rem[U];  // bytes of the frame from this lane's chunk on
+  // (wave-uniform: a scalar, so the step counters live in scalar registers)
+  const uint32_t nch = __builtin_amdgcn_readfirstlane(mx > 64 ? (mx - 64 + 15) >> 4 : 0u);
+  if (nch == 0) return 0;
+  const uint32_t n_it = (nch + G - 1) / G, K = G * n_it;
+  uint32_t tail = 0, acc = 0, q = 0, it = 0;  // (q, it): the next step's batch, iteration
+  uint32_t qq = 0, ii = 0;                    // the next step to issue
+  for (uint32_t k0 = 0; k0 < K; k0 += U * H) {
+    TailRound<G, U> R[H];
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++) {
-      const uint32_t k = k0 + u;
-      const uint32_t fr = (k >> itb) * FPI + gi;
-      const uint32_t o = 64 + 16 * ((k & itm) * G + gl);
-      const uint32_t e = (uint32_t)__shfl((int)end, (int)fr);
-      rem[u] = k < K && o < e ? e - o : 0u;
-      v[u] = rem[u] ? *reinterpret_cast<const uint4 *>(tile + (size_t)fr * slot + o)
-                    : make_uint4(0, 0, 0, 0);
-    }
+    for (uint32_t h = 0; h < H; h++)
+      R[h].issue(tile, slot, bytes, end, k0 + h * U, K, n_it, qq, ii, gi, gl);
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++) {
-      const uint32_t k = k0 + u;
-      if (k >= K) break;  // (wave-uniform)
-      uint4 x = v[u];
-      if (rem[u] < 16) x = chunk_keep(x, 0, (int)rem[u]);
-      acc = sum16x4(x, acc);
-      if ((k & itm) == itm) {  // this frame batch's last step
-        P[((k >> itb) * FPI + gi) * G + gl] = acc;
-        acc = 0;
+    for (uint32_t h = 0; h < H; h++) {
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++) {
+        if (k0 + h * U + u >= K) break;  // (wave-uniform)
+        uint4 x = R[h].v[u];
+        if (R[h].rem[u] < 16) x = chunk_keep(x, 0, (int)R[h].rem[u]);
+        acc = sum16x4(x, acc);
+        if (++it == n_it) {  // frame batch q complete: its sums to their lanes
+          it = 0;
+#pragma unroll
+          for (uint32_t m = G / 2; m > 0; m >>= 1) acc += (uint32_t)__shfl_xor((int)acc, m);
+          const uint32_t j = lane - q * FPI;  // this lane's frame in batch q (if < FPI)
+          const uint32_t got = (uint32_t)__shfl((int)acc, (int)((j & (FPI - 1)) * G));
+          if (j < FPI) tail = got;
+          acc = 0;
+          q++;
+        }
       }
     }
   }
-  wave_lds_sync();
-  uint32_t t = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < G; j++) t += P[lane * G + j];
-  wave_lds_sync();  // P is the next tile's frame image
-  return t;
+  return tail;
 }
 
 // Checksums of an IHL=5 frame whose first 64 bytes are in registers. With

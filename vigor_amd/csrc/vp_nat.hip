@@ -552,7 +552,7 @@ __device__ __forceinline__ uint32_t bucket_match_sel(const uint4 *row,
 // registers, (64-byte slots) the whole tile stored back (packets left for
 // phase B or the reprobe walk are stored unchanged). Any other tile runs
 // nat_issue / nat_finish per lane. Owner mode always takes the per-lane path.
-template <uint32_t G>
+template <uint32_t G, uint32_t H = 1>
 __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins bins,
                                           TileQueue rq) {
   __shared__ uint32_t T[kNatTabWords];
@@ -563,7 +563,11 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   load_nat_tables(T, a);  // (its barrier also covers cur)
   uint4 *S = stage[threadIdx.x >> 6];
   const uint4 *rows = reinterpret_cast<const uint4 *>(a.t.bk);
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  // wide slots: the wave index as a scalar, so tile addresses (the buffer
+  // resources of tile_tail_sums and the header gathers) are provably uniform
+  // and need no waterfall loop (cdna_hip_programming.md T20)
+  const uint32_t wv = G ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : threadIdx.x >> 6;
   const uint32_t first = a.p0 & ~63u;
   const uint32_t tiles = (a.p1 - first + 63) / 64;
   const bool lean_ok = a.own.n == 0 && rq.ent != nullptr;
@@ -579,6 +583,15 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
     const uint32_t tb = first + tile * 64;
     const uint8_t *g8 = a.frames + (size_t)tb * slot;
     const uint32_t p = tb + lane;
+    if constexpr (G > 0) {  // one buffer resource per tile: slots past the
+      // batch read as zeros
+      const uint32_t bytes = min(64u, n_all - tb) * slot;
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) r[j] = buf_ld16(g8, bytes, chunk_at(64 * j + lane));
+      m_in = p < n_all ? a.in_dev[p] : 0u;
+      m_len = p < n_all ? a.len[p] : 0u;
+      return;
+    }
     if (tb + 64 <= n_all) {  // (wave-uniform) a whole tile: no per-lane guards
 #pragma unroll
       for (uint32_t j = 0; j < 4; j++)
@@ -607,11 +620,14 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   uint32_t tile = rb * per_b + wv;
   const uint32_t tend = min(tiles, rb * per_b + per_b), tstep = 4;
   const uint32_t range0 = first + rb * per_b * 64;  // this block's first packet
-  if (tile < tend) fetch(tile);
+  // (wide slots: the headers of the wave's own tile at its start; a prefetch
+  // of the next tile's would keep 16 registers the tail sums need)
+  if (G == 0 && tile < tend) fetch(tile);
   for (; tile < tend; tile += tstep) {
     const uint32_t tb = first + tile * 64;
     uint8_t *g8 = a.frames + (size_t)tb * slot;
     uint4 *g = reinterpret_cast<uint4 *>(g8);
+    if constexpr (G > 0) fetch(tile);
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = r[j];
     wave_lds_sync();
@@ -627,18 +643,119 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       f.w[4 * k + 3] = v.w;
     }
     const uint32_t in = m_in, ln = m_len;
-    // wide slots: where this frame's L4 sum ends (64: nothing past the
-    // registers, or not a register-path frame)
-    uint32_t end = 64;
+    // wide slots: the tail sums run while the frame image stays in S; the
+    // frame is read back from it afterwards instead of held in registers
+    const uint32_t tbytes = G ? min(64u, n_all - tb) * slot : 0u;
+    auto reread = [&]() {
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) {
+        const uint4 v = S[chunk_swz(4 * lane + k)];
+        f.w[4 * k] = v.x;
+        f.w[4 * k + 1] = v.y;
+        f.w[4 * k + 2] = v.z;
+        f.w[4 * k + 3] = v.w;
+      }
+    };
     if constexpr (G > 0) {
+      // ---- wide slots: one structure for lean and per-lane tiles, so the
+      // tail sums (the bulk of the loads) are inlined once, with the fewest
+      // values live: the issue half (hash or nat_issue) and its row gather,
+      // the prefetch, the tail sums while all of those are in flight, the
+      // frame read back from S, then the finish half
+      uint32_t end = 64;  // where this frame's L4 sum ends (64: no tail)
       if (mine && nat_reg_ok(f, ln, lim)) end = 14 + bswap16((uint16_t)(f.w[4] & 0xFFFF));
+      const bool lean = lean_ok && __ballot(mine && nat_lan_fast_ok(a, f, in, ln, lim)) == ~0ull;
+      NatPend pend{kPendDone, kNone, 0, 0};
+      uint32_t rowid;
+      if (lean) {
+        rowid = home_bucket(flowid_hash_batched(T, f.w[8] >> 16, f.w[9] & 0xFFFF, f.u32at2(26),
+                                                f.u32at2(30), in, f.w[5] >> 24),
+                            a.t.bmask, a.t.mix, nat_lin(T));
+      } else {
+        pend = nat_issue(a, T, p, f, in, ln, mine, lim);
+        rowid = pend.row;
+      }
+      uint4 q[4];
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t rw = __shfl(rowid, 16 * j + (lane >> 2));
+        q[j] = rw != kNone ? rows[4 * (size_t)rw + (lane & 3)] : make_uint4(0, 0, 0, 0);
+      }
+      const uint32_t tail = tile_tail_sums<G, H>(g8, slot, tbytes, end);
+      reread();
+      wave_lds_sync();
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = q[j];
+      wave_lds_sync();
+      uint4 row[4];
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) row[k] = S[chunk_swz(4 * lane + k)];
+      uint32_t touch = kNone, smask = 0;
+      if (lean) {
+        const uint32_t proto = f.w[5] >> 24;
+        const uint32_t key[4] = {(f.w[8] >> 16) | ((f.w[9] & 0xFFFF) << 16), f.u32at2(26),
+                                 f.u32at2(30), in | (proto << 16)};
+        bool done;
+        const uint32_t idx = bucket_match_sel(row, key, &done);
+        const bool hit = done & (idx != kNone);
+        if (__ballot(!hit)) {  // misses (phase B) and full home buckets (reprobes)
+          const bool miss = done & !hit;
+          if (miss) a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
+          const uint32_t k = group_reserve(cur, kCurReprobe, !done);
+          if (!done) rq.ent[(size_t)rb * per_b * 64 + k] = p;
+          if (!hit) log_put(a.log, p, kNone);
+        }
+        if (hit) {
+          log_put(a.log, p, idx);
+          touch = idx;
+          f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
+          f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
+          fast_checksums(f, proto, bswap16((uint16_t)(f.w[4] & 0xFFFF)), tail);
+          f.w[0] = a.wan_macw0;
+          f.w[1] = a.wan_macw1;
+          f.w[2] = a.wan_macw2;
+          a.out[p] = (uint16_t)a.wan;
+          smask = proto == 6 ? 0xFu : 0x7u;  // the TCP checksum (bytes 50-51): chunk 3
+        }
+      } else {
+        bool m = false;
+        if (mine) {
+          m = nat_finish(a, T, pend, row, p, f, in, ln, touch, tail);
+          touch = route_note(a, p, touch);
+        }
+        const bool v = touch == kReprobe;  // queue on this block's reprobe slice
+        const uint32_t k = group_reserve(cur, kCurReprobe, v);
+        if (v) rq.ent[(size_t)rb * per_b * 64 + k] = p;
+        if (v) touch = kNone;
+        smask = m ? ((f.w[5] >> 24) == 6 ? 0xFu : 0x7u) : 0u;
+      }
+      bins_put(bins, cur, rb, per_b * 64, range0, p, touch);
+      // the changed header chunks of the rewritten frames, four lanes per
+      // frame (64 contiguous bytes), through the LDS tile
+      const uint64_t m0 = __ballot(smask & 1u), m1 = __ballot(smask & 2u),
+                     m2 = __ballot(smask & 4u), m3 = __ballot(smask & 8u);
+      if (m0) {  // (every stored frame stores chunk 0)
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+          S[chunk_swz(4 * lane + k)] =
+              make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
+        wave_lds_sync();
+        const uint32_t part = lane & 3;
+        const uint64_t pm = part == 0 ? m0 : part == 1 ? m1 : part == 2 ? m2 : m3;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+          const uint32_t c = 64 * j + lane;
+          if ((pm >> (c >> 2)) & 1ull) tile_st_at(g8, 64 * slot, chunk_at(c), S[chunk_swz(c)]);
+        }
+      }
+      wave_lds_sync();  // the next tile overwrites S
+      continue;
     }
     uint4 row[4];
     uint32_t touch = kNone;
-    bool store_all = false;
-    uint32_t smask = 0;  // wide slots: header chunks to store back (bit k = bytes 16k..)
-    if (lean_ok && __ballot(mine && nat_lan_fast_ok(a, f, in, ln, lim)) == ~0ull) {
-      // ---- lean tile: every lane a register-path LAN packet
+    bool store_all;
+    if (lean_ok && __ballot(mine && nat_lan_fast_ok(a, f, in, ln)) == ~0ull) {
+      // ---- lean tile: every lane a fast-path LAN packet
       const uint32_t proto = f.w[5] >> 24;
       const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
       const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
@@ -663,21 +780,11 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
 #ifdef VP_ABL_L2ROW  // diagnostic: every row from 64 fixed buckets (L2 hits)
       b0 = 0 * 16 + (lane >> 2); b1 = 16 + (lane >> 2); b2 = 32 + (lane >> 2); b3 = 48 + (lane >> 2);
 #endif
-      // 64-byte slots: the rows before the next tile's prefetch (vmcnt
-      // drains in order); wide slots: the prefetch, then the tail sums, then
-      // the rows (registers: the tail's loads in flight need them)
-      uint32_t tail = 0;
-      if constexpr (G > 0) {
-        if (tile + tstep < tend) fetch(tile + tstep);
-        tail = tile_tail_sums<G>(g8, slot, end, reinterpret_cast<uint32_t *>(S));
-      }
       const uint4 q0 = rows[4 * (size_t)b0 + part];
       const uint4 q1 = rows[4 * (size_t)b1 + part];
       const uint4 q2 = rows[4 * (size_t)b2 + part];
       const uint4 q3 = rows[4 * (size_t)b3 + part];
-      if constexpr (G == 0) {
-        if (tile + tstep < tend) fetch(tile + tstep);
-      }
+      if (tile + tstep < tend) fetch(tile + tstep);
       wave_lds_sync();
       S[chunk_swz(lane)] = q0;
       S[chunk_swz(64 + lane)] = q1;
@@ -709,7 +816,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
         f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
         f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
 #ifndef VP_ABL_NOCSUM  // diagnostic builds skip the checksums (tools/ablate.py)
-        fast_checksums(f, proto, bswap16((uint16_t)(f.w[4] & 0xFFFF)), tail);
+        fast_checksums(f, proto, bswap16((uint16_t)(f.w[4] & 0xFFFF)));
 #endif
         f.w[0] = a.wan_macw0;
         f.w[1] = a.wan_macw1;
@@ -717,7 +824,6 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
 #if !defined(VP_ABL_NOOUT) && !defined(VP_ABL_NOSIDE)  // diagnostic builds skip the out-port store
         VP_OUT_ST(a.out + p, (uint16_t)a.wan);
 #endif
-        smask = proto == 6 ? 0xFu : 0x7u;  // the TCP checksum (bytes 50-51) is in chunk 3
       }
 #ifdef VP_ABL_NOBINS  // diagnostic builds skip the touch bins
       touch = kNone;
@@ -725,21 +831,14 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       store_all = true;
     } else {
       // ---- per-lane tile (nat_issue / nat_finish)
-      const NatPend pend = nat_issue(a, T, p, f, in, ln, mine, lim);
-      uint32_t tail = 0;
-      if constexpr (G > 0) {  // (the order of the lean tile)
-        if (tile + tstep < tend) fetch(tile + tstep);
-        tail = tile_tail_sums<G>(g8, slot, end, reinterpret_cast<uint32_t *>(S));
-      }
+      const NatPend pend = nat_issue(a, T, p, f, in, ln, mine);
       uint4 q[4];
 #pragma unroll
       for (uint32_t j = 0; j < 4; j++) {
         const uint32_t rw = __shfl(pend.row, 16 * j + (lane >> 2));
         q[j] = rw != kNone ? rows[4 * (size_t)rw + (lane & 3)] : make_uint4(0, 0, 0, 0);
       }
-      if constexpr (G == 0) {
-        if (tile + tstep < tend) fetch(tile + tstep);
-      }
+      if (tile + tstep < tend) fetch(tile + tstep);
       wave_lds_sync();
 #pragma unroll
       for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = q[j];
@@ -748,7 +847,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       for (uint32_t k = 0; k < 4; k++) row[k] = S[chunk_swz(4 * lane + k)];
       bool m = false;
       if (mine) {
-        m = nat_finish(a, T, pend, row, p, f, in, ln, touch, tail);
+        m = nat_finish(a, T, pend, row, p, f, in, ln, touch);
         touch = route_note(a, p, touch);
       }
       {  // queue on this block's reprobe slice
@@ -757,60 +856,34 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
         if (v) rq.ent[(size_t)rb * per_b * 64 + k] = p;
       }
       if (touch == kReprobe) touch = kNone;
-      if constexpr (G > 0) {
-        smask = m ? ((f.w[5] >> 24) == 6 ? 0xFu : 0x7u) : 0u;
-      } else {
-        // a rewrite touches bytes 0-47; the TCP checksum (bytes 50-51) also
-        // dirties chunk 3: whole tiles are stored only when every lane rewrote
-        store_all = __ballot(m) == ~0ull;
-        if (!store_all) {
-          const uint64_t mm = __ballot(m);
-#pragma unroll
-          for (uint32_t k = 0; k < 4; k++)
-            S[chunk_swz(4 * lane + k)] =
-                make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
-          wave_lds_sync();
-#pragma unroll
-          for (uint32_t j = 0; j < 4; j++) {
-            const uint32_t c = 64 * j + lane;
-            if ((mm >> (c >> 2)) & 1ull) tile_st(g, c, S[chunk_swz(c)]);
-          }
-          wave_lds_sync();  // the next tile overwrites S
-        }
-      }
-    }
-    bins_put(bins, cur, rb, per_b * 64, range0, p, touch);
-    if constexpr (G == 0) {
-      if (store_all) {
+      // a rewrite touches bytes 0-47; the TCP checksum (bytes 50-51) also
+      // dirties chunk 3: whole tiles are stored only when every lane rewrote
+      store_all = __ballot(m) == ~0ull;
+      if (!store_all) {
+        const uint64_t mm = __ballot(m);
 #pragma unroll
         for (uint32_t k = 0; k < 4; k++)
           S[chunk_swz(4 * lane + k)] =
               make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
         wave_lds_sync();
-#pragma unroll
-        for (uint32_t j = 0; j < 4; j++) tile_st(g, 64 * j + lane, S[chunk_swz(64 * j + lane)]);
-        wave_lds_sync();  // the next tile overwrites S
-      }
-    } else {
-      // the changed header chunks of the rewritten frames, four lanes per
-      // frame (64 contiguous bytes), through the LDS tile
-      const uint64_t m0 = __ballot(smask & 1u), m1 = __ballot(smask & 2u),
-                     m2 = __ballot(smask & 4u), m3 = __ballot(smask & 8u);
-      if (m0) {  // (every stored frame stores chunk 0)
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++)
-          S[chunk_swz(4 * lane + k)] =
-              make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
-        wave_lds_sync();
-        const uint32_t part = lane & 3;
-        const uint64_t pm = part == 0 ? m0 : part == 1 ? m1 : part == 2 ? m2 : m3;
 #pragma unroll
         for (uint32_t j = 0; j < 4; j++) {
           const uint32_t c = 64 * j + lane;
-          if ((pm >> (c >> 2)) & 1ull) tile_st_at(g8, 64 * slot, chunk_at(c), S[chunk_swz(c)]);
+          if ((mm >> (c >> 2)) & 1ull) tile_st(g, c, S[chunk_swz(c)]);
         }
         wave_lds_sync();  // the next tile overwrites S
       }
+    }
+    bins_put(bins, cur, rb, per_b * 64, range0, p, touch);
+    if (store_all) {
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++)
+        S[chunk_swz(4 * lane + k)] =
+            make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
+      wave_lds_sync();
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) tile_st(g, 64 * j + lane, S[chunk_swz(64 * j + lane)]);
+      wave_lds_sync();  // the next tile overwrites S
     }
   }
   __syncthreads();
@@ -829,10 +902,14 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
 }
 
 // Wide slots (slot > 64): G lanes per frame in the tail sums.
+// Up to 8 tail chunks per lane and tile (slots <= 192 B): 4 waves per SIMD,
+// 8 loads in flight per wave. Longer tails (G = 16): 2 waves per SIMD with
+// 16 loads in flight each (measured 3 % faster at 1518-byte frames and 1.4 %
+// at 508: r03d; more waves with 8 loads each spill registers).
 template <uint32_t G>
-__global__ __launch_bounds__(256, 4) void nat_classify_wide(NatArgs a, uint32_t n_all,
-                                                           TouchBins bins, TileQueue rq) {
-  nat_tiles<G>(a, n_all, bins, rq);
+__global__ __launch_bounds__(256, G == 16 ? 2 : 4) void nat_classify_wide(
+    NatArgs a, uint32_t n_all, TouchBins bins, TileQueue rq) {
+  nat_tiles<G, G == 16 ? 2 : 1>(a, n_all, bins, rq);
 }
 
 // The classify kernel for a slot: 64 bytes, or the wide kernel whose G is the
