@@ -14,7 +14,12 @@
  * usage: nf_loop <trace.in> <trace.out> [--batch B] -- <NF options>
  * trace.in:  "VPTR" u32 n u32 slot, u16 in_dev[n], u16 len[n], i64 now[n],
  *            u8 frames[n*slot]
- * trace.out: "VPTO" u32 n u32 slot, u16 out_dev[n], u8 frames[n*slot]
+ * trace.out: "VPTO" u32 n u32 slot, u16 out_dev[n], u8 frames[n*slot],
+ *            "VPTX" u32 txmask[n]: the ports each packet leaves on, as nf.c
+ *            dispatches it: none (drop: dst == in), every port but the input
+ *            (flood, nf.c:83-96 over rte_eth_dev_count_avail() ports), or
+ *            dst (rte_eth_tx_burst). The port count comes from
+ *            VIGPATH_NB_DEVICES (default 2), as in the nf.h shims.
  */
 #include <stdbool.h>
 #include <stdint.h>
@@ -101,10 +106,20 @@ int main(int argc, char **argv) {
     }
     free(ptrs);
   }
-  for (uint32_t i = 0; i < n; i++) {
-    if (out[i] == in_dev[i]) drops++;
-    else if (out[i] == FLOOD_FRAME) floods++;
-    else tx++;
+  const char *nd = getenv("VIGPATH_NB_DEVICES");
+  const uint32_t nb_devices = nd ? (uint32_t)atoi(nd) : 2u;
+  uint32_t *txmask = calloc(n ? n : 1, 4);
+  for (uint32_t i = 0; i < n; i++) {  /* nf.c:158-175 */
+    if (out[i] == in_dev[i]) {
+      drops++;
+    } else if (out[i] == FLOOD_FRAME) {  /* flood(): nf.c:83-96 */
+      floods++;
+      for (uint32_t d = 0; d < nb_devices && d < 32; d++)
+        if (d != in_dev[i]) txmask[i] |= 1u << d;
+    } else {
+      tx++;
+      if (out[i] < 32) txmask[i] = 1u << out[i];
+    }
   }
   FILE *o = fopen(argv[2], "wb");
   if (!o) {
@@ -116,6 +131,8 @@ int main(int argc, char **argv) {
   fwrite(&slot, 4, 1, o);
   fwrite(out, 2, n, o);
   fwrite(frames, 1, (size_t)n * slot, o);
+  fwrite("VPTX", 1, 4, o);
+  fwrite(txmask, 4, n, o);
   fclose(o);
   printf("packets %u tx %llu drop %llu flood %llu\n", n, (unsigned long long)tx,
          (unsigned long long)drops, (unsigned long long)floods);

@@ -8,7 +8,8 @@ import numpy as np
 import pytest
 
 import orc
-from tracegen import mixed_fw_trace, mixed_nat_trace, mixed_pol_trace
+from tracegen import (mixed_bridge_trace, mixed_fw_trace, mixed_lb_trace,
+                      mixed_nat_trace, mixed_pol_trace)
 from vigor_amd import traces as T
 
 pytestmark = pytest.mark.gpu
@@ -31,12 +32,37 @@ def write_trace(path, frames, lens, in_dev, now, slot):
         f.write(frames.tobytes())
 
 
-def read_out(path, n, slot):
+def read_out(path, n, slot, tx=False):
     b = open(path, "rb").read()
     assert b[:4] == b"VPTO"
     out = np.frombuffer(b, np.uint16, n, 12)
     frames = np.frombuffer(b, np.uint8, n * slot, 12 + 2 * n)
-    return out, frames
+    if not tx:
+        return out, frames
+    o = 12 + 2 * n + n * slot
+    assert b[o:o + 4] == b"VPTX"
+    return out, frames, np.frombuffer(b, np.uint32, n, o + 4)
+
+
+def expected_tx(out, in_dev, nb_devices):
+    """nf.c:158-175 + flood() nf.c:83-96: the ports a packet leaves on."""
+    all_ports = (1 << nb_devices) - 1
+    m = np.where(out == 0xFFFF, all_ports & ~(1 << in_dev.astype(np.int64)),
+                 1 << np.minimum(out, 31).astype(np.int64))
+    return np.where(out == in_dev, 0, m).astype(np.uint32)
+
+
+def run_loop(tmp_path, loop, fr, ln, dv, now, slot, batch, args, nb_devices):
+    tin, tout = tmp_path / "t.in", tmp_path / "t.out"
+    write_trace(tin, fr, ln, dv, now, slot)
+    cmd = [LOOP + loop, str(tin), str(tout)]
+    if batch:
+        cmd += ["--batch", str(batch)]
+    env = dict(os.environ, VIGPATH_NB_DEVICES=str(nb_devices))
+    r = subprocess.run(cmd + ["--"] + args, capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    return read_out(tout, ln.shape[0], slot, tx=True)
 
 
 @pytest.mark.parametrize("batch", [0, 700])
@@ -124,3 +150,55 @@ def test_pol_loop_matches_oracle(tmp_path, batch):
     np.testing.assert_array_equal(out, exp_out)
     assert (out == 1).sum() > 50 and (out == 0).sum() > 50
     np.testing.assert_array_equal(frames, fr)  # the policer never writes
+
+
+SHIM_MACS3 = [bytes.fromhex("02000000000%d" % d) for d in range(3)]  # vp_nf_common.h
+
+
+@pytest.mark.parametrize("batch", [0, 700])
+def test_bridge_loop_floods_like_nf_c(tmp_path, batch):
+    """host/nf_loop_bridge: nf.c's loop linked against libvigbridge_nf.so.
+    vigbridge returns FLOOD_FRAME for unknown and broadcast destinations and
+    nf.c's flood() sends the frame on every port but the input one
+    (nf.c:83-96, 159-166); out ports, frames (never rewritten) and the
+    transmit sets equal the oracle's."""
+    rng = np.random.default_rng(6)
+    n = 3000 if batch else 400
+    fr, ln, dv, now = mixed_bridge_trace(rng, n, 120, n_dev=3)
+    cfg = orc.BridgeCfg(expiration_time=9, dyn_capacity=128, n_devices=3)
+    exp = fr.copy()
+    exp_out = orc.Oracle("bridge", cfg).run(exp, ln, dv, now, 64)
+    args = ["--expire", "9", "--capacity", "128"]
+    out, frames, txm = run_loop(tmp_path, "_bridge", fr, ln, dv, now, 64, batch, args, 3)
+    np.testing.assert_array_equal(out, exp_out)
+    assert (out == 0xFFFF).sum() > 20 and ((out != 0xFFFF) & (out != dv)).sum() > 20
+    np.testing.assert_array_equal(txm, expected_tx(exp_out, dv, 3))
+    f, e = frames.reshape(n, 64), exp.reshape(n, 64)
+    for i in range(n):
+        assert f[i, :ln[i]].tobytes() == e[i, :ln[i]].tobytes(), i
+
+
+@pytest.mark.parametrize("batch", [0, 700])
+def test_lb_loop_matches_oracle(tmp_path, batch):
+    """host/nf_loop_lb: nf.c's loop linked against libviglb_nf.so
+    (heartbeats from backends on ports 0/1, WAN traffic on port 2)."""
+    rng = np.random.default_rng(7)
+    n = 3000 if batch else 400
+    fr, ln, dv, now = mixed_lb_trace(rng, n, 150, 12)
+    cfg = orc.LbCfg(flow_capacity=256, flow_expiration_time=60_000_000,
+                    backend_capacity=16, cht_height=17,
+                    backend_expiration_time=3_600_000, wan_device=2, n_devices=3)
+    for d in range(3):
+        cfg.device_macs[d][:] = list(SHIM_MACS3[d])
+    exp = fr.copy()
+    exp_out = orc.Oracle("lb", cfg).run(exp, ln, dv, now, 64)
+    args = ["--flow-capacity", "256", "--backend-capacity", "16", "--cht-height", "17",
+            "--flow-expiration", "60000000", "--backend-expiration", "3600000",
+            "--wan", "2"]
+    out, frames, txm = run_loop(tmp_path, "_lb", fr, ln, dv, now, 64, batch, args, 3)
+    np.testing.assert_array_equal(out, exp_out)
+    assert ((out != dv)).sum() > 100
+    np.testing.assert_array_equal(txm, expected_tx(exp_out, dv, 3))
+    f, e = frames.reshape(n, 64), exp.reshape(n, 64)
+    for i in range(n):
+        assert f[i, :ln[i]].tobytes() == e[i, :ln[i]].tobytes(), i

@@ -16,8 +16,6 @@
 #   nf       tools/bench_nf.py                    -> gpurun_out/TAG_nf.log
 #   test:EXPR  pytest -m gpu -k EXPR
 #   probe[:ARG] tools/stream_probe [ARG]          -> gpurun_out/TAG_probe.log
-#   ablate:V,..  tools/ablate.py over the listed ablation builds
-#                                                 -> gpurun_out/TAG_ablate.log
 # Extra bench.py arguments for bench/trace/pmc: BENCH_ARGS env.
 set -o pipefail
 TAG=$1; shift
@@ -71,8 +69,6 @@ for step in "$@"; do
              done ;;
     probe|probe:*) a=${step#probe}; a=${a#:}
            run probe 300 tools/stream_probe $a > $O/${TAG}_probe.log 2>&1 || exit $? ;;
-    ablate:*) ABLATE_ONLY=${step#ablate:} run ablate 600 python3 tools/ablate.py 5 \
-             > $O/${TAG}_ablate.log 2>&1 || exit $? ;;
     nf) run nf 900 python3 tools/bench_nf.py > $O/${TAG}_nf.log 2>&1 || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

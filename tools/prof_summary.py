@@ -67,10 +67,16 @@ def trace(d, out, skip):
            "kernels": kernels, "rocprof_stats": stats}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
-    k = [n for n in kernels if n.endswith(KERNEL)]
+    k = [n for n in kernels if _is_kernel(n)]
     if k:
         print("%s avg %.1f us over timed launches" %
               (k[0], kernels[k[0]]["us_avg_after_warmup"]))
+
+
+def _is_kernel(name):
+    """The kernel of interest, template arguments aside
+    (vp::nat_classify_wide<16u> for PROF_KERNEL=nat_classify_wide)."""
+    return name.endswith(KERNEL) or name.split("<")[0].endswith(KERNEL)
 
 
 def pmc(out, pkts, dirs):
@@ -78,7 +84,7 @@ def pmc(out, pkts, dirs):
     for d in dirs:
         for r in _rows(d, "counter_collection.csv"):
             name = _short(_col(r, "Kernel_Name", "Kernel-Name", "KernelName"))
-            if not name.endswith(KERNEL):
+            if not _is_kernel(name):
                 continue
             c = _col(r, "Counter_Name", "Counter-Name")
             disp = int(_col(r, "Dispatch_Id", "Dispatch-Id", "Correlation_Id"))

@@ -170,53 +170,23 @@ __device__ inline void set_macs(const GFrame &f, const uint32_t mw[3]) {
   for (int k = 0; k < 3; k++) f.w32(4 * k, mw[k]);
 }
 
-// Frame-stream loads/stores (64 B per packet, read once, written once).
-// VP_ABL_NT builds mark them non-temporal so the stream does not displace the
-// flow table from the caches (tools/ablate.py measures both).
-__device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
-#ifdef VP_ABL_NT
-  typedef unsigned v4u __attribute__((ext_vector_type(4)));
-  const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p));
-  return make_uint4(v.x, v.y, v.z, v.w);
-#else
-  return *p;
-#endif
-}
-__device__ __forceinline__ void st_stream(uint4 *p, uint4 v) {
-#ifdef VP_ABL_NT
-  typedef unsigned v4u __attribute__((ext_vector_type(4)));
-  v4u x = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(x, reinterpret_cast<v4u *>(p));
-#else
-  *p = v;
-#endif
-}
+// Frame-stream loads/stores of the per-lane paths (64 B per packet, read
+// once, written once; non-temporal variants measured no faster, round 2).
+__device__ __forceinline__ uint4 ld_stream(const uint4 *p) { return *p; }
+__device__ __forceinline__ void st_stream(uint4 *p, uint4 v) { *p = v; }
 
 // Tile frame loads / stores of frames64_tiles and the vignat classify loop.
 // Stores are write-through (sc1: the written line leaves the XCD's L2 at
 // once, so the frame stream leaves fewer dirty lines between the table rows
 // and at the kernel boundary): 3.5 % faster nat_classify64 than write-back
-// stores (tools/ablate.py, VP_ABL_WBST builds keep plain stores). Ablation
-// builds also change the loads: VP_ABL_NTLD non-temporal (evict-first in L2;
-// measured 30 % slower).
-__device__ __forceinline__ uint4 tile_ld(const uint4 *p) {
-#if defined(VP_ABL_NTLD) || defined(VP_ABL_NTSC)
-  typedef unsigned v4u __attribute__((ext_vector_type(4)));
-  const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p));
-  return make_uint4(v.x, v.y, v.z, v.w);
-#else
-  return *p;
-#endif
-}
+// stores; non-temporal (evict-first) loads measured 30 % slower (round 2
+// diagnostic builds).
+__device__ __forceinline__ uint4 tile_ld(const uint4 *p) { return *p; }
 __device__ __forceinline__ void tile_st(uint4 *g, uint32_t c, uint4 v) {
-#ifndef VP_ABL_WBST
   typedef unsigned v4u __attribute__((ext_vector_type(4)));
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(g, 0, 4096, 0x00020000);
   const v4u x = {v.x, v.y, v.z, v.w};
   __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)(c * 16), 0, 16);
-#else
-  g[c] = v;
-#endif
 }
 
 // Stores of the wide-slot classify tiles: 16 bytes at byte `off` of the tile
@@ -330,20 +300,6 @@ struct TouchBins {
   uint32_t cap, pbits, bbits;
   uint32_t nsrc;  // classify blocks (the launch's grid)
 };
-// Per-packet side stores of the classify tiles (touch-bin entry, out port):
-// ablation builds make them write-through (`sc1`, relaxed agent-scope
-// atomic stores: the written lines leave the XCD's L2 at once, as the frame
-// stores do): VP_ABL_BINWT, VP_ABL_OUTWT.
-#if defined(VP_ABL_BINWT) || defined(VP_ABL_SIDEWT)
-#define VP_BIN_ST(p, v) __hip_atomic_store((p), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-#else
-#define VP_BIN_ST(p, v) (*(p) = (v))
-#endif
-#if defined(VP_ABL_OUTWT) || defined(VP_ABL_SIDEWT)
-#define VP_OUT_ST(p, v) __hip_atomic_store((p), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-#else
-#define VP_OUT_ST(p, v) (*(p) = (v))
-#endif
 
 // Touch-log entry of packet p; `log` is null in the classify kernels that
 // bin their touches.
@@ -376,8 +332,8 @@ __device__ __forceinline__ void bins_put(const TouchBins &bins, uint32_t *cur,
   const uint32_t k = group_reserve(cur, b, v);
   const bool fits = k < bins.cap;
   if (v && fits)
-    VP_BIN_ST(bins.ent + ((size_t)b * bins.nsrc + rb) * bins.cap + k,
-              (bin_local(touch, bins.bbits) << bins.pbits) | (p - range0));
+    bins.ent[((size_t)b * bins.nsrc + rb) * bins.cap + k] =
+        (bin_local(touch, bins.bbits) << bins.pbits) | (p - range0);
   const bool spill = v && !fits;
   const uint32_t o = group_reserve(cur, kCurOverflow, spill);
   if (spill) {

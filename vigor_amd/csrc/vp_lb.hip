@@ -218,13 +218,7 @@ __device__ __forceinline__ bool lb_decide(const LbArgs &a, const uint32_t *T,
   return rw(a.be_rec[bi]);
 }
 
-#ifdef VP_ABL_NOINLINE
-#define VP_LB_GENERIC_FN __device__ __noinline__
-#else
-#define VP_LB_GENERIC_FN __device__
-#endif
-VP_LB_GENERIC_FN void lb_generic_a(const LbArgs &a, const uint32_t *T,
-                                   uint32_t p) {
+__device__ void lb_generic_a(const LbArgs &a, const uint32_t *T, uint32_t p) {
   const GFrame f{a.frames + (size_t)p * a.slot, a.slot};
   const uint32_t in = a.in_dev[p];
   const L34 h = parse_l34(f, a.len[p]);

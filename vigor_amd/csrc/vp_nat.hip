@@ -173,12 +173,8 @@ __device__ __forceinline__ void macs_for(const NatArgs &a, uint32_t dst,
 
 // Generic (byte-addressed) phase A for frames outside the register fast path
 // (IP options, long frames, odd headers). Same decisions as nat_classify.
-#ifdef VP_ABL_NOINLINE
-#define VP_GENERIC_FN __device__ __noinline__
-#else
-#define VP_GENERIC_FN __device__  // inlined: measured faster (tools/ablate.py)
-#endif
-VP_GENERIC_FN uint32_t nat_generic_a(const NatArgs &a, const uint32_t *T,
+// (inlined: measured faster than a call, round 2)
+__device__ uint32_t nat_generic_a(const NatArgs &a, const uint32_t *T,
                                        uint32_t p, uint32_t in, uint32_t len) {
   GFrame f{a.frames + (size_t)p * a.slot, a.slot};
   L34 h = parse_l34(f, len);
@@ -307,9 +303,7 @@ __device__ __forceinline__ NatPend nat_issue(const NatArgs &a, const uint32_t *T
     }
     P.kind = kPendLan;
     P.b = home_bucket(hh, a.t.bmask, a.t.mix, nat_lin(T));
-#ifndef VP_ABL_NOPROBE  // diagnostic builds skip the read (tools/ablate.py)
     P.row = P.b;
-#endif
   }
   return P;
 }
@@ -359,10 +353,6 @@ __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
     macs_for(a, dst, mw);
   } else {
     const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
-#ifdef VP_ABL_NOPROBE  // diagnostic builds only (tools/ablate.py)
-    asm volatile("" ::"v"(key[0]), "v"(key[1]), "v"(key[2]), "v"(key[3]));
-    const uint32_t idx = P.b & (a.t.cap - 1);
-#else
     bool done;
     const uint32_t idx = bucket_match(row[0], row[1], row[2], row[3], key, &done);
     if (!done) {  // the bucket is full of other keys: nat_reprobe walks the
@@ -374,7 +364,6 @@ __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
         a.reprobe[wave_append(&a.t.ctl->reprobe_count, true)] = p;
       return false;
     }
-#endif
     if (idx == kNone) {  // new flow, or not yet visible: phase B
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
       log_put(a.log, p, kNone);  // phase B writes the real entry
@@ -430,11 +419,7 @@ __device__ __forceinline__ void route_publish(const NatArgs &a, const uint32_t *
 // outside the fast path take nat_generic_a). Returns the logged index.
 __device__ __forceinline__ uint32_t nat_lane(const NatArgs &a, const uint32_t *T,
                                              uint32_t p) {
-#ifdef VP_ABL_NOFRAME  // diagnostic: synthesise the bench trace's frame
-  uint4 *fp = reinterpret_cast<uint4 *>(a.frames + (size_t)(p & 63) * a.slot);
-#else
   uint4 *fp = reinterpret_cast<uint4 *>(a.frames + (size_t)p * a.slot);
-#endif
   RFrame f;
   const uint4 c0 = ld_stream(fp), c1 = ld_stream(fp + 1), c2 = ld_stream(fp + 2),
               c3 = ld_stream(fp + 3);
@@ -444,17 +429,6 @@ __device__ __forceinline__ uint32_t nat_lane(const NatArgs &a, const uint32_t *T
   f.w[12] = c3.x; f.w[13] = c3.y; f.w[14] = c3.z; f.w[15] = c3.w;
   const uint32_t in = a.in_dev[p], len = a.len[p];
   uint32_t touch = kNone;
-#ifdef VP_ABL_NOFRAME
-  {
-    const uint32_t fl = p & (a.t.cap - 1), v = fl >> 16;
-    f.set16(34, bswap16((uint16_t)(fl & 0xFFFF)));
-    f.set32at2(26, 10u | (((v >> 8) & 0xFF) << 16) | ((v & 0xFF) << 24));
-  }
-  const NatPend P = nat_issue(a, T, p, f, in, len, true);
-  const uint4 row[4] = {};
-  asm volatile("" ::"v"(nat_finish(a, T, P, row, p, f, in, len, touch)
-                            ? f.w[6] ^ f.w[10] : 0u));
-#else
   const NatPend P = nat_issue(a, T, p, f, in, len, true);
   uint4 row[4] = {};
   if (P.row != kNone) {
@@ -471,7 +445,6 @@ __device__ __forceinline__ uint32_t nat_lane(const NatArgs &a, const uint32_t *T
     if ((f.w[5] >> 24) == 6)
       st_stream(fp + 3, make_uint4(f.w[12], f.w[13], f.w[14], f.w[15]));
   }
-#endif
   return route_note(a, p, touch);
 }
 
@@ -537,6 +510,33 @@ __device__ __forceinline__ uint32_t bucket_match_sel(const uint4 *row,
   return m0 ? ix.x : e0 ? kNone : m1 ? ix.y : e1 ? kNone : m2 ? ix.z : kNone;
 }
 
+// 128-byte slots: the tail sums of the wave's tile from the registers the
+// dense fetch left (d[j] = chunk 64 j + lane: frame 8 j + lane / 8, part
+// lane % 8; parts 4-7 are the bytes 64-127 the L4 sum may cover): each
+// 8-lane group adds its frame's masked chunks, and frame f's sum goes to
+// lane f (round j = f / 8, from lane 8 (f % 8)).
+__device__ __forceinline__ uint32_t dense128_tail(const uint4 d[8], uint32_t end) {
+  const uint32_t lane = threadIdx.x & 63, part = lane & 7;
+  uint32_t tail = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 8; j++) {
+    const uint32_t e = (uint32_t)__shfl((int)end, (int)(8 * j + (lane >> 3)));
+    const uint32_t o = 16 * part;
+    uint32_t s = 0;
+    if (part >= 4 && o < e) {
+      uint4 x = d[j];
+      if (e - o < 16) x = chunk_keep(x, 0, (int)(e - o));
+      s = sum16x4(x, 0u);
+    }
+    s += (uint32_t)__shfl_xor((int)s, 1);
+    s += (uint32_t)__shfl_xor((int)s, 2);
+    s += (uint32_t)__shfl_xor((int)s, 4);
+    const uint32_t got = (uint32_t)__shfl((int)s, (int)((lane & 7) * 8));
+    if ((lane >> 3) == j) tail = got;
+  }
+  return tail;
+}
+
 // Phase A over tiles of 64 consecutive packets per wave, the frames staged
 // through the wave's LDS tile. G = 0: 64-byte slots (nat_classify64), every
 // global load/store instruction 1 KiB contiguous (the loop of frames64_tiles,
@@ -552,7 +552,7 @@ __device__ __forceinline__ uint32_t bucket_match_sel(const uint4 *row,
 // registers, (64-byte slots) the whole tile stored back (packets left for
 // phase B or the reprobe walk are stored unchanged). Any other tile runs
 // nat_issue / nat_finish per lane. Owner mode always takes the per-lane path.
-template <uint32_t G, uint32_t H = 1>
+template <uint32_t G, uint32_t H = 1, bool D = false>
 __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins bins,
                                           TileQueue rq) {
   __shared__ uint32_t T[kNatTabWords];
@@ -596,13 +596,8 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
 #pragma unroll
       for (uint32_t j = 0; j < 4; j++)
         r[j] = tile_ld(reinterpret_cast<const uint4 *>(g8 + chunk_at(64 * j + lane)));
-#ifdef VP_ABL_NOSIDE  // diagnostic: no len / in_dev loads (the bench's values)
-      m_in = 0;
-      m_len = 60;
-#else
       m_in = a.in_dev[p];
       m_len = a.len[p];
-#endif
       return;
     }
     const uint32_t avail = n_all - tb;  // in the batch
@@ -627,9 +622,25 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
     const uint32_t tb = first + tile * 64;
     uint8_t *g8 = a.frames + (size_t)tb * slot;
     uint4 *g = reinterpret_cast<uint4 *>(g8);
-    if constexpr (G > 0) fetch(tile);
+    uint4 d8[D ? 8 : 1];  // D: the whole tile (128-byte slots)
+    if constexpr (D) {
+      // 128-byte slots: the tile's 8 KiB as eight 1 KiB-contiguous loads,
+      // header chunks (part < 4 of a slot) into the frame image, the tail
+      // chunks summed from registers below (dense128_tail): one round trip
+      const uint32_t bytes = min(64u, n_all - tb) * 128u;
 #pragma unroll
-    for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = r[j];
+      for (uint32_t j = 0; j < 8; j++) d8[j] = buf_ld16(g8, bytes, (64 * j + lane) * 16);
+      const uint32_t pp = tb + lane;
+      m_in = pp < n_all ? a.in_dev[pp] : 0u;
+      m_len = pp < n_all ? a.len[pp] : 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++)
+        if ((lane & 7) < 4) S[chunk_swz(4 * (8 * j + (lane >> 3)) + (lane & 3))] = d8[j];
+    } else {
+      if constexpr (G > 0) fetch(tile);
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = r[j];
+    }
     wave_lds_sync();
     const uint32_t p = tb + lane;
     const bool mine = p >= a.p0 && p < a.p1;
@@ -664,6 +675,8 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       // frame read back from S, then the finish half
       uint32_t end = 64;  // where this frame's L4 sum ends (64: no tail)
       if (mine && nat_reg_ok(f, ln, lim)) end = 14 + bswap16((uint16_t)(f.w[4] & 0xFFFF));
+      uint32_t tail = 0;
+      if constexpr (D) tail = dense128_tail(d8, end);
       const bool lean = lean_ok && __ballot(mine && nat_lan_fast_ok(a, f, in, ln, lim)) == ~0ull;
       NatPend pend{kPendDone, kNone, 0, 0};
       uint32_t rowid;
@@ -681,7 +694,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
         const uint32_t rw = __shfl(rowid, 16 * j + (lane >> 2));
         q[j] = rw != kNone ? rows[4 * (size_t)rw + (lane & 3)] : make_uint4(0, 0, 0, 0);
       }
-      const uint32_t tail = tile_tail_sums<G, H>(g8, slot, tbytes, end);
+      if constexpr (!D) tail = tile_tail_sums<G, H>(g8, slot, tbytes, end);
       reread();
       wave_lds_sync();
 #pragma unroll
@@ -759,13 +772,8 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       const uint32_t proto = f.w[5] >> 24;
       const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
       const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
-#ifdef VP_ABL_SEQROW  // diagnostic: consecutive packets -> consecutive rows (two per row)
-      const uint32_t b = ((p >> 1) ^ (flowid_hash_batched(T, sp, dp, sip, dip, in, proto) & 0)) &
-                         a.t.bmask;
-#else
       const uint32_t b = home_bucket(flowid_hash_batched(T, sp, dp, sip, dip, in, proto),
                                      a.t.bmask, a.t.mix, nat_lin(T));
-#endif
       // lane L fetches part L % 4 of the row of packet 16 j + L / 4: the four
       // row numbers come in by ds_bpermute, issued together and waited for
       // once; named registers (an array here stays in scratch memory)
@@ -777,9 +785,6 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       asm volatile("ds_bpermute_b32 %0, %1, %2 offset:192" : "=v"(b3) : "v"(src), "v"(b));
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
       const uint32_t part = lane & 3;
-#ifdef VP_ABL_L2ROW  // diagnostic: every row from 64 fixed buckets (L2 hits)
-      b0 = 0 * 16 + (lane >> 2); b1 = 16 + (lane >> 2); b2 = 32 + (lane >> 2); b3 = 48 + (lane >> 2);
-#endif
       const uint4 q0 = rows[4 * (size_t)b0 + part];
       const uint4 q1 = rows[4 * (size_t)b1 + part];
       const uint4 q2 = rows[4 * (size_t)b2 + part];
@@ -795,13 +800,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       for (uint32_t k = 0; k < 4; k++) row[k] = S[chunk_swz(4 * lane + k)];
       const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
       bool done;
-#if defined(VP_ABL_L2ROW) || defined(VP_ABL_SEQROW)
-      asm volatile("" ::"v"(row[0].x), "v"(row[1].y), "v"(row[2].z), "v"(row[3].w));
-      done = true;
-      const uint32_t idx = p & (a.t.cap - 1);
-#else
       const uint32_t idx = bucket_match_sel(row, key, &done);
-#endif
       const bool hit = done & (idx != kNone);
       if (__ballot(!hit)) {  // misses (phase B) and full home buckets (reprobes)
         const bool miss = done & !hit;
@@ -815,19 +814,12 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
         touch = idx;
         f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
         f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
-#ifndef VP_ABL_NOCSUM  // diagnostic builds skip the checksums (tools/ablate.py)
         fast_checksums(f, proto, bswap16((uint16_t)(f.w[4] & 0xFFFF)));
-#endif
         f.w[0] = a.wan_macw0;
         f.w[1] = a.wan_macw1;
         f.w[2] = a.wan_macw2;
-#if !defined(VP_ABL_NOOUT) && !defined(VP_ABL_NOSIDE)  // diagnostic builds skip the out-port store
-        VP_OUT_ST(a.out + p, (uint16_t)a.wan);
-#endif
+        a.out[p] = (uint16_t)a.wan;
       }
-#ifdef VP_ABL_NOBINS  // diagnostic builds skip the touch bins
-      touch = kNone;
-#endif
       store_all = true;
     } else {
       // ---- per-lane tile (nat_issue / nat_finish)
@@ -912,11 +904,19 @@ __global__ __launch_bounds__(256, G == 16 ? 2 : 4) void nat_classify_wide(
   nat_tiles<G, G == 16 ? 2 : 1>(a, n_all, bins, rq);
 }
 
+// 128-byte slots (124-byte frames and the like): the dense tile (nat_tiles
+// D), one round trip for all of a tile's bytes.
+__global__ __launch_bounds__(256, 4) void nat_classify128(NatArgs a, uint32_t n_all,
+                                                         TouchBins bins, TileQueue rq) {
+  nat_tiles<4, 1, true>(a, n_all, bins, rq);
+}
+
 // The classify kernel for a slot: 64 bytes, or the wide kernel whose G is the
 // tail's 16-byte chunks (slot - 64) / 16 rounded up to a power of two, at most 16.
 typedef void (*NatTileKernel)(NatArgs, uint32_t, TouchBins, TileQueue);
 static NatTileKernel nat_tile_kernel(uint32_t slot) {
   if (slot == 64) return nat_classify64;
+  if (slot == 128) return nat_classify128;
   const uint32_t nch = (slot - 64) / 16;
   if (nch <= 1) return nat_classify_wide<1>;
   if (nch <= 2) return nat_classify_wide<2>;

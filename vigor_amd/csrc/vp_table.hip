@@ -822,17 +822,7 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const uint32_t pmask = (1u << pbits) - 1;
-#if defined(VP_ABL_FOLDKU16)  // diagnostic builds (tools/ablate.py)
-#define VP_FOLD_KU 16
-#elif defined(VP_ABL_FOLDKU32)
-#define VP_FOLD_KU 32
-#elif defined(VP_ABL_FOLDKU64)
-#define VP_FOLD_KU 64
-#endif
-#ifndef VP_FOLD_KU
-#define VP_FOLD_KU 8
-#endif
-  constexpr uint32_t kU = VP_FOLD_KU;  // source slices in flight per wave
+  constexpr uint32_t kU = 8;  // source slices in flight per wave (16-64: no faster, round 2)
   // wave w takes slices w, w + nw, ...; 64 of them per round, their sizes
   // loaded by one instruction (lane l <-> slice w + l * nw)
   for (uint32_t r0 = threadIdx.x >> 6; r0 < nsrc; r0 += 64 * nw) {
