@@ -346,6 +346,10 @@ def main():
                          "design: the headline value) or replicated on every "
                          "GPU; the other mode is measured too (extra key "
                          "other_shard_mode) unless --no-extra")
+    ap.add_argument("--route-all", action="store_true",
+                    help="profiling: one GPU running the owner-mode pipeline "
+                         "with every LAN key sent through the (single-rank "
+                         "RCCL) exchange (VIGPATH_ROUTE_ALL=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the host-resident end-to-end rate")
@@ -394,6 +398,13 @@ def main():
         cfg = vigor_amd.nat_config_from_args(
             NAT_ARGS + ["--max-flows", str(args.flows)], 2, DEV_MACS)
         nat = vigor_amd.Nat(cfg, gpu=local)
+        if args.route_all and world == 1:  # the owner pipeline on one GPU
+            import ctypes
+            from vigor_amd import shard
+            os.environ["VIGPATH_ROUTE_ALL"] = "1"
+            uid = (ctypes.c_uint8 * 128).from_buffer_copy(shard.rccl_unique_id())
+            vigor_amd._check(nat.L.vp_attach_rccl(nat.h, uid, 1, 0), "vp_attach_rccl")
+            shard.set_mode(nat, "owner")
         if world > 1:  # one vignat over all ranks
             from vigor_amd import shard
             if host_comm:
@@ -468,7 +479,10 @@ def main():
         workload = "vignat %dB frames in %dB slots, %d flows, %s order, 1xMI355X" % (
             flen, slot, args.flows, args.order)
     kname = ("nat_classify64" if slot == SLOT else "nat_classify_wide")
-    if world > 1 and mode == "owner":
+    if args.route_all:
+        workload = ("vignat %dB, %d flows, 1xMI355X, owner-mode pipeline with every key "
+                    "routed through a one-rank RCCL exchange (profiling)" % (flen, args.flows))
+    if (world > 1 and mode == "owner") or args.route_all:
         kname += "+nat_remote64"
     extra = {}
     if not args.no_extra and world == 1 and args.order == "rr":

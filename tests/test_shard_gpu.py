@@ -51,6 +51,8 @@ def _worker(rank, world, port, spec, outdir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    if spec.get("own_cap"):  # owner mode: force the padded exchange's capacity
+        os.environ["VIGPATH_OWN_CAP"] = str(spec["own_cap"])
     import vigor_amd
     from gpuh import run_gpu
     from vigor_amd import shard
@@ -156,7 +158,24 @@ SPECS = [
 def test_sharded_nat_equals_single_nf(world, spec, mode):
     """Both dictionary placements: replicated, and owner-sharded by flow hash
     (LAN lookups of other ranks' keys through the all-to-all)."""
-    spec = dict(spec, mode=mode)
+    check_sharded(dict(spec, mode=mode), world)
+
+
+@pytest.mark.parametrize("world,spec", [
+    (2, dict(SPECS[0][1], own_cap=64)),
+    (3, dict(SPECS[1][1], own_cap=8)),
+    (4, dict(SPECS[3][1], own_cap=40)),
+])
+def test_owner_padded_exchange_overflow(world, spec):
+    """Owner mode with the padded exchange's capacity forced small: segments
+    whose keys for some owner exceed it are detected on the device (every
+    rank agrees through the allreduced flag), pass 2 leaves the routed
+    packets alone and the exact exchange answers them; the results are
+    still the single NF's."""
+    check_sharded(dict(spec, mode="owner"), world)
+
+
+def check_sharded(spec, world):
     res = run_sharded(spec, world)
     fr, ln, dv, now = _trace(spec)
     cfg = orc.nat_cfg(wan=1, start_port=0, ext_ip=T.ip4(192, 168, 4, 2),

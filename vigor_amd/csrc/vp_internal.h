@@ -78,12 +78,20 @@ struct Ctl {
   uint32_t disp_count;  // inserts that passed their home bucket (since rebuild)
   uint32_t sh_live;     // entries in this rank's buckets (= n_live unless owner mode)
   uint32_t own_new;     // owner mode: union keys this rank will insert (upper bound)
+  uint32_t route_ovf;   // owner mode: some rank's keys for an owner exceeded the
+                        // padded exchange's capacity (all ranks agree: allreduced)
+  uint32_t pad_;
 };
 
 // The control block as a fold kernel publishes it into page-locked host
 // memory (tbl_fold_read_ctl, vp_table.hip); the host polls `epoch`.
+// Multi-GPU: the fold also publishes every rank's segment counters
+// (miss, defer, touch_ovf, reprobe: gathered on the device before the fold)
+// and, owner mode, this rank's key count per owner.
+constexpr int kPubGath = 4;  // words per rank
 struct CtlPub {
   Ctl ctl;
+  uint32_t xtra[(kPubGath + 1) * 64];
   uint32_t epoch;
 };
 
@@ -174,6 +182,15 @@ struct Workspace {
   uint32_t *reply = nullptr, *rreply = nullptr;
   size_t reply_n = 0, rreply_n = 0;
   uint32_t *h_tot = nullptr;  // pinned landing buffer for dtot
+  // padded exchange (owner mode): keys received per peer, the global
+  // capacity-overflow flag
+  uint32_t *rcnt = nullptr;
+  uint64_t *ovf64 = nullptr;
+  // multi-GPU: the ranks' segment counters gathered on the device before a
+  // fold (kPubGath words each) and their host copy (gath_ok: this segment's)
+  uint32_t *gath = nullptr;
+  std::vector<uint32_t> h_gath;
+  bool gath_ok = false;
   size_t bins_ent_n = 0, bins_cnt_n = 0;
   void *cub_tmp = nullptr;
   size_t cub_bytes = 0;
@@ -242,6 +259,10 @@ struct vp_ctx {
   vp::Comm *comm = nullptr;
   int shard_mode = 0;  // VP_SHARD_REPLICATED / VP_SHARD_OWNER
   uint32_t off = 0;
+  // owner mode: keys per peer the padded exchange carries in this batch (0:
+  // exact exchange), and this rank's largest per-owner key count last seen
+  uint32_t own_cap = 0;
+  uint32_t own_maxsend = 0;
   std::vector<uint32_t> rank_n;    // slice sizes of the current batch
   std::vector<uint32_t> rank_cnt;  // new keys per rank of the current segment
 };

@@ -118,7 +118,17 @@ struct Route {
   uint32_t first, range;  // packets of block b: [first + b * range, +range)
   const uint32_t *dbase;  // pass 2: [block][n] offset of the slice's replies
   const uint32_t *rreply; // pass 2: replies (index or kNone), in send order
+  // the padded exchange: owner o's replies at [o cap, (o + 1) cap); a key
+  // past its owner's cap, or any rank's overflow (*ovf), has no reply in
+  // this pass (cap == 0: the exact exchange, every key answered)
+  uint32_t cap;
+  const uint64_t *ovf;
+  // VIGPATH_ROUTE_ALL=1 (profiling): every LAN key goes through the
+  // exchange, this rank's own included (one rank: the whole pipeline at 100 %
+  // routed)
+  uint32_t all;
 };
+constexpr uint32_t kNoReply = 0xFFFFFFFAu;  // route_answer: not answered in this pass
 
 struct NatArgs {
   uint8_t *frames;
@@ -148,7 +158,7 @@ __device__ __forceinline__ bool nat_route(const NatArgs &a, uint32_t p, uint32_t
                                           const uint32_t key[4]) {
   if (!a.own.n) return false;
   const uint32_t o = owner_of(h, a.own.n);
-  if (o == a.own.r) return false;
+  if (o == a.own.r && !a.own.all) return false;
   const uint32_t k = atomicAdd(&a.own.cur[o], 1u);
   a.own.desc[((size_t)blockIdx.x * a.own.n + o) * a.own.range + k] =
       make_uint4(key[0], key[1], key[2], key[3]);
@@ -296,7 +306,7 @@ __device__ __forceinline__ NatPend nat_issue(const NatArgs &a, const uint32_t *T
     // flow_manager_get_internal (nat_flowmanager.c:67-76): map_get's hash
     const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
     const uint32_t hh = flowid_hash(T, sp, dp, sip, dip, in, proto);
-    if (a.own.n && owner_of(hh, a.own.n) != a.own.r) {  // another rank's key
+    if (a.own.n && (owner_of(hh, a.own.n) != a.own.r || a.own.all)) {  // another rank's key
       P.kind = kPendRemote;
       P.b = hh;
       return P;
@@ -1053,13 +1063,29 @@ __global__ void route_base(uint32_t *dbase, const uint32_t *dtot, uint32_t nblk,
   }
 }
 
-// One block per source block: its slices into the send buffer.
+// The padded exchange: owner o's chunk is [o cap, (o + 1) cap); a count
+// past cap sets *ovf (every rank then takes the exact exchange).
+__global__ void route_pad(uint32_t *dbase, const uint32_t *dtot, uint32_t nblk, uint32_t n,
+                          uint32_t cap, uint64_t *ovf) {
+  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nblk * n;
+       x += gridDim.x * blockDim.x) {
+    const uint32_t o = x % n;
+    dbase[x] += o * cap;
+    if (x < n && dtot[x] > cap) *ovf = 1;
+  }
+}
+
+// One block per source block: its slices into the send buffer (cap: only
+// the entries inside their owner's padded chunk).
 __global__ __launch_bounds__(256) void route_pack(const uint4 *desc, const uint32_t *dcnt,
                                                   const uint32_t *dbase, uint32_t n,
-                                                  uint32_t range, uint4 *sendk) {
+                                                  uint32_t range, uint32_t cap,
+                                                  uint4 *sendk) {
   const uint32_t b = blockIdx.x;
   for (uint32_t o = 0; o < n; o++) {
-    const uint32_t cnt = dcnt[(size_t)b * n + o], base = dbase[(size_t)b * n + o];
+    uint32_t cnt = dcnt[(size_t)b * n + o];
+    const uint32_t base = dbase[(size_t)b * n + o];
+    if (cap) cnt = min(cnt, (uint32_t)max(0, (int)((o + 1) * cap) - (int)base));
     const uint4 *src = desc + ((size_t)b * n + o) * range;
     for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) sendk[base + k] = src[k];
   }
@@ -1070,18 +1096,27 @@ __global__ __launch_bounds__(256) void route_pack(const uint4 *desc, const uint3
 // bucket fetched as one cooperative 64-byte request (wave_gather64). Answers
 // the index or kNone (a new flow: the ingest rank queues the packet for
 // phase B).
+// Padded exchange (cap > 0): n keys arrived as ranks x cap, peer q's first
+// rcnt[q] valid; no work when any rank overflowed (*ovf, published as
+// ctl->route_ovf for the host). cap == 0: n keys, all valid.
 __global__ __launch_bounds__(256) void nat_own_probe(TableDev t, const uint32_t *crc_tab,
                                                      const uint4 *keys, uint32_t n,
+                                                     uint32_t cap, const uint32_t *rcnt,
+                                                     const uint64_t *ovf, Ctl *ctl,
                                                      uint32_t *reply) {
   __shared__ uint32_t T[15 * 256];
   __shared__ uint4 stage[4][256];
+  const bool skip = cap && *ovf;
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctl->route_ovf = skip ? 1u : 0u;
+  if (skip) return;
   load_crc_tables(T, crc_tab);
   uint4 *S = stage[threadIdx.x >> 6];
   const uint32_t lane = threadIdx.x & 63;
   for (uint32_t base = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; base < n;
        base += gridDim.x * 256) {  // wave-uniform
     const uint32_t j = base + lane;
-    const bool act = j < n;
+    const bool act = j < n && (!cap || j % cap < rcnt[j / cap]);
+    if (!__ballot(act)) continue;
     const uint4 k = act ? keys[j] : make_uint4(0, 0, 0, 0);
     const uint32_t key[4] = {k.x, k.y, k.z, k.w};
     const uint32_t h = flowid_hash(T, k.x & 0xFFFF, k.x >> 16, k.y, k.z, k.w & 0xFFFF,
@@ -1122,12 +1157,14 @@ __device__ __forceinline__ void nat_lan_fast(const NatArgs &a, RFrame &f, uint32
   a.out[p] = a.wan;
 }
 
-// The answer for packet p's route (kRouteBit set).
+// The answer for packet p's route (kRouteBit set), or kNoReply.
 __device__ __forceinline__ uint32_t route_answer(const NatArgs &a, uint32_t p,
                                                  uint32_t rt) {
   const uint32_t o = (rt >> 24) & 63, k = rt & 0xFFFFFFu;
   const uint32_t blk = (p - a.own.first) / a.own.range;
-  return a.own.rreply[a.own.dbase[(size_t)blk * a.own.n + o] + k];
+  const uint32_t at = a.own.dbase[(size_t)blk * a.own.n + o] + k;
+  if (a.own.cap && (at - o * a.own.cap >= a.own.cap || *a.own.ovf)) return kNoReply;
+  return a.own.rreply[at];
 }
 
 // Pass 2 for 64-byte slots: the same coalesced tiles as pass 1; routed
@@ -1154,8 +1191,8 @@ __global__ __launch_bounds__(256, 4) void nat_remote64(NatArgs a, uint32_t n_all
           P.kind = 1;  // pass 1's own touch
           P.idx = rt;
         } else {
-          P.kind = 2;
           P.idx = route_answer(a, p, rt);
+          P.kind = P.idx == kNoReply ? 0 : 2;  // (no reply: the exact exchange's)
         }
         return P;
       },
@@ -1192,6 +1229,7 @@ __global__ void nat_remote_lane(NatArgs a) {
     const uint32_t rt = a.own.route[p];
     if (rt == kNone || !(rt & kRouteBit)) continue;
     const uint32_t idx = route_answer(a, p, rt);
+    if (idx == kNoReply) continue;  // the exact exchange answers it
     a.log[p] = idx;
     if (idx == kNone) {
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
@@ -1327,17 +1365,29 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
     ph->range1 = std::max<uint32_t>(1, (np + ph->grid1 - 1) / ph->grid1);
   }
   if (ph->range1 >= (1u << 24) - 1) return VP_ENOTSUP;
+  const uint32_t C = std::max<uint32_t>(1, c->own_cap);  // keys per peer (padded)
   const size_t slices = (size_t)ph->grid1 * n;
   VP_TRY(grow_dev(&w.desc, &w.desc_n, slices * ph->range1, c->stream));
   VP_TRY(grow_dev(&w.dcnt, &w.dcnt_n, slices, c->stream));
   VP_TRY(grow_dev(&w.dbase, &w.dbase_n, slices, c->stream));
   VP_TRY(grow_dev(&w.dtot, &w.dtot_n, kMaxDest, c->stream));
   VP_TRY(grow_dev(&w.route, &w.route_n, b->n, c->stream));
+  VP_TRY(grow_dev(&w.sendk, &w.sendk_n, (size_t)n * C, c->stream));
+  VP_TRY(grow_dev(&w.recvk, &w.recvk_n, (size_t)n * C, c->stream));
+  VP_TRY(grow_dev(&w.reply, &w.reply_n, (size_t)n * C, c->stream));
+  VP_TRY(grow_dev(&w.rreply, &w.rreply_n, (size_t)n * C, c->stream));
+  if (!w.rcnt) VP_HIP(hipMalloc((void **)&w.rcnt, 4 * kMaxDest));
+  if (!w.ovf64) VP_HIP(hipMalloc((void **)&w.ovf64, 8));
   if (!w.h_tot) VP_HIP(hipHostMalloc((void **)&w.h_tot, 4 * kMaxDest, hipHostMallocDefault));
+  static const uint32_t route_all = [] {
+    const char *e = getenv("VIGPATH_ROUTE_ALL");
+    return e && atoi(e) ? 1u : 0u;
+  }();
   a.own = Route{n, r, w.desc, w.dcnt, w.route, nullptr, first, ph->range1, w.dbase,
-                nullptr};
+                w.rreply, C, w.ovf64, route_all};
 
   VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
+  VP_HIP(hipMemsetAsync(w.ovf64, 0, 8, c->stream));
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   pm.mark();
   if (np) {
@@ -1356,45 +1406,30 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   }
   VP_HIP(hipEventRecord(c->ev1, c->stream));
   pm.mark();
+  // C1 over the padded exchange, no host round trip: owner o's keys go to
+  // [o C, (o + 1) C) of the send buffer, the per-owner counts cross in their
+  // own small all-to-all, and a count past C (any rank: allreduced) leaves
+  // the routed packets to the exact exchange below
   route_scan<<<n, 256, 0, c->stream>>>(w.dcnt, ph->grid1, n, w.dbase, w.dtot);
-  route_base<<<grid_for(slices), 256, 0, c->stream>>>(w.dbase, w.dtot, ph->grid1, n);
-  VP_HIP(hipGetLastError());
-  VP_HIP(hipMemcpyAsync(w.h_tot, w.dtot, 4ull * n, hipMemcpyDeviceToHost, c->stream));
-  VP_HIP(stream_wait(c->stream));
-  // C1 sizes: M[q * n + o] = keys rank q sends to owner o
-  std::vector<uint32_t> M((size_t)n * n);
-  VP_TRY(m.allgather_host(c, w.h_tot, M.data(), 4ull * n));
-  uint64_t S = 0, R = 0;
-  std::vector<size_t> sk(n), rk(n), sr(n), rr(n);
-  for (uint32_t q = 0; q < n; q++) {
-    S += M[(size_t)r * n + q];
-    R += M[(size_t)q * n + r];
-    sk[q] = 16ull * M[(size_t)r * n + q];
-    rk[q] = 16ull * M[(size_t)q * n + r];
-    sr[q] = 4ull * M[(size_t)q * n + r];  // answers go back the way keys came
-    rr[q] = 4ull * M[(size_t)r * n + q];
-  }
-  VP_TRY(grow_dev(&w.sendk, &w.sendk_n, S, c->stream));
-  VP_TRY(grow_dev(&w.rreply, &w.rreply_n, S, c->stream));
-  VP_TRY(grow_dev(&w.recvk, &w.recvk_n, R, c->stream));
-  VP_TRY(grow_dev(&w.reply, &w.reply_n, R, c->stream));
-  a.own.rreply = w.rreply;
-  route_pack<<<ph->grid1, 256, 0, c->stream>>>(w.desc, w.dcnt, w.dbase, n, ph->range1,
+  route_pad<<<grid_for(slices), 256, 0, c->stream>>>(w.dbase, w.dtot, ph->grid1, n, C,
+                                                     w.ovf64);
+  route_pack<<<ph->grid1, 256, 0, c->stream>>>(w.desc, w.dcnt, w.dbase, n, ph->range1, C,
                                                w.sendk);
   VP_HIP(hipGetLastError());
+  std::vector<size_t> s4(n, 4), sk(n, 16ull * C), sr(n, 4ull * C);
+  VP_TRY(m.alltoallv_dev(c, w.dtot, s4.data(), w.rcnt, s4.data()));
+  VP_TRY(m.allreduce_max_u64_dev(c, w.ovf64, 1));
   pm.mark();
-  VP_TRY(m.alltoallv_dev(c, w.sendk, sk.data(), w.recvk, rk.data()));
+  VP_TRY(m.alltoallv_dev(c, w.sendk, sk.data(), w.recvk, sk.data()));
   pm.mark();
-  if (R) {
-    nat_own_probe<<<grid_for(R, 256, 4096), 256, 0, c->stream>>>(
-        tbl_dev(t), c->crc_tab, w.recvk, (uint32_t)R, w.reply);
-    VP_HIP(hipGetLastError());
-  }
+  nat_own_probe<<<grid_for((uint64_t)n * C, 256, 4096), 256, 0, c->stream>>>(
+      tbl_dev(t), c->crc_tab, w.recvk, n * C, C, w.rcnt, w.ovf64, t.ctl, w.reply);
+  VP_HIP(hipGetLastError());
   pm.mark();
-  VP_TRY(m.alltoallv_dev(c, w.reply, sr.data(), w.rreply, rr.data()));
+  VP_TRY(m.alltoallv_dev(c, w.reply, sr.data(), w.rreply, sr.data()));
   pm.mark();
-  VP_HIP(hipEventRecord(c->ev2, c->stream));
-  if (np) {
+  auto pass2 = [&]() -> int {
+    if (!np) return 0;
     if (ph->tiles64) {
       NatArgs a2 = a;
       uint32_t grid2 = ph->bp.grid;
@@ -1409,16 +1444,65 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
       nat_remote_lane<<<grid_for(np), 256, 0, c->stream>>>(a);
     }
     VP_HIP(hipGetLastError());
-  }
+    return 0;
+  };
+  VP_HIP(hipEventRecord(c->ev2, c->stream));
+  VP_TRY(pass2());
   VP_HIP(hipEventRecord(c->ev3, c->stream));
   pm.mark();
-  VP_TRY(tbl_fold_read_ctl(c, t, ph->bp, w.log, p0, p1, now, seq0));
+  VP_TRY(tbl_fold_read_ctl(c, t, ph->bp, w.log, p0, p1, now, seq0, w.dtot));
   pm.mark();
   pm.print(m.r, np);
+  uint32_t maxsend = 0;  // for the next batch's capacity (run_batch_sharded)
+  for (uint32_t o = 0; o < n; o++)
+    if (o != r) maxsend = std::max(maxsend, w.h_gath[kPubGath * n + o]);
+  c->own_maxsend = maxsend;
   float k1 = 0.f, k2 = 0.f;
   VP_HIP(event_ms(c->ev0, c->ev1, &k1));
   VP_HIP(event_ms(c->ev2, c->ev3, &k2));
   ph->ms = k1 + k2;
+  if (!t.h_ctl.route_ovf) return 0;
+  // Some rank had more keys for an owner than C (every rank sees the flag):
+  // pass 2 answered none of the routed packets; the exact exchange does,
+  // with the sizes learned on the host, then the fold again (pass 1's own
+  // touches fold twice, to the same stamps).
+  route_scan<<<n, 256, 0, c->stream>>>(w.dcnt, ph->grid1, n, w.dbase, w.dtot);
+  route_base<<<grid_for(slices), 256, 0, c->stream>>>(w.dbase, w.dtot, ph->grid1, n);
+  VP_HIP(hipGetLastError());
+  VP_HIP(hipMemcpyAsync(w.h_tot, w.dtot, 4ull * n, hipMemcpyDeviceToHost, c->stream));
+  VP_HIP(stream_wait(c->stream));
+  std::vector<uint32_t> M((size_t)n * n);  // M[q * n + o] = keys rank q sends to owner o
+  VP_TRY(m.allgather_host(c, w.h_tot, M.data(), 4ull * n));
+  uint64_t S = 0, R = 0;
+  std::vector<size_t> ek(n), er(n), fr(n), fa(n);
+  for (uint32_t q = 0; q < n; q++) {
+    S += M[(size_t)r * n + q];
+    R += M[(size_t)q * n + r];
+    ek[q] = 16ull * M[(size_t)r * n + q];
+    er[q] = 16ull * M[(size_t)q * n + r];
+    fr[q] = 4ull * M[(size_t)q * n + r];  // answers go back the way keys came
+    fa[q] = 4ull * M[(size_t)r * n + q];
+  }
+  VP_TRY(grow_dev(&w.sendk, &w.sendk_n, S, c->stream));
+  VP_TRY(grow_dev(&w.rreply, &w.rreply_n, S, c->stream));
+  VP_TRY(grow_dev(&w.recvk, &w.recvk_n, R, c->stream));
+  VP_TRY(grow_dev(&w.reply, &w.reply_n, R, c->stream));
+  a.own.rreply = w.rreply;
+  a.own.cap = 0;
+  route_pack<<<ph->grid1, 256, 0, c->stream>>>(w.desc, w.dcnt, w.dbase, n, ph->range1, 0,
+                                               w.sendk);
+  VP_HIP(hipGetLastError());
+  VP_TRY(m.alltoallv_dev(c, w.sendk, ek.data(), w.recvk, er.data()));
+  nat_own_probe<<<grid_for(std::max<uint64_t>(R, 1), 256, 4096), 256, 0, c->stream>>>(
+      tbl_dev(t), c->crc_tab, w.recvk, (uint32_t)R, 0, nullptr, nullptr, t.ctl, w.reply);
+  VP_HIP(hipGetLastError());
+  VP_TRY(m.alltoallv_dev(c, w.reply, fr.data(), w.rreply, fa.data()));
+  VP_HIP(hipEventRecord(c->ev2, c->stream));
+  VP_TRY(pass2());
+  VP_HIP(hipEventRecord(c->ev3, c->stream));
+  VP_TRY(tbl_fold_read_ctl(c, t, ph->bp, w.log, p0, p1, now, seq0, w.dtot));
+  VP_HIP(event_ms(c->ev2, c->ev3, &k2));
+  ph->ms += k2;
   return 0;
 }
 

@@ -62,6 +62,8 @@ struct PubArgs {
   CtlPub *pub;
   const Ctl *ctl;
   uint32_t epoch;
+  const uint32_t *x0, *x1;  // extra words (CtlPub::xtra): x0[0..n0), then x1[0..n1)
+  uint32_t n0, n1;
 };
 static_assert(sizeof(Ctl) % 8 == 0, "Ctl is published as 8-byte words");
 __device__ __forceinline__ void ctl_publish(const PubArgs &a) {
@@ -76,6 +78,12 @@ __device__ __forceinline__ void ctl_publish(const PubArgs &a) {
 #pragma unroll
   for (uint32_t i = 0; i < kW; i++)
     __hip_atomic_store(d + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (uint32_t i = 0; i < a.n0 + a.n1; i++) {
+    const uint32_t *s1 = i < a.n0 ? a.x0 + i : a.x1 + (i - a.n0);
+    __hip_atomic_store(&a.pub->xtra[i],
+                       __hip_atomic_load(s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   __hip_atomic_store(&a.pub->epoch, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -245,8 +253,11 @@ int tbl_late_touches(vp_ctx *c, FlowTable &t, const uint32_t *list,
 // instead (t.ctl->touch_ovf set; apply plan.bins.oent with tbl_late_touches).
 int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
                     const NowSpec &now, uint64_t seq_base);
+// Multi-GPU: also gathers the ranks' segment counters (Workspace::h_gath;
+// owner mode: + this rank's `sends`, its key count per owner).
 int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_t *log,
-                      uint32_t p0, uint32_t p1, const NowSpec &now, uint64_t seq_base);
+                      uint32_t p0, uint32_t p1, const NowSpec &now, uint64_t seq_base,
+                      const uint32_t *sends = nullptr);
 
 // Exact min ts over allocated indices -> t.ts_floor (~0 if none).
 int tbl_exact_floor(vp_ctx *c, FlowTable &t);

@@ -6,6 +6,8 @@
 //   dchain expire            double-chain.c:772-826 (strict ts < cutoff)
 //   expire_items_single_map  expirator.c:110-218
 #include <hip/hip_runtime.h>
+
+#include <cstddef>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -940,15 +942,42 @@ int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
 // the classify and the fold; the host polls for it while the fold runs.
 // Without bins: a copy behind phase A, then the log fold. On return h_ctl
 // holds phase A's counts; the fold may still be running.
+// Multi-GPU (every rank, every segment, so the collective always matches):
+// the ranks' segment counters (miss .. reprobe, kPubGath words) are gathered
+// on the device before the fold, which publishes them with the control
+// block, and owner mode adds this rank's key count per owner (`sends`): the
+// host learns all of it with the one wait it makes anyway (union_sizes,
+// DESIGN.md §6).
 int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_t *log,
-                      uint32_t p0, uint32_t p1, const NowSpec &now, uint64_t seq_base) {
+                      uint32_t p0, uint32_t p1, const NowSpec &now, uint64_t seq_base,
+                      const uint32_t *sends) {
+  Workspace &w = c->ws;
+  const uint32_t nr = c->comm ? (uint32_t)c->comm->n : 0u;
+  const uint32_t ns = sends ? nr : 0u;
+  w.gath_ok = false;
+  if (nr) {
+    if (!w.gath) VP_TRY(dalloc(&w.gath, (size_t)kPubGath * kMaxRanks));
+    static_assert(offsetof(Ctl, reprobe_count) - offsetof(Ctl, miss_count) ==
+                      4 * (kPubGath - 1), "miss_count .. reprobe_count contiguous");
+    VP_TRY(c->comm->allgather_dev(c, &t.ctl->miss_count, w.gath, 4 * kPubGath));
+  }
   if (!bp.on) {
     VP_TRY(read_ctl_post(c, t));
     VP_TRY(tbl_touch_reduce(c, t, log, p0, p1, now, seq_base));
-    return read_ctl_wait(c, t);
+    VP_TRY(read_ctl_wait(c, t));
+    if (nr) {
+      std::vector<uint32_t> x((size_t)kPubGath * nr + ns);
+      VP_HIP(hipMemcpy(x.data(), w.gath, 4ull * kPubGath * nr, hipMemcpyDeviceToHost));
+      if (ns) VP_HIP(hipMemcpy(x.data() + kPubGath * nr, sends, 4ull * ns,
+                               hipMemcpyDeviceToHost));
+      w.h_gath.swap(x);
+      w.gath_ok = true;
+    }
+    return 0;
   }
   const uint32_t epoch = ++t.pub_epoch;
-  VP_TRY(bins_reduce(c, t, bp, p0, now, seq_base, PubArgs{t.d_pub, t.ctl, epoch}));
+  VP_TRY(bins_reduce(c, t, bp, p0, now, seq_base,
+                     PubArgs{t.d_pub, t.ctl, epoch, w.gath, sends, kPubGath * nr, ns}));
   hostprof(3);
   // poll the epoch; a stream that ends (or fails) without it is an error
   for (uint32_t spin = 1;; spin++) {
@@ -962,6 +991,10 @@ int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_
     }
   }
   memcpy(&t.h_ctl, (const void *)&t.h_pub->ctl, sizeof(Ctl));
+  if (nr) {
+    w.h_gath.assign(t.h_pub->xtra, t.h_pub->xtra + kPubGath * nr + ns);
+    w.gath_ok = true;
+  }
   return 0;
 }
 
@@ -1341,6 +1374,7 @@ int sync_tables(vp_ctx *c) {
 struct RankInfo {
   int64_t bad, n, t_first, t_last;
   uint64_t floor[2];
+  uint64_t maxsend;  // owner mode: this rank's largest per-owner key count last seen
 };
 
 // New keys of a segment, exchanged so that every rank allocates the same
@@ -1355,10 +1389,23 @@ struct RankSlices {
   uint32_t cnt[kMaxRanks], pre[kMaxRanks];
 };
 
+// The segment's new-key count of every rank. Taken from the counters the
+// fold published (tbl_fold_read_ctl) unless some rank ran reprobes after it
+// (they may find new keys): all ranks see the same gathered words, so they
+// agree on which way to go.
 int union_sizes(vp_ctx *c, uint32_t nl, uint32_t *total, uint32_t *mine_off) {
   Comm &m = *c->comm;
+  Workspace &w = c->ws;
   c->rank_cnt.assign(m.n, 0);
-  VP_TRY(m.allgather_host(c, &nl, c->rank_cnt.data(), sizeof nl));
+  bool pub = w.gath_ok;
+  for (int r = 0; pub && r < m.n; r++) pub = w.h_gath[kPubGath * r + 3] == 0;  // reprobes
+  if (pub) {
+    for (int r = 0; r < m.n; r++) c->rank_cnt[r] = w.h_gath[kPubGath * r];
+    if (c->rank_cnt[m.r] != nl) return state_fail("published miss count %u != %u",
+                                                  c->rank_cnt[m.r], nl);
+  } else {
+    VP_TRY(m.allgather_host(c, &nl, c->rank_cnt.data(), sizeof nl));
+  }
   uint32_t t = 0;
   *mine_off = 0;
   for (int r = 0; r < m.n; r++) {
@@ -1481,8 +1528,22 @@ static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
     }
   }
   for (int i = 0; i < ntabs; i++) me.floor[i] = tabs[i].t->ts_floor;
+  me.maxsend = c->own_maxsend;
   std::vector<RankInfo> all(m.n);
   VP_TRY(m.allgather_host(c, &me, all.data(), sizeof me));
+  {  // owner mode: the padded exchange's keys per peer for this batch, the
+     // same on every rank: the largest per-owner count any
+     // rank last sent (its whole slice before it knows) + 1/8 + 256, at most
+     // the largest slice; a segment that exceeds it takes the exact exchange
+    uint64_t maxs = 0, maxn = 0;
+    for (int r = 0; r < m.n; r++) {
+      maxn = std::max<uint64_t>(maxn, (uint64_t)all[r].n);
+      maxs = std::max<uint64_t>(maxs, all[r].maxsend ? all[r].maxsend : (uint64_t)all[r].n);
+    }
+    uint64_t C = (maxs + maxs / 8 + 256 + 255) & ~255ull;
+    if (const char *e = getenv("VIGPATH_OWN_CAP")) C = strtoull(e, nullptr, 10);  // tests
+    c->own_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(C, 1), std::max<uint64_t>(maxn, 1));
+  }
   int bad = 0;
   uint64_t G = 0;
   uint32_t off = 0;
