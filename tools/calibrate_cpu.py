@@ -5,6 +5,9 @@ reference's own libVig (oracle/_ref/liborc_ref.so, this container only) on
 identical traces, one pinned core, median of several samples.
 
   python3 tools/calibrate_cpu.py [flows] [packets_per_sample] [samples]
+
+Reports each implementation's median Mpps, the ratio of medians, and the
+paired per-round ratio (median and a 90 % bootstrap interval).
 """
 import json
 import os
@@ -62,8 +65,17 @@ def main():
         res[name] = {"median_mpps": round(float(np.median(r)), 3),
                      "samples": [round(x, 3) for x in r]}
     base = res["reference_libvig"]["median_mpps"]
+    ref_s = np.array(res["reference_libvig"]["samples"])
     for k in ("restated", "restated_native"):
         res[k]["ratio_to_reference"] = round(res[k]["median_mpps"] / base, 3)
+        # paired: each interleaved round's ratio (host-speed drift cancels),
+        # median with a 90 % bootstrap interval of the median
+        pr = np.array(res[k]["samples"]) / ref_s
+        rng = np.random.default_rng(0)
+        boot = np.median(rng.choice(pr, (4000, pr.size)), axis=1)
+        res[k]["paired_ratio_median"] = round(float(np.median(pr)), 3)
+        res[k]["paired_ratio_90ci"] = [round(float(np.percentile(boot, 5)), 3),
+                                       round(float(np.percentile(boot, 95)), 3)]
     res["trace"] = ("vignat 64B, %d flows warm, round robin, %d interleaved "
                     "samples of %d steady-state packets, 1 pinned core (%s)"
                     % (flows, samples, per, bench.cpu_model()))

@@ -817,7 +817,10 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
     uint32_t pbits, uint32_t bbits, uint32_t range, uint32_t L, uint32_t tcap,
     uint32_t p0, NowSpec now, uint64_t seq_base, uint64_t *ts, uint64_t *tseq,
     PubArgs pub) {
-  __shared__ uint32_t last[kBinLocalMax];  // 1 + position in the launch, 0 = none
+  // 1 + position in the launch, 0 = none; L words of dynamic LDS (16 KB at
+  // 1M flows: the 256 bin blocks spread over all CUs, where a 64 KB static
+  // array let only two blocks share a CU and left half of them idle)
+  extern __shared__ uint32_t last[];
   const uint32_t bin = blockIdx.x;
   if (bin == 0 && threadIdx.x == 0) ctl_publish(pub);
   for (uint32_t i = threadIdx.x; i < L; i += blockDim.x) last[i] = 0;
@@ -922,7 +925,7 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
 
 static int bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
                        const NowSpec &now, uint64_t seq_base, PubArgs pub) {
-  touch_bins_reduce<<<1u << plan.bins.bbits, 1024, 0, c->stream>>>(
+  touch_bins_reduce<<<1u << plan.bins.bbits, 1024, 4u * plan.L, c->stream>>>(
       plan.bins.ent, plan.bins.cnt, plan.grid, plan.bins.cap, plan.bins.pbits,
       plan.bins.bbits, plan.range, plan.L, t.cap, p0, now, seq_base, t.ts, t.tseq,
       pub);
