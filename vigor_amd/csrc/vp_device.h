@@ -671,7 +671,7 @@ struct TailRound {
       const uint32_t o = 64 + 16 * (ii * G + gl);
       const uint32_t e = (uint32_t)__shfl((int)end, (int)fr);
       off[u] = fr * slot + o;
-      rem[u] = (k0 + u < K) & (o < e) ? e - o : 0u;
+      rem[u] = ((k0 + u < K) & (o < e)) ? e - o : 0u;
       if (++ii == n_it) {
         ii = 0;
         qq++;

@@ -242,6 +242,8 @@ struct vp_ctx {
   int64_t *pol_time = nullptr;   //                  bucket_time by index
   uint32_t *pol_cnt = nullptr;   // hits per index in a segment (grouping)
   uint32_t *pol_off = nullptr;   // exclusive scan of pol_cnt
+  uint32_t *pol_runs = nullptr;  // [index][kRunMax] hit positions (grouping;
+                                 // tables up to 4M indices, else pol_off)
   uint4 *be_rec = nullptr;  // viglb backends[]: {ip, mac0-3, mac4-5|nic<<16, 0}
   uint32_t *cht = nullptr;  // viglb CHT, cht[bucket * backend_capacity + prio]
   uint32_t *dmacw = nullptr;  // per device: {s_addr[0..1] << 16, s_addr[2..5]}

@@ -67,6 +67,8 @@ struct PolArgs {
   uint64_t burst, rate, thr;  // thr = burst * 1e9 / rate (u64, as the reference)
   uint32_t *cnt;     // hits per index in this segment (phase A)
   uint32_t *rnk;     // a hit's rank in its index's run (arbitrary order)
+  uint32_t *runs;    // or (non-null) the hit's position straight into its
+                     // index's run slots: runs[index * kRunMax + rank]
   uint32_t *maxrun;  // longest run (ctl->aux_count)
   uint16_t lan, wan;
 };
@@ -127,7 +129,11 @@ __global__ __launch_bounds__(256) void pol_classify(PolArgs a) {
       a.pidx[p] = idx;
       if (a.cnt) {  // grouping path: this hit's rank in its index's run
         const uint32_t r = atomicAdd(&a.cnt[idx], 1u);
-        a.rnk[p] = r;
+        if (a.runs) {
+          if (r < kRunMax) a.runs[(size_t)idx * kRunMax + r] = p;
+        } else {
+          a.rnk[p] = r;
+        }
         lmax = max(lmax, r + 1);
       }
     } else if (len <= a.burst) {
@@ -136,6 +142,77 @@ __global__ __launch_bounds__(256) void pol_classify(PolArgs a) {
       a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
     }
   }
+  for (int o = 32; o > 0; o >>= 1) lmax = max(lmax, (uint32_t)__shfl_xor((int)lmax, o));
+  if (__lane_id() == 0 && lmax) atomicMax(a.maxrun, lmax);
+}
+
+// Phase A for 64-byte slots (frames64_tiles, vp_device.h): every frame load
+// moves 1 KiB contiguous through the wave's LDS tile, the home buckets come
+// in by cooperative 64-byte row gathers, and the CRC and layout tables sit in
+// LDS; frames are never written back. A bucket full of other keys finishes
+// its probe walk in the lane (tbl_probe_from: rare, load <= 1/3).
+struct PolPend {
+  uint32_t row;  // home bucket (gathered by frames64_tiles) or kNone
+  uint32_t dst;  // the policed destination address (row != kNone)
+};
+__global__ __launch_bounds__(256, 4) void pol_classify64(PolArgs a, uint32_t n_all) {
+  __shared__ uint32_t T[kPolTabs * 256 + 1024];
+  __shared__ uint4 stage[4][256];
+  __shared__ uint32_t cur[kCurs];
+  for (uint32_t i = threadIdx.x; i < kPolTabs * 256; i += blockDim.x) T[i] = a.crc_tab[i];
+  if (a.t.mix == kMixLin)
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) T[kPolTabs * 256 + i] = a.t.lin[i];
+  for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
+  __syncthreads();
+  const uint32_t *lin = T + kPolTabs * 256;
+  uint32_t lmax = 0;
+  frames64_tiles(
+      const_cast<uint8_t *>(a.frames), a.len, a.in_dev, a.p0, a.p1, n_all,
+      stage[threadIdx.x >> 6], reinterpret_cast<const uint4 *>(a.t.bk),
+      [&](uint32_t p, const RFrame &f, uint32_t in, uint32_t len, bool mine) {
+        PolPend P{kNone, 0};
+        if (!mine) return P;
+        // nf_then_get_rte_ipv4_header (nf-util.h:122-151), as pol_ipv4_w
+        const uint16_t unread = (uint16_t)(len - 14);
+        const uint32_t ihl = (f.w[3] >> 16) & 0x0F;
+        const uint16_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
+        const bool v4 = ((f.w[3] & 0xFFFF) == 0x0008) & (unread >= 20) & (ihl >= 5) &
+                        (unread >= tl);
+        if (!v4 || in != a.wan) {  // dropped / outgoing / unknown port
+          a.pidx[p] = kNone;
+          a.out[p] = (uint16_t)(v4 && in == a.lan ? a.wan : in);
+          return P;
+        }
+        P.dst = f.u32at2(30);
+        P.row = home_bucket(pol_hash(T, P.dst), a.t.bmask, a.t.mix, lin);
+        return P;
+      },
+      [&](const PolPend &P, const uint4 *row, uint32_t p, RFrame &, uint32_t,
+          uint32_t len, uint32_t &) -> uint32_t {
+        if (P.row == kNone) return 0u;
+        const uint32_t key[4] = {P.dst, 0, 0, 0};
+        bool done;
+        uint32_t idx = bucket_match(row[0], row[1], row[2], row[3], key, &done);
+        if (!done) idx = tbl_probe_from(a.t, (P.row + 1) & a.t.bmask, key, a.t.bmask);
+        a.pidx[p] = idx;
+        if (idx != kNone) {
+          if (a.cnt) {  // grouping path: this hit's rank in its index's run
+            const uint32_t r = atomicAdd(&a.cnt[idx], 1u);
+            if (a.runs) {
+              if (r < kRunMax) a.runs[(size_t)idx * kRunMax + r] = p;
+            } else {
+              a.rnk[p] = r;
+            }
+            lmax = max(lmax, r + 1);
+          }
+        } else if (len <= a.burst) {
+          a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
+        } else {
+          a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
+        }
+        return 0u;  // (the policer never writes frames)
+      },
+      TouchBins{}, TileQueue{}, cur);
   for (int o = 32; o > 0; o >>= 1) lmax = max(lmax, (uint32_t)__shfl_xor((int)lmax, o));
   if (__lane_id() == 0 && lmax) atomicMax(a.maxrun, lmax);
 }
@@ -284,7 +361,9 @@ __global__ void pol_scatter(const uint32_t *pidx, const uint32_t *rnk, uint32_t 
 }
 
 // One lane per index with hits: its run (<= kRunMax positions) put back in
-// packet order by an insertion sort, then replayed.
+// packet order by an insertion sort, then replayed. The run is at
+// grouped + off[k] (scan + scatter) or, off == null, at the index's own
+// kRunMax slots that phase A filled.
 __global__ void pol_runs(PolArgs a, const uint32_t *cnt, const uint32_t *off,
                          const uint32_t *grouped, uint32_t cap, NowSpec now,
                          uint64_t *bsize, int64_t *btime) {
@@ -294,7 +373,7 @@ __global__ void pol_runs(PolArgs a, const uint32_t *cnt, const uint32_t *off,
     const uint32_t c = cnt[k];
     if (c == 0) continue;
     uint32_t q[kRunMax];
-    const uint32_t *g = grouped + off[k];
+    const uint32_t *g = off ? grouped + off[k] : grouped + (size_t)k * kRunMax;
     for (uint32_t j = 0; j < c; j++) {
       const uint32_t v = g[j];
       uint32_t i = j;
@@ -372,15 +451,27 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // nf_process calls, churn cut into many segments) take the sorting path.
   const bool grouping = (uint64_t)n * 8 >= t.cap;
   a.cnt = grouping ? c->pol_cnt : nullptr;
+  a.runs = grouping ? c->pol_runs : nullptr;
 
   VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
   VP_HIP(hipMemsetAsync(a.maxrun, 0, 4, c->stream));
   if (grouping) VP_HIP(hipMemsetAsync(c->pol_cnt, 0, 4ull * t.cap, c->stream));
   VP_HIP(hipEventRecord(c->ev0, c->stream));
-  pol_classify<<<grid_for(n), 256, 0, c->stream>>>(a);
+  if (b->slot == 64 && c->coalesced_io) {
+    const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
+    pol_classify64<<<resident_grid((const void *)pol_classify64, (tiles + 3) / 4), 256, 0,
+                     c->stream>>>(a, b->n);
+  } else {
+    pol_classify<<<grid_for(n), 256, 0, c->stream>>>(a);
+  }
   VP_HIP(hipGetLastError());
   VP_HIP(hipEventRecord(c->ev1, c->stream));
-  if (grouping) {  // phase T, grouping path (speculative: no-ops unless pol_grouping_ok)
+  if (grouping && c->pol_runs) {  // phase T, grouping path with per-index
+    // run slots (phase A wrote them): no scan, no scatter
+    pol_runs<<<grid_for(t.cap), 256, 0, c->stream>>>(a, c->pol_cnt, nullptr, c->pol_runs,
+                                                     t.cap, now, c->pol_size, c->pol_time);
+    VP_HIP(hipGetLastError());
+  } else if (grouping) {  // phase T, grouping path (speculative: no-ops unless pol_grouping_ok)
     size_t need = 0;
     hipcub::DeviceScan::ExclusiveSum(nullptr, need, c->pol_cnt, c->pol_off,
                                      (int)t.cap, c->stream);

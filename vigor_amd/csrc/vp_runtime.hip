@@ -180,7 +180,7 @@ static void free_all(vp_ctx *c) {
                   w.d_out,   w.d_now,    c->crc_tab, c->macw,
                   c->st_bk,  c->st_val,  c->be_rec,   c->cht,   c->dmacw,
                   w.sbuf,    w.rbuf,     c->pol_size, c->pol_time,
-                  c->pol_cnt, c->pol_off, w.desc, w.dcnt, w.dbase, w.dtot,
+                  c->pol_cnt, c->pol_off, c->pol_runs, w.desc, w.dcnt, w.dbase, w.dtot,
                   w.route,   w.sendk,    w.recvk,  w.reply,  w.rreply};
   for (void *p : ptrs) hipFree(p);
   if (w.h_tot) hipHostFree(w.h_tot);
@@ -310,6 +310,8 @@ static int pol_init(vp_ctx *c, const vp_pol_config *cfg) {
   VP_HIP(hipMemset(c->pol_time, 0, 8ull * cfg->dyn_capacity));
   VP_TRY(dalloc(&c->pol_cnt, cfg->dyn_capacity));
   VP_TRY(dalloc(&c->pol_off, cfg->dyn_capacity));
+  if (cfg->dyn_capacity <= (1u << 22))  // 64 hit slots per index (1 GiB at 4M)
+    VP_TRY(dalloc(&c->pol_runs, 64ull * cfg->dyn_capacity));
   return 0;
 }
 
