@@ -13,14 +13,15 @@ rate is reported as new_flow_mpps).
 
 N > 1 (torch.distributed, one rank per GPU; BASELINE configs[4]): ONE vignat
 over all GPUs with 16M flows; every global batch is N x B packets and rank r
-ingests its contiguous slice r (B packets, weak scaling). By default every
-GPU holds the whole flow dictionary (--shard-mode replicated): steady-state
-packets need no data-path collective, only small all-gathers per batch, and
-new flows are all-gathered so every rank allocates identically.
---shard-mode owner shards the dictionary by flow hash (north_star): LAN
-packets whose key another GPU owns are looked up there through an RCCL
-all-to-all of 16-byte keys and 4-byte answers over xGMI, at the price of a
-second pass over the frames (DESIGN.md §6.1 measures both). Results equal
+ingests its contiguous slice r (B packets, weak scaling). By default
+(--shard-mode owner, north_star's design, the headline value) the
+dictionary is sharded by flow hash: LAN packets whose key another GPU owns
+are looked up there through an RCCL all-to-all of 16-byte keys and 4-byte
+answers over xGMI. --shard-mode replicated keeps the whole dictionary on
+every GPU: steady-state packets need no data-path collective, only small
+all-gathers per batch. The other placement is measured in the same run
+(extra key other_shard_mode). In both, new flows are
+all-gathered so every rank allocates identically. Results equal
 one nf.c over the concatenated batch in both modes (DESIGN.md §6,
 tests/test_shard_gpu.py). value = all ranks' packets / max-over-ranks time.
 `--gpus N` without a torch.distributed environment starts the N ranks
