@@ -79,6 +79,9 @@ def bench_bridge(args, dev, flood):
     warm_s = time.perf_counter() - t0
     base = len(warm) * B
     batches = [to_dev(gen(base + k * B), dev) for k in range(args.steps)]
+    if os.environ.get("BENCH_NF_SAME"):  # diagnostics: one batch's frames every step
+        fr0 = batches[0]
+        batches = [(fr0[0], fr0[1], fr0[2], fr0[3] + k * B) for k in range(args.steps)]
     mpps, kmpps, out = run(br, batches, B, dev)
     ocfg = orc.BridgeCfg(expiration_time=60_000_000, dyn_capacity=N, n_devices=2)
     cpu = None

@@ -540,6 +540,32 @@ int main(int argc, char **argv) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_out), &o, sizeof(o)));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_log), &lg, sizeof(lg)));
   }
+  if (argc > 1 && argv[1][0] == 'r') {  // uniformly random rows (SURVEY §8(d) uniform order)
+    // slot word 1 = splitmix64(slot) (bits unrelated between neighbours), the
+    // row index the kRow64 / kSide shapes fetch: the memory shape of vignat
+    // under uniform packet order, one random 64-byte row of a 32 MB table per
+    // slot, against the stride-spread index of the default runs
+    for (int rep = 0; rep < 2; rep++) {
+      for (int mode = 0; mode < 2; mode++) {
+        uint32_t *h = (uint32_t *)malloc(bytes);
+        for (size_t i = 0; i < bytes / 4; i++) {
+          uint64_t z = (i >> 4) + (mode ? 0x9E3779B97F4A7C15ull : 0);
+          if (mode) {
+            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+            z ^= z >> 31;
+          }
+          h[i] = mode ? (uint32_t)z : (uint32_t)(i * 2654435761u);
+        }
+        CK(hipMemcpy(buf, h, bytes, hipMemcpyHostToDevice));
+        free(h);
+        printf("row index: %s\n", mode ? "splitmix64 (uniform)" : "stride spread (default)");
+        run<kRow64, 1, 4>("rmw64+row", buf, dst, table, rmask, tiles, sink, cus);
+        run<kSide, 1, 4>("row+side", buf, dst, table, rmask, tiles, sink, cus);
+      }
+    }
+    return 0;
+  }
   if (argc > 1 && argv[1][0] == 'g') {  // one tile per wave + per-block costs
     uint32_t *tb, *cu, *en;
     CK(hipMalloc(&tb, 15 * 256 * 4));

@@ -402,7 +402,9 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
                                                const TouchBins &bins,
                                                const TileQueue &rq,
                                                uint32_t *cur) {
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // (the wave index as a scalar: the tile stores' buffer resources are
+  // provably uniform, no waterfall loops)
+  const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t first = p0 & ~63u;
   const uint32_t tiles = (p1 - first + 63) / 64;
   uint4 r[4];

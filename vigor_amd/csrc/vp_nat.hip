@@ -574,10 +574,11 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   uint4 *S = stage[threadIdx.x >> 6];
   const uint4 *rows = reinterpret_cast<const uint4 *>(a.t.bk);
   const uint32_t lane = threadIdx.x & 63;
-  // wide slots: the wave index as a scalar, so tile addresses (the buffer
-  // resources of tile_tail_sums and the header gathers) are provably uniform
-  // and need no waterfall loop (cdna_hip_programming.md T20)
-  const uint32_t wv = G ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : threadIdx.x >> 6;
+  // the wave index as a scalar, so tile addresses (the buffer resources of the
+  // tile stores, tile_tail_sums and the header gathers) are provably uniform
+  // and need no waterfall loop (cdna_hip_programming.md T20; as a vector
+  // value every 64-byte tile store ran a readfirstlane loop)
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t first = a.p0 & ~63u;
   const uint32_t tiles = (a.p1 - first + 63) / 64;
   const bool lean_ok = a.own.n == 0 && rq.ent != nullptr;

@@ -234,7 +234,7 @@ struct BinsPlan {
   TouchBins bins;
 };
 int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
-                  uint32_t p1, BinsPlan *plan);
+                  uint32_t p1, BinsPlan *plan, uint32_t waves = 4);
 // ts of the indices the reprobe kernels touched (after their tseq atomicMax;
 // the queue as in reprobe_slices, vp_device.h).
 int tbl_reprobe_stamp(vp_ctx *c, FlowTable &t, const uint32_t *list,
@@ -324,7 +324,7 @@ uint32_t grid_for(uint64_t n, uint32_t block = 256, uint32_t max_blocks = 2048);
 // VIGPATH_BLOCKS_PER_CU overrides the per-CU count), at most work_blocks. A
 // larger grid leaves the blocks that do not fit to run after the first wave
 // of blocks, as a tail at lower occupancy.
-uint32_t resident_grid(const void *kernel, uint64_t work_blocks);
+uint32_t resident_grid(const void *kernel, uint64_t work_blocks, int threads = 256);
 uint32_t next_pow2(uint64_t v);
 int cub_reserve(vp_ctx *c, size_t bytes);
 

@@ -28,7 +28,7 @@ uint32_t grid_for(uint64_t n, uint32_t block, uint32_t max_blocks) {
   return (uint32_t)(g < max_blocks ? g : max_blocks);
 }
 
-uint32_t resident_grid(const void *kernel, uint64_t work_blocks) {
+uint32_t resident_grid(const void *kernel, uint64_t work_blocks, int threads) {
   struct Entry {
     const void *kernel;
     int dev;
@@ -47,7 +47,7 @@ uint32_t resident_grid(const void *kernel, uint64_t work_blocks) {
       int c = 0, p = 0;
       if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) !=
               hipSuccess ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&p, kernel, 256, 0) !=
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&p, kernel, threads, 0) !=
               hipSuccess)
         (void)hipGetLastError();
       cus = (uint32_t)std::max(c, 1);
@@ -873,13 +873,13 @@ static uint32_t ceil_log2(uint64_t v) {
 }
 
 int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
-                  uint32_t p1, BinsPlan *plan) {
+                  uint32_t p1, BinsPlan *plan, uint32_t waves) {
   Workspace &w = c->ws;
   *plan = BinsPlan{};
   const char *env = getenv("VIGPATH_TOUCH_BINS");  // diagnostics: 0 = off
   if ((env && !atoi(env)) || (p0 & 63) || p1 <= p0) return 0;
   const uint32_t tiles = (p1 - p0 + 63) / 64;
-  const uint32_t grid = resident_grid(kernel, (tiles + 3) / 4);
+  const uint32_t grid = resident_grid(kernel, (tiles + waves - 1) / waves, 64 * (int)waves);
   const uint32_t per_b = (tiles + grid - 1) / grid;
   const uint32_t range = per_b * 64;
   // the fewest bins (>= 256) whose in-bin index range fits the fold's LDS
