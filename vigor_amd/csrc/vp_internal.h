@@ -241,8 +241,9 @@ struct vp_ctx {
   uint64_t *pol_size = nullptr;  // vigpol dyn_vals: bucket_size by index
   int64_t *pol_time = nullptr;   //                  bucket_time by index
   uint32_t *pol_cnt = nullptr;   // hits per index in a segment (grouping)
+  bool pol_cnt_clean = false;     // pol_cnt is all zero (the replay cleared it)
   uint32_t *pol_off = nullptr;   // exclusive scan of pol_cnt
-  uint32_t *pol_runs = nullptr;  // [index][kRunMax] hit positions (grouping;
+  uint32_t *pol_runs = nullptr;  // [kRunMax][index] hit positions (grouping;
                                  // tables up to 4M indices, else pol_off)
   uint4 *be_rec = nullptr;  // viglb backends[]: {ip, mac0-3, mac4-5|nic<<16, 0}
   uint32_t *cht = nullptr;  // viglb CHT, cht[bucket * backend_capacity + prio]

@@ -40,6 +40,7 @@
 // the LoadBalancedFlow (lb_flow.h:6-12), the upper 24 bits carry
 // flow_id_to_backend_id, so a hit resolves in one bucket read.
 #include <hip/hip_runtime.h>
+#include <cstddef>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -55,7 +56,8 @@ namespace vp {
 static const int kLbFlowPos[13] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 13, 16};
 constexpr int kLbFlowMsg = 20;
 // ip_addr hash: one CRC step over the u32 address.
-constexpr int kLbTabs = 13 + 4;
+constexpr uint32_t kLbFlowTabs = 13;  // LoadBalancedFlow's CRC byte positions
+constexpr int kLbTabs = 13 + 4;        // + ip_addr's four
 
 __device__ __forceinline__ uint32_t lbflow_hash(const uint32_t *T, uint32_t sip,
                                                 uint32_t dip, uint32_t sp,
@@ -68,8 +70,7 @@ __device__ __forceinline__ uint32_t lbflow_hash(const uint32_t *T, uint32_t sip,
          T[10 * 256 + (dp & 0xFF)] ^ T[11 * 256 + ((dp >> 8) & 0xFF)] ^
          T[12 * 256 + (proto & 0xFF)];
 }
-__device__ __forceinline__ uint32_t ip_hash(const uint32_t *T, uint32_t ip) {
-  const uint32_t *I = T + 13 * 256;
+__device__ __forceinline__ uint32_t ip_hash(const uint32_t *I, uint32_t ip) {
   return I[0 * 256 + (ip & 0xFF)] ^ I[1 * 256 + ((ip >> 8) & 0xFF)] ^
          I[2 * 256 + ((ip >> 16) & 0xFF)] ^ I[3 * 256 + (ip >> 24)];
 }
@@ -182,26 +183,26 @@ __device__ __forceinline__ void lb_rewrite_generic(const LbArgs &a, const GFrame
 // handed to `rw` with the backend record; the rest are queued (M / S).
 // The backend touch log (log2) is written only for heartbeats: phase A lists
 // them (hbl) and the segment applies them as late touches.
+// lb_process_heartbit for a packet from a backend; the packet itself is
+// dropped. I = the ip_addr hash tables.
+__device__ __forceinline__ void lb_heartbeat(const LbArgs &a, const uint32_t *I, uint32_t p,
+                                             uint32_t in, uint32_t sip) {
+  const uint32_t key[4] = {sip, 0, 0, 0};
+  const uint32_t bi = tbl_probe(a.bt, ip_hash(I, sip), key);
+  a.out[p] = (uint16_t)in;
+  a.log[p] = kNone;
+  a.log2[p] = bi;  // kNone: queued, the round writes the real entry
+  const uint32_t k = wave_append(&a.bt.ctl->defer_count, true);  // heartbeats seen
+  if (a.hbl) a.hbl[k] = p;
+  if (bi == kNone) a.hb[wave_append(&a.bt.ctl->miss_count, true)] = p;
+}
+
+// A WAN packet after its flow lookup (fi, and the entry's word 3): a flow
+// with a live backend is handed to `rw` with the backend record; the rest
+// are queued (M: no flow, S: its backend is gone).
 template <class Rw>
-__device__ __forceinline__ bool lb_decide(const LbArgs &a, const uint32_t *T,
-                                          uint32_t p, uint32_t in, uint32_t sip,
-                                          uint32_t dip, uint32_t sp, uint32_t dp,
-                                          uint32_t proto, Rw rw, uint32_t *touch = nullptr) {
-  if (in != a.wan) {  // lb_process_heartbit; the packet itself is dropped
-    const uint32_t key[4] = {sip, 0, 0, 0};
-    const uint32_t bi = tbl_probe(a.bt, ip_hash(T, sip), key);
-    a.out[p] = (uint16_t)in;
-    a.log[p] = kNone;
-    a.log2[p] = bi;  // kNone: queued, the round writes the real entry
-    const uint32_t k = wave_append(&a.bt.ctl->defer_count, true);  // heartbeats seen
-    if (a.hbl) a.hbl[k] = p;
-    if (bi == kNone) a.hb[wave_append(&a.bt.ctl->miss_count, true)] = p;
-    return false;
-  }
-  uint32_t w3 = 0;
-  const uint32_t fi =
-      flow_probe(a.ft, lbflow_hash(T, sip, dip, sp, dp, proto), sip, dip,
-                 sp | (dp << 16), proto, &w3);
+__device__ __forceinline__ bool lb_flow_found(const LbArgs &a, uint32_t p, uint32_t fi,
+                                              uint32_t w3, Rw rw, uint32_t *touch) {
   if (fi == kNone) {
     a.log[p] = kNone;
     a.miss[wave_append(&a.ft.ctl->miss_count, true)] = p;
@@ -218,7 +219,32 @@ __device__ __forceinline__ bool lb_decide(const LbArgs &a, const uint32_t *T,
   return rw(a.be_rec[bi]);
 }
 
-__device__ void lb_generic_a(const LbArgs &a, const uint32_t *T, uint32_t p) {
+// Decision for a parsed packet (phase A / re-classification). Heartbeats are
+// logged or queued (H); WAN packets hitting a flow with a live backend are
+// handed to `rw` with the backend record; the rest are queued (M / S).
+// The backend touch log (log2) is written only for heartbeats: phase A lists
+// them (hbl) and the segment applies them as late touches. T = the flow hash
+// tables, I = the ip_addr hash tables.
+template <class Rw>
+__device__ __forceinline__ bool lb_decide(const LbArgs &a, const uint32_t *T,
+                                          const uint32_t *I, uint32_t p, uint32_t in,
+                                          uint32_t sip, uint32_t dip, uint32_t sp,
+                                          uint32_t dp, uint32_t proto, Rw rw,
+                                          uint32_t *touch = nullptr) {
+  if (in != a.wan) {
+    lb_heartbeat(a, I, p, in, sip);
+    return false;
+  }
+  uint32_t w3 = 0;
+  const uint32_t fi =
+      flow_probe(a.ft, lbflow_hash(T, sip, dip, sp, dp, proto), sip, dip,
+                 sp | (dp << 16), proto, &w3);
+  return lb_flow_found(a, p, fi, w3, rw, touch);
+}
+
+__device__ __forceinline__ void lb_generic_a(const LbArgs &a, const uint32_t *T,
+                                             const uint32_t *I,
+                                             uint32_t p) {
   const GFrame f{a.frames + (size_t)p * a.slot, a.slot};
   const uint32_t in = a.in_dev[p];
   const L34 h = parse_l34(f, a.len[p]);
@@ -230,36 +256,10 @@ __device__ void lb_generic_a(const LbArgs &a, const uint32_t *T, uint32_t p) {
   const uint32_t proto = f.r8(h.ip + 9);
   const uint32_t sp = f.r16(h.l4), dp = f.r16(h.l4 + 2);
   const uint32_t sip = f.r32(h.ip + 12), dip = f.r32(h.ip + 16);
-  lb_decide(a, T, p, in, sip, dip, sp, dp, proto, [&](uint4 rec) {
+  lb_decide(a, T, I, p, in, sip, dip, sp, dp, proto, [&](uint4 rec) {
     lb_rewrite_generic(a, f, h, rec, p);
     return false;
   });
-}
-
-__device__ __forceinline__ bool lb_fast(const LbArgs &a, const uint32_t *T,
-                                        uint32_t p, RFrame &f, uint32_t in,
-                                        uint32_t len, uint32_t &touch) {
-  const uint32_t et = f.w[3] & 0xFFFF;
-  const uint32_t ihl = (f.w[3] >> 16) & 0x0F;
-  const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
-  if (!(et == 0x0008 && ihl == 5 && tl <= 50)) {
-    lb_generic_a(a, T, p);
-    return false;
-  }
-  const uint16_t unread = (uint16_t)(len - 14);
-  const uint32_t proto = f.w[5] >> 24;
-  const bool ok = (unread >= 20) & (unread >= tl) &
-                  ((proto == 6) | (proto == 17)) & ((uint32_t)(len - 34) >= 4u);
-  if (!ok) {
-    a.out[p] = (uint16_t)in;
-    a.log[p] = kNone;
-    return false;
-  }
-  const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
-  const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
-  return lb_decide(a, T, p, in, sip, dip, sp, dp, proto, [&](uint4 rec) {
-    return lb_rewrite_fast(a, f, rec, proto, tl, p);
-  }, &touch);
 }
 
 __device__ __forceinline__ void lb_load_tables(uint32_t *T, const uint32_t *g) {
@@ -267,27 +267,88 @@ __device__ __forceinline__ void lb_load_tables(uint32_t *T, const uint32_t *g) {
   __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void lb_classify64(LbArgs a, uint32_t n_all,
-                                                    TouchBins bins) {
-  __shared__ uint32_t T[kLbTabs * 256];
+// Phase A for 64-byte slots (frames64_tiles, vp_device.h): frames 1 KiB
+// contiguous per load through the wave's LDS tile, and a WAN packet's flow
+// bucket gathered cooperatively (four lanes per 64-byte row) between the
+// issue and finish halves, as vignat's tiles do. LDS holds the 13 flow-hash
+// position tables and the allocation-order layout's four byte tables; the
+// backend-address tables (heartbeats only) are read from global memory.
+struct LbPend {
+  uint32_t row;   // the flow's home bucket (kind 2), or kNone
+  uint32_t kind;  // 0: done; 1: byte path; 2: WAN flow; 3: heartbeat
+};
+__global__ __launch_bounds__(256, 4) void lb_classify64(LbArgs a, uint32_t n_all,
+                                                       TouchBins bins) {
+  __shared__ uint32_t T[kLbFlowTabs * 256 + 1024];  // + the layout's byte tables
   __shared__ uint4 stage[4][256];
   __shared__ uint32_t cur[kCurs];
   for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
-  lb_load_tables(T, a.crc_tab);  // (its barrier also covers cur)
-  struct NoPend {
-    uint32_t row;
-  };
+  for (uint32_t i = threadIdx.x; i < kLbFlowTabs * 256; i += blockDim.x) T[i] = a.crc_tab[i];
+  const uint32_t *lin = T + kLbFlowTabs * 256;
+  if (a.ft.mix == kMixLin)
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) T[kLbFlowTabs * 256 + i] = a.ft.lin[i];
+  __syncthreads();
+  const uint32_t *I = a.crc_tab + kLbFlowTabs * 256;  // ip_addr tables (global)
   frames64_tiles(
       a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
-      nullptr,
-      [&](uint32_t, const RFrame &, uint32_t, uint32_t, bool) {
-        return NoPend{kNone};
+      reinterpret_cast<const uint4 *>(a.ft.bk),
+      [&](uint32_t p, const RFrame &f, uint32_t in, uint32_t len, bool mine) {
+        LbPend P{kNone, 0};
+        if (!mine) return P;
+        const uint32_t et = f.w[3] & 0xFFFF;
+        const uint32_t ihl = (f.w[3] >> 16) & 0x0F;
+        const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
+        if (!(et == 0x0008 && ihl == 5 && tl <= 50)) {
+          P.kind = 1;  // byte-addressed path (lb_generic_a)
+          return P;
+        }
+        const uint16_t unread = (uint16_t)(len - 14);
+        const uint32_t proto = f.w[5] >> 24;
+        const bool ok = (unread >= 20) & (unread >= tl) &
+                        ((proto == 6) | (proto == 17)) & ((uint32_t)(len - 34) >= 4u);
+        if (!ok) {
+          a.out[p] = (uint16_t)in;
+          a.log[p] = kNone;
+          return P;
+        }
+        if (in != a.wan) {
+          P.kind = 3;
+          return P;
+        }
+        const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
+        P.kind = 2;
+        P.row = home_bucket(lbflow_hash(T, f.u32at2(26), f.u32at2(30), sp, dp, proto),
+                            a.ft.bmask, a.ft.mix, lin);
+        return P;
       },
-      [&](NoPend, const uint4 *, uint32_t p, RFrame &f, uint32_t in, uint32_t len,
-          uint32_t &touch) -> uint32_t {
+      [&](const LbPend &P, const uint4 *row, uint32_t p, RFrame &f, uint32_t in,
+          uint32_t len, uint32_t &touch) -> uint32_t {
+        if (P.kind == 0) return 0u;
+        if (P.kind == 1) {
+          lb_generic_a(a, T, I, p);
+          return 0u;
+        }
+        const uint32_t proto = f.w[5] >> 24;
+        const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
+        const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
+        const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
+        if (P.kind == 3) {
+          lb_heartbeat(a, I, p, in, sip);
+          return 0u;
+        }
+        // map_get on the flow table from the gathered home bucket (word 3:
+        // protocol byte | backend << 8)
+        const uint32_t key[4] = {sip, dip, sp | (dp << 16), proto};
+        uint32_t w3 = 0;
+        bool done;
+        uint32_t fi = bucket_match<0xFFu>(row[0], row[1], row[2], row[3], key, &done, &w3);
+        if (!done)
+          fi = tbl_probe_from<0xFFu>(a.ft, (P.row + 1) & a.ft.bmask, key, a.ft.bmask, &w3);
+        const bool rw = lb_flow_found(a, p, fi, w3, [&](uint4 rec) {
+          return lb_rewrite_fast(a, f, rec, proto, tl, p);
+        }, &touch);
         // dst address, MACs and checksums: bytes 0-47, and the TCP checksum
-        if (!lb_fast(a, T, p, f, in, len, touch)) return 0u;
-        return (f.w[5] >> 24) == 6 ? 0xFu : 0x7u;
+        return rw ? (proto == 6 ? 0xFu : 0x7u) : 0u;
       },
       bins, TileQueue{}, cur);
 }
@@ -297,14 +358,14 @@ __global__ __launch_bounds__(256) void lb_classify(LbArgs a) {
   lb_load_tables(T, a.crc_tab);
   for (uint32_t p = a.p0 + blockIdx.x * blockDim.x + threadIdx.x; p < a.p1;
        p += gridDim.x * blockDim.x)
-    lb_generic_a(a, T, p);
+    lb_generic_a(a, T, T + kLbFlowTabs * 256, p);
 }
 
 // Re-classify queued packets (unmodified frames) against the current state.
 __global__ void lb_resolve(LbArgs a, const uint32_t *list, uint32_t n) {
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
        j += gridDim.x * blockDim.x)
-    lb_generic_a(a, a.crc_tab, list[j]);
+    lb_generic_a(a, a.crc_tab, a.crc_tab + kLbFlowTabs * 256, list[j]);
 }
 
 struct Parsed {
@@ -424,7 +485,7 @@ __global__ void lb_hb_keys(LbArgs a, const uint32_t *list, uint32_t n,
     uint32_t *k = mkey + 4 * (size_t)j;
     k[0] = q.sip;
     k[1] = k[2] = k[3] = 0;
-    mhash[j] = ip_hash(a.crc_tab, q.sip);
+    mhash[j] = ip_hash(a.crc_tab + kLbFlowTabs * 256, q.sip);
   }
 }
 
@@ -551,9 +612,14 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.wan = c->lb.wan_device;
   a.n_dev = c->lb.n_devices;
 
-  VP_TRY(zero_queues(c));
-  VP_HIP(hipMemsetAsync(&c->ft2.ctl->defer_count, 0, 4, c->stream));  // heartbeats
-  VP_HIP(hipMemsetAsync(&c->ft.ctl->touch_ovf, 0, 4, c->stream));
+  // the counters are still zero after a segment that queued nothing (no
+  // misses, stale flows, heartbeats or bin overflows): no reset launches
+  if (!c->ft.ctl_clean) {
+    VP_TRY(zero_queues(c));
+    VP_HIP(hipMemsetAsync(&c->ft2.ctl->defer_count, 0, 4, c->stream));  // heartbeats
+    VP_HIP(hipMemsetAsync(&c->ft.ctl->touch_ovf, 0, 4, c->stream));
+  }
+  c->ft.ctl_clean = false;
   BinsPlan bp{};
   const bool tiles64 = b->slot == 64 && c->coalesced_io;
   VP_HIP(hipEventRecord(c->ev0, c->stream));
@@ -571,13 +637,24 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   VP_HIP(hipGetLastError());
   VP_HIP(hipEventRecord(c->ev1, c->stream));
   a.hbl = nullptr;  // re-classification rounds list no heartbeat twice
-  // phase A's counts are copied out before the fold and waited for alone
-  VP_TRY(read_ctl2_post(c, c->ft2, c->ft));
-  if (bp.on)  // optimistic fold
-    VP_TRY(tbl_bins_reduce(c, c->ft, bp, p0, now, c->seq));
-  else
+  if (bp.on) {
+    // optimistic fold; its first thread publishes phase A's counts (the flow
+    // table's control block, and the backend table's H and heartbeat counts
+    // as extra words), which the host waits for while the fold runs
+    static_assert(offsetof(Ctl, defer_count) == offsetof(Ctl, miss_count) + 4, "H, heartbeats");
+    const uint32_t epoch = ++c->ft.pub_epoch;
+    VP_TRY(tbl_bins_reduce(c, c->ft, bp, p0, now, c->seq,
+                           PubArgs{c->ft.d_pub, c->ft.ctl, epoch, &c->ft2.ctl->miss_count,
+                                   nullptr, 2, 0}));
+    VP_TRY(tbl_wait_pub(c, c->ft, epoch));
+    c->ft2.h_ctl.miss_count = c->ft.h_pub->xtra[0];
+    c->ft2.h_ctl.defer_count = c->ft.h_pub->xtra[1];
+  } else {
+    // phase A's counts are copied out before the fold and waited for alone
+    VP_TRY(read_ctl2_post(c, c->ft2, c->ft));
     VP_TRY(tbl_touch_reduce(c, c->ft, w.log, p0, p1, now, c->seq));
-  VP_TRY(read_ctl2_wait(c, c->ft2, c->ft));
+    VP_TRY(read_ctl2_wait(c, c->ft2, c->ft));
+  }
   float kms = 0.f;
   VP_HIP(event_ms(c->ev0, c->ev1, &kms));
   *ms += kms;
@@ -663,6 +740,7 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // steady state: frames and ports complete, only the flow fold may still
   // run (not when it reads the caller's time array)
   c->fold_pending = !(nm || ns || nh || ovf || nhb) && !b->now;
+  c->ft.ctl_clean = !(nm || ns || nh || ovf || nhb);
   return 0;
 }
 

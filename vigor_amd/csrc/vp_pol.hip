@@ -68,8 +68,10 @@ struct PolArgs {
   uint32_t *cnt;     // hits per index in this segment (phase A)
   uint32_t *rnk;     // a hit's rank in its index's run (arbitrary order)
   uint32_t *runs;    // or (non-null) the hit's position straight into its
-                     // index's run slots: runs[index * kRunMax + rank]
-  uint32_t *maxrun;  // longest run (ctl->aux_count)
+                     // index's run slots: runs[rank * cap + index] (rank-major:
+                     // a tile of packets with consecutive indices writes
+                     // consecutive slots, and the replay lanes read them so)
+  uint32_t *runover; // set when a run is longer than kRunMax (ctl->aux_count)
   uint16_t lan, wan;
 };
 
@@ -103,7 +105,7 @@ __global__ __launch_bounds__(256) void pol_classify(PolArgs a) {
   for (uint32_t i = threadIdx.x; i < kPolTabs * 256; i += blockDim.x)
     T[i] = a.crc_tab[i];
   __syncthreads();
-  uint32_t lmax = 0;
+  bool over = false;
   for (uint32_t p = a.p0 + blockIdx.x * blockDim.x + threadIdx.x; p < a.p1;
        p += gridDim.x * blockDim.x) {
     const uint32_t in = a.in_dev[p], len = a.len[p];
@@ -130,11 +132,11 @@ __global__ __launch_bounds__(256) void pol_classify(PolArgs a) {
       if (a.cnt) {  // grouping path: this hit's rank in its index's run
         const uint32_t r = atomicAdd(&a.cnt[idx], 1u);
         if (a.runs) {
-          if (r < kRunMax) a.runs[(size_t)idx * kRunMax + r] = p;
+          if (r < kRunMax) a.runs[(size_t)r * a.t.cap + idx] = p;
         } else {
           a.rnk[p] = r;
         }
-        lmax = max(lmax, r + 1);
+        over |= r >= kRunMax;
       }
     } else if (len <= a.burst) {
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
@@ -142,8 +144,7 @@ __global__ __launch_bounds__(256) void pol_classify(PolArgs a) {
       a.defer[wave_append(&a.t.ctl->defer_count, true)] = p;
     }
   }
-  for (int o = 32; o > 0; o >>= 1) lmax = max(lmax, (uint32_t)__shfl_xor((int)lmax, o));
-  if (__lane_id() == 0 && lmax) atomicMax(a.maxrun, lmax);
+  if (__ballot(over) && __lane_id() == 0) *a.runover = 1;
 }
 
 // Phase A for 64-byte slots (frames64_tiles, vp_device.h): every frame load
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(256, 4) void pol_classify64(PolArgs a, uint32_t n_a
   for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
   __syncthreads();
   const uint32_t *lin = T + kPolTabs * 256;
-  uint32_t lmax = 0;
+  bool over = false;
   frames64_tiles(
       const_cast<uint8_t *>(a.frames), a.len, a.in_dev, a.p0, a.p1, n_all,
       stage[threadIdx.x >> 6], reinterpret_cast<const uint4 *>(a.t.bk),
@@ -199,11 +200,11 @@ __global__ __launch_bounds__(256, 4) void pol_classify64(PolArgs a, uint32_t n_a
           if (a.cnt) {  // grouping path: this hit's rank in its index's run
             const uint32_t r = atomicAdd(&a.cnt[idx], 1u);
             if (a.runs) {
-              if (r < kRunMax) a.runs[(size_t)idx * kRunMax + r] = p;
+              if (r < kRunMax) a.runs[(size_t)r * a.t.cap + idx] = p;
             } else {
               a.rnk[p] = r;
             }
-            lmax = max(lmax, r + 1);
+            over |= r >= kRunMax;
           }
         } else if (len <= a.burst) {
           a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
@@ -213,8 +214,7 @@ __global__ __launch_bounds__(256, 4) void pol_classify64(PolArgs a, uint32_t n_a
         return 0u;  // (the policer never writes frames)
       },
       TouchBins{}, TileQueue{}, cur);
-  for (int o = 32; o > 0; o >>= 1) lmax = max(lmax, (uint32_t)__shfl_xor((int)lmax, o));
-  if (__lane_id() == 0 && lmax) atomicMax(a.maxrun, lmax);
+  if (__ballot(over) && __lane_id() == 0) *a.runover = 1;
 }
 
 // ------------------------------------------------------------- phase B --
@@ -344,7 +344,7 @@ __global__ void pol_buckets(PolArgs a, const uint32_t *skey, const uint32_t *sva
 // host has read the counts back, and check them on the device: in steady
 // state the replay overlaps the control read-back instead of following it.
 __device__ __forceinline__ bool pol_grouping_ok(const Ctl *ctl) {
-  return (ctl->miss_count | ctl->defer_count) == 0 && ctl->aux_count <= kRunMax;
+  return (ctl->miss_count | ctl->defer_count | ctl->aux_count) == 0;
 }
 
 // Grouping path: hits scattered to their index's run (off = exclusive scan
@@ -362,20 +362,24 @@ __global__ void pol_scatter(const uint32_t *pidx, const uint32_t *rnk, uint32_t 
 
 // One lane per index with hits: its run (<= kRunMax positions) put back in
 // packet order by an insertion sort, then replayed. The run is at
-// grouped + off[k] (scan + scatter) or, off == null, at the index's own
-// kRunMax slots that phase A filled.
-__global__ void pol_runs(PolArgs a, const uint32_t *cnt, const uint32_t *off,
+// grouped + off[k] (scan + scatter) or, off == null, in the index's slots
+// that phase A filled (rank-major: slot j at grouped[j * cap + k]); the
+// lane clears the index's count for the next segment. The first thread
+// publishes phase A's control block to the host (ctl_publish), which learns
+// the counts while the replay runs.
+__global__ void pol_runs(PolArgs a, uint32_t *cnt, const uint32_t *off,
                          const uint32_t *grouped, uint32_t cap, NowSpec now,
-                         uint64_t *bsize, int64_t *btime) {
+                         uint64_t *bsize, int64_t *btime, PubArgs pub) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctl_publish(pub);
   if (!pol_grouping_ok(a.t.ctl)) return;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < cap;
        k += gridDim.x * blockDim.x) {
     const uint32_t c = cnt[k];
     if (c == 0) continue;
+    cnt[k] = 0;
     uint32_t q[kRunMax];
-    const uint32_t *g = off ? grouped + off[k] : grouped + (size_t)k * kRunMax;
     for (uint32_t j = 0; j < c; j++) {
-      const uint32_t v = g[j];
+      const uint32_t v = off ? grouped[off[k] + j] : grouped[(size_t)j * cap + k];
       uint32_t i = j;
       while (i > 0 && q[i - 1] > v) {
         q[i] = q[i - 1];
@@ -444,7 +448,7 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.lan = c->pol.lan_device;
   a.wan = c->pol.wan_device;
   a.rnk = w.aux;
-  a.maxrun = &t.ctl->aux_count;
+  a.runover = &t.ctl->aux_count;
   const uint32_t n = p1 - p0;
   // The grouping path costs O(capacity) per segment (clear, scan and one
   // lane per index); segments much shorter than the table (per-packet
@@ -453,9 +457,18 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.cnt = grouping ? c->pol_cnt : nullptr;
   a.runs = grouping ? c->pol_runs : nullptr;
 
-  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
-  VP_HIP(hipMemsetAsync(a.maxrun, 0, 4, c->stream));
-  if (grouping) VP_HIP(hipMemsetAsync(c->pol_cnt, 0, 4ull * t.cap, c->stream));
+  // the counters (and the hit counts) are still zero after a segment whose
+  // phase A queued nothing and whose replay cleared its counts
+  if (!t.ctl_clean) {
+    VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
+    VP_HIP(hipMemsetAsync(a.runover, 0, 4, c->stream));
+  }
+  if (grouping && !c->pol_cnt_clean)
+    VP_HIP(hipMemsetAsync(c->pol_cnt, 0, 4ull * t.cap, c->stream));
+  t.ctl_clean = false;
+  c->pol_cnt_clean = false;
+  const uint32_t epoch = ++t.pub_epoch;  // phase A's counts, published by pol_runs
+  const PubArgs pub{t.d_pub, t.ctl, epoch, nullptr, nullptr, 0, 0};
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   if (b->slot == 64 && c->coalesced_io) {
     const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
@@ -469,7 +482,8 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   if (grouping && c->pol_runs) {  // phase T, grouping path with per-index
     // run slots (phase A wrote them): no scan, no scatter
     pol_runs<<<grid_for(t.cap), 256, 0, c->stream>>>(a, c->pol_cnt, nullptr, c->pol_runs,
-                                                     t.cap, now, c->pol_size, c->pol_time);
+                                                     t.cap, now, c->pol_size, c->pol_time,
+                                                     pub);
     VP_HIP(hipGetLastError());
   } else if (grouping) {  // phase T, grouping path (speculative: no-ops unless pol_grouping_ok)
     size_t need = 0;
@@ -482,10 +496,13 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
                                                     c->pol_off, w.sval, t.ctl);
     pol_runs<<<grid_for(t.cap), 256, 0, c->stream>>>(a, c->pol_cnt, c->pol_off,
                                                      w.sval, t.cap, now,
-                                                     c->pol_size, c->pol_time);
+                                                     c->pol_size, c->pol_time, pub);
     VP_HIP(hipGetLastError());
   }
-  VP_TRY(read_ctl(c, t));
+  if (grouping)
+    VP_TRY(tbl_wait_pub(c, t, epoch));
+  else
+    VP_TRY(read_ctl(c, t));
   float kms = 0.f;
   VP_HIP(event_ms(c->ev0, c->ev1, &kms));
   *ms += kms;
@@ -517,7 +534,11 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.t = tbl_dev(t);
   // the grouping path already ran (every policed packet was a counted
   // phase-A hit and runs are short): nothing left
-  if (grouping && !nmiss && !ndefer && t.h_ctl.aux_count <= kRunMax) return 0;
+  if (grouping && !nmiss && !ndefer && t.h_ctl.aux_count == 0) {
+    t.ctl_clean = true;       // nothing counted
+    c->pol_cnt_clean = true;  // pol_runs cleared every count it read
+    return 0;
+  }
   // phase T, sorting path: (index, packet) pairs sorted by index; radix sort
   // is stable, so each index's packets stay in packet order
   uint32_t bits = 1;
@@ -560,6 +581,7 @@ int pol_process_device(vp_ctx *c, const vp_dev_batch *b) {
     VP_HIP(hipMemcpyAsync(&last, d_last, 4, hipMemcpyDeviceToHost, c->stream));
     VP_HIP(hipStreamSynchronize(c->stream));
     exp_end = (uint32_t)(last + 1);
+    c->ft.ctl_clean = false;  // (aux_count held the answer)
   }
   ExpiringTable tabs[1] = {{&c->ft, pol_cutoff}};
   return run_batch(c, b, tabs, 1, pol_segment, exp_end);

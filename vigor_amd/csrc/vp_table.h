@@ -252,9 +252,11 @@ int tbl_late_touches(vp_ctx *c, FlowTable &t, const uint32_t *list,
 // Fold the bins into ts/tseq. A touch that found its slice full was queued
 // instead (t.ctl->touch_ovf set; apply plan.bins.oent with tbl_late_touches).
 int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
-                    const NowSpec &now, uint64_t seq_base);
+                    const NowSpec &now, uint64_t seq_base,
+                    const PubArgs &pub = PubArgs{});
 // Multi-GPU: also gathers the ranks' segment counters (Workspace::h_gath;
 // owner mode: + this rank's `sends`, its key count per owner).
+int tbl_wait_pub(vp_ctx *c, FlowTable &t, uint32_t epoch);
 int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_t *log,
                       uint32_t p0, uint32_t p1, const NowSpec &now, uint64_t seq_base,
                       const uint32_t *sends = nullptr);

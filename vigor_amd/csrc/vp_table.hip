@@ -812,6 +812,7 @@ int tbl_touch_reduce(vp_ctx *c, FlowTable &t, const uint32_t *log, uint32_t p0,
 // packet (one write while classifying, one read here).
 constexpr uint32_t kBinLocalMax = 16384;  // in-bin indices held in LDS
 
+template <uint32_t kU>  // 64-entry chunks in flight per wave
 __global__ __launch_bounds__(1024) void touch_bins_reduce(
     const uint32_t *ent, const uint32_t *cnt, uint32_t nsrc, uint32_t cap,
     uint32_t pbits, uint32_t bbits, uint32_t range, uint32_t L, uint32_t tcap,
@@ -827,32 +828,39 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const uint32_t pmask = (1u << pbits) - 1;
-  constexpr uint32_t kU = 8;  // source slices in flight per wave (16-64: no faster, round 2)
   // wave w takes slices w, w + nw, ...; 64 of them per round, their sizes
-  // loaded by one instruction (lane l <-> slice w + l * nw)
+  // loaded by one instruction (lane l <-> slice w + l * nw). The round's
+  // slices are one list of 64-entry chunks (chunk t of the list belongs to
+  // the lane whose exclusive prefix of chunk counts covers t), read kU chunks
+  // at a time whatever the slices' lengths.
   for (uint32_t r0 = threadIdx.x >> 6; r0 < nsrc; r0 += 64 * nw) {
     const uint32_t my = r0 + lane * nw;
     const uint32_t nv = my < nsrc ? cnt[(size_t)bin * nsrc + my] : 0;
-    for (uint32_t i = 0; i < 64; i += kU) {
-      uint32_t n[kU], e[kU];
+    const uint32_t ch = (nv + 63) >> 6;
+    uint32_t inc = ch;  // inclusive prefix over the wave
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const uint32_t t = (uint32_t)__shfl_up((int)inc, o);
+      if (lane >= o) inc += t;
+    }
+    const uint32_t exc = inc - ch;
+    const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
+    for (uint32_t t0 = 0; t0 < total; t0 += kU) {
+      uint32_t e[kU], lim[kU], base[kU];
 #pragma unroll
       for (uint32_t u = 0; u < kU; u++) {
-        n[u] = __shfl(nv, i + u);
-        const uint32_t sb = r0 + (i + u) * nw;
-        e[u] = lane < n[u] ? ent[((size_t)bin * nsrc + sb) * cap + lane] : 0;
+        const uint32_t t = t0 + u;
+        const uint64_t own = __ballot(exc <= t && t < inc);  // (none past the list)
+        const uint32_t l = own ? (uint32_t)__ffsll((unsigned long long)own) - 1 : 0u;
+        const uint32_t k = (t - __builtin_amdgcn_readlane(exc, l)) << 6;
+        const uint32_t sb = r0 + l * nw;
+        lim[u] = own ? __builtin_amdgcn_readlane(nv, l) - k : 0u;
+        base[u] = sb * range + 1;
+        e[u] = lane < lim[u] ? ent[((size_t)bin * nsrc + sb) * cap + k + lane] : 0u;
       }
 #pragma unroll
-      for (uint32_t u = 0; u < kU; u++) {
-        const uint32_t sb = r0 + (i + u) * nw;
-        if (lane < n[u])
-          atomicMax(&last[e[u] >> pbits], sb * range + (e[u] & pmask) + 1);
-        for (uint32_t k = 64; k < n[u]; k += 64) {  // slices longer than 64
-          if (k + lane < n[u]) {
-            const uint32_t x = ent[((size_t)bin * nsrc + sb) * cap + k + lane];
-            atomicMax(&last[x >> pbits], sb * range + (x & pmask) + 1);
-          }
-        }
-      }
+      for (uint32_t u = 0; u < kU; u++)
+        if (lane < lim[u]) atomicMax(&last[e[u] >> pbits], base[u] + (e[u] & pmask));
     }
   }
   __syncthreads();
@@ -925,7 +933,15 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
 
 static int bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
                        const NowSpec &now, uint64_t seq_base, PubArgs pub) {
-  touch_bins_reduce<<<1u << plan.bins.bbits, 1024, 4u * plan.L, c->stream>>>(
+  // chunks in flight per fold wave (VIGPATH_FOLD_U: 8, 16 or 32)
+  static const uint32_t fold_u = [] {
+    const char *e = getenv("VIGPATH_FOLD_U");
+    const int v = e ? atoi(e) : 0;
+    return v == 8 || v == 32 ? (uint32_t)v : 16u;
+  }();
+  auto *fold = fold_u == 8 ? touch_bins_reduce<8> : fold_u == 32 ? touch_bins_reduce<32>
+                                                                 : touch_bins_reduce<16>;
+  fold<<<1u << plan.bins.bbits, 1024, 4u * plan.L, c->stream>>>(
       plan.bins.ent, plan.bins.cnt, plan.grid, plan.bins.cap, plan.bins.pbits,
       plan.bins.bbits, plan.range, plan.L, t.cap, p0, now, seq_base, t.ts, t.tseq,
       pub);
@@ -934,8 +950,8 @@ static int bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p
 }
 
 int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
-                    const NowSpec &now, uint64_t seq_base) {
-  return bins_reduce(c, t, plan, p0, now, seq_base, PubArgs{});
+                    const NowSpec &now, uint64_t seq_base, const PubArgs &pub) {
+  return bins_reduce(c, t, plan, p0, now, seq_base, pub);
 }
 
 // Phase A's control block for the host, and the fold of phase A's touches
@@ -951,6 +967,24 @@ int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
 // block, and owner mode adds this rank's key count per owner (`sends`): the
 // host learns all of it with the one wait it makes anyway (union_sizes,
 // DESIGN.md §6).
+// Wait for the control block a kernel published with `epoch` (ctl_publish)
+// and copy it to t.h_ctl; a stream that ends (or fails) without it is an
+// error.
+int tbl_wait_pub(vp_ctx *c, FlowTable &t, uint32_t epoch) {
+  for (uint32_t spin = 1;; spin++) {
+    if (__atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE) == epoch) break;
+    if ((spin & 1023) == 0) {
+      const hipError_t e = hipStreamQuery(c->stream);
+      if (e == hipSuccess && __atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE) != epoch)
+        return state_fail("a kernel ended without publishing epoch %u (seen %u)", epoch,
+                          __atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE));
+      if (e != hipSuccess && e != hipErrorNotReady) VP_HIP(e);
+    }
+  }
+  memcpy(&t.h_ctl, (const void *)&t.h_pub->ctl, sizeof(Ctl));
+  return 0;
+}
+
 int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_t *log,
                       uint32_t p0, uint32_t p1, const NowSpec &now, uint64_t seq_base,
                       const uint32_t *sends) {
@@ -982,18 +1016,7 @@ int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_
   VP_TRY(bins_reduce(c, t, bp, p0, now, seq_base,
                      PubArgs{t.d_pub, t.ctl, epoch, w.gath, sends, kPubGath * nr, ns}));
   hostprof(3);
-  // poll the epoch; a stream that ends (or fails) without it is an error
-  for (uint32_t spin = 1;; spin++) {
-    if (__atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE) == epoch) break;
-    if ((spin & 1023) == 0) {
-      const hipError_t e = hipStreamQuery(c->stream);
-      if (e == hipSuccess && __atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE) != epoch)
-        return state_fail("fold ended without publishing epoch %u (seen %u)", epoch,
-                          __atomic_load_n(&t.h_pub->epoch, __ATOMIC_ACQUIRE));
-      if (e != hipSuccess && e != hipErrorNotReady) VP_HIP(e);
-    }
-  }
-  memcpy(&t.h_ctl, (const void *)&t.h_pub->ctl, sizeof(Ctl));
+  VP_TRY(tbl_wait_pub(c, t, epoch));
   if (nr) {
     w.h_gath.assign(t.h_pub->xtra, t.h_pub->xtra + kPubGath * nr + ns);
     w.gath_ok = true;
