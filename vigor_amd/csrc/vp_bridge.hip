@@ -125,22 +125,27 @@ __device__ __forceinline__ uint4 eth_words(const BridgeArgs &a, uint32_t p) {
 
 // One dynamic-table bucket against a MAC (words 0-1): the index and *port
 // (entry word 2) on a match; kNone with *done on an empty entry; kNone with
-// !*done when the probe continues in the next bucket.
+// !*done when the probe continues in the next bucket. Entries in order, the
+// first match or empty entry decides; branch-free with static indices (an
+// early return per entry made the entry number dynamic and put the whole
+// row in scratch memory: 64 B per packet of stores, the bridge's write
+// traffic in round 2).
 __device__ __forceinline__ uint32_t mac_match(const uint4 *row, uint32_t m0, uint32_t m1,
                                               uint32_t *port, bool *done) {
   const uint4 ix = row[3];
-  const uint32_t id[3] = {ix.x, ix.y, ix.z};
-  *done = true;
-#pragma unroll
-  for (int e = 0; e < 3; e++) {
-    if (id[e] == kEmpty) return kNone;
-    if (id[e] != kTomb && row[e].x == m0 && row[e].y == m1) {
-      *port = row[e].z;
-      return id[e];
-    }
-  }
-  *done = false;
-  return kNone;
+  const bool e0 = ix.x == kEmpty, e1 = ix.y == kEmpty, e2 = ix.z == kEmpty;
+  const bool h0 = !e0 & (ix.x != kTomb) & (row[0].x == m0) & (row[0].y == m1);
+  const bool h1 = !e1 & (ix.y != kTomb) & (row[1].x == m0) & (row[1].y == m1);
+  const bool h2 = !e2 & (ix.z != kTomb) & (row[2].x == m0) & (row[2].y == m1);
+  const bool t0 = h0 | e0, t1 = h1 | e1;
+  const bool s1 = !t0 & h1, s2 = !t0 & !t1 & h2;
+  // (masks, not a select: a select of row[e].z became a load through a
+  // selected address, with the row in scratch memory again)
+  const uint32_t z = (row[0].z & (0u - (uint32_t)h0)) | (row[1].z & (0u - (uint32_t)s1)) |
+                     (row[2].z & (0u - (uint32_t)s2));
+  if (h0 | s1 | s2) *port = z;
+  *done = t0 | t1 | h2 | e2;
+  return h0 ? ix.x : e0 ? kNone : h1 ? ix.y : e1 ? kNone : h2 ? ix.z : kNone;
 }
 
 // Phase A. Blocks own contiguous ranges of 64-packet tiles, their four waves

@@ -288,36 +288,44 @@ __global__ void pol_sort_keys(const uint32_t *pidx, uint32_t p0, uint32_t n,
 // (policer_main.c:91-100: bucket = burst - size, time = now). The run's last
 // packet is the index's last rejuvenation: the lane stamps ts/tseq itself
 // (no touch-log fold for vigpol).
-template <class Next>
+// N > 0: the loop unrolled N times (c <= N), so a run held in an N-element
+// register array is indexed statically (a dynamically indexed array lives in
+// scratch memory: per-lane stores and loads through the caches).
+template <uint32_t N = 0, class Next>
 __device__ __forceinline__ void pol_replay(const PolArgs &a, uint32_t k,
                                            uint32_t c, Next next, const NowSpec &now,
                                            uint64_t *bsize, int64_t *btime) {
   uint64_t size = bsize[k];
   uint64_t btu = (uint64_t)btime[k];
   uint32_t p = 0;
-  for (uint32_t j = 0; j < c; j++) {
+  auto step = [&](uint32_t j) {
     p = next(j);
-    {
-      const uint64_t len = a.len[p];
-      const uint64_t tu = (uint64_t)now.at(p);
-      bool fwd;
-      if (j == 0 && a.t.birth[k] == a.seq_base + p) {
-        size = a.burst - len;  // new flow: forwarded (policer_main.c:91-103)
-        fwd = true;
-      } else {  // policer_main.c:39-72
-        const uint64_t diff = tu - btu;
-        if (diff < a.thr) {
-          size += diff * a.rate / kNsPerS;
-          if (size > a.burst) size = a.burst;
-        } else {
-          size = a.burst;
-        }
-        fwd = size > len;
-        if (fwd) size -= len;
+    const uint64_t len = a.len[p];
+    const uint64_t tu = (uint64_t)now.at(p);
+    bool fwd;
+    if (j == 0 && a.t.birth[k] == a.seq_base + p) {
+      size = a.burst - len;  // new flow: forwarded (policer_main.c:91-103)
+      fwd = true;
+    } else {  // policer_main.c:39-72
+      const uint64_t diff = tu - btu;
+      if (diff < a.thr) {
+        size += diff * a.rate / kNsPerS;
+        if (size > a.burst) size = a.burst;
+      } else {
+        size = a.burst;
       }
-      btu = tu;
-      a.out[p] = fwd ? a.lan : a.wan;
+      fwd = size > len;
+      if (fwd) size -= len;
     }
+    btu = tu;
+    a.out[p] = fwd ? a.lan : a.wan;
+  };
+  if constexpr (N > 0) {
+#pragma unroll
+    for (uint32_t j = 0; j < N; j++)
+      if (j < c) step(j);
+  } else {
+    for (uint32_t j = 0; j < c; j++) step(j);
   }
   bsize[k] = size;
   btime[k] = (int64_t)btu;
@@ -377,6 +385,24 @@ __global__ void pol_runs(PolArgs a, uint32_t *cnt, const uint32_t *off,
     const uint32_t c = cnt[k];
     if (c == 0) continue;
     cnt[k] = 0;
+    if (!off && c <= 8) {
+      // short runs (the common case: a batch revisits each address a few
+      // times) in registers: padded with ~0, sorted by an odd-even
+      // transposition network, replayed with static indices
+      uint32_t r[8];
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++) r[j] = j < c ? grouped[(size_t)j * cap + k] : ~0u;
+#pragma unroll
+      for (uint32_t round = 0; round < 8; round++)
+#pragma unroll
+        for (uint32_t j = round & 1; j + 1 < 8; j += 2) {
+          const uint32_t lo = min(r[j], r[j + 1]), hi = max(r[j], r[j + 1]);
+          r[j] = lo;
+          r[j + 1] = hi;
+        }
+      pol_replay<8>(a, k, c, [&](uint32_t j) { return r[j]; }, now, bsize, btime);
+      continue;
+    }
     uint32_t q[kRunMax];
     for (uint32_t j = 0; j < c; j++) {
       const uint32_t v = off ? grouped[off[k] + j] : grouped[(size_t)j * cap + k];
