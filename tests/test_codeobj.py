@@ -1,0 +1,102 @@
+"""The built gfx950 code objects keep the hot kernels out of scratch memory.
+
+A kernel with a private segment stores per-lane arrays or register spills
+through the caches to HBM: round 2's bridge_classify wrote 64 B per packet
+that way (a bucket row array indexed dynamically), 8x its real output
+(DESIGN.md 5.1). This test reads the kernel descriptors of the device code
+that ships in vigor_amd/libvigpath.so (the .hip_fatbin section: one offload
+bundle per translation unit) with the ROCm LLVM tools and checks the
+private segment sizes. CPU only: no GPU needed.
+"""
+from __future__ import annotations
+
+import os
+import re
+import shutil
+import struct
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "vigor_amd", "libvigpath.so")
+LLVM = "/opt/rocm/llvm/bin"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+# per-packet kernels of the steady state: no private segment at all
+NO_SCRATCH = ["bridge_classify", "lb_classify64", "fw_classify64", "pol_classify64",
+              "nat_remote64", "nat_own_probe", "touch_bins_reduce"]
+# the vignat tile kernels keep a few register spills on the per-lane path,
+# outside the lean tile (bytes per lane)
+SMALL_SPILLS = {"nat_classify64": 32}
+
+
+def _code_objects(tmp):
+    objcopy = os.path.join(LLVM, "llvm-objcopy")
+    fat = os.path.join(tmp, "fatbin")
+    subprocess.run([objcopy, "--dump-section", ".hip_fatbin=" + fat, LIB], check=True,
+                   capture_output=True)
+    data = open(fat, "rb").read()
+    out = []
+    start = data.find(MAGIC)
+    while start != -1:
+        n = struct.unpack_from("<Q", data, start + 24)[0]
+        p = start + 32
+        for _ in range(n):
+            off, size, idlen = struct.unpack_from("<QQQ", data, p)
+            p += 24
+            tid = data[p:p + idlen].decode()
+            p += idlen
+            if "gfx950" in tid:
+                path = os.path.join(tmp, "co%d.o" % len(out))
+                with open(path, "wb") as fh:
+                    fh.write(data[start + off:start + off + size])
+                out.append(path)
+        start = data.find(MAGIC, start + 1)
+    return out
+
+
+def _private_segments():
+    """{mangled kernel name: private segment bytes} over every code object."""
+    sizes = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        for co in _code_objects(tmp):
+            notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", co],
+                                   check=True, capture_output=True, text=True).stdout
+            name = None
+            for line in notes.splitlines():
+                m = re.match(r"\s+\.name:\s+(\S+)", line)
+                if m:
+                    name = m.group(1)
+                m = re.match(r"\s+\.private_segment_fixed_size:\s+(\d+)", line)
+                if m and name:
+                    sizes[name] = int(m.group(1))
+    return sizes
+
+
+@pytest.fixture(scope="module")
+def segments():
+    if not os.path.exists(LIB):
+        pytest.skip("libvigpath.so not built")
+    if not shutil.which("llvm-readelf", path=LLVM):
+        pytest.skip("ROCm LLVM tools absent")
+    return _private_segments()
+
+
+def _find(segments, short):
+    hits = {k: v for k, v in segments.items() if re.search(r"\d%s[EI]" % re.escape(short), k)}
+    assert hits, "kernel %s not found in the code objects" % short
+    return hits
+
+
+@pytest.mark.parametrize("kernel", NO_SCRATCH)
+def test_hot_kernels_have_no_private_segment(segments, kernel):
+    for name, size in _find(segments, kernel).items():
+        assert size == 0, "%s keeps %d bytes per lane in scratch memory" % (name, size)
+
+
+@pytest.mark.parametrize("kernel", sorted(SMALL_SPILLS))
+def test_vignat_tile_spills_stay_small(segments, kernel):
+    for name, size in _find(segments, kernel).items():
+        assert size <= SMALL_SPILLS[kernel], "%s: %d bytes of scratch" % (name, size)

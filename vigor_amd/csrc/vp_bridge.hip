@@ -350,7 +350,9 @@ static int bridge_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
   const uint32_t grid = bp.on ? bp.grid : resident_grid((const void *)bridge_classify,
                                                         (tiles + 3) / 4);
-  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. touch_ovf
+  // (still zero after a segment that learned nothing: no reset launch)
+  if (!t.ctl_clean) VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. touch_ovf
+  t.ctl_clean = false;
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   BridgeArgs a1 = a;
   if (bp.on) a1.log = nullptr;
@@ -370,6 +372,7 @@ static int bridge_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // nothing learned: provisional floods stand; only the fold may still run
   // (not when it reads the caller's time array)
   c->fold_pending = !nmiss && !ovf && !b->now;
+  t.ctl_clean = !nmiss && !ovf;
   if (!nmiss) return 0;
 
   size_t need = 0;

@@ -411,7 +411,9 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     rq = TileQueue{w.reprobe, w.reprobe_cnt, &t.ctl->reprobe_count};
     a.tileq = 1;
   }
-  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
+  // (still zero after a segment that queued nothing: no reset launch)
+  if (!t.ctl_clean) VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
+  t.ctl_clean = false;
   VP_HIP(hipEventRecord(c->ev0, c->stream));
   if (p1 > p0) {
     if (tiles64) {
@@ -477,6 +479,7 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // steady state: frames and ports complete, only the stamp fold may run
   // (not when it reads the caller's time array)
   c->fold_pending = !b->now && !nre && !nmiss && !ndefer && !ovf;
+  t.ctl_clean = !nre && !nmiss && !ndefer && !ovf;
   return 0;
 }
 
