@@ -4,6 +4,10 @@
 set -o pipefail
 O=gpurun_out; mkdir -p $O; export TMPDIR=/tmp
 T=r03k
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/${T}_pytest.log 2>&1 || exit $?
+for u in 8 16 32; do
+  VIGPATH_FOLD_U=$u timeout -k 10 300 python3 bench.py --no-cpu --no-e2e --no-extra > $O/${T}_fold$u.log 2>&1 || exit $?
+done
 for c in WRITE_SIZE FETCH_SIZE; do
   rm -rf $O/${T}_brsame_$c
   BENCH_NF_SAME=1 timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/${T}_brsame_$c -- \

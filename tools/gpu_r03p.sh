@@ -11,3 +11,8 @@ for nf in pol lb fw; do
       python3 tools/bench_nf.py --only $nf --no-cpu --steps 3 > $O/${T}_${nf}_$c.log 2>&1 || exit $?
   done
 done
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "wide or edge" > $O/${T}_pytest_wide0.log 2>&1 || exit $?
+VIGPATH_W128_FULL=1 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "wide or edge" > $O/${T}_pytest_wide1.log 2>&1 || exit $?
+for f in 0 1 0 1; do
+  VIGPATH_W128_FULL=$f timeout -k 10 300 python3 bench.py --slot 128 --no-cpu --no-e2e --no-extra >> $O/${T}_w128_$f.log 2>&1 || exit $?
+done
