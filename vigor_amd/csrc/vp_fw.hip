@@ -258,7 +258,9 @@ __global__ __launch_bounds__(256, 4) void fw_classify64(FwArgs a, uint32_t n_all
       },
       [&](const FwPend &P, const uint4 *row, uint32_t p, RFrame &f, uint32_t in,
           uint32_t len, uint32_t &touch) -> uint32_t {
-        return fw_finish(a, T, P, row, p, f, in, len, touch) ? 0x1u : 0u;  // MACs
+        // the MACs change (bytes 0-11); the whole slot is stored back, a
+        // whole-line write
+        return fw_finish(a, T, P, row, p, f, in, len, touch) ? 0xFu : 0u;
       },
       bins, rq, cur);
 }

@@ -209,14 +209,18 @@ __device__ __forceinline__ bool lb_flow_found(const LbArgs &a, uint32_t p, uint3
     return false;
   }
   const uint32_t bi = w3 >> 8;
-  if (a.bt.slot_of[bi] == kNone) {  // backend gone: erase + re-lookup
+  // the backend's liveness and record in one round trip (both depend on bi
+  // only; the record of a dead backend is read and ignored)
+  const uint32_t live = a.bt.slot_of[bi];
+  const uint4 rec = a.be_rec[bi];
+  if (live == kNone) {  // backend gone: erase + re-lookup
     a.log[p] = kNone;
     a.stale[wave_append(&a.ft.ctl->defer_count, true)] = p;
     return false;
   }
   a.log[p] = fi;
   if (touch) *touch = fi;
-  return rw(a.be_rec[bi]);
+  return rw(rec);
 }
 
 // Decision for a parsed packet (phase A / re-classification). Heartbeats are
@@ -347,8 +351,10 @@ __global__ __launch_bounds__(256, 4) void lb_classify64(LbArgs a, uint32_t n_all
         const bool rw = lb_flow_found(a, p, fi, w3, [&](uint4 rec) {
           return lb_rewrite_fast(a, f, rec, proto, tl, p);
         }, &touch);
-        // dst address, MACs and checksums: bytes 0-47, and the TCP checksum
-        return rw ? (proto == 6 ? 0xFu : 0x7u) : 0u;
+        // dst address, MACs and checksums change bytes 0-47 (and the TCP
+        // checksum 50-51): the whole 64-byte slot is stored back, since a
+        // partial-line write costs more than a whole one
+        return rw ? 0xFu : 0u;
       },
       bins, TileQueue{}, cur);
 }

@@ -739,7 +739,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
           f.w[1] = a.wan_macw1;
           f.w[2] = a.wan_macw2;
           a.out[p] = (uint16_t)a.wan;
-          smask = proto == 6 ? 0xFu : 0x7u;  // the TCP checksum (bytes 50-51): chunk 3
+          smask = 0xFu;  // bytes 0-47 (and the TCP checksum 50-51): the whole first 64 B
         }
       } else {
         bool m = false;
@@ -751,7 +751,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
         const uint32_t k = group_reserve(cur, kCurReprobe, v);
         if (v) rq.ent[(size_t)rb * per_b * 64 + k] = p;
         if (v) touch = kNone;
-        smask = m ? ((f.w[5] >> 24) == 6 ? 0xFu : 0x7u) : 0u;
+        smask = m ? 0xFu : 0u;  // (whole 64-byte pieces: no partial-sector writes)
       }
       bins_put(bins, cur, rb, per_b * 64, range0, p, touch);
       // the changed header chunks of the rewritten frames, four lanes per
@@ -1218,7 +1218,7 @@ __global__ __launch_bounds__(256, 4) void nat_remote64(NatArgs a, uint32_t n_all
           return 0u;
         }
         nat_lan_fast(a, f, p, P.idx);
-        return (f.w[5] >> 24) == 6 ? 0xFu : 0x7u;
+        return 0xFu;  // the whole slot: whole-line writes
       },
       bins, TileQueue{}, cur);
 }
