@@ -561,7 +561,8 @@ __device__ __forceinline__ uint32_t dense128_tail(const uint4 d[8], uint32_t end
 // cooperative bucket-row gather, branch-free match, rewrite and checksums in
 // registers, (64-byte slots) the whole tile stored back (packets left for
 // phase B or the reprobe walk are stored unchanged). Any other tile runs
-// nat_issue / nat_finish per lane. Owner mode always takes the per-lane path.
+// nat_issue / nat_finish per lane. Owner mode's pass 1 has a lean tile of its
+// own (keys of other ranks routed, this rank's looked up).
 template <uint32_t G, uint32_t H = 1, bool D = false>
 __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins bins,
                                           TileQueue rq) {
@@ -582,6 +583,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   const uint32_t first = a.p0 & ~63u;
   const uint32_t tiles = (a.p1 - first + 63) / 64;
   const bool lean_ok = a.own.n == 0 && rq.ent != nullptr;
+  const bool lean_own = G == 0 && a.own.n != 0 && rq.ent != nullptr;  // owner pass 1
   const uint32_t slot = G ? a.slot : 64u;
   const uint32_t lim = slot - 14;  // total_length bound of the register path
   // byte offset in the tile of chunk c (packet c / 4, part c % 4)
@@ -832,6 +834,85 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
         a.out[p] = (uint16_t)a.wan;
       }
       store_all = true;
+    } else if (lean_own && __ballot(mine && nat_lan_fast_ok(a, f, in, ln)) == ~0ull) {
+      // ---- owner mode, pass 1, every lane a fast-path LAN packet: keys
+      // another rank owns leave for their owner (nat_route); this rank's are
+      // looked up as in the lean tile above and their frames rewritten
+      const uint32_t proto = f.w[5] >> 24;
+      const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
+      const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
+      const uint32_t h = flowid_hash_batched(T, sp, dp, sip, dip, in, proto);
+      const uint32_t o = owner_of(h, a.own.n);
+      const bool routed = o != a.own.r || a.own.all;
+      const uint32_t b = routed ? kNone : home_bucket(h, a.t.bmask, a.t.mix, nat_lin(T));
+      uint32_t b0, b1, b2, b3;
+      const uint32_t src = lane & ~3u;  // byte address of lane L / 4
+      asm volatile("ds_bpermute_b32 %0, %1, %2" : "=v"(b0) : "v"(src), "v"(b));
+      asm volatile("ds_bpermute_b32 %0, %1, %2 offset:64" : "=v"(b1) : "v"(src), "v"(b));
+      asm volatile("ds_bpermute_b32 %0, %1, %2 offset:128" : "=v"(b2) : "v"(src), "v"(b));
+      asm volatile("ds_bpermute_b32 %0, %1, %2 offset:192" : "=v"(b3) : "v"(src), "v"(b));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
+      // a routed packet's lanes read bucket 0 (an L1 hit) and ignore it: a
+      // conditional load here became a load through a selected address
+      // (flat, with a zero row in scratch memory)
+      const uint32_t part = lane & 3;
+      const uint4 q0 = rows[4 * (size_t)(b0 != kNone ? b0 : 0u) + part];
+      const uint4 q1 = rows[4 * (size_t)(b1 != kNone ? b1 : 0u) + part];
+      const uint4 q2 = rows[4 * (size_t)(b2 != kNone ? b2 : 0u) + part];
+      const uint4 q3 = rows[4 * (size_t)(b3 != kNone ? b3 : 0u) + part];
+      if (tile + tstep < tend) fetch(tile + tstep);
+      wave_lds_sync();
+      S[chunk_swz(lane)] = q0;
+      S[chunk_swz(64 + lane)] = q1;
+      S[chunk_swz(128 + lane)] = q2;
+      S[chunk_swz(192 + lane)] = q3;
+      wave_lds_sync();
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) row[k] = S[chunk_swz(4 * lane + k)];
+      const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
+      bool m = false;
+      uint32_t t1 = kRouted;
+      if (routed) {
+        nat_route(a, p, h, key);
+      } else {
+        bool done;
+        const uint32_t idx = bucket_match_sel(row, key, &done);
+        t1 = !done ? kReprobe : idx;  // kNone: a new flow, phase B
+        if (done & (idx == kNone)) a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
+        if (done & (idx != kNone)) {
+          f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
+          f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
+          fast_checksums(f, proto, bswap16((uint16_t)(f.w[4] & 0xFFFF)));
+          f.w[0] = a.wan_macw0;
+          f.w[1] = a.wan_macw1;
+          f.w[2] = a.wan_macw2;
+          a.out[p] = (uint16_t)a.wan;
+          m = true;
+        }
+      }
+      touch = route_note(a, p, t1);  // (the touch log is off in owner pass 1)
+      {  // queue on this block's reprobe slice
+        const bool v = touch == kReprobe;
+        const uint32_t k = group_reserve(cur, kCurReprobe, v);
+        if (v) rq.ent[(size_t)rb * per_b * 64 + k] = p;
+      }
+      touch = kNone;
+      // the rewritten frames only (pass 2 rewrites the routed ones), whole slots
+      store_all = false;
+      const uint64_t mm = __ballot(m);
+      if (mm) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+          S[chunk_swz(4 * lane + k)] =
+              make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
+        wave_lds_sync();
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+          const uint32_t c = 64 * j + lane;
+          if ((mm >> (c >> 2)) & 1ull) tile_st(g, c, S[chunk_swz(c)]);
+        }
+      }
+      wave_lds_sync();  // the next tile overwrites S
     } else {
       // ---- per-lane tile (nat_issue / nat_finish)
       const NatPend pend = nat_issue(a, T, p, f, in, ln, mine);
