@@ -12,7 +12,8 @@ import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-LIB_PATH = os.path.join(PKG, "libvigpath.so")
+# VIGPATH_LIB: another build of the same ABI, for diagnostics (A/B builds)
+LIB_PATH = os.environ.get("VIGPATH_LIB") or os.path.join(PKG, "libvigpath.so")
 MAX_DEV = 32
 FLOOD_FRAME = 0xFFFF
 
