@@ -287,9 +287,15 @@ int vp_table_stats_get(vp_ctx *ctx, int table, vp_table_stats *out);
  * ("" if none was recorded). The text stays until the thread's next failure. */
 const char *vp_last_error(void);
 
-/* Per-context kernel timing of the last vp_process_device call: time of the
- * dominant classification kernel in ms (HIP events on the stream it ran on),
- * summed over its launches, and the number of launches. */
+/* Per-context kernel timing (diagnostics, off by default): with on != 0,
+ * every vp_process_device call brackets its classification kernel launches
+ * with HIP events on the stream they run on (about 6 us of kernel-boundary
+ * time per call). */
+int vp_kernel_timing(vp_ctx *ctx, int on);
+
+/* Kernel timing of the last vp_process_device call: time of the dominant
+ * classification kernel in ms, summed over its launches (0 while
+ * vp_kernel_timing is off), and the number of launches. */
 int vp_last_kernel_ms(vp_ctx *ctx, float *ms, int *launches);
 
 /* Build identification (e.g. "vigpath gfx950"). */

@@ -37,19 +37,30 @@ def to_dev(tr, dev):
 
 
 def run(nf, batches, B, dev):
+    """Step rate over the first half of `batches` (no timing events), kernel
+    rate over the second half (each classify launch between HIP events)."""
+    half = len(batches) // 2
     out = torch.zeros(B, dtype=torch.int16, device=dev)
-    kms = []
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for fr, ln, dv, t in batches:
-        nf.process_device(fr, ln, dv, out, SLOT, now0=t, now_step=1)
-        kms.append(nf.last_kernel_ms())
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    n = B * len(batches)
-    kernel_s = sum(m for m, _ in kms) / 1e3
+
+    def timed(part):
+        kms = []
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for fr, ln, dv, t in part:
+            nf.process_device(fr, ln, dv, out, SLOT, now0=t, now_step=1)
+            kms.append(nf.last_kernel_ms())
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, kms
+
+    nf.kernel_timing(False)
+    el, _ = timed(batches[:half])
+    nf.kernel_timing(True)
+    _, kms = timed(batches[half:])
+    nf.kernel_timing(False)
+    kernel_s = max(1e-12, sum(m for m, _ in kms) / 1e3)
     launches = sum(k for _, k in kms)
-    return n / el / 1e6, n / launches / (kernel_s / launches) / 1e6, out
+    n = B * half
+    return n / el / 1e6, B * (len(batches) - half) / kernel_s / 1e6, out
 
 
 def cpu_rate(kind, cfg, warm, sample, statics=None):
@@ -78,10 +89,10 @@ def bench_bridge(args, dev, flood):
     run(br, warm, B, dev)
     warm_s = time.perf_counter() - t0
     base = len(warm) * B
-    batches = [to_dev(gen(base + k * B), dev) for k in range(args.steps)]
+    batches = [to_dev(gen(base + k * B), dev) for k in range(2 * args.steps)]
     if os.environ.get("BENCH_NF_SAME"):  # diagnostics: one batch's frames every step
         fr0 = batches[0]
-        batches = [(fr0[0], fr0[1], fr0[2], fr0[3] + k * B) for k in range(args.steps)]
+        batches = [(fr0[0], fr0[1], fr0[2], fr0[3] + k * B) for k in range(2 * args.steps)]
     mpps, kmpps, out = run(br, batches, B, dev)
     ocfg = orc.BridgeCfg(expiration_time=60_000_000, dyn_capacity=N, n_devices=2)
     cpu = None
@@ -119,7 +130,7 @@ def bench_lb(args, dev):
     run(lb, warm, B, dev)
     warm_s = time.perf_counter() - t0
     base = len(warm) * B
-    batches = [to_dev(gen(base + k * B), dev) for k in range(args.steps)]
+    batches = [to_dev(gen(base + k * B), dev) for k in range(2 * args.steps)]
     mpps, kmpps, out = run(lb, batches, B, dev)
     cpu = None
     if not args.no_cpu:
@@ -155,7 +166,7 @@ def bench_fw(args, dev):
     run(fw, warm, B, dev)
     warm_s = time.perf_counter() - t0
     base = len(warm) * B
-    batches = [to_dev(gen(base + k * B, 4), dev) for k in range(args.steps)]
+    batches = [to_dev(gen(base + k * B, 4), dev) for k in range(2 * args.steps)]
     mpps, kmpps, out = run(fw, batches, B, dev)
     cpu = None
     if not args.no_cpu:
@@ -189,7 +200,7 @@ def bench_pol(args, dev):
     run(pol, warm, B, dev)
     warm_s = time.perf_counter() - t0
     base = len(warm) * B
-    batches = [to_dev(gen(base + k * B), dev) for k in range(args.steps)]
+    batches = [to_dev(gen(base + k * B), dev) for k in range(2 * args.steps)]
     mpps, kmpps, out = run(pol, batches, B, dev)
     cpu = None
     if not args.no_cpu:

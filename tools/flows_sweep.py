@@ -25,6 +25,7 @@ for nf in SIZES:
         cfg = vigor_amd.nat_config_from_args(
             bench.NAT_ARGS + ["--max-flows", str(nf)], 2, bench.DEV_MACS)
         nat = vigor_amd.Nat(cfg, 0, libpath=lp)
+        nat.kernel_timing(True)
         bank = bench.FlowBank(nf, 0, dev)
         start = 0
         ms = []

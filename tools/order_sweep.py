@@ -46,6 +46,7 @@ def main():
         cfg = vigor_amd.nat_config_from_args(
             bench.NAT_ARGS + ["--max-flows", str(NF)], 2, bench.DEV_MACS)
         nat = vigor_amd.Nat(cfg, 0, libpath=lp)
+        nat.kernel_timing(True)
         fill(bank, buf, 0, "rr")  # warm-up: every flow allocated
         nat.process_device(buf, lens, ind, out, 64, now0=T.NOW0, now_step=1)
         start = B

@@ -117,7 +117,7 @@ EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_fw_create",
            "vp_process_host", "vp_process_host_batch", "vp_nat_dump", "vp_bridge_dump", "vp_lb_dump",
            "vp_fw_dump", "vp_comm_unique_id", "vp_attach_rccl",
            "vp_attach_comm", "vp_shard_mode", "vp_sync_state", "vp_live_count",
-           "vp_last_kernel_ms", "vp_version", "vp_table_stats_get",
+           "vp_kernel_timing", "vp_last_kernel_ms", "vp_version", "vp_table_stats_get",
            "vp_last_error"]
 
 _libs = {}
@@ -188,6 +188,8 @@ def lib(path: str | None = None):
     L.vp_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float),
                                     C.POINTER(C.c_int)]
     L.vp_last_kernel_ms.restype = C.c_int
+    L.vp_kernel_timing.argtypes = [C.c_void_p, C.c_int]
+    L.vp_kernel_timing.restype = C.c_int
     L.vp_table_stats_get.argtypes = [C.c_void_p, C.c_int, C.POINTER(TableStatsC)]
     L.vp_table_stats_get.restype = C.c_int
     L.vp_last_error.argtypes = []

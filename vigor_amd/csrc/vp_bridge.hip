@@ -353,15 +353,15 @@ static int bridge_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // (still zero after a segment that learned nothing: no reset launch)
   if (!t.ctl_clean) VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. touch_ovf
   t.ctl_clean = false;
-  VP_HIP(hipEventRecord(c->ev0, c->stream));
+  VP_HIP(ev_record(c->ktime, c->ev0, c->stream));
   BridgeArgs a1 = a;
   if (bp.on) a1.log = nullptr;
   bridge_classify<<<grid, 256, 0, c->stream>>>(a1, bp.bins);
   VP_HIP(hipGetLastError());
-  VP_HIP(hipEventRecord(c->ev1, c->stream));
+  VP_HIP(ev_record(c->ktime, c->ev1, c->stream));
   VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, c->seq));
   float kms = 0.f;
-  VP_HIP(event_ms(c->ev0, c->ev1, &kms));
+  VP_HIP(ev_ms(c->ktime, c->ev0, c->ev1, &kms));
   *ms += kms;
   *launches += 1;
   const bool ovf = bp.on && t.h_ctl.touch_ovf != 0;

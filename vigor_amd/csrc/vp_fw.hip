@@ -416,7 +416,7 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // (still zero after a segment that queued nothing: no reset launch)
   if (!t.ctl_clean) VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
   t.ctl_clean = false;
-  VP_HIP(hipEventRecord(c->ev0, c->stream));
+  VP_HIP(ev_record(c->ktime, c->ev0, c->stream));
   if (p1 > p0) {
     if (tiles64) {
       FwArgs a64 = a;
@@ -427,7 +427,7 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     }
     VP_HIP(hipGetLastError());
   }
-  VP_HIP(hipEventRecord(c->ev1, c->stream));
+  VP_HIP(ev_record(c->ktime, c->ev1, c->stream));
   // phase A's counts, and the fold of its touches behind them; queued
   // packets follow as late touches
   VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, seq0));
@@ -446,7 +446,7 @@ static int fw_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     VP_TRY(tbl_late_touches(c, t, bp.bins.oent, bp.bins.ocnt, 0, range64, grid64,
                             w.log, now, seq0));
   float kms = 0.f;
-  VP_HIP(event_ms(c->ev0, c->ev1, &kms));
+  VP_HIP(ev_ms(c->ktime, c->ev0, c->ev1, &kms));
   *ms += kms;
   *launches += 1;
   const uint32_t nmiss = t.h_ctl.miss_count, ndefer = t.h_ctl.defer_count;

@@ -34,6 +34,16 @@ int state_fail(const char *fmt, ...);
 // latency to every batch's control-block read-back.
 hipError_t stream_wait(hipStream_t s);
 hipError_t event_ms(hipEvent_t a, hipEvent_t b, float *ms);
+// Per-launch kernel timing (vp_kernel_timing): the classify launch between
+// two events, summed into vp_last_kernel_ms. Off by default: the events cost
+// a step about 6 us of kernel-boundary time.
+inline hipError_t ev_record(bool on, hipEvent_t e, hipStream_t s) {
+  return on ? hipEventRecord(e, s) : hipSuccess;
+}
+inline hipError_t ev_ms(bool on, hipEvent_t a, hipEvent_t b, float *ms) {
+  *ms = 0.f;
+  return on ? event_ms(a, b, ms) : hipSuccess;
+}
 // Host-side stage clock (VIGPATH_HOSTPROF=1, diagnostics): hostprof(k)
 // stamps stage k of the current call; the call's stamps go to stderr.
 void hostprof(int k);
@@ -228,6 +238,7 @@ struct vp_ctx {
   // (results complete): run_batch returns without waiting for it.
   bool fold_pending = false;
   float last_ms = 0.f;
+  bool ktime = false;  // vp_kernel_timing: events around the classify launch
   int last_launches = 0;
   uint64_t seq = 0;       // packets processed so far (global packet order)
   int64_t last_now = -1;  // time of the last packet processed

@@ -628,7 +628,7 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   c->ft.ctl_clean = false;
   BinsPlan bp{};
   const bool tiles64 = b->slot == 64 && c->coalesced_io;
-  VP_HIP(hipEventRecord(c->ev0, c->stream));
+  VP_HIP(ev_record(c->ktime, c->ev0, c->stream));
   if (tiles64) {
     // the flow touches also go to the touch bins (the log stays complete:
     // the rounds below refold it whenever a queue is non-empty)
@@ -641,7 +641,7 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     lb_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
   }
   VP_HIP(hipGetLastError());
-  VP_HIP(hipEventRecord(c->ev1, c->stream));
+  VP_HIP(ev_record(c->ktime, c->ev1, c->stream));
   a.hbl = nullptr;  // re-classification rounds list no heartbeat twice
   if (bp.on) {
     // optimistic fold; its first thread publishes phase A's counts (the flow
@@ -662,7 +662,7 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     VP_TRY(read_ctl2_wait(c, c->ft2, c->ft));
   }
   float kms = 0.f;
-  VP_HIP(event_ms(c->ev0, c->ev1, &kms));
+  VP_HIP(ev_ms(c->ktime, c->ev0, c->ev1, &kms));
   *ms += kms;
   *launches += 1;
   const uint32_t nm = c->ft.h_ctl.miss_count, ns = c->ft.h_ctl.defer_count;

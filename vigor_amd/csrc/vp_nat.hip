@@ -1470,7 +1470,7 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
 
   VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
   VP_HIP(hipMemsetAsync(w.ovf64, 0, 8, c->stream));
-  VP_HIP(hipEventRecord(c->ev0, c->stream));
+  VP_HIP(ev_record(c->ktime, c->ev0, c->stream));
   pm.mark();
   if (np) {
     if (ph->tiles64) {
@@ -1486,7 +1486,7 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   } else {
     VP_HIP(hipMemsetAsync(w.dcnt, 0, sizeof(uint32_t) * slices, c->stream));
   }
-  VP_HIP(hipEventRecord(c->ev1, c->stream));
+  VP_HIP(ev_record(c->ktime, c->ev1, c->stream));
   pm.mark();
   // C1 over the padded exchange, no host round trip: owner o's keys go to
   // [o C, (o + 1) C) of the send buffer, the per-owner counts cross in their
@@ -1528,9 +1528,9 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
     VP_HIP(hipGetLastError());
     return 0;
   };
-  VP_HIP(hipEventRecord(c->ev2, c->stream));
+  VP_HIP(ev_record(c->ktime, c->ev2, c->stream));
   VP_TRY(pass2());
-  VP_HIP(hipEventRecord(c->ev3, c->stream));
+  VP_HIP(ev_record(c->ktime, c->ev3, c->stream));
   pm.mark();
   VP_TRY(tbl_fold_read_ctl(c, t, ph->bp, w.log, p0, p1, now, seq0, w.dtot));
   pm.mark();
@@ -1540,8 +1540,8 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
     if (o != r) maxsend = std::max(maxsend, w.h_gath[kPubGath * n + o]);
   c->own_maxsend = maxsend;
   float k1 = 0.f, k2 = 0.f;
-  VP_HIP(event_ms(c->ev0, c->ev1, &k1));
-  VP_HIP(event_ms(c->ev2, c->ev3, &k2));
+  VP_HIP(ev_ms(c->ktime, c->ev0, c->ev1, &k1));
+  VP_HIP(ev_ms(c->ktime, c->ev2, c->ev3, &k2));
   ph->ms = k1 + k2;
   if (!t.h_ctl.route_ovf) return 0;
   // Some rank had more keys for an owner than C (every rank sees the flag):
@@ -1579,11 +1579,11 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
       tbl_dev(t), c->crc_tab, w.recvk, (uint32_t)R, 0, nullptr, nullptr, t.ctl, w.reply);
   VP_HIP(hipGetLastError());
   VP_TRY(m.alltoallv_dev(c, w.reply, fr.data(), w.rreply, fa.data()));
-  VP_HIP(hipEventRecord(c->ev2, c->stream));
+  VP_HIP(ev_record(c->ktime, c->ev2, c->stream));
   VP_TRY(pass2());
-  VP_HIP(hipEventRecord(c->ev3, c->stream));
+  VP_HIP(ev_record(c->ktime, c->ev3, c->stream));
   VP_TRY(tbl_fold_read_ctl(c, t, ph->bp, w.log, p0, p1, now, seq0, w.dtot));
-  VP_HIP(event_ms(c->ev2, c->ev3, &k2));
+  VP_HIP(ev_ms(c->ktime, c->ev2, c->ev3, &k2));
   ph->ms += k2;
   return 0;
 }
@@ -1647,15 +1647,20 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     if (tiles64) {
       NatArgs a64 = a;
       if (bp.on) a64.log = nullptr;  // touches go to the bins only
-      VP_HIP(launch_timed(tk, grid64, 256, c->stream, c->ev0, c->ev1, a64,
-                          (uint32_t)b->n, bp.bins, rq));
+      if (c->ktime) {
+        VP_HIP(launch_timed(tk, grid64, 256, c->stream, c->ev0, c->ev1, a64,
+                            (uint32_t)b->n, bp.bins, rq));
+      } else {
+        tk<<<grid64, 256, 0, c->stream>>>(a64, (uint32_t)b->n, bp.bins, rq);
+        VP_HIP(hipGetLastError());
+      }
     } else {
       VP_HIP(launch_timed(nat_classify, grid_for(p1 - p0), 256, c->stream, c->ev0,
                           c->ev1, a));
     }
   } else {
-    VP_HIP(hipEventRecord(c->ev0, c->stream));
-    VP_HIP(hipEventRecord(c->ev1, c->stream));
+    VP_HIP(ev_record(c->ktime, c->ev0, c->stream));
+    VP_HIP(ev_record(c->ktime, c->ev1, c->stream));
   }
   // Phase A's counts for the host, and the fold of its touches right away;
   // the packets it queued (reprobes, overflowed bin entries, phase B/C) are
@@ -1664,7 +1669,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   hostprof(2);
   VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, seq0));
   hostprof(4);
-  VP_HIP(event_ms(c->ev0, c->ev1, &ph.ms));
+  VP_HIP(ev_ms(c->ktime, c->ev0, c->ev1, &ph.ms));
   hostprof(5);
   }  // !owner
   a.own.n = 0;  // below: this rank's own table only

@@ -495,7 +495,7 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   c->pol_cnt_clean = false;
   const uint32_t epoch = ++t.pub_epoch;  // phase A's counts, published by pol_runs
   const PubArgs pub{t.d_pub, t.ctl, epoch, nullptr, nullptr, 0, 0};
-  VP_HIP(hipEventRecord(c->ev0, c->stream));
+  VP_HIP(ev_record(c->ktime, c->ev0, c->stream));
   if (b->slot == 64 && c->coalesced_io) {
     const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
     pol_classify64<<<resident_grid((const void *)pol_classify64, (tiles + 3) / 4), 256, 0,
@@ -504,7 +504,7 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     pol_classify<<<grid_for(n), 256, 0, c->stream>>>(a);
   }
   VP_HIP(hipGetLastError());
-  VP_HIP(hipEventRecord(c->ev1, c->stream));
+  VP_HIP(ev_record(c->ktime, c->ev1, c->stream));
   if (grouping && c->pol_runs) {  // phase T, grouping path with per-index
     // run slots (phase A wrote them): no scan, no scatter
     pol_runs<<<grid_for(t.cap), 256, 0, c->stream>>>(a, c->pol_cnt, nullptr, c->pol_runs,
@@ -530,7 +530,7 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   else
     VP_TRY(read_ctl(c, t));
   float kms = 0.f;
-  VP_HIP(event_ms(c->ev0, c->ev1, &kms));
+  VP_HIP(ev_ms(c->ktime, c->ev0, c->ev1, &kms));
   *ms += kms;
   *launches += 1;
   const uint32_t nmiss = t.h_ctl.miss_count, ndefer = t.h_ctl.defer_count;

@@ -831,6 +831,12 @@ int vp_table_stats_get(vp_ctx *c, int table, vp_table_stats *out) {
 
 const char *vp_last_error(void) { return vp::g_last_error; }
 
+int vp_kernel_timing(vp_ctx *c, int on) {
+  if (!c) return VP_EINVAL;
+  c->ktime = on != 0;
+  return 0;
+}
+
 int vp_last_kernel_ms(vp_ctx *c, float *ms, int *launches) {
   if (!c || !ms || !launches) return VP_EINVAL;
   *ms = c->last_ms;

@@ -80,6 +80,12 @@ class NfBase:
         """Multi-GPU: merge the ranks' timestamps (collective)."""
         _check(self.L.vp_sync_state(self.h), "vp_sync_state")
 
+    def kernel_timing(self, on: bool = True):
+        """Bracket every classification kernel launch with HIP events
+        (vp_kernel_timing; off by default: the events cost a step about 6 us),
+        so that last_kernel_ms() reports its time."""
+        _check(self.L.vp_kernel_timing(self.h, 1 if on else 0), "vp_kernel_timing")
+
     def last_kernel_ms(self):
         if not hasattr(self, "_kms"):  # (built once: called every batch)
             ms, k = C.c_float(), C.c_int()
