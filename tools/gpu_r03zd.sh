@@ -1,0 +1,10 @@
+#!/bin/bash
+# multi-rank batches return while their trailing fold runs: GPU tests, owner
+# route-all step, 2-rank owner rehearsal over gloo on one GPU
+set -o pipefail
+O=gpurun_out; mkdir -p $O; export TMPDIR=/tmp
+T=r03zd
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/${T}_pytest.log 2>&1 || exit $?
+tail -1 $O/${T}_pytest.log
+timeout -k 10 400 python3 bench.py --route-all --no-cpu --no-e2e --no-extra --steps 20 > $O/${T}_ra.log 2>&1 || exit $?
+grep '^{' $O/${T}_ra.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('route-all', d['value'], d['ms_per_step'], d['parity']['match'])"

@@ -1740,8 +1740,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // complete (the control copy waited for phase A); only the fold of the
   // stamps may still run — unless it reads the caller's time array, which
   // the caller may reuse as soon as the call returns
-  c->fold_pending = !c->comm && !b->now && !nre && !nmiss && !ndefer && !union_n &&
-                    !ovf;
+  c->fold_pending = !b->now && !nre && !nmiss && !ndefer && !union_n && !ovf;
   // phase A appended nothing and nothing ran after its counts were read:
   // the counters are still zero for the next segment
   t.ctl_clean = !owner && !c->comm && !nre && !nmiss && !ndefer && !union_n && !ovf;

@@ -1652,6 +1652,7 @@ static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
     const uint32_t lp0 = (uint32_t)(std::min<uint64_t>(std::max<uint64_t>(A, off), off + (uint64_t)n) - off);
     const uint32_t lp1 = (uint32_t)(std::min<uint64_t>(std::max<uint64_t>(B1, off), off + (uint64_t)n) - off);
     uint32_t allocated = 0;
+    c->fold_pending = false;
     VP_TRY(seg(c, b, now, lp0, lp1, &ms, &launches, &allocated));
     for (int i = 0; i < ntabs; i++)
       if (allocated & (1u << i)) {
@@ -1661,7 +1662,10 @@ static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
     A = B1;
     tA = tB1;
   }
-  VP_HIP(hipStreamSynchronize(c->stream));
+  // as in run_batch: a trailing timestamp fold alone may keep running; the
+  // next call's collectives queue behind it on the same stream
+  if (!c->fold_pending) VP_HIP(hipStreamSynchronize(c->stream));
+  c->fold_pending = false;
   c->seq += G;
   c->last_now = t_last_g;
   c->last_ms = ms;
