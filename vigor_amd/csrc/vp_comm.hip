@@ -22,14 +22,29 @@ static int nccl_fail(ncclResult_t e, const char *what) {
     if (e_ != ncclSuccess) return nccl_fail(e_, #call); \
   } while (0)
 
-// RCCL on device buffers; host variants stage through a device buffer.
+// RCCL on device buffers; host variants stage through a page-locked host
+// buffer and a device buffer (a copy from pageable memory is staged by the
+// runtime synchronously: the per-batch RankInfo gather spent ~30 us in
+// its two copies).
 struct RcclComm : Comm {
   ncclComm_t comm = nullptr;
   void *stage = nullptr;
   size_t stage_bytes = 0;
+  uint8_t *hstage = nullptr;
+  size_t hstage_bytes = 0;
   ~RcclComm() override {
     if (comm) ncclCommDestroy(comm);
     if (stage) hipFree(stage);
+    if (hstage) hipHostFree(hstage);
+  }
+  int reserve_host(size_t bytes) {
+    if (bytes <= hstage_bytes) return 0;
+    if (hstage) hipHostFree(hstage);
+    hstage = nullptr;
+    hstage_bytes = 0;
+    VP_HIP(hipHostMalloc((void **)&hstage, bytes, hipHostMallocDefault));
+    hstage_bytes = bytes;
+    return 0;
   }
   int reserve(size_t bytes) {
     if (bytes <= stage_bytes) return 0;
@@ -42,12 +57,15 @@ struct RcclComm : Comm {
   }
   int allgather_host(vp_ctx *c, const void *send, void *recv, size_t bytes) override {
     VP_TRY(reserve(bytes * (n + 1)));
-    uint8_t *s = static_cast<uint8_t *>(stage);
-    VP_HIP(hipMemcpyAsync(s, send, bytes, hipMemcpyHostToDevice, c->stream));
+    VP_TRY(reserve_host(bytes * (n + 1)));
+    uint8_t *s = static_cast<uint8_t *>(stage), *h = hstage;
+    memcpy(h, send, bytes);
+    VP_HIP(hipMemcpyAsync(s, h, bytes, hipMemcpyHostToDevice, c->stream));
     VP_NCCL(ncclAllGather(s, s + bytes, bytes, ncclUint8, comm, c->stream));
-    VP_HIP(hipMemcpyAsync(recv, s + bytes, bytes * n, hipMemcpyDeviceToHost,
+    VP_HIP(hipMemcpyAsync(h + bytes, s + bytes, bytes * n, hipMemcpyDeviceToHost,
                           c->stream));
     VP_HIP(hipStreamSynchronize(c->stream));
+    memcpy(recv, h + bytes, bytes * n);
     return 0;
   }
   int allgather_dev(vp_ctx *c, const void *send, void *recv, size_t bytes) override {

@@ -196,6 +196,7 @@ struct Workspace {
   // capacity-overflow flag
   uint32_t *rcnt = nullptr;
   uint64_t *ovf64 = nullptr;
+  bool ovf64_clean = false;  // ovf64 is zero (the last exchange did not overflow)
   // multi-GPU: the ranks' segment counters gathered on the device before a
   // fold (kPubGath words each) and their host copy (gath_ok: this segment's)
   uint32_t *gath = nullptr;

@@ -1468,8 +1468,12 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   a.own = Route{n, r, w.desc, w.dcnt, w.route, nullptr, first, ph->range1, w.dbase,
                 w.rreply, C, w.ovf64, route_all};
 
-  VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
-  VP_HIP(hipMemsetAsync(w.ovf64, 0, 8, c->stream));
+  // (counters still zero after a segment that appended nothing, and the
+  // overflow flag after an exchange that fit: no reset launches)
+  if (!t.ctl_clean) VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
+  t.ctl_clean = false;
+  if (!w.ovf64_clean) VP_HIP(hipMemsetAsync(w.ovf64, 0, 8, c->stream));
+  w.ovf64_clean = false;
   VP_HIP(ev_record(c->ktime, c->ev0, c->stream));
   pm.mark();
   if (np) {
@@ -1543,6 +1547,7 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   VP_HIP(ev_ms(c->ktime, c->ev0, c->ev1, &k1));
   VP_HIP(ev_ms(c->ktime, c->ev2, c->ev3, &k2));
   ph->ms = k1 + k2;
+  w.ovf64_clean = !t.h_ctl.route_ovf;  // (every rank's flag was 0: allreduced)
   if (!t.h_ctl.route_ovf) return 0;
   // Some rank had more keys for an owner than C (every rank sees the flag):
   // pass 2 answered none of the routed packets; the exact exchange does,
@@ -1743,7 +1748,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   c->fold_pending = !b->now && !nre && !nmiss && !ndefer && !union_n && !ovf;
   // phase A appended nothing and nothing ran after its counts were read:
   // the counters are still zero for the next segment
-  t.ctl_clean = !owner && !c->comm && !nre && !nmiss && !ndefer && !union_n && !ovf;
+  t.ctl_clean = !nre && !nmiss && !ndefer && !union_n && !ovf;
   return 0;
 }
 
