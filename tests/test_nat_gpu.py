@@ -308,7 +308,8 @@ def test_lean_tiles(max_flows, n_flows, expire_us, mix, monkeypatch):
 
 def test_prepared_device_step():
     """Nat.device_step (the bench's prepared C-ABI call over fixed buffers,
-    affine time) gives what the oracle gives, batch after batch."""
+    affine time) gives what the oracle gives, batch after batch, with the
+    per-launch timing events (vp_kernel_timing) off, on and off again."""
     import torch
     nf = 1 << 12
     nat, o = make_pair(max_flows=nf)
@@ -320,6 +321,7 @@ def test_prepared_device_step():
     o_t = torch.zeros(B, dtype=torch.int16, device=d)
     step = nat.device_step(f_t, l_t, i_t, o_t, 64)
     for j in range(3):
+        nat.kernel_timing(j == 1)
         fr, ln, dv, now = T.nat_lan_trace(B, nf + 100, start=j * B)
         f_t.copy_(torch.from_numpy(fr))
         l_t.copy_(torch.from_numpy(ln.view(np.int16)))
@@ -328,6 +330,8 @@ def test_prepared_device_step():
         exp_out = o.run(exp, ln, dv, now, 64)
         step(int(now[0]), 1)
         torch.cuda.synchronize()
+        ms, launches = nat.last_kernel_ms()
+        assert launches >= 1 and (ms > 0) == (j == 1), (j, ms, launches)
         assert np.array_equal(o_t.cpu().numpy().view(np.uint16), exp_out)
         assert np.array_equal(f_t.cpu().numpy(), exp)
     check_state(nat, o, nf)

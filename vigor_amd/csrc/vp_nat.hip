@@ -1105,9 +1105,13 @@ __global__ __launch_bounds__(256) void nat_reprobe(NatArgs a, const uint32_t *li
 // answers come back in the same order, and pass 2 finishes the packets.
 
 // Per owner o (one block each): exclusive scan over blocks of dcnt[.][o].
+// The padded exchange (cap > 0): owner o's chunk is [o cap, (o + 1) cap), and
+// a count past cap sets *ovf (every rank then takes the exact exchange,
+// DESIGN.md §6); cap == 0: offsets inside the owner's chunk (route_base).
 __global__ __launch_bounds__(256) void route_scan(const uint32_t *dcnt, uint32_t nblk,
                                                   uint32_t n, uint32_t *dbase,
-                                                  uint32_t *dtot) {
+                                                  uint32_t *dtot, uint32_t cap,
+                                                  uint64_t *ovf) {
   __shared__ uint32_t part[256];
   const uint32_t o = blockIdx.x;
   const uint32_t per = (nblk + 255) / 256;
@@ -1124,9 +1128,10 @@ __global__ __launch_bounds__(256) void route_scan(const uint32_t *dcnt, uint32_t
       acc += v;
     }
     dtot[o] = acc;
+    if (cap && acc > cap) *ovf = 1;
   }
   __syncthreads();
-  uint32_t acc = part[threadIdx.x];
+  uint32_t acc = part[threadIdx.x] + o * cap;
   for (uint32_t b = b0; b < b1; b++) {
     dbase[(size_t)b * n + o] = acc;
     acc += dcnt[(size_t)b * n + o];
@@ -1142,18 +1147,6 @@ __global__ void route_base(uint32_t *dbase, const uint32_t *dtot, uint32_t nblk,
     uint32_t start = 0;
     for (uint32_t q = 0; q < o; q++) start += dtot[q];
     dbase[x] += start;
-  }
-}
-
-// The padded exchange: owner o's chunk is [o cap, (o + 1) cap); a count
-// past cap sets *ovf (every rank then takes the exact exchange).
-__global__ void route_pad(uint32_t *dbase, const uint32_t *dtot, uint32_t nblk, uint32_t n,
-                          uint32_t cap, uint64_t *ovf) {
-  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nblk * n;
-       x += gridDim.x * blockDim.x) {
-    const uint32_t o = x % n;
-    dbase[x] += o * cap;
-    if (x < n && dtot[x] > cap) *ovf = 1;
   }
 }
 
@@ -1496,9 +1489,8 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   // [o C, (o + 1) C) of the send buffer, the per-owner counts cross in their
   // own small all-to-all, and a count past C (any rank: allreduced) leaves
   // the routed packets to the exact exchange below
-  route_scan<<<n, 256, 0, c->stream>>>(w.dcnt, ph->grid1, n, w.dbase, w.dtot);
-  route_pad<<<grid_for(slices), 256, 0, c->stream>>>(w.dbase, w.dtot, ph->grid1, n, C,
-                                                     w.ovf64);
+  route_scan<<<n, 256, 0, c->stream>>>(w.dcnt, ph->grid1, n, w.dbase, w.dtot, C,
+                                       w.ovf64);
   route_pack<<<ph->grid1, 256, 0, c->stream>>>(w.desc, w.dcnt, w.dbase, n, ph->range1, C,
                                                w.sendk);
   VP_HIP(hipGetLastError());
@@ -1553,7 +1545,8 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   // pass 2 answered none of the routed packets; the exact exchange does,
   // with the sizes learned on the host, then the fold again (pass 1's own
   // touches fold twice, to the same stamps).
-  route_scan<<<n, 256, 0, c->stream>>>(w.dcnt, ph->grid1, n, w.dbase, w.dtot);
+  route_scan<<<n, 256, 0, c->stream>>>(w.dcnt, ph->grid1, n, w.dbase, w.dtot, 0,
+                                       nullptr);
   route_base<<<grid_for(slices), 256, 0, c->stream>>>(w.dbase, w.dtot, ph->grid1, n);
   VP_HIP(hipGetLastError());
   VP_HIP(hipMemcpyAsync(w.h_tot, w.dtot, 4ull * n, hipMemcpyDeviceToHost, c->stream));
