@@ -193,7 +193,7 @@ def cpu_baseline(n_flows: int, sample: int):
         o.run(fr, ln, dv, now, SLOT)
         per = max(1, sample // CPU_SAMPLES)
         pos = n_flows
-        for _ in range(CPU_SAMPLES):
+        for _ in range(CPU_SAMPLES + 1):  # the first sample is a warm-up
             fr, ln, dv, now = T.nat_lan_trace(per, n_flows, start=pos)
             t0 = time.perf_counter()
             o.run(fr, ln, dv, now, SLOT)
@@ -201,7 +201,8 @@ def cpu_baseline(n_flows: int, sample: int):
             pos += per
     finally:
         os.sched_setaffinity(0, mask)
-    return float(np.median(rates)), rates, per * CPU_SAMPLES, core
+    warm, rates = rates[0], rates[1:]
+    return float(np.median(rates)), rates, per * CPU_SAMPLES, core, warm
 
 
 def golden_batch_digest(flows: int, batch: int):
@@ -407,7 +408,7 @@ def main():
             from vigor_amd import shard
             os.environ["VIGPATH_ROUTE_ALL"] = "1"
             uid = (ctypes.c_uint8 * 128).from_buffer_copy(shard.rccl_unique_id())
-            vigor_amd._check(nat.L.vp_attach_rccl(nat.h, uid, 1, 0), "vp_attach_rccl")
+            vigor_amd._check(nat.L.vp_attach_rccl(nat.h, uid, 1, 0), "vp_attach_rccl", nat.L)
             shard.set_mode(nat, "owner")
         if world > 1:  # one vignat over all ranks
             from vigor_amd import shard
@@ -540,12 +541,14 @@ def main():
     if rank == 0:
         cpu = None
         if not args.no_cpu and world == 1 and slot == SLOT:
-            cmpps, rates, sample, core = cpu_baseline(args.flows, args.cpu_sample)
+            cmpps, rates, sample, core, warm = cpu_baseline(args.flows, args.cpu_sample)
             cpu = {"value": round(cmpps, 3), "unit": "Mpps", "cores": 1,
                    "kind": "port",
                    "samples": [round(r, 3) for r in rates],
+                   "warmup_sample": round(warm, 3),
                    "spread": round((max(rates) - min(rates)) / cmpps, 4),
-                   "sample": "median of %d samples, %d steady-state packets in "
+                   "sample": "median of %d samples after one discarded warm-up "
+                             "sample, %d steady-state packets in "
                              "all, of the same trace (64B, %d flows warm, round "
                              "robin); oracle restatement built here -O3 "
                              "-march=native with hardware crc32 (oracle/"

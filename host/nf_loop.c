@@ -16,9 +16,15 @@
  *            u8 frames[n*slot]
  * trace.out: "VPTO" u32 n u32 slot, u16 out_dev[n], u8 frames[n*slot],
  *            "VPTX" u32 txmask[n]: the ports each packet leaves on, as nf.c
- *            dispatches it: none (drop: dst == in), every port but the input
- *            (flood, nf.c:83-96 over rte_eth_dev_count_avail() ports), or
- *            dst (rte_eth_tx_burst). The port count comes from
+ *            dispatches it. Per-packet path (VIGOR_BATCH_SIZE == 1,
+ *            nf.c:158-175): none (drop: dst == in), every port but the input
+ *            (flood(mbuf, VIGOR_DEVICES_COUNT), nf.c:83-96, where
+ *            VIGOR_DEVICES_COUNT = rte_eth_dev_count_avail(), nf.c:57), or
+ *            dst (rte_eth_tx_burst). With --batch and two ports, nf.c's
+ *            batched loop (nf.c:186-209): every packet that is not dropped,
+ *            floods included, goes to port 1 - in. The reference's batched
+ *            loop refuses any other port count (nf.c:179-182); there the
+ *            per-packet dispatch is kept. The port count comes from
  *            VIGPATH_NB_DEVICES (default 2), as in the nf.h shims.
  */
 #include <stdbool.h>
@@ -109,9 +115,13 @@ int main(int argc, char **argv) {
   const char *nd = getenv("VIGPATH_NB_DEVICES");
   const uint32_t nb_devices = nd ? (uint32_t)atoi(nd) : 2u;
   uint32_t *txmask = calloc(n ? n : 1, 4);
+  const bool batch_dispatch = batch != 0 && nb_devices == 2;  /* nf.c:186-209 */
   for (uint32_t i = 0; i < n; i++) {  /* nf.c:158-175 */
     if (out[i] == in_dev[i]) {
       drops++;
+    } else if (batch_dispatch) {  /* mbufs_to_send -> tx_burst(1 - VIGOR_DEVICE) */
+      if (out[i] == FLOOD_FRAME) floods++; else tx++;
+      if (in_dev[i] < 2) txmask[i] = 1u << (1 - in_dev[i]);
     } else if (out[i] == FLOOD_FRAME) {  /* flood(): nf.c:83-96 */
       floods++;
       for (uint32_t d = 0; d < nb_devices && d < 32; d++)

@@ -161,9 +161,45 @@ typedef struct vp_dev_batch {
  * completes entirely before the call returns. */
 int vp_process_device(vp_ctx *ctx, const vp_dev_batch *batch, void *stream);
 
-/* Host-resident batch shaped like a DPDK rx burst: frames[i] -> mbuf data of
- * len[i] bytes (rte_pktmbuf_mtod, nf.c:154), rewritten in place. Staged
- * through pinned memory with hipMemcpyAsync. */
+/* Host memory the GPU may read and write frames in directly: a DPDK mbuf
+ * pool's memory (the hugepages rte_pktmbuf_pool_create, nf.c:235-242, lays
+ * the mbufs out in), registered once after the pool is created. Page-locked
+ * and mapped for the context's GPU (hipHostRegister; memory that is page-
+ * locked already, e.g. hipHostMalloc'd, is only mapped). At most 16 ranges,
+ * not overlapping. vp_unregister_host takes the base passed to
+ * vp_register_host; vp_destroy unregisters what is left. */
+int vp_register_host(vp_ctx *ctx, void *base, size_t bytes);
+int vp_unregister_host(vp_ctx *ctx, void *base);
+
+/* Host-resident batch shaped like DPDK rx bursts (nf.c:186-214): frames[i]
+ * is the data of mbuf i (rte_pktmbuf_mtod, nf.c:154), len[i] its pkt_len,
+ * in_dev[i] its port; every frame is rewritten in place and out_dev[i] gets
+ * nf_process's return value, as calling nf_process on every packet in order
+ * would (nf.c:150-176). Time: now[i], or now0 + i * now_step when now is
+ * NULL (nf.c stamps one polling sweep with one current_time(), nf.c:56).
+ * Frames inside memory registered with vp_register_host are read and written
+ * by the GPU in place, in pipelined chunks: per frame the
+ * first 64 bytes and, for vignat, the bytes its L4 checksum covers cross
+ * PCIe inbound, and the bytes a rewrite can change (the first min(len, 64)
+ * of a frame that is not dropped) outbound. Other frames are gathered and
+ * scattered on the host through pinned staging. Bytes past a frame's length
+ * read as 0 and are never written. Per-packet arrays in page-locked memory
+ * are DMA'd in place. Frames and out_dev hold the results when the call
+ * returns. */
+typedef struct vp_mbuf_batch {
+  uint32_t n;
+  uint8_t *const *frames;
+  const uint16_t *len;
+  const uint16_t *in_dev;
+  const int64_t *now;
+  int64_t now0;
+  int64_t now_step;
+  uint16_t *out_dev;
+} vp_mbuf_batch;
+int vp_process_mbufs(vp_ctx *ctx, const vp_mbuf_batch *batch);
+
+/* The same with a per-packet time array (the batch form of nf_process the
+ * nf.h shims call). */
 int vp_process_batch(vp_ctx *ctx, uint32_t n, const uint16_t *in_dev,
                      uint8_t *const *frames, const uint16_t *len,
                      const int64_t *now, uint16_t *out_dev);

@@ -159,9 +159,12 @@ SHIM_MACS3 = [bytes.fromhex("02000000000%d" % d) for d in range(3)]  # vp_nf_com
 def test_bridge_loop_floods_like_nf_c(tmp_path, batch):
     """host/nf_loop_bridge: nf.c's loop linked against libvigbridge_nf.so.
     vigbridge returns FLOOD_FRAME for unknown and broadcast destinations and
-    nf.c's flood() sends the frame on every port but the input one
-    (nf.c:83-96, 159-166); out ports, frames (never rewritten) and the
-    transmit sets equal the oracle's."""
+    the per-packet path's flood() sends the frame on every port but the input
+    one (flood(mbuf, VIGOR_DEVICES_COUNT), nf.c:83-96, 159-166). With three
+    ports the dispatch is the per-packet path's in both runs: nf.c's batched
+    loop refuses any port count but two (nf.c:179-182), so batch=700 batches
+    only the processing (vp_process_batch). Out ports, frames (never
+    rewritten) and the transmit sets equal the oracle's."""
     rng = np.random.default_rng(6)
     n = 3000 if batch else 400
     fr, ln, dv, now = mixed_bridge_trace(rng, n, 120, n_dev=3)

@@ -111,6 +111,13 @@ class DevBatchC(C.Structure):
                 ("now_step", C.c_int64), ("out_dev", C.c_void_p)]
 
 
+class MbufBatchC(C.Structure):
+    """vp_mbuf_batch (include/vigpath.h): a DPDK-shaped host batch."""
+    _fields_ = [("n", C.c_uint32), ("frames", C.c_void_p), ("len", C.c_void_p),
+                ("in_dev", C.c_void_p), ("now", C.c_void_p), ("now0", C.c_int64),
+                ("now_step", C.c_int64), ("out_dev", C.c_void_p)]
+
+
 # every symbol include/vigpath.h declares
 EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_fw_create",
            "vp_pol_create", "vp_pol_dump", "vp_destroy", "vp_process_device", "vp_process_batch",
@@ -118,7 +125,7 @@ EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_fw_create",
            "vp_fw_dump", "vp_comm_unique_id", "vp_attach_rccl",
            "vp_attach_comm", "vp_shard_mode", "vp_sync_state", "vp_live_count",
            "vp_kernel_timing", "vp_last_kernel_ms", "vp_version", "vp_table_stats_get",
-           "vp_last_error"]
+           "vp_last_error", "vp_register_host", "vp_unregister_host", "vp_process_mbufs"]
 
 _libs = {}
 
@@ -166,6 +173,12 @@ def lib(path: str | None = None):
                                    C.POINTER(C.c_void_p), C.c_void_p,
                                    C.c_void_p, C.c_void_p]
     L.vp_process_batch.restype = C.c_int
+    L.vp_process_mbufs.argtypes = [C.c_void_p, C.POINTER(MbufBatchC)]
+    L.vp_process_mbufs.restype = C.c_int
+    L.vp_register_host.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    L.vp_register_host.restype = C.c_int
+    L.vp_unregister_host.argtypes = [C.c_void_p, C.c_void_p]
+    L.vp_unregister_host.restype = C.c_int
     L.vp_nat_dump.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.vp_nat_dump.restype = C.c_int
     L.vp_bridge_dump.argtypes = [C.c_void_p] * 5
@@ -198,11 +211,20 @@ def lib(path: str | None = None):
     return L
 
 
-def _check(rc: int, what: str):
+_DETAILED = (-5, -12, -71)  # VP_EIO, VP_ENOMEM, VP_ESTATE record vp_last_error()
+
+
+def _check(rc: int, what: str, L=None):
+    """Raise VigpathError for a failing vp_* return code. `L` is the library
+    that made the call (the first one loaded if omitted). Only the codes that
+    record a reason (VP_EIO / VP_ENOMEM / VP_ESTATE) carry vp_last_error():
+    the others record nothing, and the thread's text would belong to an
+    earlier failure."""
     if rc != 0:
         detail = ""
-        L = next(iter(_libs.values()), None)
-        if L is not None:
+        if L is None:
+            L = next(iter(_libs.values()), None)
+        if L is not None and rc in _DETAILED:
             detail = (L.vp_last_error() or b"").decode(errors="replace")
         raise VigpathError(rc, what, detail)
 

@@ -146,8 +146,11 @@ __device__ inline uint16_t finish_l4(uint32_t l4sum, uint32_t ph) {
 }
 
 // nf_set_rte_ipv4_udptcp_checksum (nf-util.c:45-64), generic byte form.
+// `tail`: the raw sum of the frame's bytes past the slot that the L4 sum
+// covers (a 64-byte header slot of a longer host frame, vp_mbuf.hip; the
+// slot's own bytes past 64 read as 0), else 0.
 __device__ inline void set_checksums(const GFrame &f, uint32_t ip,
-                                     uint32_t l4) {
+                                     uint32_t l4, uint32_t tail = 0) {
   f.w16(ip + 10, 0);
   uint8_t proto = f.r8(ip + 9);
   uint32_t at = proto == 6 ? l4 + 16 : l4 + 6;
@@ -157,7 +160,7 @@ __device__ inline void set_checksums(const GFrame &f, uint32_t ip,
     uint16_t c = 0;
     if (l3 >= 20) {
       uint32_t l4len = l3 - 20;
-      c = finish_l4(raw_cksum(f, l4, l4len),
+      c = finish_l4(fold16(raw_sum(f, l4, l4len) + tail),
                     phdr_cksum(f.r32(ip + 12), f.r32(ip + 16), proto, l4len));
     }
     f.w16(at, c);

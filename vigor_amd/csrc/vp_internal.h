@@ -220,7 +220,36 @@ struct Workspace {
   hipEvent_t ev_in[3] = {}, ev_done[3] = {}, ev_out[3] = {};  // per buffer set
   uint8_t *h_meta = nullptr;
   size_t h_meta_bytes = 0;
+  // host frames (vp_process_mbufs, vp_mbuf.hip): kMbufSets buffer sets of
+  // mb_cap packets each -- mbuf data pointers, 64-byte header slots, tail
+  // sums, per-set flags (device; their host copy in h_mbflags) -- and the
+  // whole-frame slots of a chunk that needs them (mb_full)
+  static constexpr int kMbufSets = 4;
+  uint64_t *mb_ptr = nullptr;
+  uint8_t *mb_slots = nullptr;
+  uint32_t *mb_tail = nullptr, *mb_flags = nullptr, *h_mbflags = nullptr;
+  size_t mb_cap = 0;
+  uint16_t *mb_len = nullptr, *mb_in = nullptr, *mb_out = nullptr;
+  int64_t *mb_now = nullptr;
+  uint8_t *mb_full = nullptr;
+  size_t mb_full_bytes = 0;
+  uint8_t *st_meta = nullptr;  // staged_range's device len / in / out / now
+  size_t st_meta_n = 0;
+  uint8_t *h_mbmeta = nullptr;  // pinned staging of pageable per-packet arrays
+  size_t h_mbmeta_bytes = 0;
+  hipEvent_t mb_ev_in[kMbufSets] = {}, mb_ev_done[kMbufSets] = {},
+             mb_ev_out[kMbufSets] = {};
 };
+
+// Host memory registered for direct access by the context's GPU
+// (vp_register_host): frames in [hbase, hend) are read and written at
+// address + delta by the mbuf kernels (vp_mbuf.hip).
+struct HostMap {
+  uint64_t hbase, hend;
+  int64_t delta;
+  bool ours;  // hipHostRegister'ed by the library (unregistered on release)
+};
+constexpr int kMaxHostMaps = 16;
 
 }  // namespace vp
 
@@ -256,7 +285,9 @@ struct vp_ctx {
   bool pol_cnt_clean = false;     // pol_cnt is all zero (the replay cleared it)
   uint32_t *pol_off = nullptr;   // exclusive scan of pol_cnt
   uint32_t *pol_runs = nullptr;  // [kRunMax][index] hit positions (grouping;
+                                 // allocated by the first grouping segment,
                                  // tables up to 4M indices, else pol_off)
+  bool pol_runs_tried = false;   // that allocation was attempted
   uint4 *be_rec = nullptr;  // viglb backends[]: {ip, mac0-3, mac4-5|nic<<16, 0}
   uint32_t *cht = nullptr;  // viglb CHT, cht[bucket * backend_capacity + prio]
   uint32_t *dmacw = nullptr;  // per device: {s_addr[0..1] << 16, s_addr[2..5]}
@@ -280,4 +311,12 @@ struct vp_ctx {
   uint32_t own_maxsend = 0;
   std::vector<uint32_t> rank_n;    // slice sizes of the current batch
   std::vector<uint32_t> rank_cnt;  // new keys per rank of the current segment
+  // multi-GPU: this rank broke an invariant (union_sizes); every rank returns
+  // VP_ESTATE from the next batch on, decided from the RankInfo gather
+  bool estate_pending = false;
+  // host memory the GPU reads frames from in place (vp_register_host)
+  std::vector<vp::HostMap> hmaps;
+  // during vp_process_mbufs: tail sums of the 64-byte header slots the
+  // current device batch holds (vp_nat.hip NatArgs::tail), else null
+  const uint32_t *hdr_tail = nullptr;
 };

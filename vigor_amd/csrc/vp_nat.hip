@@ -150,7 +150,20 @@ struct NatArgs {
   uint32_t ext_ip;
   uint16_t wan, start_port, n_dev;
   Route own;
+  // Host frames (vp_process_mbufs, vp_mbuf.hip): 64-byte header slots of
+  // longer frames, tail[p] = the raw sum of frame p's bytes [64, end) the L4
+  // checksum covers (0 where nothing lies past 64); null otherwise.
+  const uint32_t *tail;
 };
+
+// The register path's total_length bound for 64-byte slots (every L4 byte in
+// the slot), or any total_length for header slots with tail sums.
+__device__ __forceinline__ uint32_t nat_lim64(const NatArgs &a) {
+  return a.tail ? 0xFFFFu : 50u;
+}
+__device__ __forceinline__ uint32_t nat_tail(const NatArgs &a, uint32_t p) {
+  return a.tail ? a.tail[p] : 0u;
+}
 
 // Owner mode: hand the LAN packet with key `key` (hash h) to its owner if
 // that is another rank. Returns true when routed.
@@ -240,7 +253,7 @@ __device__ uint32_t nat_generic_a(const NatArgs &a, const uint32_t *T,
     f.w16(h.l4, (uint16_t)(a.start_port + idx));
     dst = a.wan;
   }
-  set_checksums(f, h.ip, h.l4);
+  set_checksums(f, h.ip, h.l4, nat_tail(a, p));
   uint32_t mw[3];
   macs_for(a, dst, mw);
   set_macs(f, mw);
@@ -439,7 +452,7 @@ __device__ __forceinline__ uint32_t nat_lane(const NatArgs &a, const uint32_t *T
   f.w[12] = c3.x; f.w[13] = c3.y; f.w[14] = c3.z; f.w[15] = c3.w;
   const uint32_t in = a.in_dev[p], len = a.len[p];
   uint32_t touch = kNone;
-  const NatPend P = nat_issue(a, T, p, f, in, len, true);
+  const NatPend P = nat_issue(a, T, p, f, in, len, true, nat_lim64(a));
   uint4 row[4] = {};
   if (P.row != kNone) {
     const uint4 *q = reinterpret_cast<const uint4 *>(a.t.bk + P.row);
@@ -448,7 +461,7 @@ __device__ __forceinline__ uint32_t nat_lane(const NatArgs &a, const uint32_t *T
     row[2] = q[2];
     row[3] = q[3];
   }
-  if (nat_finish(a, T, P, row, p, f, in, len, touch)) {
+  if (nat_finish(a, T, P, row, p, f, in, len, touch, nat_tail(a, p))) {
     st_stream(fp, make_uint4(f.w[0], f.w[1], f.w[2], f.w[3]));
     st_stream(fp + 1, make_uint4(f.w[4], f.w[5], f.w[6], f.w[7]));
     st_stream(fp + 2, make_uint4(f.w[8], f.w[9], f.w[10], f.w[11]));
@@ -563,9 +576,10 @@ __device__ __forceinline__ uint32_t dense128_tail(const uint4 d[8], uint32_t end
 // phase B or the reprobe walk are stored unchanged). Any other tile runs
 // nat_issue / nat_finish per lane. Owner mode's pass 1 has a lean tile of its
 // own (keys of other ranks routed, this rank's looked up).
-template <uint32_t G, uint32_t H = 1, bool D = false>
+template <uint32_t G, uint32_t H = 1, bool D = false, bool X = false>
 __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins bins,
                                           TileQueue rq) {
+  static_assert(!X || G == 0, "header slots (X) are 64-byte slots");
   __shared__ uint32_t T[kNatTabWords];
   __shared__ uint4 stage[4][256];
   __shared__ uint32_t cur[kCurs];
@@ -586,16 +600,20 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   const bool lean_own = G == 0 && a.own.n != 0 && rq.ent != nullptr;  // owner pass 1
   const uint32_t slot = G ? a.slot : 64u;
   const uint32_t lim = slot - 14;  // total_length bound of the register path
+  // 64-byte slots: every L4 byte in the slot, or (X: header slots of longer
+  // host frames) any total_length, the L4 sum's rest from a.tail
+  const uint32_t lim64 = X ? 0xFFFFu : 50u;
   // byte offset in the tile of chunk c (packet c / 4, part c % 4)
   auto chunk_at = [&](uint32_t c) -> uint32_t {
     return G ? (c >> 2) * slot + (c & 3) * 16 : c * 16;
   };
   uint4 r[4];
-  uint32_t m_in = 0, m_len = 0;
+  uint32_t m_in = 0, m_len = 0, m_tail = 0;
   auto fetch = [&](uint32_t tile) {
     const uint32_t tb = first + tile * 64;
     const uint8_t *g8 = a.frames + (size_t)tb * slot;
     const uint32_t p = tb + lane;
+    if constexpr (X) m_tail = p < n_all ? a.tail[p] : 0u;
     if constexpr (G > 0) {  // one buffer resource per tile: slots past the
       // batch read as zeros
       const uint32_t bytes = min(64u, n_all - tb) * slot;
@@ -666,7 +684,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       f.w[4 * k + 2] = v.z;
       f.w[4 * k + 3] = v.w;
     }
-    const uint32_t in = m_in, ln = m_len;
+    const uint32_t in = m_in, ln = m_len, xtail = X ? m_tail : 0u;
     // wide slots: the tail sums run while the frame image stays in S; the
     // frame is read back from it afterwards instead of held in registers
     const uint32_t tbytes = G ? min(64u, n_all - tb) * slot : 0u;
@@ -780,7 +798,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
     uint4 row[4];
     uint32_t touch = kNone;
     bool store_all;
-    if (lean_ok && __ballot(mine && nat_lan_fast_ok(a, f, in, ln)) == ~0ull) {
+    if (lean_ok && __ballot(mine && nat_lan_fast_ok(a, f, in, ln, lim64)) == ~0ull) {
       // ---- lean tile: every lane a fast-path LAN packet
       const uint32_t proto = f.w[5] >> 24;
       const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
@@ -827,7 +845,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
         touch = idx;
         f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
         f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
-        fast_checksums(f, proto, bswap16((uint16_t)(f.w[4] & 0xFFFF)));
+        fast_checksums(f, proto, bswap16((uint16_t)(f.w[4] & 0xFFFF)), xtail);
         f.w[0] = a.wan_macw0;
         f.w[1] = a.wan_macw1;
         f.w[2] = a.wan_macw2;
@@ -915,7 +933,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       wave_lds_sync();  // the next tile overwrites S
     } else {
       // ---- per-lane tile (nat_issue / nat_finish)
-      const NatPend pend = nat_issue(a, T, p, f, in, ln, mine);
+      const NatPend pend = nat_issue(a, T, p, f, in, ln, mine, lim64);
       uint4 q[4];
 #pragma unroll
       for (uint32_t j = 0; j < 4; j++) {
@@ -931,7 +949,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       for (uint32_t k = 0; k < 4; k++) row[k] = S[chunk_swz(4 * lane + k)];
       bool m = false;
       if (mine) {
-        m = nat_finish(a, T, pend, row, p, f, in, ln, touch);
+        m = nat_finish(a, T, pend, row, p, f, in, ln, touch, xtail);
         touch = route_note(a, p, touch);
       }
       {  // queue on this block's reprobe slice
@@ -985,6 +1003,13 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
   nat_tiles<0>(a, n_all, bins, rq);
 }
 
+// 64-byte header slots of longer host frames (vp_process_mbufs, vp_mbuf.hip):
+// the 64-byte tile loop with the L4 sum's rest of every frame from a.tail.
+__global__ __launch_bounds__(256, 4) void nat_classify64x(NatArgs a, uint32_t n_all,
+                                                         TouchBins bins, TileQueue rq) {
+  nat_tiles<0, 1, false, true>(a, n_all, bins, rq);
+}
+
 // Wide slots (slot > 64): G lanes per frame in the tail sums.
 // Up to 8 tail chunks per lane and tile (slots <= 192 B): 4 waves per SIMD,
 // 8 loads in flight per wave. Longer tails (G = 16): 2 waves per SIMD with
@@ -1006,8 +1031,8 @@ __global__ __launch_bounds__(256, 4) void nat_classify128(NatArgs a, uint32_t n_
 // The classify kernel for a slot: 64 bytes, or the wide kernel whose G is the
 // tail's 16-byte chunks (slot - 64) / 16 rounded up to a power of two, at most 16.
 typedef void (*NatTileKernel)(NatArgs, uint32_t, TouchBins, TileQueue);
-static NatTileKernel nat_tile_kernel(uint32_t slot) {
-  if (slot == 64) return nat_classify64;
+static NatTileKernel nat_tile_kernel(uint32_t slot, bool hdr_tail = false) {
+  if (slot == 64) return hdr_tail ? nat_classify64x : nat_classify64;
   if (slot == 128) return nat_classify128;
   const uint32_t nch = (slot - 64) / 16;
   if (nch <= 1) return nat_classify_wide<1>;
@@ -1045,7 +1070,7 @@ __device__ void nat_write_lan(const NatArgs &a, uint32_t p, uint32_t idx) {
   const L34 h = parse_l34(f, a.len[p]);
   f.w32(h.ip + 12, a.ext_ip);
   f.w16(h.l4, (uint16_t)(a.start_port + idx));
-  set_checksums(f, h.ip, h.l4);
+  set_checksums(f, h.ip, h.l4, nat_tail(a, p));
   const uint32_t mw[3] = {a.wan_macw0, a.wan_macw1, a.wan_macw2};
   set_macs(f, mw);
   a.out[p] = a.wan;
@@ -1087,11 +1112,11 @@ __global__ __launch_bounds__(256) void nat_reprobe(NatArgs a, const uint32_t *li
         a.frames, a.slot, a.len, a.in_dev, reinterpret_cast<const uint8_t *>(a.t.bk),
         a.t.bmask, p, act, S,
         [&](uint32_t q, const RFrame &f, uint32_t in, uint32_t len, bool mine) {
-          return nat_issue(a, T, q, f, in, len, mine);
+          return nat_issue(a, T, q, f, in, len, mine, nat_lim64(a));
         },
         [&](const NatPend &P, const uint4 *row, uint32_t q, RFrame &f, uint32_t in,
             uint32_t len, uint32_t &touch) {
-          return nat_finish(a, T, P, row, q, f, in, len, touch);
+          return nat_finish(a, T, P, row, q, f, in, len, touch, nat_tail(a, q));
         });
   });
 }
@@ -1342,7 +1367,7 @@ __global__ void nat_defer_finish(NatArgs a, const uint32_t *list, uint32_t n) {
     f.w32(h.ip + 16, k1);
     f.w16(h.l4 + 2, (uint16_t)(k0 & 0xFFFF));
     const uint32_t dst = k3 & 0xFFFF;
-    set_checksums(f, h.ip, h.l4);
+    set_checksums(f, h.ip, h.l4, nat_tail(a, p));
     uint32_t mw[3];
     macs_for(a, dst, mw);
     set_macs(f, mw);
@@ -1359,9 +1384,13 @@ static inline int64_t nat_cutoff(const vp_ctx *c, int64_t t) {
   return (int64_t)((uint64_t)t - e);
 }
 
+// Device scratch of at least `count` elements. It is also reallocated down
+// when it holds more than twice what is asked and over 64 MiB (the padded
+// exchange's buffers after the first batches settle C).
 template <class T>
 static int grow_dev(T **p, size_t *have, size_t count, hipStream_t s) {
-  if (count <= *have && *p) return 0;
+  const bool oversized = *have > 2 * std::max<size_t>(count, 1) && sizeof(T) * *have > (64u << 20);
+  if (count <= *have && *p && !oversized) return 0;
   VP_HIP(hipStreamSynchronize(s));
   hipFree(*p);
   *p = nullptr;
@@ -1616,15 +1645,17 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.wan = c->nat.wan_device;
   a.start_port = c->nat.start_port;
   a.n_dev = c->nat.n_devices;
+  a.tail = c->hdr_tail;  // (vp_process_mbufs' header slots; null otherwise)
 
   const bool owner = c->shard_mode == VP_SHARD_OWNER && c->comm;
+  if (owner && a.tail) return VP_ENOTSUP;  // (vp_mbuf.hip never asks for it)
   PhaseA ph{};
   if (owner) VP_TRY(nat_phase_a_owner(c, b, a, now, p0, p1, seq0, &ph));
   // tiles of 64 packets (64-byte slots, or wider ones: nat_tiles): the
   // classify launch also bins its touches (TouchBins) and queues reprobes
   // per block (TileQueue)
   const bool tiles64 = owner ? ph.tiles64 : p1 > p0 && c->coalesced_io;
-  const NatTileKernel tk = nat_tile_kernel(b->slot);
+  const NatTileKernel tk = nat_tile_kernel(b->slot, a.tail != nullptr);
   BinsPlan bp = ph.bp;
   uint32_t grid64 = ph.grid1, range64 = ph.range1;
   TileQueue rq{};

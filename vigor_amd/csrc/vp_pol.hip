@@ -448,6 +448,23 @@ static inline int64_t pol_cutoff(const vp_ctx *c, int64_t t) {
   return (int64_t)((uint64_t)t - exp_time);
 }
 
+// The grouping path's run slots (kRunMax per index: 1 GiB at 4M indices),
+// allocated once, by the first segment that groups, for tables up to 4M
+// indices; a failed allocation leaves the scan + scatter grouping path
+// (pol_runs null), which needs no slots.
+static int pol_runs_reserve(vp_ctx *c) {
+  if (c->pol_runs_tried) return 0;
+  c->pol_runs_tried = true;
+  const uint32_t cap = c->ft.cap;
+  if (cap > (1u << 22)) return 0;
+  const hipError_t e = hipMalloc((void **)&c->pol_runs, sizeof(uint32_t) * kRunMax * cap);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    c->pol_runs = nullptr;
+  }
+  return 0;
+}
+
 static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
                        uint32_t p0, uint32_t p1, float *ms, int *launches,
                        uint32_t *allocated) {
@@ -480,6 +497,7 @@ static int pol_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // lane per index); segments much shorter than the table (per-packet
   // nf_process calls, churn cut into many segments) take the sorting path.
   const bool grouping = (uint64_t)n * 8 >= t.cap;
+  if (grouping) VP_TRY(pol_runs_reserve(c));
   a.cnt = grouping ? c->pol_cnt : nullptr;
   a.runs = grouping ? c->pol_runs : nullptr;
 

@@ -175,6 +175,18 @@ static void free_all(vp_ctx *c) {
   tbl_free(c->ft2);
   Workspace &w = c->ws;
   ws_release(w);
+  for (const HostMap &h : c->hmaps)  // (registered by vp_register_host)
+    if (h.ours) hipHostUnregister(reinterpret_cast<void *>(h.hbase));
+  void *mb[] = {w.mb_ptr, w.mb_slots, w.mb_tail, w.mb_flags, w.mb_len, w.mb_in,
+                w.mb_out, w.mb_now, w.mb_full, w.st_meta};
+  for (void *p : mb) hipFree(p);
+  if (w.h_mbflags) hipHostFree(w.h_mbflags);
+  if (w.h_mbmeta) hipHostFree(w.h_mbmeta);
+  for (int i = 0; i < Workspace::kMbufSets; i++) {
+    if (w.mb_ev_in[i]) hipEventDestroy(w.mb_ev_in[i]);
+    if (w.mb_ev_done[i]) hipEventDestroy(w.mb_ev_done[i]);
+    if (w.mb_ev_out[i]) hipEventDestroy(w.mb_ev_out[i]);
+  }
   void *ptrs[] = {w.hist, w.hoff, w.cub_tmp, w.d_frames, w.d_len,    w.d_in,
                   w.bins_ent, w.bins_cnt,
                   w.d_out,   w.d_now,    c->crc_tab, c->macw,
@@ -310,8 +322,8 @@ static int pol_init(vp_ctx *c, const vp_pol_config *cfg) {
   VP_HIP(hipMemset(c->pol_time, 0, 8ull * cfg->dyn_capacity));
   VP_TRY(dalloc(&c->pol_cnt, cfg->dyn_capacity));
   VP_TRY(dalloc(&c->pol_off, cfg->dyn_capacity));
-  if (cfg->dyn_capacity <= (1u << 22))  // 64 hit slots per index (1 GiB at 4M)
-    VP_TRY(dalloc(&c->pol_runs, 64ull * cfg->dyn_capacity));
+  // (the run slots of the grouping path, 64 per index, are allocated by the
+  // first segment that groups: vp_pol.hip pol_runs_reserve)
   return 0;
 }
 
@@ -337,25 +349,6 @@ static int stage_meta(vp_ctx *c, uint32_t n) {
   VP_TRY(dalloc(&w.d_out, n));
   VP_TRY(dalloc(&w.d_now, n));
   w.d_meta_n = n;
-  return 0;
-}
-
-static int stage_frames(vp_ctx *c, size_t bytes) {
-  Workspace &w = c->ws;
-  if (bytes > w.d_frames_bytes) {
-    hipFree(w.d_frames);
-    w.d_frames = nullptr;
-    w.d_frames_bytes = 0;
-    VP_HIP(hipMalloc((void **)&w.d_frames, bytes));
-    w.d_frames_bytes = bytes;
-  }
-  if (bytes > w.h_frames_bytes) {
-    if (w.h_frames) hipHostFree(w.h_frames);
-    w.h_frames = nullptr;
-    w.h_frames_bytes = 0;
-    VP_HIP(hipHostMalloc((void **)&w.h_frames, bytes, hipHostMallocDefault));
-    w.h_frames_bytes = bytes;
-  }
   return 0;
 }
 
@@ -672,31 +665,6 @@ int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
   return rc;
 }
 
-static int run_staged(vp_ctx *c, uint32_t n, uint32_t slot, const uint16_t *in_dev,
-                      const uint16_t *len, const int64_t *now, uint16_t *out_dev) {
-  Workspace &w = c->ws;
-  VP_HIP(hipMemcpyAsync(w.d_frames, w.h_frames, (size_t)n * slot,
-                        hipMemcpyHostToDevice, c->stream));
-  VP_HIP(hipMemcpyAsync(w.d_len, len, 2ull * n, hipMemcpyHostToDevice, c->stream));
-  VP_HIP(hipMemcpyAsync(w.d_in, in_dev, 2ull * n, hipMemcpyHostToDevice, c->stream));
-  VP_HIP(hipMemcpyAsync(w.d_now, now, 8ull * n, hipMemcpyHostToDevice, c->stream));
-  vp_dev_batch b{};
-  b.frames = w.d_frames;
-  b.slot = slot;
-  b.n = n;
-  b.len = w.d_len;
-  b.in_dev = w.d_in;
-  b.now = w.d_now;
-  b.out_dev = w.d_out;
-  VP_TRY(vp_process_device(c, &b, nullptr));
-  VP_HIP(hipMemcpyAsync(w.h_frames, w.d_frames, (size_t)n * slot,
-                        hipMemcpyDeviceToHost, c->stream));
-  VP_HIP(hipMemcpyAsync(out_dev, w.d_out, 2ull * n, hipMemcpyDeviceToHost,
-                        c->stream));
-  VP_HIP(hipStreamSynchronize(c->stream));
-  return 0;
-}
-
 int vp_process_host_batch(vp_ctx *c, const vp_host_batch *b) {
   if (!c || !b) return VP_EINVAL;
   if (b->n && (!b->in_dev || !b->frames || !b->len || !b->out_dev)) return VP_EINVAL;
@@ -720,29 +688,6 @@ int vp_process_host(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
   b.now = now;
   b.out_dev = out_dev;
   return vp_process_host_batch(c, &b);
-}
-
-int vp_process_batch(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
-                     uint8_t *const *frames, const uint16_t *len,
-                     const int64_t *now, uint16_t *out_dev) {
-  if (!c || (n && (!in_dev || !frames || !len || !now || !out_dev)))
-    return VP_EINVAL;
-  if (n == 0) return 0;
-  if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
-  uint32_t maxlen = 64;
-  for (uint32_t i = 0; i < n; i++) maxlen = std::max<uint32_t>(maxlen, len[i]);
-  const uint32_t slot = (maxlen + 15) & ~15u;
-  VP_TRY(stage_meta(c, n));
-  VP_TRY(stage_frames(c, (size_t)n * slot));
-  uint8_t *h = c->ws.h_frames;
-  for (uint32_t i = 0; i < n; i++) {  // gather the mbuf data into slots
-    memcpy(h + (size_t)i * slot, frames[i], len[i]);
-    memset(h + (size_t)i * slot + len[i], 0, slot - len[i]);
-  }
-  VP_TRY(run_staged(c, n, slot, in_dev, len, now, out_dev));
-  for (uint32_t i = 0; i < n; i++)  // scatter back in place
-    memcpy(frames[i], h + (size_t)i * slot, len[i]);
-  return 0;
 }
 
 int vp_nat_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *keys) {

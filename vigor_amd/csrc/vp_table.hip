@@ -1428,8 +1428,15 @@ int union_sizes(vp_ctx *c, uint32_t nl, uint32_t *total, uint32_t *mine_off) {
   for (int r = 0; pub && r < m.n; r++) pub = w.h_gath[kPubGath * r + 3] == 0;  // reprobes
   if (pub) {
     for (int r = 0; r < m.n; r++) c->rank_cnt[r] = w.h_gath[kPubGath * r];
-    if (c->rank_cnt[m.r] != nl) return state_fail("published miss count %u != %u",
-                                                  c->rank_cnt[m.r], nl);
+    // A broken invariant on this rank alone must not leave the other ranks
+    // waiting in this segment's collectives: the segment goes on with the
+    // gathered counts (all ranks agree on them), this call returns VP_ESTATE
+    // at its end, and every rank returns it from the next call on (the
+    // RankInfo gather carries the flag, run_batch_sharded).
+    if (c->rank_cnt[m.r] != nl && !c->estate_pending) {
+      (void)state_fail("published miss count %u != %u", c->rank_cnt[m.r], nl);
+      c->estate_pending = true;
+    }
   } else {
     VP_TRY(m.allgather_host(c, &nl, c->rank_cnt.data(), sizeof nl));
   }
@@ -1496,6 +1503,7 @@ int union_exchange(vp_ctx *c, uint32_t nl, const NowSpec &now) {
     rs.maxn = std::max(rs.maxn, c->rank_cnt[r]);
   }
   const size_t bytes = sizeof(NewRec) * (size_t)rs.maxn;
+  nl = std::min(nl, c->rank_cnt[m.r]);  // (differs only after a broken invariant)
   VP_HIP(hipStreamSynchronize(c->stream));  // buffers may be reallocated
   VP_TRY(grow(&w.sbuf, &w.sbuf_bytes, bytes));
   VP_TRY(grow(&w.rbuf, &w.rbuf_bytes, bytes * m.n));
@@ -1554,6 +1562,7 @@ static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
       me.t_last = b->now0 + (int64_t)(n - 1) * b->now_step;
     }
   }
+  if (c->estate_pending) me.bad |= 4;  // an earlier call broke an invariant
   for (int i = 0; i < ntabs; i++) me.floor[i] = tabs[i].t->ts_floor;
   me.maxsend = c->own_maxsend;
   std::vector<RankInfo> all(m.n);
@@ -1562,10 +1571,15 @@ static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
      // same on every rank: the largest per-owner count any
      // rank last sent (its whole slice before it knows) + 1/8 + 256, at most
      // the largest slice; a segment that exceeds it takes the exact exchange
+    // (a rank that has sent nothing yet: its slice's uniform share per owner;
+    // a skewed first batch takes the exact exchange once, and no rank pins
+    // ranks x slice entries of exchange buffers)
     uint64_t maxs = 0, maxn = 0;
     for (int r = 0; r < m.n; r++) {
       maxn = std::max<uint64_t>(maxn, (uint64_t)all[r].n);
-      maxs = std::max<uint64_t>(maxs, all[r].maxsend ? all[r].maxsend : (uint64_t)all[r].n);
+      maxs = std::max<uint64_t>(maxs, all[r].maxsend
+                                          ? all[r].maxsend
+                                          : ((uint64_t)all[r].n + m.n - 1) / m.n);
     }
     uint64_t C = (maxs + maxs / 8 + 256 + 255) & ~255ull;
     if (const char *e = getenv("VIGPATH_OWN_CAP")) C = strtoull(e, nullptr, 10);  // tests
@@ -1589,6 +1603,8 @@ static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
     }
     G += (uint64_t)all[r].n;
   }
+  if (bad & 4) return c->estate_pending ? VP_ESTATE
+                                         : state_fail("another rank broke an invariant");
   if (bad & 1) return VP_EINVAL;
   if (bad & 2) return VP_ENOTSUP;
   if (G == 0) return 0;
@@ -1666,6 +1682,7 @@ static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
   // next call's collectives queue behind it on the same stream
   if (!c->fold_pending) VP_HIP(hipStreamSynchronize(c->stream));
   c->fold_pending = false;
+  if (c->estate_pending) return VP_ESTATE;  // (union_sizes; the text is recorded)
   c->seq += G;
   c->last_now = t_last_g;
   c->last_ms = ms;

@@ -12,8 +12,8 @@ import ctypes as C
 
 import numpy as np
 
-from . import (BridgeConfigC, DevBatchC, FwConfigC, LbConfigC, NatConfigC,
-               PolConfigC, TableStatsC, _check, lib)
+from . import (BridgeConfigC, DevBatchC, FwConfigC, LbConfigC, MbufBatchC,
+               NatConfigC, PolConfigC, TableStatsC, _check, lib)
 
 
 def _dptr(t):
@@ -26,6 +26,9 @@ class NfBase:
     def __init__(self, libpath=None):
         self.h = C.c_void_p()
         self.L = lib(libpath)
+
+    def _ck(self, rc: int, what: str):
+        _check(rc, what, self.L)  # vp_last_error() of this instance's library
 
     def close(self):
         if getattr(self, "h", None) and self.h.value:
@@ -51,7 +54,7 @@ class NfBase:
                       now=now.data_ptr() if now is not None else None,
                       now0=now0, now_step=now_step, out_dev=out.data_ptr())
         s = C.c_void_p(stream.cuda_stream) if stream is not None else None
-        _check(self.L.vp_process_device(self.h, C.byref(b), s),
+        self._ck(self.L.vp_process_device(self.h, C.byref(b), s),
                "vp_process_device")
 
     def device_step(self, frames, lens, in_dev, out, slot: int):
@@ -65,46 +68,46 @@ class NfBase:
         b = DevBatchC(frames=frames.data_ptr(), slot=slot, n=n,
                       len=lens.data_ptr(), in_dev=in_dev.data_ptr(), now=None,
                       now0=0, now_step=0, out_dev=out.data_ptr())
-        ref, fn, h = C.byref(b), self.L.vp_process_device, self.h
+        ref, fn, h, L = C.byref(b), self.L.vp_process_device, self.h, self.L
         keep = (frames, lens, in_dev, out)
 
         def step(now0: int, now_step: int):
             b.now0, b.now_step = now0, now_step
             rc = fn(h, ref, None)
             if rc:
-                _check(rc, "vp_process_device")
+                _check(rc, "vp_process_device", L)
         step.tensors = keep
         return step
 
     def sync_state(self):
         """Multi-GPU: merge the ranks' timestamps (collective)."""
-        _check(self.L.vp_sync_state(self.h), "vp_sync_state")
+        self._ck(self.L.vp_sync_state(self.h), "vp_sync_state")
 
     def kernel_timing(self, on: bool = True):
         """Bracket every classification kernel launch with HIP events
         (vp_kernel_timing; off by default: the events cost a step about 6 us),
         so that last_kernel_ms() reports its time."""
-        _check(self.L.vp_kernel_timing(self.h, 1 if on else 0), "vp_kernel_timing")
+        self._ck(self.L.vp_kernel_timing(self.h, 1 if on else 0), "vp_kernel_timing")
 
     def last_kernel_ms(self):
         if not hasattr(self, "_kms"):  # (built once: called every batch)
             ms, k = C.c_float(), C.c_int()
             self._kms = (ms, k, C.byref(ms), C.byref(k))
         ms, k, rms, rk = self._kms
-        _check(self.L.vp_last_kernel_ms(self.h, rms, rk), "vp_last_kernel_ms")
+        self._ck(self.L.vp_last_kernel_ms(self.h, rms, rk), "vp_last_kernel_ms")
         return ms.value, k.value
 
     def table_stats(self, table: int = 0) -> dict:
         """vp_table_stats_get: live / shard_live / tombstones / buckets /
         rebuilds / layout of table 0 (flows) or 1 (viglb backends)."""
         st = TableStatsC()
-        _check(self.L.vp_table_stats_get(self.h, table, C.byref(st)), "vp_table_stats_get")
+        self._ck(self.L.vp_table_stats_get(self.h, table, C.byref(st)), "vp_table_stats_get")
         return {k: int(getattr(st, k)) for k, _ in TableStatsC._fields_ if k != "pad"}
 
     def live_count(self) -> int:
         v = self.L.vp_live_count(self.h)
         if v < 0:
-            _check(int(v), "vp_live_count")
+            self._ck(int(v), "vp_live_count")
         return int(v)
 
     # ----------------------------------------------------------- host --
@@ -119,7 +122,7 @@ class NfBase:
         now = np.ascontiguousarray(now, np.int64)
         out = np.zeros(n, np.uint16)
         P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
-        _check(self.L.vp_process_host(self.h, n, P(in_dev), P(frames), slot,
+        self._ck(self.L.vp_process_host(self.h, n, P(in_dev), P(frames), slot,
                                      P(lens), P(now), P(out)),
                "vp_process_host")
         return out
@@ -141,7 +144,7 @@ class NfBase:
                       in_dev=in_dev.ctypes.data,
                       now=now.ctypes.data if now is not None else None,
                       now0=now0, now_step=now_step, out_dev=out.ctypes.data)
-        _check(self.L.vp_process_host_batch(self.h, C.byref(b)), "vp_process_host_batch")
+        self._ck(self.L.vp_process_host_batch(self.h, C.byref(b)), "vp_process_host_batch")
 
     def process_mbufs(self, bufs, in_dev, now):
         """Per-frame host buffers (bytearray each, mbuf-like), rewritten in
@@ -159,9 +162,58 @@ class NfBase:
         now = np.ascontiguousarray(now, np.int64)
         out = np.zeros(n, np.uint16)
         P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
-        _check(self.L.vp_process_batch(self.h, n, P(in_dev), ptrs, P(lens),
+        self._ck(self.L.vp_process_batch(self.h, n, P(in_dev), ptrs, P(lens),
                                       P(now), P(out)), "vp_process_batch")
         return out
+
+    def register_host(self, arr: np.ndarray):
+        """vp_register_host: the GPU reads and writes frames inside `arr`
+        (e.g. an mbuf pool) in place from now on (vp_process_mbufs)."""
+        assert arr.flags.c_contiguous
+        self._ck(self.L.vp_register_host(self.h, C.c_void_p(arr.ctypes.data), arr.nbytes),
+                 "vp_register_host")
+        self._hostmaps = getattr(self, "_hostmaps", []) + [arr]
+
+    def unregister_host(self, arr: np.ndarray):
+        self._ck(self.L.vp_unregister_host(self.h, C.c_void_p(arr.ctypes.data)),
+                 "vp_unregister_host")
+        self._hostmaps = [a for a in getattr(self, "_hostmaps", []) if a is not arr]
+
+    def process_mbuf_batch(self, ptrs: np.ndarray, lens, in_dev, out, now=None,
+                           now0: int = 0, now_step: int = 0):
+        """vp_process_mbufs: ptrs (u64, n) = each frame's host address (the
+        mbuf data pointers of an rx burst), lens / in_dev (u16, n), out (u16,
+        n) receives the out ports; now (i64, n) or None for affine time.
+        Arrays in page-locked memory are DMA'd in place."""
+        n = int(ptrs.shape[0])
+        assert ptrs.dtype == np.uint64 and ptrs.flags.c_contiguous
+        for a in (lens, in_dev, out):
+            assert a.flags.c_contiguous and a.itemsize == 2 and a.shape[0] == n
+        if now is not None:
+            assert now.dtype == np.int64 and now.flags.c_contiguous
+        b = MbufBatchC(n=n, frames=ptrs.ctypes.data, len=lens.ctypes.data,
+                       in_dev=in_dev.ctypes.data,
+                       now=now.ctypes.data if now is not None else None,
+                       now0=now0, now_step=now_step, out_dev=out.ctypes.data)
+        self._ck(self.L.vp_process_mbufs(self.h, C.byref(b)), "vp_process_mbufs")
+
+    def mbuf_step(self, ptrs, lens, in_dev, out):
+        """A prepared vp_process_mbufs call over fixed host arrays with affine
+        time: returns f(now0, now_step) (the batch descriptor built once, as
+        device_step)."""
+        n = int(ptrs.shape[0])
+        b = MbufBatchC(n=n, frames=ptrs.ctypes.data, len=lens.ctypes.data,
+                       in_dev=in_dev.ctypes.data, now=None, now0=0, now_step=0,
+                       out_dev=out.ctypes.data)
+        ref, fn, h, L = C.byref(b), self.L.vp_process_mbufs, self.h, self.L
+
+        def step(now0: int, now_step: int):
+            b.now0, b.now_step = now0, now_step
+            rc = fn(h, ref)
+            if rc:
+                _check(rc, "vp_process_mbufs", L)
+        step.arrays = (ptrs, lens, in_dev, out)
+        return step
 
     def process(self, device: int, buffer: bytearray, now: int) -> int:
         """nf_process for one packet (nf.h:13)."""
@@ -174,7 +226,7 @@ class Nat(NfBase):
     def __init__(self, cfg: NatConfigC, gpu: int = 0, libpath=None):
         super().__init__(libpath)
         self.cfg = cfg
-        _check(self.L.vp_nat_create(C.byref(cfg), gpu, C.byref(self.h)),
+        self._ck(self.L.vp_nat_create(C.byref(cfg), gpu, C.byref(self.h)),
                "vp_nat_create")
 
     def dump(self):
@@ -183,7 +235,7 @@ class Nat(NfBase):
         ts = np.zeros(n, np.int64)
         keys = np.zeros(n * 16, np.uint8)
         P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
-        _check(self.L.vp_nat_dump(self.h, P(alloc), P(ts), P(keys)),
+        self._ck(self.L.vp_nat_dump(self.h, P(alloc), P(ts), P(keys)),
                "vp_nat_dump")
         return alloc, ts, keys.reshape(n, 16)
 
@@ -194,7 +246,7 @@ class Bridge(NfBase):
     def __init__(self, cfg: BridgeConfigC, gpu: int = 0, libpath=None):
         super().__init__(libpath)
         self.cfg = cfg
-        _check(self.L.vp_bridge_create(C.byref(cfg), gpu, C.byref(self.h)),
+        self._ck(self.L.vp_bridge_create(C.byref(cfg), gpu, C.byref(self.h)),
                "vp_bridge_create")
 
     def dump(self):
@@ -205,7 +257,7 @@ class Bridge(NfBase):
         macs = np.zeros(n * 6, np.uint8)
         port = np.zeros(n, np.uint16)
         P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
-        _check(self.L.vp_bridge_dump(self.h, P(alloc), P(ts), P(macs), P(port)),
+        self._ck(self.L.vp_bridge_dump(self.h, P(alloc), P(ts), P(macs), P(port)),
                "vp_bridge_dump")
         return alloc, ts, macs.reshape(n, 6), port
 
@@ -216,7 +268,7 @@ class Lb(NfBase):
     def __init__(self, cfg: LbConfigC, gpu: int = 0, libpath=None):
         super().__init__(libpath)
         self.cfg = cfg
-        _check(self.L.vp_lb_create(C.byref(cfg), gpu, C.byref(self.h)),
+        self._ck(self.L.vp_lb_create(C.byref(cfg), gpu, C.byref(self.h)),
                "vp_lb_create")
 
     def dump(self):
@@ -228,7 +280,7 @@ class Lb(NfBase):
         ba, bt = np.zeros(nb, np.uint8), np.zeros(nb, np.int64)
         bi, bm = np.zeros(nb, np.uint32), np.zeros(nb * 6, np.uint8)
         bn = np.zeros(nb, np.uint16)
-        _check(self.L.vp_lb_dump(self.h, *[C.c_void_p(x.ctypes.data) for x in
+        self._ck(self.L.vp_lb_dump(self.h, *[C.c_void_p(x.ctypes.data) for x in
                                            (fa, ft, fk, fb, ba, bt, bi, bm, bn)]),
                "vp_lb_dump")
         return ((fa, ft, fk.reshape(nf_, 16), fb),
@@ -241,7 +293,7 @@ class Fw(NfBase):
     def __init__(self, cfg: FwConfigC, gpu: int = 0, libpath=None):
         super().__init__(libpath)
         self.cfg = cfg
-        _check(self.L.vp_fw_create(C.byref(cfg), gpu, C.byref(self.h)),
+        self._ck(self.L.vp_fw_create(C.byref(cfg), gpu, C.byref(self.h)),
                "vp_fw_create")
 
     def dump(self):
@@ -252,7 +304,7 @@ class Fw(NfBase):
         keys = np.zeros(n * 16, np.uint8)
         dev = np.zeros(n, np.uint32)
         P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
-        _check(self.L.vp_fw_dump(self.h, P(alloc), P(ts), P(keys), P(dev)),
+        self._ck(self.L.vp_fw_dump(self.h, P(alloc), P(ts), P(keys), P(dev)),
                "vp_fw_dump")
         return alloc, ts, keys.reshape(n, 16), dev
 
@@ -265,7 +317,7 @@ class Pol(NfBase):
     def __init__(self, cfg: PolConfigC, gpu: int = 0, libpath=None):
         super().__init__(libpath)
         self.cfg = cfg
-        _check(self.L.vp_pol_create(C.byref(cfg), gpu, C.byref(self.h)),
+        self._ck(self.L.vp_pol_create(C.byref(cfg), gpu, C.byref(self.h)),
                "vp_pol_create")
 
     def dump(self):
@@ -278,6 +330,6 @@ class Pol(NfBase):
         size = np.zeros(n, np.uint64)
         btime = np.zeros(n, np.int64)
         P = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
-        _check(self.L.vp_pol_dump(self.h, P(alloc), P(ts), P(keys), P(size),
+        self._ck(self.L.vp_pol_dump(self.h, P(alloc), P(ts), P(keys), P(size),
                                   P(btime)), "vp_pol_dump")
         return alloc, ts, keys, size, btime

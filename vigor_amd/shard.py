@@ -111,7 +111,7 @@ class TorchComm:
 def rccl_unique_id() -> bytes:
     L = lib()
     buf = (C.c_uint8 * 128)()
-    _check(L.vp_comm_unique_id(buf), "vp_comm_unique_id")
+    _check(L.vp_comm_unique_id(buf), "vp_comm_unique_id", L)
     return bytes(buf)
 
 
@@ -119,7 +119,7 @@ def set_mode(nf, mode: str):
     """Dictionary placement (vp_shard_mode): "replicated" (every rank holds
     every key) or "owner" (keys sharded by flow hash, LAN lookups of other
     ranks' keys through an all-to-all)."""
-    _check(nf.L.vp_shard_mode(nf.h, MODES[mode]), "vp_shard_mode")
+    _check(nf.L.vp_shard_mode(nf.h, MODES[mode]), "vp_shard_mode", nf.L)
 
 
 def attach_rccl(nf, rank: int, world: int, group=None, mode: str = "replicated"):
@@ -129,7 +129,7 @@ def attach_rccl(nf, rank: int, world: int, group=None, mode: str = "replicated")
     obj = [rccl_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0, group=group)
     buf = (C.c_uint8 * 128).from_buffer_copy(obj[0])
-    _check(nf.L.vp_attach_rccl(nf.h, buf, world, rank), "vp_attach_rccl")
+    _check(nf.L.vp_attach_rccl(nf.h, buf, world, rank), "vp_attach_rccl", nf.L)
     set_mode(nf, mode)
 
 
@@ -139,7 +139,7 @@ def attach_torch(nf, rank: int, world: int, group=None,
     object alive as long as `nf`."""
     comm = TorchComm(group)
     _check(nf.L.vp_attach_comm(nf.h, C.byref(comm.ops), world, rank),
-           "vp_attach_comm")
+           "vp_attach_comm", nf.L)
     nf._comm = comm
     set_mode(nf, mode)
     return comm

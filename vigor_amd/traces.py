@@ -264,3 +264,57 @@ def _avalanche(h: np.ndarray) -> np.ndarray:
         np.multiply(h, np.uint64(0x94D049BB133111EB), out=h)
         np.bitwise_xor(h, h >> np.uint64(31), out=h)
     return h
+
+
+class MbufPool:
+    """A DPDK-shaped mbuf pool in host memory (SURVEY.md §8(d) "End-to-end":
+    2 KB buffers, 128 B headroom): `n` elements of `stride` bytes, each a
+    128-byte struct rte_mbuf, RTE_PKTMBUF_HEADROOM (128 B) and a 2048-byte
+    data room (DPDK's RTE_MBUF_DEFAULT_BUF_SIZE = 2048 + 128), so a frame
+    starts at `data_off` = 256 into its element (rte_pktmbuf_mtod). `mem` is
+    one flat uint8 array (page-locked when `pinned`, as DPDK's hugepages are
+    to the NIC); vp_register_host maps it for the GPU."""
+
+    def __init__(self, n: int, stride: int = 2304, data_off: int = 256,
+                 pinned: bool = False):
+        self.n, self.stride, self.data_off = n, stride, data_off
+        if pinned:
+            import torch
+            self.mem = torch.zeros(n * stride, dtype=torch.uint8).pin_memory().numpy()
+        else:  # page-aligned, as hugepages are
+            raw = np.zeros(n * stride + 4096, np.uint8)
+            a = (-raw.ctypes.data) % 4096
+            self.mem = raw[a:a + n * stride]
+        self.rows = self.mem.reshape(n, stride)
+
+    def ptrs(self, bufs: np.ndarray, shift: np.ndarray | None = None) -> np.ndarray:
+        """The data pointers (u64) of mbufs `bufs` (+ per-frame byte shifts)."""
+        off = np.asarray(bufs, np.uint64) * np.uint64(self.stride) + np.uint64(self.data_off)
+        if shift is not None:
+            off = off + np.asarray(shift, np.uint64)
+        return (np.uint64(self.mem.ctypes.data) + off).astype(np.uint64)
+
+    def put(self, bufs: np.ndarray, frames: np.ndarray, slot: int, lens: np.ndarray,
+            shift: np.ndarray | None = None):
+        """Frame i (len[i] bytes of its `slot`-byte slot in `frames`) into
+        mbuf bufs[i]. Equal lengths and shifts are copied in one step."""
+        f = frames.reshape(-1, slot)
+        lens = np.asarray(lens)
+        o = self.data_off
+        if shift is None and (lens == lens[0]).all():
+            L = int(lens[0])
+            self.rows[np.asarray(bufs), o:o + L] = f[:, :L]
+            return
+        for i, b in enumerate(np.asarray(bufs)):
+            s = o + (int(shift[i]) if shift is not None else 0)
+            self.rows[b, s:s + int(lens[i])] = f[i, :int(lens[i])]
+
+    def get(self, bufs: np.ndarray, slot: int, lens: np.ndarray,
+            shift: np.ndarray | None = None) -> np.ndarray:
+        """The frames back in `slot`-byte slots (zeros past each length)."""
+        out = np.zeros((len(bufs), slot), np.uint8)
+        o = self.data_off
+        for i, b in enumerate(np.asarray(bufs)):
+            s = o + (int(shift[i]) if shift is not None else 0)
+            out[i, :int(lens[i])] = self.rows[b, s:s + int(lens[i])]
+        return out.reshape(-1)
