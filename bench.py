@@ -256,6 +256,100 @@ def end_to_end(nat, bank, dev, start: int, steps: int = 3):
     return B * steps / el / 1e6
 
 
+MBUF_BATCH = 1 << 22
+IMIX = ((7, 60), (4, 566), (1, 1514))  # 7:4:1 of 64 / 570 / 1518-byte wire frames
+
+
+def imix_lengths(p: np.ndarray) -> np.ndarray:
+    """Frame length of packet p in the mixed-size burst: IMIX 7:4:1."""
+    r = p % 12
+    return np.where(r < 7, 60, np.where(r < 11, 566, 1514)).astype(np.uint16)
+
+
+def end_to_end_mbuf(nat, bank, dev, start: int, steps: int = 3, imix: bool = False):
+    """SURVEY.md §8(d) "End-to-end" in DPDK's own shape (nf.c:186-214): every
+    frame in its own mbuf of a pool in page-locked host memory (2304-byte
+    elements: a 128-byte rte_mbuf, 128 B headroom and a 2 KB data room, the
+    frame at data_off 256; traces.MbufPool), registered once with
+    vp_register_host, and a batch = the data pointers of MBUF_BATCH packets in
+    rx order (a random permutation of the pool: a mempool hands buffers back
+    in no particular order), their lengths and ports. vp_process_mbufs reads
+    each frame's first 64 bytes, and the bytes its L4 checksum covers past
+    them, from host memory on the GPU, processes them and writes the
+    rewritten header bytes back (vp_mbuf.hip). Frames: the bench trace (64 B,
+    round robin over the warm flows), or IMIX 7:4:1 of 60 / 566 / 1514-byte
+    frames (random payload past 64 B). The pool's frames are refilled
+    between steps (untimed); each call is timed alone, its inputs in host
+    memory when it starts and its results there when it returns. Returns a
+    dict for the bench line."""
+    import torch
+    B = MBUF_BATCH
+    rng = np.random.default_rng(7)
+    pool = T.MbufPool(B, pinned=True)
+    bufs = rng.permutation(B)
+    pin = lambda a: torch.from_numpy(np.ascontiguousarray(a)).pin_memory().numpy()  # noqa
+    ptrs = pin(pool.ptrs(bufs))
+    lens = pin(imix_lengths(np.arange(B)) if imix else np.full(B, 60, np.uint16))
+    ind = pin(np.zeros(B, np.uint16))
+    out = pin(np.zeros(B, np.uint16))
+    if imix:  # payload past byte 64, the same in every step (never rewritten)
+        pool.rows[:, 256 + 64:] = rng.integers(0, 256, (1, pool.stride - 256 - 64),
+                                               dtype=np.uint8)
+    tl = lens.astype(np.int64) - 14
+    hdr = np.empty((B, 64), np.uint8)
+    d = torch.empty(B * SLOT, dtype=torch.uint8, device=dev)
+    nat.register_host(pool.mem)
+    call = nat.mbuf_step(ptrs, lens, ind, out)
+    times = []
+    try:
+        for k in range(steps + 1):  # step 0 allocates the staging, untimed
+            p0 = start + k * B
+            bank.fill(d, p0)
+            hdr[:] = d.view(B, SLOT).cpu().numpy()
+            if imix:  # total_length and the UDP length of each frame
+                hdr[:, 16] = (tl >> 8).astype(np.uint8)
+                hdr[:, 17] = (tl & 0xFF).astype(np.uint8)
+                hdr[:, 38] = ((tl - 20) >> 8).astype(np.uint8)
+                hdr[:, 39] = ((tl - 20) & 0xFF).astype(np.uint8)
+            pool.rows[bufs, 256:256 + 64] = hdr
+            t0 = time.perf_counter()
+            call(T.NOW0 + p0, 1)
+            el = time.perf_counter() - t0
+            if k:
+                times.append(el)
+        assert (out == 1).all()
+        # property check of a sample of the last batch, read back from the
+        # mbufs: IPv4 and UDP checksums verify over each frame's bytes, the
+        # source is the external address
+        idx = np.linspace(0, B - 1, 2048).astype(np.int64)
+        smp = np.zeros((len(idx), 2048), np.uint8)
+        for j, i in enumerate(idx):
+            L = int(lens[i])
+            smp[j, :L] = pool.rows[bufs[i], 256:256 + L]
+        chk = verify_sample(torch.from_numpy(smp.reshape(-1)), 2048, T.ip4(192, 168, 4, 2),
+                            k=len(idx))
+    finally:
+        nat.unregister_host(pool.mem)
+    el = sum(times)
+    mpps = B * len(times) / el / 1e6
+    avg = float(lens.mean())
+    pin_in = 8 + 2 + 2 + float(np.mean(np.maximum(64, (lens.astype(np.int64) + 15) // 16 * 16)))
+    pin_out = 2 + float(np.mean(np.minimum(lens, 64)))
+    return {"value": round(mpps, 1), "unit": "Mpps",
+            "gbit_per_s": round(mpps * 1e6 * avg * 8 / 1e9, 1),
+            "frames": ("IMIX 7:4:1 of 60/566/1514 B (mean %.1f B)" % avg) if imix
+                      else "64 B (60 B + FCS), the bench trace",
+            "path": "page-locked mbuf pool (2304-byte elements, data_off 256), pointer "
+                    "array in shuffled rx order -> vp_process_mbufs: GPU reads each "
+                    "frame's header (+ the L4-summed bytes past 64) from host memory, "
+                    "processes 64-byte header slots, writes the rewritten bytes back "
+                    "(vp_mbuf.hip)",
+            "batch_packets": B, "steps": len(times),
+            "ms_per_batch": round(el / len(times) * 1e3, 3),
+            "pcie_bytes_per_packet": {"in": round(pin_in, 1), "out": round(pin_out, 1)},
+            "parity": chk}
+
+
 def launch_ranks(n: int) -> int:
     """--gpus N > 1 without a torch.distributed environment: start one rank
     per GPU as child processes (torch.distributed.run), before anything here
@@ -283,7 +377,7 @@ def cpu_model() -> str:
 
 
 def timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank, first, steps,
-                order="rr", host_comm=False):
+                order="rr", host_comm=False, stages=None):
     """Fill one buffer per step (batches first .. first + steps - 1 of this
     rank's slices, `order`), then time exactly `steps` prepared
     vp_process_device calls between barriers + synchronisations. Returns
@@ -305,6 +399,9 @@ def timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank, first, 
     for k in range(steps):
         calls[k](T.NOW0 + gstart(first + k), 1)
         kms.append(nat.last_kernel_ms())
+        if stages is not None:  # owner mode's phase-A stages (timing pass)
+            for name, ms in nat.last_stage_ms().items():
+                stages[name] = stages.get(name, 0.0) + ms / steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -465,9 +562,19 @@ def main():
     # the kernel-timing pass: the next `steps` batches of the same workload,
     # each classify launch between HIP events on the stream it runs on
     nat.kernel_timing(True)
+    owner_run = (world > 1 and mode == "owner") or args.route_all
+    stages = {} if owner_run else None
     el_k, kms, bufs = timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank,
-                                  args.warmup + args.steps, args.steps, args.order, host_comm)
+                                  args.warmup + args.steps, args.steps, args.order, host_comm,
+                                  stages)
     del bufs
+    stages_max = None
+    if stages and world > 1:  # the slowest rank per stage
+        names = sorted(stages)
+        t = torch.tensor([stages[k] for k in names], dtype=torch.float64,
+                         device="cpu" if host_comm else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        stages_max = {k: float(v) for k, v in zip(names, t.tolist())}
     per_launch_s, pkts_per_launch, achieved = kernel_rate(kms, B, args.steps, alg_bytes)
     traffic = None  # PMC bytes of the same kernel (profiles/, per launch)
     tpath = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE)
@@ -525,6 +632,10 @@ def main():
                        "(vp_process_host_batch, affine time)" % E2E_CHUNK,
                "batch_packets": E2E_BATCH,
                "pcie_bytes_per_packet": SLOT + 4 + SLOT + 2}
+        base = (args.warmup + 3 * args.steps) * B + 4 * E2E_BATCH
+        extra["end_to_end_mbuf"] = end_to_end_mbuf(nat, bank, dev, base)
+        extra["end_to_end_mbuf_imix"] = end_to_end_mbuf(nat, bank, dev,
+                                                        base + 4 * MBUF_BATCH, imix=True)
     if world > 1 and not args.no_extra:
         # the other dictionary placement, same workload
         other = "replicated" if mode == "owner" else "owner"
@@ -591,6 +702,15 @@ def main():
             "new_flow_mpps": round(new_flow_mpps, 2) if new_flow_mpps else None,
             "end_to_end": e2e,
         }
+        if stages:
+            line["stages_ms"] = {
+                "rank0": {k: round(v, 4) for k, v in stages.items()},
+                "max_over_ranks": ({k: round(v, 4) for k, v in stages_max.items()}
+                                   if stages_max else None),
+                "source": "the kernel-timing pass: HIP events between the owner "
+                          "pipeline's stages of every segment (vp_last_stage_ms), "
+                          "mean per step on rank 0; that pass's step: %.4f ms"
+                          % (el_k / args.steps * 1e3)}
         line.update(extra)
         print(json.dumps(line), flush=True)
     if world > 1:

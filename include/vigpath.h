@@ -334,6 +334,15 @@ int vp_kernel_timing(vp_ctx *ctx, int on);
  * vp_kernel_timing is off), and the number of launches. */
 int vp_last_kernel_ms(vp_ctx *ctx, float *ms, int *launches);
 
+/* Owner-sharded multi-GPU contexts (VP_SHARD_OWNER) with kernel timing on:
+ * the last vp_process_device call's phase-A stage times in ms, summed over
+ * its segments, from HIP events between the stages: ms[0] pass 1 (classify,
+ * keys routed), ms[1] offsets (counts all-to-all, overflow all-reduce),
+ * ms[2] keys all-to-all, ms[3] owner probe, ms[4] answers all-to-all,
+ * ms[5] pass 2 (routed packets rewritten, touches binned), ms[6] fold.
+ * *stages = 7, or 0 when nothing was recorded. ms must hold 7 floats. */
+int vp_last_stage_ms(vp_ctx *ctx, float *ms, int *stages);
+
 /* Build identification (e.g. "vigpath gfx950"). */
 const char *vp_version(void);
 

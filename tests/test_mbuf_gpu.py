@@ -117,7 +117,7 @@ def test_nat_unregistered_and_unaligned(monkeypatch):
     exp = fr.copy()
     exp_out = o.run(exp, ln, dv, now, SLOT)
     pool = T.MbufPool(2 * n, pinned=True)
-    bufs = rng.permutation(2 * n)[:n]
+    bufs = rng.permutation(n)             # the registered half
     bufs[2400:3000] = n + np.arange(600)  # chunk 4: all in the unregistered half
     bufs[100] = n + 700                   # chunk 0: one frame there
     pool.put(bufs, fr, SLOT, ln, shift)

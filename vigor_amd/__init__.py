@@ -125,7 +125,8 @@ EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_fw_create",
            "vp_fw_dump", "vp_comm_unique_id", "vp_attach_rccl",
            "vp_attach_comm", "vp_shard_mode", "vp_sync_state", "vp_live_count",
            "vp_kernel_timing", "vp_last_kernel_ms", "vp_version", "vp_table_stats_get",
-           "vp_last_error", "vp_register_host", "vp_unregister_host", "vp_process_mbufs"]
+           "vp_last_error", "vp_register_host", "vp_unregister_host", "vp_process_mbufs",
+           "vp_last_stage_ms"]
 
 _libs = {}
 
@@ -201,6 +202,8 @@ def lib(path: str | None = None):
     L.vp_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float),
                                     C.POINTER(C.c_int)]
     L.vp_last_kernel_ms.restype = C.c_int
+    L.vp_last_stage_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int)]
+    L.vp_last_stage_ms.restype = C.c_int
     L.vp_kernel_timing.argtypes = [C.c_void_p, C.c_int]
     L.vp_kernel_timing.restype = C.c_int
     L.vp_table_stats_get.argtypes = [C.c_void_p, C.c_int, C.POINTER(TableStatsC)]

@@ -64,6 +64,11 @@ hipError_t launch_timed(void (*k)(P...), dim3 grid, dim3 block, hipStream_t s,
   return hipExtLaunchKernel((const void *)k, grid, block, ptrs, 0, s, e0, e1, 0);
 }
 
+// Owner-mode phase A stages (vp_last_stage_ms).
+constexpr int kStages = 7;
+inline constexpr const char *kStageNames[kStages] = {
+    "pass1", "offsets", "a2a_keys", "probe", "a2a_answers", "pass2", "fold"};
+
 struct Comm;  // vp_comm.hip: collectives between the ranks of one NF
 constexpr int kMaxRanks = 64;
 
@@ -269,6 +274,10 @@ struct vp_ctx {
   bool fold_pending = false;
   float last_ms = 0.f;
   bool ktime = false;  // vp_kernel_timing: events around the classify launch
+  // owner mode with ktime: the last call's phase-A stage times (ms, summed
+  // over its segments; vp_last_stage_ms)
+  float stage_ms[vp::kStages] = {};
+  int stage_n = 0;
   int last_launches = 0;
   uint64_t seq = 0;       // packets processed so far (global packet order)
   int64_t last_now = -1;  // time of the last packet processed

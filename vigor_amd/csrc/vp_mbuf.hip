@@ -549,14 +549,20 @@ int vp_register_host(vp_ctx *c, void *base, size_t bytes) {
   for (const HostMap &h : c->hmaps)
     if (hb < h.hend && hb + bytes > h.hbase) return VP_EINVAL;  // overlaps
   HostMap h{hb, hb + bytes, 0, false};
-  hipError_t e = hipHostRegister(base, bytes, hipHostRegisterMapped);
-  if (e == hipSuccess) {
-    h.ours = true;
-  } else if (e == hipErrorHostMemoryAlreadyRegistered) {
-    (void)hipGetLastError();  // page-locked already (hipHostMalloc, a DPDK pool)
-  } else {
-    return hip_fail(e, "hipHostRegister", __FILE__, __LINE__);
+  // page-locked already (hipHostMalloc'd, or registered by the application):
+  // only mapped; else registered here (and unregistered with the context)
+  hipPointerAttribute_t pa;
+  const bool pinned = hipPointerGetAttributes(&pa, base) == hipSuccess &&
+                      pa.type == hipMemoryTypeHost;
+  (void)hipGetLastError();
+  if (!pinned) {
+    const hipError_t r = hipHostRegister(base, bytes, hipHostRegisterMapped);
+    if (r != hipSuccess && r != hipErrorHostMemoryAlreadyRegistered)
+      return hip_fail(r, "hipHostRegister", __FILE__, __LINE__);
+    (void)hipGetLastError();
+    h.ours = r == hipSuccess;
   }
+  hipError_t e;
   void *d = nullptr;
   e = hipHostGetDevicePointer(&d, base, 0);
   if (e != hipSuccess) {

@@ -1192,52 +1192,76 @@ __global__ __launch_bounds__(256) void route_pack(const uint4 *desc, const uint3
 }
 
 // The owner side of C1: map_get (find_key, map-impl-pow2.c:629-732) of every
-// received FlowId in this rank's buckets, a wave of 64 keys at a time, each
-// bucket fetched as one cooperative 64-byte request (wave_gather64). Answers
-// the index or kNone (a new flow: the ingest rank queues the packet for
-// phase B).
+// received FlowId in this rank's buckets. Tiles of 64 keys per wave (one
+// 1 KiB load; the next tile's keys in flight while this one is matched), a
+// persistent grid with a contiguous tile range per block (keys arrive in
+// their senders' packet order, so a block's keys reuse nearby rows, as in
+// nat_tiles), the hash from the LDS position tables with the 15 reads issued
+// together (flowid_hash_batched), the home bucket through the layout's
+// tables in LDS, one cooperative 64-byte row request per key
+// (wave_gather64) and the branch-free match; a key whose home bucket holds
+// three other keys walks on bucket by bucket (rare). Answers the index or
+// kNone (a new flow: the ingest rank queues the packet for phase B).
 // Padded exchange (cap > 0): n keys arrived as ranks x cap, peer q's first
 // rcnt[q] valid; no work when any rank overflowed (*ovf, published as
 // ctl->route_ovf for the host). cap == 0: n keys, all valid.
-__global__ __launch_bounds__(256) void nat_own_probe(TableDev t, const uint32_t *crc_tab,
-                                                     const uint4 *keys, uint32_t n,
-                                                     uint32_t cap, const uint32_t *rcnt,
-                                                     const uint64_t *ovf, Ctl *ctl,
-                                                     uint32_t *reply) {
-  __shared__ uint32_t T[15 * 256];
+__global__ __launch_bounds__(256, 4) void nat_own_probe(TableDev t, const uint32_t *crc_tab,
+                                                        const uint4 *keys, uint32_t n,
+                                                        uint32_t cap, const uint32_t *rcnt,
+                                                        const uint64_t *ovf, Ctl *ctl,
+                                                        uint32_t *reply) {
+  __shared__ uint32_t T[kNatTabWords];
   __shared__ uint4 stage[4][256];
   const bool skip = cap && *ovf;
   if (blockIdx.x == 0 && threadIdx.x == 0) ctl->route_ovf = skip ? 1u : 0u;
   if (skip) return;
-  load_crc_tables(T, crc_tab);
+  if (t.mix == kMixLin)
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) T[kCrcWords + i] = t.lin[i];
+  load_crc_tables(T, crc_tab);  // (its barrier covers the layout tables)
   uint4 *S = stage[threadIdx.x >> 6];
   const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t base = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; base < n;
-       base += gridDim.x * 256) {  // wave-uniform
-    const uint32_t j = base + lane;
-    const bool act = j < n && (!cap || j % cap < rcnt[j / cap]);
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t tiles = (n + 63) / 64;
+  const uint32_t per_b = (tiles + gridDim.x - 1) / gridDim.x;
+  const uint32_t tend = min(tiles, blockIdx.x * per_b + per_b);
+  auto valid_at = [&](uint32_t j) {
+    return j < n && (!cap || j % cap < rcnt[j / cap]);
+  };
+  uint32_t tile = blockIdx.x * per_b + wv;
+  bool vn = false;
+  uint4 kn = make_uint4(0, 0, 0, 0);
+  if (tile < tend) {
+    vn = valid_at(tile * 64 + lane);
+    if (vn) kn = keys[tile * 64 + lane];
+  }
+  for (; tile < tend; tile += 4) {
+    const uint32_t j = tile * 64 + lane;
+    const bool act = vn;
+    const uint4 k = kn;
+    if (tile + 4 < tend) {  // the next tile's keys
+      vn = valid_at(j + 256);
+      kn = vn ? keys[j + 256] : make_uint4(0, 0, 0, 0);
+    }
     if (!__ballot(act)) continue;
-    const uint4 k = act ? keys[j] : make_uint4(0, 0, 0, 0);
     const uint32_t key[4] = {k.x, k.y, k.z, k.w};
-    const uint32_t h = flowid_hash(T, k.x & 0xFFFF, k.x >> 16, k.y, k.z, k.w & 0xFFFF,
-                                   (k.w >> 16) & 0xFF);
-    uint32_t b = home_bucket(h, t.bmask, t.mix, t.lin), res = kNone;
-    bool live = act;
-    for (uint32_t step = 0;; step++) {
-      uint4 row[4];
-      wave_gather64(reinterpret_cast<const uint8_t *>(t.bk), 64, live ? b : kNone, S,
-                    row);
+    const uint32_t h = flowid_hash_batched(T, k.x & 0xFFFF, k.x >> 16, k.y, k.z,
+                                           k.w & 0xFFFF, (k.w >> 16) & 0xFF);
+    uint32_t b = home_bucket(h, t.bmask, t.mix, nat_lin(T));
+    uint4 row[4];
+    wave_gather64(reinterpret_cast<const uint8_t *>(t.bk), 64, act ? b : kNone, S, row);
+    bool done;
+    uint32_t res = bucket_match_sel(row, key, &done);
+    bool live = act && !done;
+    for (uint32_t step = 1; __ballot(live) && step <= t.bmask; step++) {  // (rare)
+      b = (b + 1) & t.bmask;
+      wave_gather64(reinterpret_cast<const uint8_t *>(t.bk), 64, live ? b : kNone, S, row);
       if (live) {
-        bool done;
-        const uint32_t idx = bucket_match(row[0], row[1], row[2], row[3], key, &done);
+        const uint32_t r2 = bucket_match(row[0], row[1], row[2], row[3], key, &done);
         if (done) {
-          res = idx;
+          res = r2;
           live = false;
-        } else {
-          b = (b + 1) & t.bmask;
         }
       }
-      if (!__ballot(live) || step >= t.bmask) break;
     }
     if (act) reply[j] = res;
   }
@@ -1411,15 +1435,18 @@ struct PhaseA {
   float ms;
 };
 
-// VIGPATH_PHASES=1: per-segment stage times of the owner-mode phase A on
-// stderr (diagnostics; events on the context's stream).
+// Owner-mode stage times: HIP events between the stages of every segment's
+// phase A when kernel timing is on (vp_kernel_timing: the timing pass of
+// bench.py --gpus N), summed into vp_ctx::stage_ms for vp_last_stage_ms;
+// VIGPATH_PHASES=1 also prints them per segment on stderr (diagnostics).
 struct PhaseMarks {
-  hipEvent_t ev[8] = {};
+  hipEvent_t ev[kStages + 1] = {};
   int n = 0;
-  bool on = false;
-  explicit PhaseMarks(hipStream_t s) : stream(s) {
+  bool on = false, print_on = false;
+  PhaseMarks(hipStream_t s, bool timing) : stream(s) {
     const char *e = getenv("VIGPATH_PHASES");
-    on = e && atoi(e);
+    print_on = e && atoi(e);
+    on = timing || print_on;
     if (on)
       for (auto &x : ev) (void)hipEventCreate(&x);
   }
@@ -1428,20 +1455,20 @@ struct PhaseMarks {
       for (auto &x : ev) (void)hipEventDestroy(x);
   }
   void mark() {
-    if (on && n < 8) (void)hipEventRecord(ev[n++], stream);
+    if (on && n <= kStages) (void)hipEventRecord(ev[n++], stream);
   }
-  void print(int rank, uint32_t np) {
+  void finish(vp_ctx *c, int rank, uint32_t np) {
     if (!on || n < 2) return;
     (void)hipEventSynchronize(ev[n - 1]);
-    static const char *names[] = {"pass1", "offsets", "a2a_keys", "probe",
-                                  "a2a_answers", "pass2", "fold"};
-    fprintf(stderr, "vigpath owner r%d n=%u:", rank, np);
+    if (print_on) fprintf(stderr, "vigpath owner r%d n=%u:", rank, np);
     for (int i = 1; i < n; i++) {
       float ms = 0.f;
       (void)hipEventElapsedTime(&ms, ev[i - 1], ev[i]);
-      fprintf(stderr, " %s %.3f", names[i - 1], ms);
+      c->stage_ms[i - 1] += ms;
+      if (print_on) fprintf(stderr, " %s %.3f", kStageNames[i - 1], ms);
     }
-    fprintf(stderr, " ms\n");
+    c->stage_n = std::max(c->stage_n, n - 1);
+    if (print_on) fprintf(stderr, " ms\n");
   }
   hipStream_t stream;
 };
@@ -1449,7 +1476,7 @@ struct PhaseMarks {
 static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
                              const NowSpec &now, uint32_t p0, uint32_t p1,
                              uint64_t seq0, PhaseA *ph) {
-  PhaseMarks pm(c->stream);
+  PhaseMarks pm(c->stream, c->ktime);
   FlowTable &t = c->ft;
   Workspace &w = c->ws;
   Comm &m = *c->comm;
@@ -1529,8 +1556,9 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   pm.mark();
   VP_TRY(m.alltoallv_dev(c, w.sendk, sk.data(), w.recvk, sk.data()));
   pm.mark();
-  nat_own_probe<<<grid_for((uint64_t)n * C, 256, 4096), 256, 0, c->stream>>>(
-      tbl_dev(t), c->crc_tab, w.recvk, n * C, C, w.rcnt, w.ovf64, t.ctl, w.reply);
+  nat_own_probe<<<resident_grid((const void *)nat_own_probe, ((uint64_t)n * C + 255) / 256), 256,
+                  0, c->stream>>>(tbl_dev(t), c->crc_tab, w.recvk, n * C, C, w.rcnt, w.ovf64,
+                                  t.ctl, w.reply);
   VP_HIP(hipGetLastError());
   pm.mark();
   VP_TRY(m.alltoallv_dev(c, w.reply, sr.data(), w.rreply, sr.data()));
@@ -1559,7 +1587,7 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   pm.mark();
   VP_TRY(tbl_fold_read_ctl(c, t, ph->bp, w.log, p0, p1, now, seq0, w.dtot));
   pm.mark();
-  pm.print(m.r, np);
+  pm.finish(c, m.r, np);
   uint32_t maxsend = 0;  // for the next batch's capacity (run_batch_sharded)
   for (uint32_t o = 0; o < n; o++)
     if (o != r) maxsend = std::max(maxsend, w.h_gath[kPubGath * n + o]);
@@ -1602,8 +1630,9 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
                                                w.sendk);
   VP_HIP(hipGetLastError());
   VP_TRY(m.alltoallv_dev(c, w.sendk, ek.data(), w.recvk, er.data()));
-  nat_own_probe<<<grid_for(std::max<uint64_t>(R, 1), 256, 4096), 256, 0, c->stream>>>(
-      tbl_dev(t), c->crc_tab, w.recvk, (uint32_t)R, 0, nullptr, nullptr, t.ctl, w.reply);
+  nat_own_probe<<<resident_grid((const void *)nat_own_probe, (std::max<uint64_t>(R, 1) + 255) / 256),
+                  256, 0, c->stream>>>(tbl_dev(t), c->crc_tab, w.recvk, (uint32_t)R, 0, nullptr,
+                                       nullptr, t.ctl, w.reply);
   VP_HIP(hipGetLastError());
   VP_TRY(m.alltoallv_dev(c, w.reply, fr.data(), w.rreply, fa.data()));
   VP_HIP(ev_record(c->ktime, c->ev2, c->stream));

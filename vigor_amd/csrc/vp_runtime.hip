@@ -782,6 +782,13 @@ int vp_kernel_timing(vp_ctx *c, int on) {
   return 0;
 }
 
+int vp_last_stage_ms(vp_ctx *c, float *ms, int *stages) {
+  if (!c || !ms || !stages) return VP_EINVAL;
+  for (int i = 0; i < kStages; i++) ms[i] = c->stage_ms[i];
+  *stages = c->stage_n;
+  return 0;
+}
+
 int vp_last_kernel_ms(vp_ctx *c, float *ms, int *launches) {
   if (!c || !ms || !launches) return VP_EINVAL;
   *ms = c->last_ms;

@@ -1538,6 +1538,8 @@ static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
   const uint32_t n = b->n;
   c->last_ms = 0.f;
   c->last_launches = 0;
+  for (float &x : c->stage_ms) x = 0.f;
+  c->stage_n = 0;
   // 1. every rank's slice size, time range and floors (one small gather);
   //    errors are decided from the gathered data so all ranks agree
   RankInfo me{};
