@@ -92,38 +92,42 @@ def frame_len_for(slot: int) -> int:
 
 
 class FlowBank:
-    """Per-flow header bytes of the synthetic trace, on the device. Wider
-    slots carry a fixed payload pattern (the L4 checksum sums it); 64-byte
-    slots the reference's zero payload."""
+    """Per-flow header bytes of the synthetic trace, on the device: bytes
+    24-37 (IPv4 checksum, addresses, ports) of flow i's frame. Default keys:
+    the bench flows (10.0.0.0 + (i >> 16) : i & 0xFFFF -> 0.0.0.0:0,
+    SURVEY.md §8(d)); `keys` = (src_ip, dst_ip, src_port, dst_port) arrays
+    (traces.random_flow_keys). Wider slots carry a fixed payload pattern (the
+    L4 checksum sums it); 64-byte slots the reference's zero payload."""
 
-    def __init__(self, n_flows: int, flow_base: int, dev, slot: int = 64):
+    def __init__(self, n_flows: int, flow_base: int, dev, slot: int = 64, keys=None):
         fl = np.arange(flow_base, flow_base + n_flows, dtype=np.int64)
-        src = T.ip4(10, 0, 0, 0) + (fl >> 16)
-        sp = fl & 0xFFFF
-        z = np.zeros_like(fl)
+        if keys is None:
+            z = np.zeros_like(fl)
+            keys = (T.ip4(10, 0, 0, 0) + (fl >> 16), z, fl & 0xFFFF, z)
         flen = frame_len_for(slot)
-        f, _ = T.udp_frames(src, z, sp, z, slot=slot, frame_len=flen)
+        f, _ = T.udp_frames(*keys, slot=slot, frame_len=flen)
         f = f.reshape(n_flows, slot)
         tmpl = f[0].copy()
         if slot > 64:  # (64 B: the reference's zero payload, bench.lua:61-71)
             tmpl[42:flen] = (np.arange(42, flen) * 7 % 251).astype(np.uint8)
         self.template = torch.from_numpy(tmpl).to(dev)
-        self.var = torch.from_numpy(np.ascontiguousarray(
-            np.concatenate([f[:, 24:30], f[:, 34:36]], axis=1))).to(dev)
+        self.var = torch.from_numpy(np.ascontiguousarray(f[:, 24:38])).to(dev)
         self.n = n_flows
         self.slot = slot
         self.frame_len = flen
 
-    def fill(self, frames: torch.Tensor, start: int, order: str = "rr"):
+    def fill_flows(self, frames: torch.Tensor, fl: torch.Tensor):
+        """Slot j of `frames` = the frame of flow fl[j]."""
         S = self.slot
         B = frames.shape[0] // S
         fv = frames.view(B, S)
         fv.copy_(self.template.expand(B, S))
+        fv[:, 24:38] = self.var.index_select(0, fl)
+
+    def fill(self, frames: torch.Tensor, start: int, order: str = "rr"):
+        B = frames.shape[0] // self.slot
         p = torch.arange(start, start + B, device=frames.device)
-        fl = uniform_flows(p, self.n) if order == "uniform" else p % self.n
-        v = self.var.index_select(0, fl)
-        fv[:, 24:30] = v[:, 0:6]
-        fv[:, 34:36] = v[:, 6:8]
+        self.fill_flows(frames, uniform_flows(p, self.n) if order == "uniform" else p % self.n)
 
 
 def verify_sample(frames: torch.Tensor, slot: int, ext_ip: int, k: int = 4096):
@@ -348,6 +352,201 @@ def end_to_end_mbuf(nat, bank, dev, start: int, steps: int = 3, imix: bool = Fal
             "ms_per_batch": round(el / len(times) * 1e3, 3),
             "pcie_bytes_per_packet": {"in": round(pin_in, 1), "out": round(pin_out, 1)},
             "parity": chk}
+
+
+# ------------------------------------------------------ extra workloads --
+# BASELINE configs[2] and [3] and two vignat variants,
+# each a steady state at 2^24 packets per step like the headline, its last
+# timed batch checked against the reference's digest of that exact batch
+# (tests/golden/bench_configs.npz, made by tests/golden/make_bench_golden.py
+# with the oracle glue over the reference's own libVig).
+EXTRA_STEPS = 8
+LB_MACS = [bytes([0x10 * d + i for i in range(6)]) for d in range(3)]
+
+
+def golden_configs():
+    path = os.path.join(ROOT, "tests", "golden", "bench_configs.npz")
+    if not os.path.exists(path):
+        return {}
+    with np.load(path, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def steady_workload(nf, batch_of, warm: int, steps: int, B: int, dev, golden=None,
+                    kernel="", times=None, state=None):
+    """Batches 0 .. warm-1 untimed (allocation), then `steps` timed calls
+    (batches warm ..) without timing events, each from its own buffer filled
+    before the timed region; the last timed batch's digest against golden[k]
+    (the reference's digest of batch k); then a kernel-timing pass over the
+    next `steps` batches. batch_of(k, buf) fills buf (B * 64 bytes) with batch
+    k's frames and returns (lens, in_dev, now0, now_step) device tensors /
+    ints. Returns the line's dict."""
+    out = torch.zeros(B, dtype=torch.int16, device=dev)
+
+    def run(k0, n, events):
+        nf.kernel_timing(events)
+        bufs, args = [], []
+        for k in range(k0, k0 + n):
+            b = torch.empty(B * SLOT, dtype=torch.uint8, device=dev)
+            args.append(batch_of(k, b))
+            bufs.append(b)
+        kms = []
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for b, (ln, ind, n0, st) in zip(bufs, args):
+            nf.process_device(b, ln, ind, out, SLOT, now0=n0, now_step=st)
+            if events:
+                kms.append(nf.last_kernel_ms())
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        nf.kernel_timing(False)
+        return el, kms, bufs[-1]
+
+    t0 = time.perf_counter()
+    run(0, warm, False)
+    warm_s = time.perf_counter() - t0
+    el, _, last = run(warm, steps, False)
+    k_last = warm + steps - 1
+    parity = None
+    if golden is not None and k_last < len(golden):
+        got = T.batch_digest(last.cpu().numpy(), out.cpu().numpy().view(np.uint16), SLOT)
+        want = int(golden[k_last])
+        parity = {"batch": k_last, "batch_digest": "%016x" % got, "golden": "%016x" % want,
+                  "match": got == want,
+                  "source": "tests/golden/bench_configs.npz (reference libVig)"}
+        if state is not None and k_last == len(golden) - 1:  # (vignat: dchain state)
+            alloc, ts, _ = nf.dump()
+            sd = T.state_digest(alloc, ts)
+            parity.update({"state_digest": "%016x" % sd, "state_golden": "%016x" % int(state),
+                           "state_match": sd == int(state)})
+    del last
+    _, kms, last = run(warm + steps, steps, True)
+    del last
+    per_launch_s, pkts, achieved = kernel_rate(kms, B, steps, ALG_BYTES)
+    mpps = B * steps / el / 1e6
+    line = {"value": round(mpps, 1), "unit": "Mpps", "ms_per_step": round(el / steps * 1e3, 4),
+            "batch_packets": B, "steps": steps, "warm_batches": warm,
+            "warm_s": round(warm_s, 2),
+            "kernel": kernel, "kernel_ms_per_launch": round(per_launch_s * 1e3, 4),
+            "kernel_mpps": round(pkts / per_launch_s / 1e6, 1),
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "frac_step": round(mpps * 1e6 * ALG_BYTES / 1e9 / HBM_PEAK_GBS, 4),
+            "frac_basis": "92 B per packet (SURVEY.md §8(d) vignat basis), 8 TB/s",
+            "parity": parity}
+    if times is not None:
+        line.update(times)
+    return line
+
+
+def host_batch(dev, frames, lens, in_dev):
+    """A host-generated batch on the device (frames, lens, in_dev tensors)."""
+    return (torch.from_numpy(frames).to(dev),
+            torch.from_numpy(lens.astype(np.uint16).view(np.int16)).to(dev),
+            torch.from_numpy(in_dev.astype(np.uint16).view(np.int16)).to(dev))
+
+
+def bench_bridge_c3(dev, B, steps, golden):
+    """BASELINE configs[2]: vigbridge 64 B, 1M MACs (traces.bridge_trace:
+    station k on port k & 1, frame p from station p mod N to p + N/2). Batch
+    0 learns every station; from batch 1 on every frame hits (the batches'
+    frames are the same, their times advance)."""
+    N = 1 << 20
+    cfg = vigor_amd.bridge_config_from_args(["--capacity", str(N), "--expire", "60000000"], 2)
+    br = vigor_amd.Bridge(cfg, gpu=0)
+    fr, ln, dv, _ = T.bridge_trace(B, N)
+    src, lens, ind = host_batch(dev, fr, ln, dv)
+    del fr
+
+    def batch_of(k, buf):
+        buf.copy_(src)
+        return lens, ind, T.NOW0 + k * B, 1
+    r = steady_workload(br, batch_of, 1, steps, B, dev, golden, "bridge_classify")
+    br.close()
+    r["workload"] = "vigbridge 64B, 1M MACs, learn + lookup (BASELINE configs[2])"
+    return r
+
+
+def bench_lb_c4(dev, B, steps, golden):
+    """BASELINE configs[3]: viglb 64 B, 256 backends (heartbeats first) / 1M
+    flows (traces.lb_traffic on port 2)."""
+    N = 1 << 20
+    argv = ["--flow-capacity", str(N), "--backend-capacity", "256", "--cht-height", "257",
+            "--flow-expiration", "60000000", "--backend-expiration", "3600000000",
+            "--wan", "2"]
+    lb = vigor_amd.Lb(vigor_amd.lb_config_from_args(argv, 3, LB_MACS), gpu=0)
+    hb = T.lb_heartbeats(256)
+    f0, l0, d0 = host_batch(dev, hb[0], hb[1], hb[2])
+    lb.process_device(f0, l0, d0, torch.zeros(256, dtype=torch.int16, device=dev), SLOT,
+                      now=torch.from_numpy(hb[3]).to(dev))
+    fr, ln, dv, _ = T.lb_traffic(B, N)
+    src, lens, ind = host_batch(dev, fr, ln, dv)
+    del fr
+
+    def batch_of(k, buf):
+        buf.copy_(src)
+        return lens, ind, T.NOW0 + k * B, 1
+    r = steady_workload(lb, batch_of, 1, steps, B, dev, golden, "lb_classify64")
+    lb.close()
+    r["workload"] = "viglb 64B, 256 backends / 1M flows (BASELINE configs[3])"
+    return r
+
+
+def make_nat(flows, expire_us=60_000_000):
+    args = [a for a in NAT_ARGS]
+    args[args.index("--expire") + 1] = str(expire_us)
+    cfg = vigor_amd.nat_config_from_args(args + ["--max-flows", str(flows)], 2, DEV_MACS)
+    return vigor_amd.Nat(cfg, gpu=0)
+
+
+def bench_nat_random(dev, B, steps, golden):
+    """vignat 64 B, 1M flows whose 5-tuples have no counter structure
+    (traces.random_flow_keys), round robin: the allocation-order layout does
+    not fit them, the table keeps the CRC bits."""
+    N = 1 << 20
+    nat = make_nat(N)
+    bank = FlowBank(N, 0, dev, keys=T.random_flow_keys(N))
+    lens = torch.full((B,), 60, dtype=torch.int16, device=dev)
+    ind = torch.zeros(B, dtype=torch.int16, device=dev)
+
+    def batch_of(k, buf):
+        bank.fill(buf, k * B)
+        return lens, ind, T.NOW0 + k * B, 1
+    r = steady_workload(nat, batch_of, 1, steps, B, dev, golden, "nat_classify64")
+    r["table_layout"] = nat.table_stats()["layout"]
+    nat.close()
+    r["workload"] = "vignat 64B, 1M flows with random 5-tuples, round robin"
+    return r
+
+
+def bench_nat_churn(dev, B, steps, golden, state=None):
+    """vignat 64 B with steady turnover at the reference's latency-run expiry
+    (1 s, run-middlebox.sh:16; traces.churn_trace): 2^18 flow slots round
+    robin, a quarter of them starting new flows every batch while the flows
+    they retire expire 1 s after their last packet; one timestamp per batch
+    (250 ms apart; nf.c stamps a polling sweep with one current_time(),
+    nf.c:56). Per steady batch: 65,536 new flows allocated (phase B) and
+    65,536 expired at its first packet (expire_items_single_map,
+    expirator.c:110-218), every other packet a hit."""
+    W = T.CHURN_W
+    nat = make_nat(1 << 20, T.CHURN_EXPIRE_US)
+    warm = 8
+    epochs = (warm + 2 * steps + 3) // 4 + 1
+    bank = FlowBank(epochs * W, 0, dev)
+    lens = torch.full((B,), 60, dtype=torch.int16, device=dev)
+    ind = torch.zeros(B, dtype=torch.int16, device=dev)
+    p = torch.arange(B, device=dev)
+    slot_id = p % W
+
+    def batch_of(k, buf):
+        bank.fill_flows(buf, (k + slot_id % 4) // 4 * W + slot_id)
+        return lens, ind, T.NOW0 + k * T.CHURN_DT, 0
+    r = steady_workload(nat, batch_of, warm, steps, B, dev, golden, "nat_classify64",
+                        state=state)
+    r["live_flows"] = nat.live_count()
+    nat.close()
+    r["workload"] = ("vignat 64B, steady turnover at 1 s expiry: 2^18 flows round robin, "
+                     "65,536 new and 65,536 expiring per 2^24-packet batch")
+    return r
 
 
 def launch_ranks(n: int) -> int:
@@ -636,6 +835,18 @@ def main():
         extra["end_to_end_mbuf"] = end_to_end_mbuf(nat, bank, dev, base)
         extra["end_to_end_mbuf_imix"] = end_to_end_mbuf(nat, bank, dev,
                                                         base + 4 * MBUF_BATCH, imix=True)
+    if (world == 1 and not args.no_extra and slot == SLOT and args.order == "rr"
+            and not args.route_all and args.flows == 1 << 20):
+        nat.close()
+        bank = None
+        torch.cuda.empty_cache()
+        gold = golden_configs()
+        steps_x = min(args.steps, EXTRA_STEPS)
+        extra["config3_bridge"] = bench_bridge_c3(dev, B, steps_x, gold.get("bridge"))
+        extra["config4_lb"] = bench_lb_c4(dev, B, steps_x, gold.get("lb"))
+        extra["nat_random_keys"] = bench_nat_random(dev, B, steps_x, gold.get("random"))
+        extra["nat_churn"] = bench_nat_churn(dev, B, steps_x, gold.get("churn"),
+                                             gold.get("churn_state"))
     if world > 1 and not args.no_extra:
         # the other dictionary placement, same workload
         other = "replicated" if mode == "owner" else "owner"

@@ -79,7 +79,7 @@ struct RcclComm : Comm {
   // one grouped send/recv per peer: every pair of GPUs talks over its own
   // xGMI link at once
   int alltoallv_dev(vp_ctx *c, const void *send, const size_t *sbytes, void *recv,
-                    const size_t *rbytes) override {
+                    const size_t *rbytes, bool skip_self) override {
     const uint8_t *s = static_cast<const uint8_t *>(send);
     uint8_t *d = static_cast<uint8_t *>(recv);
     size_t so = 0, ro = 0;
@@ -91,7 +91,7 @@ struct RcclComm : Comm {
       ro += rbytes[q];
     }
     if (sbytes[r] != rbytes[r]) return VP_EINVAL;
-    if (sbytes[r])
+    if (sbytes[r] && !skip_self)
       VP_HIP(hipMemcpyAsync(d + roff[r], s + soff[r], sbytes[r],
                             hipMemcpyDeviceToDevice, c->stream));
     VP_NCCL(ncclGroupStart());
@@ -156,10 +156,11 @@ struct HostComm : Comm {
     return 0;
   }
   int alltoallv_dev(vp_ctx *c, const void *send, const size_t *sbytes, void *recv,
-                    const size_t *rbytes) override {
+                    const size_t *rbytes, bool skip_self) override {
     if (!ops.alltoallv) return VP_ENOTSUP;
-    size_t st = 0, rt = 0;
+    size_t st = 0, rt = 0, r0 = 0;  // r0: where this rank's own chunk lands in recv
     for (int q = 0; q < n; q++) {
+      if (q == r) r0 = rt;
       st += sbytes[q];
       rt += rbytes[q];
     }
@@ -169,10 +170,16 @@ struct HostComm : Comm {
     VP_HIP(hipStreamSynchronize(c->stream));
     if (ops.alltoallv(ops.user, hs.data(), sbytes, hr.data(), rbytes))
       return comm_fail("alltoallv");
-    if (rt) {
-      VP_HIP(hipMemcpyAsync(recv, hr.data(), rt, hipMemcpyHostToDevice, c->stream));
-      VP_HIP(hipStreamSynchronize(c->stream));
-    }
+    // (skip_self: the callback moved every chunk, the own one is not copied
+    // back: the caller wrote it in place)
+    const size_t own = skip_self ? rbytes[r] : 0;
+    uint8_t *d = static_cast<uint8_t *>(recv);
+    if (r0)
+      VP_HIP(hipMemcpyAsync(d, hr.data(), r0, hipMemcpyHostToDevice, c->stream));
+    if (rt > r0 + own)
+      VP_HIP(hipMemcpyAsync(d + r0 + own, hr.data() + r0 + own, rt - r0 - own,
+                            hipMemcpyHostToDevice, c->stream));
+    VP_HIP(hipStreamSynchronize(c->stream));
     return 0;
   }
 };

@@ -326,6 +326,9 @@ __device__ __forceinline__ uint32_t bin_index(uint32_t bin, uint32_t local,
 // Append packet p's touch (kNone: none) to block rb's slice of its bin
 // (wave-uniform call; `range` = packets per block, range0 = the block's first
 // packet). A full slice logs the touch alone on the block's overflow queue.
+// kOvf: the overflow queue's LDS cursor (a kernel whose tables stay at 256
+// bins keeps only cursors 0..256, kOvf = 256, to make room in LDS).
+template <uint32_t kOvf = kCurOverflow>
 __device__ __forceinline__ void bins_put(const TouchBins &bins, uint32_t *cur,
                                          uint32_t rb, uint32_t range, uint32_t range0,
                                          uint32_t p, uint32_t touch) {
@@ -338,7 +341,7 @@ __device__ __forceinline__ void bins_put(const TouchBins &bins, uint32_t *cur,
     bins.ent[((size_t)b * bins.nsrc + rb) * bins.cap + k] =
         (bin_local(touch, bins.bbits) << bins.pbits) | (p - range0);
   const bool spill = v && !fits;
-  const uint32_t o = group_reserve(cur, kCurOverflow, spill);
+  const uint32_t o = group_reserve(cur, kOvf, spill);
   if (spill) {
     bins.olog[p] = touch;
     bins.oent[(size_t)rb * range + o] = p;
@@ -346,6 +349,7 @@ __device__ __forceinline__ void bins_put(const TouchBins &bins, uint32_t *cur,
 }
 
 // After the block's last bins_put and a barrier: publish its slice sizes.
+template <uint32_t kOvf = kCurOverflow>
 __device__ __forceinline__ void bins_publish(const TouchBins &bins, const uint32_t *cur,
                                              uint32_t rb) {
   if (!bins.ent) return;
@@ -354,7 +358,7 @@ __device__ __forceinline__ void bins_publish(const TouchBins &bins, const uint32
     bins.cnt[(size_t)b * bins.nsrc + rb] = c < bins.cap ? c : bins.cap;
   }
   if (threadIdx.x == 0) {
-    const uint32_t o = cur[kCurOverflow];
+    const uint32_t o = cur[kOvf];
     bins.ocnt[rb] = o;
     if (o) *bins.ovf = 1;
   }
@@ -394,7 +398,7 @@ __device__ __forceinline__ void bins_publish(const TouchBins &bins, const uint32
 // XCD-aware range order, as every block streams its own DRAM
 // pages and its packets' table rows stay near each other in its XCD's L2.
 // `cur` is kCurs LDS counters, zeroed by the kernel before its barrier.
-template <class Issue, class Finish>
+template <uint32_t kOvf = kCurOverflow, class Issue, class Finish>
 __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
                                                const uint16_t *len,
                                                const uint16_t *in_dev,
@@ -479,7 +483,7 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
       if (v) rq.ent[(size_t)rb * per_b * 64 + k] = p;
     }
     if (touch == kReprobe) touch = kNone;
-    bins_put(bins, cur, rb, per_b * 64, range0, p, touch);
+    bins_put<kOvf>(bins, cur, rb, per_b * 64, range0, p, touch);
     if (mod) {
 #pragma unroll
       for (uint32_t k = 0; k < 4; k++)
@@ -500,7 +504,7 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
     wave_lds_sync();  // the next tile overwrites S
   }
   if (bins.ent || rq.ent) __syncthreads();
-  bins_publish(bins, cur, rb);
+  bins_publish<kOvf>(bins, cur, rb);
   if (rq.ent && threadIdx.x == 0) {
     const uint32_t c = cur[kCurReprobe];
     rq.cnt[rb] = c;

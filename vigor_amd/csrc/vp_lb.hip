@@ -123,6 +123,11 @@ struct LbArgs {
   uint32_t *miss, *stale, *hb;  // queues M, S, H
   uint32_t *hbl;  // phase A: every heartbeat's position (its backend touch)
   uint16_t wan, n_dev;
+  // phase A with touch bins (lb_classify64): a hit's touch goes to the bins
+  // only and a dropped packet logs nothing; the packets the rounds finish
+  // log their touches themselves and are applied after the fold as late
+  // touches (lb_segment)
+  bool binned;
 };
 
 // cht_find_preferred_available_backend: bucket = (u64)hash % height, the
@@ -190,7 +195,7 @@ __device__ __forceinline__ void lb_heartbeat(const LbArgs &a, const uint32_t *I,
   const uint32_t key[4] = {sip, 0, 0, 0};
   const uint32_t bi = tbl_probe(a.bt, ip_hash(I, sip), key);
   a.out[p] = (uint16_t)in;
-  a.log[p] = kNone;
+  if (!a.binned) a.log[p] = kNone;
   a.log2[p] = bi;  // kNone: queued, the round writes the real entry
   const uint32_t k = wave_append(&a.bt.ctl->defer_count, true);  // heartbeats seen
   if (a.hbl) a.hbl[k] = p;
@@ -200,25 +205,35 @@ __device__ __forceinline__ void lb_heartbeat(const LbArgs &a, const uint32_t *I,
 // A WAN packet after its flow lookup (fi, and the entry's word 3): a flow
 // with a live backend is handed to `rw` with the backend record; the rest
 // are queued (M: no flow, S: its backend is gone).
+// `brec`: the backends staged in LDS by lb_classify64 (record, .w = live),
+// or null: their liveness and record from global memory.
 template <class Rw>
 __device__ __forceinline__ bool lb_flow_found(const LbArgs &a, uint32_t p, uint32_t fi,
-                                              uint32_t w3, Rw rw, uint32_t *touch) {
+                                              uint32_t w3, Rw rw, uint32_t *touch,
+                                              const uint4 *brec = nullptr) {
   if (fi == kNone) {
-    a.log[p] = kNone;
+    if (!a.binned) a.log[p] = kNone;
     a.miss[wave_append(&a.ft.ctl->miss_count, true)] = p;
     return false;
   }
   const uint32_t bi = w3 >> 8;
-  // the backend's liveness and record in one round trip (both depend on bi
-  // only; the record of a dead backend is read and ignored)
-  const uint32_t live = a.bt.slot_of[bi];
-  const uint4 rec = a.be_rec[bi];
-  if (live == kNone) {  // backend gone: erase + re-lookup
-    a.log[p] = kNone;
+  // the backend's liveness and record: one LDS read, or one global round trip
+  // (both depend on bi only; the record of a dead backend is read and ignored)
+  uint4 rec;
+  bool live;
+  if (brec) {
+    rec = brec[bi];
+    live = rec.w != 0;
+  } else {
+    live = a.bt.slot_of[bi] != kNone;
+    rec = a.be_rec[bi];
+  }
+  if (!live) {  // backend gone: erase + re-lookup
+    if (!a.binned) a.log[p] = kNone;
     a.stale[wave_append(&a.ft.ctl->defer_count, true)] = p;
     return false;
   }
-  a.log[p] = fi;
+  if (!a.binned) a.log[p] = fi;
   if (touch) *touch = fi;
   return rw(rec);
 }
@@ -254,7 +269,7 @@ __device__ __forceinline__ void lb_generic_a(const LbArgs &a, const uint32_t *T,
   const L34 h = parse_l34(f, a.len[p]);
   if (!h.ok) {
     a.out[p] = (uint16_t)in;
-    a.log[p] = kNone;
+    if (!a.binned) a.log[p] = kNone;
     return;
   }
   const uint32_t proto = f.r8(h.ip + 9);
@@ -281,19 +296,35 @@ struct LbPend {
   uint32_t row;   // the flow's home bucket (kind 2), or kNone
   uint32_t kind;  // 0: done; 1: byte path; 2: WAN flow; 3: heartbeat
 };
+// The backends (up to 256: the BASELINE config's 256) are staged in LDS
+// beside the tables, record and liveness in one 16-byte entry (the backend
+// table does not change during phase A: heartbeats wait for the rounds), so a
+// hit's backend costs one LDS read instead of a dependent global round trip.
+// To make room, the tile loop keeps only the cursors of 256 touch bins and
+// the overflow queue's (lb_segment keeps the flow table's bins at 256).
+constexpr uint32_t kLbLdsBackends = 256;
+constexpr uint32_t kLbCurs = 257;  // bins 0..255, the overflow queue at 256
 __global__ __launch_bounds__(256, 4) void lb_classify64(LbArgs a, uint32_t n_all,
                                                        TouchBins bins) {
   __shared__ uint32_t T[kLbFlowTabs * 256 + 1024];  // + the layout's byte tables
   __shared__ uint4 stage[4][256];
-  __shared__ uint32_t cur[kCurs];
-  for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
+  __shared__ uint32_t cur[kLbCurs];
+  __shared__ uint4 brec[kLbLdsBackends];
+  for (uint32_t i = threadIdx.x; i < kLbCurs; i += blockDim.x) cur[i] = 0;
   for (uint32_t i = threadIdx.x; i < kLbFlowTabs * 256; i += blockDim.x) T[i] = a.crc_tab[i];
   const uint32_t *lin = T + kLbFlowTabs * 256;
   if (a.ft.mix == kMixLin)
     for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) T[kLbFlowTabs * 256 + i] = a.ft.lin[i];
+  const bool lds_be = a.bcap <= kLbLdsBackends;
+  if (lds_be)
+    for (uint32_t b = threadIdx.x; b < a.bcap; b += blockDim.x) {
+      uint4 r = a.be_rec[b];
+      r.w = a.bt.slot_of[b] != kNone ? 1u : 0u;
+      brec[b] = r;
+    }
   __syncthreads();
   const uint32_t *I = a.crc_tab + kLbFlowTabs * 256;  // ip_addr tables (global)
-  frames64_tiles(
+  frames64_tiles<kLbCurs - 1>(
       a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
       reinterpret_cast<const uint4 *>(a.ft.bk),
       [&](uint32_t p, const RFrame &f, uint32_t in, uint32_t len, bool mine) {
@@ -312,7 +343,7 @@ __global__ __launch_bounds__(256, 4) void lb_classify64(LbArgs a, uint32_t n_all
                         ((proto == 6) | (proto == 17)) & ((uint32_t)(len - 34) >= 4u);
         if (!ok) {
           a.out[p] = (uint16_t)in;
-          a.log[p] = kNone;
+          if (!a.binned) a.log[p] = kNone;
           return P;
         }
         if (in != a.wan) {
@@ -350,7 +381,7 @@ __global__ __launch_bounds__(256, 4) void lb_classify64(LbArgs a, uint32_t n_all
           fi = tbl_probe_from<0xFFu>(a.ft, (P.row + 1) & a.ft.bmask, key, a.ft.bmask, &w3);
         const bool rw = lb_flow_found(a, p, fi, w3, [&](uint4 rec) {
           return lb_rewrite_fast(a, f, rec, proto, tl, p);
-        }, &touch);
+        }, &touch, lds_be ? brec : nullptr);
         // dst address, MACs and checksums change bytes 0-47 (and the TCP
         // checksum 50-51): the whole 64-byte slot is stored back, since a
         // partial-line write costs more than a whole one
@@ -630,13 +661,16 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   const bool tiles64 = b->slot == 64 && c->coalesced_io;
   VP_HIP(ev_record(c->ktime, c->ev0, c->stream));
   if (tiles64) {
-    // the flow touches also go to the touch bins (the log stays complete:
-    // the rounds below refold it whenever a queue is non-empty)
+    // the flow touches go to the touch bins (256 of them: lb_classify64 keeps
+    // 256 bin cursors; a larger table logs every touch and refolds the log)
     VP_TRY(tbl_bins_plan(c, c->ft, (const void *)lb_classify64, p0, p1, &bp));
+    if (bp.on && bp.bins.bbits > 8) bp = BinsPlan{};
     const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
     const uint32_t grid =
         bp.on ? bp.grid : resident_grid((const void *)lb_classify64, (tiles + 3) / 4);
-    lb_classify64<<<grid, 256, 0, c->stream>>>(a, b->n, bp.bins);
+    LbArgs a64 = a;
+    a64.binned = bp.on;
+    lb_classify64<<<grid, 256, 0, c->stream>>>(a64, b->n, bp.bins);
   } else {
     lb_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
   }
@@ -669,6 +703,7 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   const uint32_t nh = c->ft2.h_ctl.miss_count, nhb = c->ft2.h_ctl.defer_count;
   const bool ovf = bp.on && c->ft.h_ctl.touch_ovf != 0;
 
+  std::vector<uint32_t> M_all, S_all;  // phase A's queues (multi-round segments)
   if (nm || ns || nh) {
     VP_TRY(sort_list(c, w.miss, w.miss_sorted, nm));
     VP_TRY(sort_list(c, w.defer, w.defer_sorted, ns));
@@ -685,6 +720,8 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
       VP_HIP(hipMemcpyAsync(H.data(), w.aux_sorted, 4ull * nh,
                             hipMemcpyDeviceToHost, c->stream));
       VP_HIP(hipStreamSynchronize(c->stream));
+      M_all = M;
+      S_all = S;
       uint32_t im = 0, is = 0, ih = 0;
       bool first = true;
       std::vector<uint32_t> rl;
@@ -738,8 +775,34 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
       }
     }
   }
-  // the rounds completed the log (or a bin slice overflowed): refold it
-  if (nm || ns || nh || ovf) VP_TRY(tbl_touch_reduce(c, c->ft, w.log, p0, p1, now, c->seq));
+  if (bp.on) {
+    // the fold applied phase A's binned touches; the packets the rounds
+    // finished (the M and S queues) and the touches a full bin slice queued
+    // follow as late touches (last toucher in packet order still wins)
+    if (ovf)
+      VP_TRY(tbl_late_touches(c, c->ft, bp.bins.oent, bp.bins.ocnt, 0, bp.range, bp.grid,
+                              w.log, now, c->seq));
+    if (nm || ns) {
+      const uint32_t *lm = w.miss_sorted, *ls = w.defer_sorted;
+      if (nh) {  // (the rounds re-sorted the queues: the phase-A lists again)
+        VP_HIP(hipMemcpyAsync(w.rlist, M_all.data(), 4ull * nm, hipMemcpyHostToDevice,
+                              c->stream));
+        VP_HIP(hipMemcpyAsync(w.rlist + nm, S_all.data(), 4ull * ns, hipMemcpyHostToDevice,
+                              c->stream));
+        lm = w.rlist;
+        ls = w.rlist + nm;
+      }
+      if (nm)
+        VP_TRY(tbl_late_touches(c, c->ft, lm, nullptr, nm, 256, (nm + 255) / 256, w.log, now,
+                                c->seq));
+      if (ns)
+        VP_TRY(tbl_late_touches(c, c->ft, ls, nullptr, ns, 256, (ns + 255) / 256, w.log, now,
+                                c->seq));
+    }
+  } else if (nm || ns || nh) {
+    // the rounds completed the log: refold it
+    VP_TRY(tbl_touch_reduce(c, c->ft, w.log, p0, p1, now, c->seq));
+  }
   if (nhb)  // the heartbeats' backend touches (log2 holds only theirs)
     VP_TRY(tbl_late_touches(c, c->ft2, w.hbl, nullptr, nhb, 256, (nhb + 255) / 256,
                             w.log2, now, c->seq));

@@ -1204,12 +1204,17 @@ __global__ __launch_bounds__(256) void route_pack(const uint4 *desc, const uint3
 // kNone (a new flow: the ingest rank queues the packet for phase B).
 // Padded exchange (cap > 0): n keys arrived as ranks x cap, peer q's first
 // rcnt[q] valid; no work when any rank overflowed (*ovf, published as
-// ctl->route_ovf for the host). cap == 0: n keys, all valid.
+// ctl->route_ovf for the host). This rank's own keys (q == self) are read
+// where they were packed (`own_keys`, the send buffer, same layout) and
+// answered in place (`own_reply`, the answers' receive buffer): the
+// exchanges skip the rank's own chunk. cap == 0: n keys, all valid.
 __global__ __launch_bounds__(256, 4) void nat_own_probe(TableDev t, const uint32_t *crc_tab,
                                                         const uint4 *keys, uint32_t n,
                                                         uint32_t cap, const uint32_t *rcnt,
                                                         const uint64_t *ovf, Ctl *ctl,
-                                                        uint32_t *reply) {
+                                                        uint32_t *reply, uint32_t self,
+                                                        const uint4 *own_keys,
+                                                        uint32_t *own_reply) {
   __shared__ uint32_t T[kNatTabWords];
   __shared__ uint4 stage[4][256];
   const bool skip = cap && *ovf;
@@ -1227,12 +1232,14 @@ __global__ __launch_bounds__(256, 4) void nat_own_probe(TableDev t, const uint32
   auto valid_at = [&](uint32_t j) {
     return j < n && (!cap || j % cap < rcnt[j / cap]);
   };
+  auto own = [&](uint32_t j) { return cap && j / cap == self; };
   uint32_t tile = blockIdx.x * per_b + wv;
   bool vn = false;
   uint4 kn = make_uint4(0, 0, 0, 0);
   if (tile < tend) {
-    vn = valid_at(tile * 64 + lane);
-    if (vn) kn = keys[tile * 64 + lane];
+    const uint32_t j = tile * 64 + lane;
+    vn = valid_at(j);
+    if (vn) kn = (own(j) ? own_keys : keys)[j];
   }
   for (; tile < tend; tile += 4) {
     const uint32_t j = tile * 64 + lane;
@@ -1240,7 +1247,7 @@ __global__ __launch_bounds__(256, 4) void nat_own_probe(TableDev t, const uint32
     const uint4 k = kn;
     if (tile + 4 < tend) {  // the next tile's keys
       vn = valid_at(j + 256);
-      kn = vn ? keys[j + 256] : make_uint4(0, 0, 0, 0);
+      kn = vn ? (own(j + 256) ? own_keys : keys)[j + 256] : make_uint4(0, 0, 0, 0);
     }
     if (!__ballot(act)) continue;
     const uint32_t key[4] = {k.x, k.y, k.z, k.w};
@@ -1263,7 +1270,7 @@ __global__ __launch_bounds__(256, 4) void nat_own_probe(TableDev t, const uint32
         }
       }
     }
-    if (act) reply[j] = res;
+    if (act) (own(j) ? own_reply : reply)[j] = res;
   }
 }
 
@@ -1550,18 +1557,20 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   route_pack<<<ph->grid1, 256, 0, c->stream>>>(w.desc, w.dcnt, w.dbase, n, ph->range1, C,
                                                w.sendk);
   VP_HIP(hipGetLastError());
+  // (this rank's own chunk stays where route_pack put it: the probe reads
+  // it from sendk and answers it into rreply, no self copies)
   std::vector<size_t> s4(n, 4), sk(n, 16ull * C), sr(n, 4ull * C);
   VP_TRY(m.alltoallv_dev(c, w.dtot, s4.data(), w.rcnt, s4.data()));
   VP_TRY(m.allreduce_max_u64_dev(c, w.ovf64, 1));
   pm.mark();
-  VP_TRY(m.alltoallv_dev(c, w.sendk, sk.data(), w.recvk, sk.data()));
+  VP_TRY(m.alltoallv_dev(c, w.sendk, sk.data(), w.recvk, sk.data(), true));
   pm.mark();
   nat_own_probe<<<resident_grid((const void *)nat_own_probe, ((uint64_t)n * C + 255) / 256), 256,
                   0, c->stream>>>(tbl_dev(t), c->crc_tab, w.recvk, n * C, C, w.rcnt, w.ovf64,
-                                  t.ctl, w.reply);
+                                  t.ctl, w.reply, r, w.sendk, w.rreply);
   VP_HIP(hipGetLastError());
   pm.mark();
-  VP_TRY(m.alltoallv_dev(c, w.reply, sr.data(), w.rreply, sr.data()));
+  VP_TRY(m.alltoallv_dev(c, w.reply, sr.data(), w.rreply, sr.data(), true));
   pm.mark();
   auto pass2 = [&]() -> int {
     if (!np) return 0;
@@ -1632,7 +1641,7 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   VP_TRY(m.alltoallv_dev(c, w.sendk, ek.data(), w.recvk, er.data()));
   nat_own_probe<<<resident_grid((const void *)nat_own_probe, (std::max<uint64_t>(R, 1) + 255) / 256),
                   256, 0, c->stream>>>(tbl_dev(t), c->crc_tab, w.recvk, (uint32_t)R, 0, nullptr,
-                                       nullptr, t.ctl, w.reply);
+                                       nullptr, t.ctl, w.reply, kNone, nullptr, nullptr);
   VP_HIP(hipGetLastError());
   VP_TRY(m.alltoallv_dev(c, w.reply, fr.data(), w.rreply, fa.data()));
   VP_HIP(ev_record(c->ktime, c->ev2, c->stream));

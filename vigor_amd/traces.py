@@ -318,3 +318,62 @@ class MbufPool:
             s = o + (int(shift[i]) if shift is not None else 0)
             out[i, :int(lens[i])] = self.rows[b, s:s + int(lens[i])]
         return out.reshape(-1)
+
+
+def random_flow_keys(n_flows: int, seed: int = 0xF10E5):
+    """Flow i of the unstructured-key workload: a 5-tuple with no counter
+    structure (src_ip a bijective mix of i, so the n keys are distinct;
+    dst_ip, ports from splitmix64), for the random-key steady state the
+    allocation-order layout cannot fit."""
+    i = np.arange(n_flows, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = (i * np.uint64(0x9E3779B1)) & np.uint64(0xFFFFFFFF)   # odd multiplier: bijective
+        x = x ^ (x >> np.uint64(15))                               # (xorshift: bijective)
+        x = (x * np.uint64(0x2C1B3C6D)) & np.uint64(0xFFFFFFFF)
+        src_ip = (x ^ (x >> np.uint64(12))).astype(np.int64)
+        r = splitmix64(seed, i)
+    dst_ip = (r & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    sp = ((r >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.int64)
+    dp = ((r >> np.uint64(48)) & np.uint64(0xFFFF)).astype(np.int64)
+    return src_ip, dst_ip, sp, dp
+
+
+# Steady turnover (SURVEY.md §8(f) rank 1 at the reference's latency-run
+# expiry, run-middlebox.sh:16): CHURN_W flow slots in round robin; slot s of
+# batch k carries flow epoch(s, k) * CHURN_W + s with epoch = (k + s % 4) // 4,
+# so every batch a quarter of the slots (CHURN_W / 4 flows) starts new flows
+# while the flows they retire go idle; batch k is stamped NOW0 + k *
+# CHURN_DT (one current_time() per batch, as nf.c stamps a polling sweep,
+# nf.c:56), and with 1 s expiry a retired flow expires at the first packet of
+# the fifth batch after its last one. Live flows settle at 2 * CHURN_W.
+CHURN_W = 1 << 18
+CHURN_DT = 250_000_000
+CHURN_EXPIRE_US = 1_000_000
+
+
+def churn_flow_ids(p: np.ndarray, k: int, w: int = CHURN_W) -> np.ndarray:
+    """Flow ids of packets p (positions in batch k) of the turnover trace."""
+    s = np.asarray(p, np.int64) % w
+    return (k + s % 4) // 4 * w + s
+
+
+def churn_trace(k: int, n_packets: int, start: int = 0, w: int = CHURN_W, slot: int = 64):
+    """Packets [start, start + n_packets) of batch k of the turnover trace
+    (vignat flow keys of churn_flow_ids; time NOW0 + k * CHURN_DT)."""
+    fl = churn_flow_ids(np.arange(start, start + n_packets), k, w)
+    z = np.zeros_like(fl)
+    frames, lens = udp_frames(ip4(10, 0, 0, 0) + (fl >> 16), z, fl & 0xFFFF, z, slot=slot)
+    in_dev = np.zeros(n_packets, np.uint16)
+    now = np.full(n_packets, NOW0 + k * CHURN_DT, np.int64)
+    return frames, lens, in_dev, now
+
+
+def random_key_trace(n_packets: int, n_flows: int, start: int = 0, slot: int = 64,
+                     keys=None):
+    """Round robin over the random_flow_keys flows, time NOW0 + p ns."""
+    src, dst, sp, dp = keys if keys is not None else random_flow_keys(n_flows)
+    fl = flow_order(n_packets, n_flows, "rr", start=start)
+    frames, lens = udp_frames(src[fl], dst[fl], sp[fl], dp[fl], slot=slot)
+    in_dev = np.zeros(n_packets, np.uint16)
+    now = NOW0 + np.arange(start, start + n_packets, dtype=np.int64)
+    return frames, lens, in_dev, now
