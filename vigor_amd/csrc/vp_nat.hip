@@ -535,15 +535,19 @@ __device__ __forceinline__ uint32_t bucket_match_sel(const uint4 *row,
 
 // 128-byte slots: the tail sums of the wave's tile from the registers the
 // dense fetch left (d[j] = chunk 64 j + lane: frame 8 j + lane / 8, part
-// lane % 8; parts 4-7 are the bytes 64-127 the L4 sum may cover): each
-// 8-lane group adds its frame's masked chunks, and frame f's sum goes to
-// lane f (round j = f / 8, from lane 8 (f % 8)).
-__device__ __forceinline__ uint32_t dense128_tail(const uint4 d[8], uint32_t end) {
+// lane % 8; parts 4-7 are the bytes 64-127 the L4 sum may cover), right
+// after the loads so the 8 chunks die early: each 8-lane group takes its
+// frame's end, 14 + total_length (bytes 16-17: part 1, the group's second
+// lane; only register-path frames, whose total_length is at most 114, use
+// the sum), adds the masked chunks, and frame f's sum goes to lane f (round
+// j = f / 8, from lane 8 (f % 8)).
+__device__ __forceinline__ uint32_t dense128_tail(const uint4 d[8]) {
   const uint32_t lane = threadIdx.x & 63, part = lane & 7;
   uint32_t tail = 0;
 #pragma unroll
   for (uint32_t j = 0; j < 8; j++) {
-    const uint32_t e = (uint32_t)__shfl((int)end, (int)(8 * j + (lane >> 3)));
+    const uint32_t w4 = (uint32_t)__shfl((int)d[j].x, (int)((lane & ~7u) | 1u));
+    const uint32_t e = min(128u, 14u + bswap16((uint16_t)(w4 & 0xFFFF)));
     const uint32_t o = 16 * part;
     uint32_t s = 0;
     if (part >= 4 && o < e) {
@@ -654,6 +658,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
     uint8_t *g8 = a.frames + (size_t)tb * slot;
     uint4 *g = reinterpret_cast<uint4 *>(g8);
     uint4 d8[D ? 8 : 1];  // D: the whole tile (128-byte slots)
+    uint32_t tail128 = 0;
     if constexpr (D) {
       // 128-byte slots: the tile's 8 KiB as eight 1 KiB-contiguous loads,
       // header chunks (part < 4 of a slot) into the frame image, the tail
@@ -667,6 +672,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
 #pragma unroll
       for (uint32_t j = 0; j < 8; j++)
         if ((lane & 7) < 4) S[chunk_swz(4 * (8 * j + (lane >> 3)) + (lane & 3))] = d8[j];
+      tail128 = dense128_tail(d8);
     } else {
       if constexpr (G > 0) fetch(tile);
 #pragma unroll
@@ -705,9 +711,8 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       // the prefetch, the tail sums while all of those are in flight, the
       // frame read back from S, then the finish half
       uint32_t end = 64;  // where this frame's L4 sum ends (64: no tail)
-      if (mine && nat_reg_ok(f, ln, lim)) end = 14 + bswap16((uint16_t)(f.w[4] & 0xFFFF));
-      uint32_t tail = 0;
-      if constexpr (D) tail = dense128_tail(d8, end);
+      if (!D && mine && nat_reg_ok(f, ln, lim)) end = 14 + bswap16((uint16_t)(f.w[4] & 0xFFFF));
+      uint32_t tail = tail128;
       const bool lean = lean_ok && __ballot(mine && nat_lan_fast_ok(a, f, in, ln, lim)) == ~0ull;
       NatPend pend{kPendDone, kNone, 0, 0};
       uint32_t rowid;
@@ -1233,44 +1238,86 @@ __global__ __launch_bounds__(256, 4) void nat_own_probe(TableDev t, const uint32
     return j < n && (!cap || j % cap < rcnt[j / cap]);
   };
   auto own = [&](uint32_t j) { return cap && j / cap == self; };
-  uint32_t tile = blockIdx.x * per_b + wv;
-  bool vn = false;
-  uint4 kn = make_uint4(0, 0, 0, 0);
-  if (tile < tend) {
-    const uint32_t j = tile * 64 + lane;
-    vn = valid_at(j);
-    if (vn) kn = (own(j) ? own_keys : keys)[j];
-  }
-  for (; tile < tend; tile += 4) {
-    const uint32_t j = tile * 64 + lane;
-    const bool act = vn;
-    const uint4 k = kn;
-    if (tile + 4 < tend) {  // the next tile's keys
-      vn = valid_at(j + 256);
-      kn = vn ? (own(j + 256) ? own_keys : keys)[j + 256] : make_uint4(0, 0, 0, 0);
+  // Software-pipelined over the wave's tiles: in the iteration for tile t
+  // the keys of tile t + 2 are loaded, tile t + 1 is hashed and its rows
+  // requested, and tile t's rows (requested one iteration earlier) are
+  // matched: two tiles' row requests in flight per wave.
+  const uint4 *rows = reinterpret_cast<const uint4 *>(t.bk);
+  struct Tile {
+    bool act;
+    uint4 k;
+  };
+  auto load = [&](uint32_t tl) {
+    Tile x{false, make_uint4(0, 0, 0, 0)};
+    if (tl < tend) {
+      const uint32_t j = tl * 64 + lane;
+      x.act = valid_at(j);
+      if (x.act) x.k = (own(j) ? own_keys + j : keys + j)[0];
     }
-    if (!__ballot(act)) continue;
-    const uint32_t key[4] = {k.x, k.y, k.z, k.w};
-    const uint32_t h = flowid_hash_batched(T, k.x & 0xFFFF, k.x >> 16, k.y, k.z,
-                                           k.w & 0xFFFF, (k.w >> 16) & 0xFF);
-    uint32_t b = home_bucket(h, t.bmask, t.mix, nat_lin(T));
-    uint4 row[4];
-    wave_gather64(reinterpret_cast<const uint8_t *>(t.bk), 64, act ? b : kNone, S, row);
-    bool done;
-    uint32_t res = bucket_match_sel(row, key, &done);
-    bool live = act && !done;
-    for (uint32_t step = 1; __ballot(live) && step <= t.bmask; step++) {  // (rare)
-      b = (b + 1) & t.bmask;
-      wave_gather64(reinterpret_cast<const uint8_t *>(t.bk), 64, live ? b : kNone, S, row);
-      if (live) {
-        const uint32_t r2 = bucket_match(row[0], row[1], row[2], row[3], key, &done);
-        if (done) {
-          res = r2;
-          live = false;
+    return x;
+  };
+  struct Rows {
+    uint32_t b;
+    uint4 q0, q1, q2, q3;
+  };
+  auto request = [&](const Tile &x) {  // hash, request the home rows
+    const uint4 k = x.k;
+    Rows r;
+    r.b = home_bucket(flowid_hash_batched(T, k.x & 0xFFFF, k.x >> 16, k.y, k.z, k.w & 0xFFFF,
+                                          (k.w >> 16) & 0xFF),
+                      t.bmask, t.mix, nat_lin(T));
+    const uint32_t want = x.act ? r.b : kNone;
+    // lane L: part L % 4 of the row of key 16 j + L / 4
+    auto part = [&](uint32_t j) {
+      const uint32_t rw = (uint32_t)__shfl((int)want, (int)(16 * j + (lane >> 2)));
+      return rw != kNone ? rows[4 * (size_t)rw + (lane & 3)] : make_uint4(0, 0, 0, 0);
+    };
+    r.q0 = part(0);
+    r.q1 = part(1);
+    r.q2 = part(2);
+    r.q3 = part(3);
+    return r;
+  };
+  uint32_t tile = blockIdx.x * per_b + wv;
+  Tile cur = load(tile), nxt = load(tile + 4);
+  const Rows zero{0, make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0),
+                  make_uint4(0, 0, 0, 0)};
+  Rows rc = __ballot(cur.act) ? request(cur) : zero;
+  for (; tile < tend; tile += 4) {
+    const Tile after = load(tile + 8);
+    const Rows rn = __ballot(nxt.act) ? request(nxt) : zero;
+    if (__ballot(cur.act)) {
+      const uint32_t j = tile * 64 + lane;
+      const uint32_t key[4] = {cur.k.x, cur.k.y, cur.k.z, cur.k.w};
+      uint4 row[4];
+      wave_lds_sync();  // (earlier readers of S are done)
+      S[chunk_swz(lane)] = rc.q0;
+      S[chunk_swz(64 + lane)] = rc.q1;
+      S[chunk_swz(128 + lane)] = rc.q2;
+      S[chunk_swz(192 + lane)] = rc.q3;
+      wave_lds_sync();
+#pragma unroll
+      for (uint32_t kk = 0; kk < 4; kk++) row[kk] = S[chunk_swz(4 * lane + kk)];
+      bool done;
+      uint32_t res = bucket_match_sel(row, key, &done);
+      bool live = cur.act && !done;
+      uint32_t b = rc.b;
+      for (uint32_t step = 1; __ballot(live) && step <= t.bmask; step++) {  // (rare)
+        b = (b + 1) & t.bmask;
+        wave_gather64(reinterpret_cast<const uint8_t *>(t.bk), 64, live ? b : kNone, S, row);
+        if (live) {
+          const uint32_t r2 = bucket_match(row[0], row[1], row[2], row[3], key, &done);
+          if (done) {
+            res = r2;
+            live = false;
+          }
         }
       }
+      if (cur.act) (own(j) ? own_reply + j : reply + j)[0] = res;
     }
-    if (act) (own(j) ? own_reply : reply)[j] = res;
+    cur = nxt;
+    nxt = after;
+    rc = rn;
   }
 }
 
