@@ -809,7 +809,8 @@ int tbl_touch_reduce(vp_ctx *c, FlowTable &t, const uint32_t *log, uint32_t p0,
 // in-bin index in LDS, reading every source block's slice of its bin (one
 // contiguous region: the slices are bin-major), then
 // writes ts/tseq in runs of 64 consecutive indices. About 8 B of traffic per
-// packet (one write while classifying, one read here).
+// packet (one write while classifying, one read here); a run entry
+// (kBinRunFlag, vp_device.h) stands for 64 packets' touches in 4 bytes.
 constexpr uint32_t kBinLocalMax = 16384;  // in-bin indices held in LDS
 
 template <uint32_t kU>  // 64-entry chunks in flight per wave
@@ -859,8 +860,15 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
         e[u] = lane < lim[u] ? ent[((size_t)bin * nsrc + sb) * cap + k + lane] : 0u;
       }
 #pragma unroll
-      for (uint32_t u = 0; u < kU; u++)
-        if (lane < lim[u]) atomicMax(&last[e[u] >> pbits], base[u] + (e[u] & pmask));
+      for (uint32_t u = 0; u < kU; u++) {
+        const bool run = lane < lim[u] && (e[u] & kBinRunFlag);
+        if (lane < lim[u] && !run) atomicMax(&last[e[u] >> pbits], base[u] + (e[u] & pmask));
+        for (uint64_t m = __ballot(run); m; m &= m - 1) {  // (a run: 64 touches)
+          const uint32_t er = __builtin_amdgcn_readlane(e[u], __ffsll((unsigned long long)m) - 1);
+          atomicMax(&last[((er & ~kBinRunFlag) >> pbits) + lane],
+                    base[u] + (er & pmask) + lane);
+        }
+      }
     }
   }
   __syncthreads();
@@ -900,7 +908,7 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   const uint32_t nbins = 1u << bbits;
   const uint32_t L = (uint32_t)in_bin(bbits);
   const uint32_t pbits = std::max<uint32_t>(1, ceil_log2(range));
-  if (L > kBinLocalMax || ceil_log2(L) + pbits > 32) return 0;
+  if (L > kBinLocalMax || ceil_log2(L) + pbits > 31) return 0;  // (bit 31: kBinRunFlag)
   // twice a uniform share of a block's packets per bin, and at least two
   // waves' worth (a wave touching 64 consecutive indices fills one bin)
   const uint32_t cap =
