@@ -302,6 +302,7 @@ struct TouchBins {
   uint32_t *olog;  // olog[p] = index of an overflowed touch
   uint32_t cap, pbits, bbits;
   uint32_t nsrc;  // classify blocks (the launch's grid)
+  uint32_t runs;  // run entries: 0 off, 1 plain store, 2 non-temporal store
 };
 
 // Touch-log entry of packet p; `log` is null in the classify kernels that
@@ -345,15 +346,20 @@ __device__ __forceinline__ void bins_put(const TouchBins &bins, uint32_t *cur,
   const uint32_t q0 = __builtin_amdgcn_readfirstlane(p);
   const bool in_run = t0 != kNone && (t0 & (kBinRun - 1)) == 0 && touch == t0 + lane &&
                       p == q0 + lane;
-  if (__ballot(in_run) == ~0ull) {
+  if (bins.runs && __ballot(in_run) == ~0ull) {
     const uint32_t b0 = bin_of(t0, bins.bbits);
     uint32_t k = 0;
     if (lane == 0) k = atomicAdd(&cur[b0], 1u);
     k = __builtin_amdgcn_readfirstlane(k);
     if (k < bins.cap) {
-      if (lane == 0)
-        bins.ent[((size_t)b0 * bins.nsrc + rb) * bins.cap + k] =
-            kBinRunFlag | (bin_local(t0, bins.bbits) << bins.pbits) | (q0 - range0);
+      const uint32_t e = kBinRunFlag | (bin_local(t0, bins.bbits) << bins.pbits) | (q0 - range0);
+      uint32_t *dst = bins.ent + ((size_t)b0 * bins.nsrc + rb) * bins.cap + k;
+      if (lane == 0) {
+        if (bins.runs == 2)
+          __builtin_nontemporal_store(e, dst);
+        else
+          *dst = e;
+      }
       return;
     }
     // (a full slice: the 64 touches overflow one by one below)

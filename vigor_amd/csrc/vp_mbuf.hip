@@ -212,13 +212,10 @@ static MbufPlan mbuf_plan(const vp_ctx *c) {
   }
 }
 
-static uint32_t mbuf_blocks() {
-  static const uint32_t b = [] {
-    const char *e = getenv("VIGPATH_MBUF_BLOCKS");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? (uint32_t)v : 256u;
-  }();
-  return b;
+static uint32_t mbuf_blocks() {  // (read per batch: tools/mbuf_probe.py sweeps it)
+  const char *e = getenv("VIGPATH_MBUF_BLOCKS");
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? (uint32_t)v : 256u;
 }
 
 // Wait for an event by polling (the host thread polls, as a DPDK lcore does;

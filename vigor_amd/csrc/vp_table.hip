@@ -934,8 +934,10 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   plan->grid = grid;
   plan->range = range;
   plan->L = L;
+  const char *re = getenv("VIGPATH_BIN_RUNS");  // diagnostics: 0 off, 2 non-temporal
+  const uint32_t runs = re ? (uint32_t)atoi(re) : 1u;
   plan->bins = TouchBins{w.bins_ent, w.bins_cnt, &t.ctl->touch_ovf, w.ovf_q,
-                         w.ovf_cnt, w.log, cap, pbits, bbits, grid};
+                         w.ovf_cnt, w.log, cap, pbits, bbits, grid, runs};
   return 0;
 }
 

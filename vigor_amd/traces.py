@@ -273,12 +273,24 @@ class MbufPool:
     data room (DPDK's RTE_MBUF_DEFAULT_BUF_SIZE = 2048 + 128), so a frame
     starts at `data_off` = 256 into its element (rte_pktmbuf_mtod). `mem` is
     one flat uint8 array (page-locked when `pinned`, as DPDK's hugepages are
-    to the NIC); vp_register_host maps it for the GPU."""
+    to the NIC; on 2 MB transparent huge pages when `huge`, as DPDK's are
+    hugepages, then page-locked by vp_register_host); vp_register_host maps
+    it for the GPU."""
 
     def __init__(self, n: int, stride: int = 2304, data_off: int = 256,
-                 pinned: bool = False):
+                 pinned: bool = False, huge: bool = False):
         self.n, self.stride, self.data_off = n, stride, data_off
-        if pinned:
+        if huge:
+            import mmap
+            H = 1 << 21
+            self._map = mmap.mmap(-1, n * stride + H)
+            raw = np.frombuffer(self._map, np.uint8)
+            a = (-raw.ctypes.data) % H
+            if hasattr(mmap, "MADV_HUGEPAGE"):
+                self._map.madvise(mmap.MADV_HUGEPAGE)
+            self.mem = raw[a:a + n * stride]
+            self.mem[::4096] = 0  # (fault the pages in)
+        elif pinned:
             import torch
             self.mem = torch.zeros(n * stride, dtype=torch.uint8).pin_memory().numpy()
         else:  # page-aligned, as hugepages are
