@@ -53,6 +53,7 @@ def main():
         print(json.dumps({"thp": open("/sys/kernel/mm/transparent_hugepage/enabled").read().strip()}))
     except OSError:
         pass
+    start = 4 * B  # (times only move forward, across pools too)
     for kind in args.pools.split(","):
         pool = T.MbufPool(B, pinned=kind == "pinned", huge=kind == "huge")
         nat.register_host(pool.mem)
@@ -61,7 +62,6 @@ def main():
         ind = pin(np.zeros(B, np.uint16))
         out = pin(np.zeros(B, np.uint16))
         rng = np.random.default_rng(3)
-        start = 4 * B
         hdr = np.empty((B, 64), np.uint8)
         for var in args.variants.split(","):
             if var == "shuffled":

@@ -818,7 +818,7 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
     const uint32_t *ent, const uint32_t *cnt, uint32_t nsrc, uint32_t cap,
     uint32_t pbits, uint32_t bbits, uint32_t range, uint32_t L, uint32_t tcap,
     uint32_t p0, NowSpec now, uint64_t seq_base, uint64_t *ts, uint64_t *tseq,
-    PubArgs pub) {
+    PubArgs pub, uint32_t diag) {
   // 1 + position in the launch, 0 = none; L words of dynamic LDS (16 KB at
   // 1M flows: the 256 bin blocks spread over all CUs, where a 64 KB static
   // array let only two blocks share a CU and left half of them idle)
@@ -845,7 +845,7 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
       if (lane >= o) inc += t;
     }
     const uint32_t exc = inc - ch;
-    const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
+    const uint32_t total = (diag & 1) ? 0u : __builtin_amdgcn_readlane(inc, 63);
     for (uint32_t t0 = 0; t0 < total; t0 += kU) {
       uint32_t e[kU], lim[kU], base[kU];
 #pragma unroll
@@ -872,6 +872,7 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
     }
   }
   __syncthreads();
+  if (diag & 2) return;
   for (uint32_t l = threadIdx.x; l < L; l += blockDim.x) {
     const uint32_t v = last[l];
     const uint32_t i = bin_index(bin, l, bbits);
@@ -935,7 +936,7 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   plan->range = range;
   plan->L = L;
   const char *re = getenv("VIGPATH_BIN_RUNS");  // diagnostics: 0 off, 2 non-temporal
-  const uint32_t runs = re ? (uint32_t)atoi(re) : 1u;
+  const uint32_t runs = re ? (uint32_t)atoi(re) : 0u;  // (off: 15 % slower classify, r04e)
   plan->bins = TouchBins{w.bins_ent, w.bins_cnt, &t.ctl->touch_ovf, w.ovf_q,
                          w.ovf_cnt, w.log, cap, pbits, bbits, grid, runs};
   return 0;
@@ -950,12 +951,17 @@ static int bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p
     const int v = e ? atoi(e) : 0;
     return v == 16 || v == 32 ? (uint32_t)v : 8u;
   }();
+  // diagnostics only (wrong stamps): 1 skips the entries, 2 the stamp writes
+  static const uint32_t diag = [] {
+    const char *e = getenv("VIGPATH_FOLD_DIAG");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
   auto *fold = fold_u == 8 ? touch_bins_reduce<8> : fold_u == 32 ? touch_bins_reduce<32>
                                                                  : touch_bins_reduce<16>;
   fold<<<1u << plan.bins.bbits, 1024, 4u * plan.L, c->stream>>>(
       plan.bins.ent, plan.bins.cnt, plan.grid, plan.bins.cap, plan.bins.pbits,
       plan.bins.bbits, plan.range, plan.L, t.cap, p0, now, seq_base, t.ts, t.tseq,
-      pub);
+      pub, diag);
   VP_HIP(hipGetLastError());
   return 0;
 }
