@@ -19,4 +19,4 @@ for d in 0 1 2 3; do
 done
 VIGPATH_FOLD_U=32 step u32 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r04f_u32 -o run -- $T
 VIGPATH_BIN_RUNS=1 VIGPATH_FOLD_U=32 step runs_u32 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r04f_runs_u32 -o run -- $T
-step mbufprobe 500 python -u tools/mbuf_probe.py --pools huge,pinned --variants shuffled,dense --chunks 1048576 --blocks 256
+step mbufprobe 600 python -u tools/mbuf_probe.py --pools huge,pinned --variants shuffled,dense --chunks 1048576,262144 --blocks 256 --streams 2,1

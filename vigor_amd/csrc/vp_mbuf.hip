@@ -504,13 +504,17 @@ static int mbuf_pipeline(vp_ctx *c, const vp_mbuf_batch *b) {
     VP_HIP(hipEventRecord(w.mb_ev_done[i], c->stream));
     return 0;
   };
+  // VIGPATH_MBUF_STREAMS=1: write-backs on the gather stream, so PCIe reads
+  // and writes of the GPU alternate chunk by chunk instead of mixing
+  const char *se = getenv("VIGPATH_MBUF_STREAMS");
+  hipStream_t ws = se && atoi(se) == 1 ? w.cstream : w.dstream;
   auto issue_scatter = [&](uint32_t k) -> int {
     if (staged[k]) return 0;
     const uint32_t i = k % S, m = cnt(k);
-    VP_HIP(hipStreamWaitEvent(w.dstream, w.mb_ev_done[i], 0));
+    VP_HIP(hipStreamWaitEvent(ws, w.mb_ev_done[i], 0));
     const uint32_t wb = wslot[k] ? pl.wb_full : pl.wb_hdr;
     if (wb && m) {
-      mbuf_scatter<<<std::min<uint32_t>(G, (m + 63) / 64), 256, 0, w.dstream>>>(
+      mbuf_scatter<<<std::min<uint32_t>(G, (m + 63) / 64), 256, 0, ws>>>(
           w.mb_ptr + (size_t)i * ch, w.mb_len + (size_t)i * ch, w.mb_in + (size_t)i * ch,
           w.mb_out + (size_t)i * ch, m, mt,
           wslot[k] ? w.mb_full : w.mb_slots + (size_t)i * ch * 64, wslot[k] ? wslot[k] : 64,
@@ -518,8 +522,8 @@ static int mbuf_pipeline(vp_ctx *c, const vp_mbuf_batch *b) {
       VP_HIP(hipGetLastError());
     }
     VP_HIP(hipMemcpyAsync(hout(k), w.mb_out + (size_t)i * ch, 2ull * m, hipMemcpyDeviceToHost,
-                          w.dstream));
-    VP_HIP(hipEventRecord(w.mb_ev_out[i], w.dstream));
+                          ws));
+    VP_HIP(hipEventRecord(w.mb_ev_out[i], ws));
     return 0;
   };
   for (uint32_t k = 0; k < std::min<uint32_t>(K, 2); k++) VP_TRY(issue_gather(k));
