@@ -851,13 +851,27 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
 #pragma unroll
       for (uint32_t u = 0; u < kU; u++) {
         const uint32_t t = t0 + u;
-        const uint64_t own = __ballot(exc <= t && t < inc);  // (none past the list)
-        const uint32_t l = own ? (uint32_t)__ffsll((unsigned long long)own) - 1 : 0u;
+        uint64_t own = __ballot(exc <= t && t < inc);  // (none past the list)
+        uint32_t l = own ? (uint32_t)__ffsll((unsigned long long)own) - 1 : 0u;
+        if (diag & 16) {  // (diagnostics: one chunk per slice assumed)
+          l = t & 63;
+          own = 1;
+        }
         const uint32_t k = (t - __builtin_amdgcn_readlane(exc, l)) << 6;
         const uint32_t sb = r0 + l * nw;
         lim[u] = own ? __builtin_amdgcn_readlane(nv, l) - k : 0u;
         base[u] = sb * range + 1;
-        e[u] = lane < lim[u] ? ent[((size_t)bin * nsrc + sb) * cap + k + lane] : 0u;
+        if (diag & 8)  // (diagnostics: no entry loads)
+          e[u] = lane < lim[u] ? ((t * 64 + lane) % L) << pbits : 0u;
+        else
+          e[u] = lane < lim[u] ? ent[((size_t)bin * nsrc + sb) * cap + k + lane] : 0u;
+      }
+      if (diag & 4) {  // (diagnostics: no LDS atomics)
+        uint32_t acc = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) acc |= e[u];
+        if (acc == 0x7FFFFFFFu) last[lane] = acc;
+        continue;
       }
 #pragma unroll
       for (uint32_t u = 0; u < kU; u++) {
@@ -951,7 +965,8 @@ static int bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p
     const int v = e ? atoi(e) : 0;
     return v == 16 || v == 32 ? (uint32_t)v : 8u;
   }();
-  // diagnostics only (wrong stamps): 1 skips the entries, 2 the stamp writes
+  // diagnostics only (wrong stamps): 1 skips the entries, 2 the stamp writes,
+  // 4 the LDS atomics, 8 the entry loads, 16 the chunk search
   static const uint32_t diag = [] {
     const char *e = getenv("VIGPATH_FOLD_DIAG");
     return e ? (uint32_t)atoi(e) : 0u;
