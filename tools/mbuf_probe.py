@@ -32,8 +32,6 @@ def main():
     ap.add_argument("--variants", default="shuffled,sequential,dense")
     ap.add_argument("--chunks", default="1048576")
     ap.add_argument("--blocks", default="256")
-    ap.add_argument("--streams", default="2",
-                    help="VIGPATH_MBUF_STREAMS: 2 write-backs on their own stream, 1 on the gather's")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--pools", default="pinned",
                     help="pinned (page-locked 4 KB pages), huge (2 MB THP, registered)")
@@ -76,9 +74,7 @@ def main():
                 bufs = None
                 ptrs = pin(np.uint64(pool.mem.ctypes.data) + np.arange(B, dtype=np.uint64) * 64)
             for ch in args.chunks.split(","):
-                for blk, st in [(b, t) for b in args.blocks.split(",")
-                                for t in args.streams.split(",")]:
-                    os.environ["VIGPATH_MBUF_STREAMS"] = st
+                for blk in args.blocks.split(","):
                     os.environ["VIGPATH_HOST_CHUNK"] = ch
                     os.environ["VIGPATH_MBUF_BLOCKS"] = blk
                     call = nat.mbuf_step(ptrs, lens, ind, out)
@@ -99,7 +95,6 @@ def main():
                     assert (out == 1).all()
                     el = sum(times) / len(times)
                     print(json.dumps({"pool": kind, "layout": var, "chunk": int(ch), "blocks": int(blk),
-                                      "streams": int(st),
                                       "ms_per_call": round(el * 1e3, 3),
                                       "mpps": round(B / el / 1e6, 1)}), flush=True)
         nat.unregister_host(pool.mem)

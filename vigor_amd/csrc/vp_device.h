@@ -302,7 +302,6 @@ struct TouchBins {
   uint32_t *olog;  // olog[p] = index of an overflowed touch
   uint32_t cap, pbits, bbits;
   uint32_t nsrc;  // classify blocks (the launch's grid)
-  uint32_t runs;  // run entries: 0 off, 1 plain store, 2 non-temporal store
 };
 
 // Touch-log entry of packet p; `log` is null in the classify kernels that
@@ -324,13 +323,6 @@ __device__ __forceinline__ uint32_t bin_index(uint32_t bin, uint32_t local,
          (local & (kBinRun - 1));
 }
 
-// Run entries: a wave whose 64 packets p0 .. p0 + 63 touch the 64
-// consecutive indices i0 .. i0 + 63 of one bin run (i0 a multiple of 64: a
-// tile of round-robin traffic over allocation-ordered flows) appends the
-// single entry kBinRunFlag | (in-bin of i0) << pbits | (p0 - range0), which
-// the fold expands to the 64 touches: 4 bytes per 64 packets instead of 256.
-constexpr uint32_t kBinRunFlag = 0x80000000u;
-
 // Append packet p's touch (kNone: none) to block rb's slice of its bin
 // (wave-uniform call; `range` = packets per block, range0 = the block's first
 // packet). A full slice logs the touch alone on the block's overflow queue.
@@ -341,29 +333,6 @@ __device__ __forceinline__ void bins_put(const TouchBins &bins, uint32_t *cur,
                                          uint32_t rb, uint32_t range, uint32_t range0,
                                          uint32_t p, uint32_t touch) {
   if (!bins.ent) return;
-  const uint32_t lane = __lane_id();
-  const uint32_t t0 = __builtin_amdgcn_readfirstlane(touch);
-  const uint32_t q0 = __builtin_amdgcn_readfirstlane(p);
-  const bool in_run = t0 != kNone && (t0 & (kBinRun - 1)) == 0 && touch == t0 + lane &&
-                      p == q0 + lane;
-  if (bins.runs && __ballot(in_run) == ~0ull) {
-    const uint32_t b0 = bin_of(t0, bins.bbits);
-    uint32_t k = 0;
-    if (lane == 0) k = atomicAdd(&cur[b0], 1u);
-    k = __builtin_amdgcn_readfirstlane(k);
-    if (k < bins.cap) {
-      const uint32_t e = kBinRunFlag | (bin_local(t0, bins.bbits) << bins.pbits) | (q0 - range0);
-      uint32_t *dst = bins.ent + ((size_t)b0 * bins.nsrc + rb) * bins.cap + k;
-      if (lane == 0) {
-        if (bins.runs == 2)
-          __builtin_nontemporal_store(e, dst);
-        else
-          *dst = e;
-      }
-      return;
-    }
-    // (a full slice: the 64 touches overflow one by one below)
-  }
   const bool v = touch != kNone;
   const uint32_t b = v ? bin_of(touch, bins.bbits) : 0;
   const uint32_t k = group_reserve(cur, b, v);

@@ -809,8 +809,7 @@ int tbl_touch_reduce(vp_ctx *c, FlowTable &t, const uint32_t *log, uint32_t p0,
 // in-bin index in LDS, reading every source block's slice of its bin (one
 // contiguous region: the slices are bin-major), then
 // writes ts/tseq in runs of 64 consecutive indices. About 8 B of traffic per
-// packet (one write while classifying, one read here); a run entry
-// (kBinRunFlag, vp_device.h) stands for 64 packets' touches in 4 bytes.
+// packet (one write while classifying, one read here).
 constexpr uint32_t kBinLocalMax = 16384;  // in-bin indices held in LDS
 
 template <uint32_t kU>  // 64-entry chunks in flight per wave
@@ -818,7 +817,7 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
     const uint32_t *ent, const uint32_t *cnt, uint32_t nsrc, uint32_t cap,
     uint32_t pbits, uint32_t bbits, uint32_t range, uint32_t L, uint32_t tcap,
     uint32_t p0, NowSpec now, uint64_t seq_base, uint64_t *ts, uint64_t *tseq,
-    PubArgs pub, uint32_t diag) {
+    PubArgs pub) {
   // 1 + position in the launch, 0 = none; L words of dynamic LDS (16 KB at
   // 1M flows: the 256 bin blocks spread over all CUs, where a 64 KB static
   // array let only two blocks share a CU and left half of them idle)
@@ -845,48 +844,26 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
       if (lane >= o) inc += t;
     }
     const uint32_t exc = inc - ch;
-    const uint32_t total = (diag & 1) ? 0u : __builtin_amdgcn_readlane(inc, 63);
+    const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
     for (uint32_t t0 = 0; t0 < total; t0 += kU) {
       uint32_t e[kU], lim[kU], base[kU];
 #pragma unroll
       for (uint32_t u = 0; u < kU; u++) {
         const uint32_t t = t0 + u;
-        uint64_t own = __ballot(exc <= t && t < inc);  // (none past the list)
-        uint32_t l = own ? (uint32_t)__ffsll((unsigned long long)own) - 1 : 0u;
-        if (diag & 16) {  // (diagnostics: one chunk per slice assumed)
-          l = t & 63;
-          own = 1;
-        }
+        const uint64_t own = __ballot(exc <= t && t < inc);  // (none past the list)
+        const uint32_t l = own ? (uint32_t)__ffsll((unsigned long long)own) - 1 : 0u;
         const uint32_t k = (t - __builtin_amdgcn_readlane(exc, l)) << 6;
         const uint32_t sb = r0 + l * nw;
         lim[u] = own ? __builtin_amdgcn_readlane(nv, l) - k : 0u;
         base[u] = sb * range + 1;
-        if (diag & 8)  // (diagnostics: no entry loads)
-          e[u] = lane < lim[u] ? ((t * 64 + lane) % L) << pbits : 0u;
-        else
-          e[u] = lane < lim[u] ? ent[((size_t)bin * nsrc + sb) * cap + k + lane] : 0u;
-      }
-      if (diag & 4) {  // (diagnostics: no LDS atomics)
-        uint32_t acc = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++) acc |= e[u];
-        if (acc == 0x7FFFFFFFu) last[lane] = acc;
-        continue;
+        e[u] = lane < lim[u] ? ent[((size_t)bin * nsrc + sb) * cap + k + lane] : 0u;
       }
 #pragma unroll
-      for (uint32_t u = 0; u < kU; u++) {
-        const bool run = lane < lim[u] && (e[u] & kBinRunFlag);
-        if (lane < lim[u] && !run) atomicMax(&last[e[u] >> pbits], base[u] + (e[u] & pmask));
-        for (uint64_t m = __ballot(run); m; m &= m - 1) {  // (a run: 64 touches)
-          const uint32_t er = __builtin_amdgcn_readlane(e[u], __ffsll((unsigned long long)m) - 1);
-          atomicMax(&last[((er & ~kBinRunFlag) >> pbits) + lane],
-                    base[u] + (er & pmask) + lane);
-        }
-      }
+      for (uint32_t u = 0; u < kU; u++)
+        if (lane < lim[u]) atomicMax(&last[e[u] >> pbits], base[u] + (e[u] & pmask));
     }
   }
   __syncthreads();
-  if (diag & 2) return;
   for (uint32_t l = threadIdx.x; l < L; l += blockDim.x) {
     const uint32_t v = last[l];
     const uint32_t i = bin_index(bin, l, bbits);
@@ -923,7 +900,7 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   const uint32_t nbins = 1u << bbits;
   const uint32_t L = (uint32_t)in_bin(bbits);
   const uint32_t pbits = std::max<uint32_t>(1, ceil_log2(range));
-  if (L > kBinLocalMax || ceil_log2(L) + pbits > 31) return 0;  // (bit 31: kBinRunFlag)
+  if (L > kBinLocalMax || ceil_log2(L) + pbits > 32) return 0;
   // twice a uniform share of a block's packets per bin, and at least two
   // waves' worth (a wave touching 64 consecutive indices fills one bin)
   const uint32_t cap =
@@ -949,10 +926,8 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   plan->grid = grid;
   plan->range = range;
   plan->L = L;
-  const char *re = getenv("VIGPATH_BIN_RUNS");  // diagnostics: 0 off, 2 non-temporal
-  const uint32_t runs = re ? (uint32_t)atoi(re) : 0u;  // (off: 15 % slower classify, r04e)
   plan->bins = TouchBins{w.bins_ent, w.bins_cnt, &t.ctl->touch_ovf, w.ovf_q,
-                         w.ovf_cnt, w.log, cap, pbits, bbits, grid, runs};
+                         w.ovf_cnt, w.log, cap, pbits, bbits, grid};
   return 0;
 }
 
@@ -965,18 +940,12 @@ static int bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p
     const int v = e ? atoi(e) : 0;
     return v == 16 || v == 32 ? (uint32_t)v : 8u;
   }();
-  // diagnostics only (wrong stamps): 1 skips the entries, 2 the stamp writes,
-  // 4 the LDS atomics, 8 the entry loads, 16 the chunk search
-  static const uint32_t diag = [] {
-    const char *e = getenv("VIGPATH_FOLD_DIAG");
-    return e ? (uint32_t)atoi(e) : 0u;
-  }();
   auto *fold = fold_u == 8 ? touch_bins_reduce<8> : fold_u == 32 ? touch_bins_reduce<32>
                                                                  : touch_bins_reduce<16>;
   fold<<<1u << plan.bins.bbits, 1024, 4u * plan.L, c->stream>>>(
       plan.bins.ent, plan.bins.cnt, plan.grid, plan.bins.cap, plan.bins.pbits,
       plan.bins.bbits, plan.range, plan.L, t.cap, p0, now, seq_base, t.ts, t.tseq,
-      pub, diag);
+      pub);
   VP_HIP(hipGetLastError());
   return 0;
 }
