@@ -2,7 +2,8 @@
 frame in its own mbuf of a pool (2304-byte elements, data at 256: DPDK's
 rte_mbuf + headroom + 2 KB data room), the batch a pointer array in rx order
 (reference nf.c:186-214), frames read and rewritten in place by the GPU
-through vp_register_host. Out ports, the frames' bytes and the final state
+through vp_register_host (mode "gpu") or gathered and written back by host
+threads (mode "host"). Out ports, the frames' bytes and the final state
 are compared with the oracle run over the same packets (frames in slots,
 bytes past each length zero: the mbuf path reads them as 0)."""
 import numpy as np
@@ -17,6 +18,10 @@ import test_nat_gpu as NG
 pytestmark = pytest.mark.gpu
 
 SLOT = 2048  # the oracle's slots (frames up to 1518 B)
+
+# VIGPATH_MBUF_MODE: "gpu" (the GPU reads and writes the registered mbufs),
+# "host" (host threads gather headers into pinned slots and write them back)
+MODES = ["gpu", "host"]
 
 
 def zero_past_len(fr, ln, slot):
@@ -58,12 +63,14 @@ def compare(pool, bufs, ln, exp, exp_out, out, slot, shift=None):
     assert not badf, "frame mismatch at %s" % badf[:10]
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("chunk", ["700", "4096"])
-def test_nat_mixed_sizes(chunk, monkeypatch):
+def test_nat_mixed_sizes(chunk, mode, monkeypatch):
     """60-1518-byte frames (tail sums over the bytes past 64, padding past
     total_length, TCP and UDP), WAN replies, malformed frames, new flows and
     hits, churn; several chunks of the pipeline."""
     monkeypatch.setenv("VIGPATH_HOST_CHUNK", chunk)
+    monkeypatch.setenv("VIGPATH_MBUF_MODE", mode)
     rng = np.random.default_rng(41)
     n = 6000
     fr, ln, dv, now = wide_nat_trace(rng, n, 300, SLOT)
@@ -78,12 +85,14 @@ def test_nat_mixed_sizes(chunk, monkeypatch):
     NG.check_state(nat, o, 512)
 
 
-def test_nat_options_take_whole_frames(monkeypatch):
+@pytest.mark.parametrize("mode", MODES)
+def test_nat_options_take_whole_frames(mode, monkeypatch):
     """IPv4 options on frames longer than 64 bytes (the rewrite reaches past
     byte 64: the chunk takes whole-frame slots), short and odd frames, IHL <
     5, total_length past the packet (edge_nat_trace), mixed with plain
     chunks; affine time."""
     monkeypatch.setenv("VIGPATH_HOST_CHUNK", "500")
+    monkeypatch.setenv("VIGPATH_MBUF_MODE", mode)
     rng = np.random.default_rng(42)
     n = 3000
     fr, ln, dv = edge_nat_trace(rng, n, 200, slot=SLOT, long_frames=True)
@@ -101,12 +110,14 @@ def test_nat_options_take_whole_frames(monkeypatch):
     NG.check_state(nat, o, 512)
 
 
-def test_nat_unregistered_and_unaligned(monkeypatch):
+@pytest.mark.parametrize("mode", MODES)
+def test_nat_unregistered_and_unaligned(mode, monkeypatch):
     """Frames outside the registered memory (their chunks are staged through
     the host), frames at data offsets that are not multiples of 16 (read and
     written byte by byte), a pinned pool and pinned arrays."""
     import torch
     monkeypatch.setenv("VIGPATH_HOST_CHUNK", "600")
+    monkeypatch.setenv("VIGPATH_MBUF_MODE", mode)
     rng = np.random.default_rng(43)
     n = 4000
     fr, ln, dv, now = wide_nat_trace(rng, n, 200, SLOT, max_len=600)
@@ -161,12 +172,14 @@ def _other(kind):
     return M.make_pair()
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("kind", ["fw", "pol", "bridge", "lb"])
-def test_other_nfs(kind, monkeypatch):
+def test_other_nfs(kind, mode, monkeypatch):
     """vigfw (MACs rewritten: header slots), vigpol and vigbridge (never
     rewritten: no write-back), viglb (whole-frame slots) through the mbuf
     path, frames longer than 64 bytes where the NF reads them."""
     monkeypatch.setenv("VIGPATH_HOST_CHUNK", "800")
+    monkeypatch.setenv("VIGPATH_MBUF_MODE", mode)
     rng = np.random.default_rng(45)
     n = 3000
     slot = 256

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--chunks", default="1048576")
     ap.add_argument("--blocks", default="256")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--modes", default="gpu",
+                    help="VIGPATH_MBUF_MODE values: gpu (zero-copy), host (host threads gather)")
     ap.add_argument("--pools", default="pinned",
                     help="pinned (page-locked 4 KB pages), huge (2 MB THP, registered)")
     args = ap.parse_args()
@@ -74,7 +76,9 @@ def main():
                 bufs = None
                 ptrs = pin(np.uint64(pool.mem.ctypes.data) + np.arange(B, dtype=np.uint64) * 64)
             for ch in args.chunks.split(","):
-                for blk in args.blocks.split(","):
+                for blk, mode in [(b, m) for b in args.blocks.split(",")
+                                  for m in args.modes.split(",")]:
+                    os.environ["VIGPATH_MBUF_MODE"] = mode
                     os.environ["VIGPATH_HOST_CHUNK"] = ch
                     os.environ["VIGPATH_MBUF_BLOCKS"] = blk
                     call = nat.mbuf_step(ptrs, lens, ind, out)
@@ -95,6 +99,8 @@ def main():
                     assert (out == 1).all()
                     el = sum(times) / len(times)
                     print(json.dumps({"pool": kind, "layout": var, "chunk": int(ch), "blocks": int(blk),
+                                      "mode": mode,
+                                      "threads": os.environ.get("VIGPATH_MBUF_THREADS", "8"),
                                       "ms_per_call": round(el * 1e3, 3),
                                       "mpps": round(B / el / 1e6, 1)}), flush=True)
         nat.unregister_host(pool.mem)

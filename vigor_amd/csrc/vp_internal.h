@@ -242,6 +242,11 @@ struct Workspace {
   size_t st_meta_n = 0;
   uint8_t *h_mbmeta = nullptr;  // pinned staging of pageable per-packet arrays
   size_t h_mbmeta_bytes = 0;
+  // host-gather mode: pinned header slots and tail sums the host threads
+  // fill (kMbufSets sets of mb_hcap packets)
+  uint8_t *h_mbslots = nullptr;
+  uint32_t *h_mbtail = nullptr;
+  size_t mb_hcap = 0;
   hipEvent_t mb_ev_in[kMbufSets] = {}, mb_ev_done[kMbufSets] = {},
              mb_ev_out[kMbufSets] = {};
 };

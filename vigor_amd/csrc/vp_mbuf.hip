@@ -33,8 +33,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "vp_comm.h"
@@ -533,6 +538,252 @@ static int mbuf_pipeline(vp_ctx *c, const vp_mbuf_batch *b) {
   return 0;
 }
 
+// ------------------------------------------------------ host-gather mode --
+// The same batch with the host's cores doing the scattered part: worker
+// threads copy every frame's first 64 bytes (and, for vignat, the raw sum of
+// its bytes [64, 14 + total_length)) out of its mbuf into pinned header slots,
+// the slots cross PCIe as one DMA per chunk, and after processing the threads
+// copy the bytes a rewrite can change back into the mbufs of the frames that
+// were not dropped. The GPU never touches host frames (nothing to register);
+// PCIe carries large DMA transfers instead of one 64-byte read and one write
+// request per frame (the zero-copy mode's bound). While chunk
+// k is copied and processed, the threads write back chunk k - 1 and gather
+// chunk k + 1. VIGPATH_MBUF_MODE=host|gpu picks the mode, VIGPATH_MBUF_THREADS
+// the threads (default 8, the caller's thread included).
+class HostPool {
+ public:
+  explicit HostPool(unsigned n) : n_(std::max(1u, n)) {
+    for (unsigned i = 1; i < n_; i++) th_.emplace_back([this] { loop(); });
+  }
+  unsigned size() const { return n_; }
+  // fn(part) for every part in [0, parts), over the pool and the caller;
+  // returns when all parts are done
+  void run(uint32_t parts, const std::function<void(uint32_t)> &fn) {
+    std::lock_guard<std::mutex> one(run_m_);
+    uint64_t gen;
+    {
+      std::lock_guard<std::mutex> g(m_);
+      gen = ++gen_;
+      fn_ = &fn;
+      parts_ = parts;
+      done_ = 0;
+      next_.store(gen << 32);  // (job tag | next part: a late thread never takes a part of another job)
+    }
+    cv_.notify_all();
+    work(gen, &fn, parts);
+    std::unique_lock<std::mutex> g(m_);
+    done_cv_.wait(g, [&] { return done_ == parts; });
+  }
+
+ private:
+  void work(uint64_t gen, const std::function<void(uint32_t)> *fn, uint32_t parts) {
+    uint32_t mine = 0;
+    uint64_t cur = next_.load();
+    while ((cur >> 32) == gen && (uint32_t)cur < parts) {
+      if (next_.compare_exchange_weak(cur, cur + 1)) {
+        (*fn)((uint32_t)cur);
+        mine++;
+        cur = next_.load();
+      }
+    }
+    if (mine) {
+      std::lock_guard<std::mutex> g(m_);
+      done_ += mine;
+      if (done_ == parts) done_cv_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> g(m_);
+    for (;;) {
+      cv_.wait(g, [&] { return gen_ != seen; });
+      seen = gen_;
+      const std::function<void(uint32_t)> *fn = fn_;
+      const uint32_t parts = parts_;
+      g.unlock();
+      work(seen, fn, parts);
+      g.lock();
+    }
+  }
+  unsigned n_;
+  std::vector<std::thread> th_;
+  std::mutex m_, run_m_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(uint32_t)> *fn_ = nullptr;
+  uint32_t parts_ = 0, done_ = 0;
+  uint64_t gen_ = 0;
+  std::atomic<uint64_t> next_{0};
+};
+
+static HostPool &host_pool() {  // (process-wide; its threads live as long as the process)
+  static HostPool *p = [] {
+    const char *e = getenv("VIGPATH_MBUF_THREADS");
+    const int v = e ? atoi(e) : 0;
+    return new HostPool(v > 0 ? (unsigned)std::min(v, 256) : 8u);
+  }();
+  return *p;
+}
+
+static bool mbuf_mode_host() {
+  const char *e = getenv("VIGPATH_MBUF_MODE");
+  return e && !strcmp(e, "host");
+}
+
+// One frame of L bytes into its 64-byte header slot (zeros past L) and, with
+// `tail`, its tail sum: the plain sum of the little-endian 16-bit words of
+// bytes [64, min(L, 14 + total_length)) of an IPv4 IHL-5 frame (an odd last
+// byte as a word of its own), the arithmetic of mbuf_gather_hdr's sum16x4.
+// Returns kMbWhole where mbuf_gather_hdr would (rule kRuleNoOpt).
+static inline uint32_t host_gather_one(const uint8_t *f, uint32_t L, uint8_t *d, uint32_t *tail,
+                                       const MbufPlan &pl) {
+  const uint32_t nb = std::min<uint32_t>(L, 64);
+  memcpy(d, f, nb);
+  if (nb < 64) memset(d + nb, 0, 64 - nb);
+  const bool ip = d[12] == 0x08 && d[13] == 0x00;
+  const uint32_t ihl = d[14] & 0x0F;
+  if (pl.tail) {
+    uint32_t s = 0;
+    if (ip && ihl == 5) {
+      const uint32_t end = std::min<uint32_t>(L, 14u + ((uint32_t)d[16] << 8 | d[17]));
+      uint32_t o = 64;
+      for (; o + 1 < end; o += 2) s += (uint32_t)f[o] | (uint32_t)f[o + 1] << 8;
+      if (o < end) s += f[o];
+    }
+    *tail = s;
+  }
+  return pl.rule == kRuleNoOpt && L > 64 && ip && ihl > 5 ? kMbWhole : 0u;
+}
+
+static int mbuf_host_pipeline(vp_ctx *c, const vp_mbuf_batch *b, const MbufPlan &pl) {
+  Workspace &w = c->ws;
+  CtxTailGuard guard{c};
+  constexpr uint32_t S = Workspace::kMbufSets;
+  const uint32_t n = b->n;
+  uint32_t ch = 1u << 20;
+  if (const char *e = getenv("VIGPATH_HOST_CHUNK")) ch = std::max(1, atoi(e));
+  ch = std::min<uint32_t>(ch, std::max<uint32_t>(n, 1));
+  const uint32_t K = (n + ch - 1) / ch;
+  VP_TRY(mbuf_reserve(c, ch));
+  if (ch > w.mb_hcap) {
+    VP_HIP(hipDeviceSynchronize());
+    if (w.h_mbslots) hipHostFree(w.h_mbslots);
+    if (w.h_mbtail) hipHostFree(w.h_mbtail);
+    w.h_mbslots = nullptr;
+    w.h_mbtail = nullptr;
+    w.mb_hcap = 0;
+    VP_HIP(hipHostMalloc((void **)&w.h_mbslots, 64ull * S * ch, hipHostMallocDefault));
+    VP_HIP(hipHostMalloc((void **)&w.h_mbtail, 4ull * S * ch, hipHostMallocDefault));
+    w.mb_hcap = ch;
+  }
+  const bool pin_len = host_pinned(b->len), pin_in = host_pinned(b->in_dev),
+             pin_out = host_pinned(b->out_dev), pin_now = b->now && host_pinned(b->now);
+  HostPool &hp = host_pool();
+  auto cnt = [&](uint32_t k) { return std::min(ch, n - k * ch); };
+  auto hm = [&](uint32_t k, size_t at) { return w.h_mbmeta + (size_t)(k % S) * 22 * ch + at * ch; };
+  auto src = [&](const void *arr, bool pinned, size_t esz, size_t at, uint32_t k) {
+    const uint8_t *a = static_cast<const uint8_t *>(arr) + (size_t)k * ch * esz;
+    if (pinned) return a;
+    memcpy(hm(k, at), a, esz * cnt(k));
+    return static_cast<const uint8_t *>(hm(k, at));
+  };
+  auto hout = [&](uint32_t k) {
+    return pin_out ? b->out_dev + (size_t)k * ch : reinterpret_cast<uint16_t *>(hm(k, 20));
+  };
+  auto slots = [&](uint32_t k) { return w.h_mbslots + (size_t)(k % S) * ch * 64; };
+  auto tails = [&](uint32_t k) { return w.h_mbtail + (size_t)(k % S) * ch; };
+  // pieces per pool job: several per thread, frame lengths vary
+  const uint32_t parts = 4 * hp.size();
+  auto gather = [&](uint32_t k) {
+    const uint32_t m = cnt(k), k0 = k * ch;
+    uint8_t *hs = slots(k);
+    uint32_t *ht = tails(k);
+    std::atomic<uint32_t> flags{0};
+    hp.run(parts, [&](uint32_t part) {
+      const uint32_t lo = (uint32_t)((uint64_t)m * part / parts),
+                     hi = (uint32_t)((uint64_t)m * (part + 1) / parts);
+      uint32_t fl = 0;
+      for (uint32_t j = lo; j < hi; j++)
+        fl |= host_gather_one(b->frames[k0 + j], b->len[k0 + j], hs + (size_t)j * 64, ht + j, pl);
+      if (fl) flags.fetch_or(fl);
+    });
+    return flags.load();
+  };
+  auto launch = [&](uint32_t k) -> int {
+    const uint32_t i = k % S, m = cnt(k);
+    if (k >= S) VP_HIP(hipStreamWaitEvent(w.cstream, w.mb_ev_out[i], 0));
+    VP_HIP(hipMemcpyAsync(w.mb_slots + (size_t)i * ch * 64, slots(k), 64ull * m,
+                          hipMemcpyHostToDevice, w.cstream));
+    if (pl.tail)
+      VP_HIP(hipMemcpyAsync(w.mb_tail + (size_t)i * ch, tails(k), 4ull * m,
+                            hipMemcpyHostToDevice, w.cstream));
+    VP_HIP(hipMemcpyAsync(w.mb_len + (size_t)i * ch, src(b->len, pin_len, 2, 8, k), 2ull * m,
+                          hipMemcpyHostToDevice, w.cstream));
+    VP_HIP(hipMemcpyAsync(w.mb_in + (size_t)i * ch, src(b->in_dev, pin_in, 2, 10, k), 2ull * m,
+                          hipMemcpyHostToDevice, w.cstream));
+    if (b->now)
+      VP_HIP(hipMemcpyAsync(w.mb_now + (size_t)i * ch, src(b->now, pin_now, 8, 12, k), 8ull * m,
+                            hipMemcpyHostToDevice, w.cstream));
+    VP_HIP(hipEventRecord(w.mb_ev_in[i], w.cstream));
+    VP_HIP(hipStreamWaitEvent(c->stream, w.mb_ev_in[i], 0));
+    vp_dev_batch db{};
+    db.n = m;
+    db.frames = w.mb_slots + (size_t)i * ch * 64;
+    db.slot = 64;
+    db.len = w.mb_len + (size_t)i * ch;
+    db.in_dev = w.mb_in + (size_t)i * ch;
+    db.now = b->now ? w.mb_now + (size_t)i * ch : nullptr;
+    db.now0 = b->now0 + (int64_t)k * ch * b->now_step;
+    db.now_step = b->now_step;
+    db.out_dev = w.mb_out + (size_t)i * ch;
+    c->hdr_tail = pl.tail ? w.mb_tail + (size_t)i * ch : nullptr;
+    c->host_now = b->now ? b->now + (size_t)k * ch : nullptr;
+    const int rc = vp_process_device(c, &db, nullptr);
+    c->hdr_tail = nullptr;
+    c->host_now = nullptr;
+    VP_TRY(rc);
+    VP_HIP(hipEventRecord(w.mb_ev_done[i], c->stream));
+    VP_HIP(hipStreamWaitEvent(w.dstream, w.mb_ev_done[i], 0));
+    if (pl.wb_hdr)
+      VP_HIP(hipMemcpyAsync(slots(k), w.mb_slots + (size_t)i * ch * 64, 64ull * m,
+                            hipMemcpyDeviceToHost, w.dstream));
+    VP_HIP(hipMemcpyAsync(hout(k), w.mb_out + (size_t)i * ch, 2ull * m, hipMemcpyDeviceToHost,
+                          w.dstream));
+    VP_HIP(hipEventRecord(w.mb_ev_out[i], w.dstream));
+    return 0;
+  };
+  auto scatter = [&](uint32_t k) -> int {
+    const uint32_t i = k % S, m = cnt(k), k0 = k * ch;
+    VP_HIP(event_poll(w.mb_ev_out[i]));
+    if (!pin_out) memcpy(b->out_dev + k0, hm(k, 20), 2ull * m);
+    if (!pl.wb_hdr) return 0;
+    const uint8_t *hs = slots(k);
+    const uint16_t *out = b->out_dev + k0, *in = b->in_dev + k0;
+    hp.run(parts, [&](uint32_t part) {
+      const uint32_t lo = (uint32_t)((uint64_t)m * part / parts),
+                     hi = (uint32_t)((uint64_t)m * (part + 1) / parts);
+      for (uint32_t j = lo; j < hi; j++)
+        if (out[j] != in[j])  // (a dropped frame's mbuf is freed: nf.c:159-160)
+          memcpy(b->frames[k0 + j], hs + (size_t)j * 64,
+                 std::min<uint32_t>(b->len[k0 + j], pl.wb_hdr));
+    });
+    return 0;
+  };
+  bool pending = false;  // chunk k - 1 launched, not yet written back
+  for (uint32_t k = 0; k < K; k++) {
+    if (gather(k) & kMbWhole) {  // IPv4 options on a long frame: whole frames
+      if (pending) VP_TRY(scatter(k - 1));
+      pending = false;
+      VP_TRY(staged_range(c, b, k * ch, cnt(k)));
+      continue;
+    }
+    VP_TRY(launch(k));
+    if (pending) VP_TRY(scatter(k - 1));
+    pending = true;
+  }
+  if (pending) VP_TRY(scatter(K - 1));
+  return 0;
+}
+
 }  // namespace vp
 
 using namespace vp;
@@ -610,6 +861,8 @@ int vp_process_mbufs(vp_ctx *c, const vp_mbuf_batch *b) {
   if (!b->now && (b->now_step < 0 || b->now0 < 0)) return VP_ENOTSUP;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
   if (b->n == 0 && !c->comm) return 0;
+  const MbufPlan pl = mbuf_plan(c);
+  if (pl.header && !c->comm && mbuf_mode_host()) return mbuf_host_pipeline(c, b, pl);
   if (c->hmaps.empty()) return staged_range(c, b, 0, b->n);
   return mbuf_pipeline(c, b);
 }

@@ -182,6 +182,8 @@ static void free_all(vp_ctx *c) {
   for (void *p : mb) hipFree(p);
   if (w.h_mbflags) hipHostFree(w.h_mbflags);
   if (w.h_mbmeta) hipHostFree(w.h_mbmeta);
+  if (w.h_mbslots) hipHostFree(w.h_mbslots);
+  if (w.h_mbtail) hipHostFree(w.h_mbtail);
   for (int i = 0; i < Workspace::kMbufSets; i++) {
     if (w.mb_ev_in[i]) hipEventDestroy(w.mb_ev_in[i]);
     if (w.mb_ev_done[i]) hipEventDestroy(w.mb_ev_done[i]);
