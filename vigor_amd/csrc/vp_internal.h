@@ -197,9 +197,14 @@ struct Workspace {
   uint32_t *reply = nullptr, *rreply = nullptr;
   size_t reply_n = 0, rreply_n = 0;
   uint32_t *h_tot = nullptr;  // pinned landing buffer for dtot
-  // padded exchange (owner mode): keys received per peer, the global
-  // capacity-overflow flag
-  uint32_t *rcnt = nullptr;
+  // padded exchange (owner mode): per-block slice counts by owner (cnt_t)
+  // and as received by peer (rcnt_t), each owner's needed chunk size (dneed,
+  // published for the next batch's capacity), the global slice-overflow
+  // flag; the exact exchange's tight send buffer (xsend)
+  uint32_t *cnt_t = nullptr, *rcnt_t = nullptr, *dneed = nullptr;
+  size_t cnt_t_n = 0, rcnt_t_n = 0, dneed_n = 0;
+  uint4 *xsend = nullptr;
+  size_t xsend_n = 0;
   uint64_t *ovf64 = nullptr;
   bool ovf64_clean = false;  // ovf64 is zero (the last exchange did not overflow)
   // multi-GPU: the ranks' segment counters gathered on the device before a

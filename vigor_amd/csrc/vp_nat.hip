@@ -127,6 +127,11 @@ struct Route {
   // exchange, this rank's own included (one rank: the whole pipeline at 100 %
   // routed)
   uint32_t all;
+  // padded exchange: owner o's chunk of the send buffer is one slice of
+  // `sub` keys per block, block b's keys for o at o cap + b sub + k (k <
+  // sub; pass 1 writes them there itself, past sub into desc)
+  uint4 *sendk;
+  uint32_t sub;
 };
 constexpr uint32_t kNoReply = 0xFFFFFFFAu;  // route_answer: not answered in this pass
 
@@ -173,8 +178,11 @@ __device__ __forceinline__ bool nat_route(const NatArgs &a, uint32_t p, uint32_t
   const uint32_t o = owner_of(h, a.own.n);
   if (o == a.own.r && !a.own.all) return false;
   const uint32_t k = atomicAdd(&a.own.cur[o], 1u);
-  a.own.desc[((size_t)blockIdx.x * a.own.n + o) * a.own.range + k] =
-      make_uint4(key[0], key[1], key[2], key[3]);
+  const uint4 v = make_uint4(key[0], key[1], key[2], key[3]);
+  if (k < a.own.sub)  // (the padded exchange's own slice: no packing pass)
+    a.own.sendk[(size_t)o * a.own.cap + (size_t)blockIdx.x * a.own.sub + k] = v;
+  else
+    a.own.desc[((size_t)blockIdx.x * a.own.n + o) * a.own.range + k] = v;
   a.own.route[p] = kRouteBit | (o << 24) | k;
   return true;
 }
@@ -1127,21 +1135,59 @@ __global__ __launch_bounds__(256) void nat_reprobe(NatArgs a, const uint32_t *li
 }
 
 // ------------------------------------------------------- owner mode --
-//  After pass 1 each block has a slice of keys per owner rank
-// (desc, dcnt). route_scan + route_base give every slice its offset in the
-// send buffer (grouped by owner, ranks in order, blocks in order inside),
-// route_pack gathers the slices there; the keys go to their owners
-// (all-to-all), nat_own_probe answers them against the owner's buckets, the
-// answers come back in the same order, and pass 2 finishes the packets.
+//  Pass 1 leaves each block's keys per owner rank in the
+// padded send buffer, owner o's chunk [o cap, (o + 1) cap) cut into one
+// slice of `sub` keys per block (keys past a slice in desc). route_counts
+// gives the owners their per-block counts (exchanged beside the keys) and
+// flags a slice that overflowed; the keys go to their owners (all-to-all),
+// nat_own_probe answers them against the owner's buckets, the answers come
+// back in the same slots, and pass 2 finishes the packets. After an overflow
+// (any rank) the exact exchange packs every slice tight: route_scan +
+// route_base give the slices their offsets, route_pack gathers them.
 
-// Per owner o (one block each): exclusive scan over blocks of dcnt[.][o].
-// The padded exchange (cap > 0): owner o's chunk is [o cap, (o + 1) cap), and
-// a count past cap sets *ovf (every rank then takes the exact exchange,
-// DESIGN.md §6); cap == 0: offsets inside the owner's chunk (route_base).
+// The slice counts travel as one row per owner: [blocks, sub, count of
+// block 0, 1, ...] (ranks may run different pass-1 grids for one segment).
+constexpr uint32_t kSliceRowMax = 4096;  // pass-1 blocks
+constexpr uint32_t kSliceRow = 2 + kSliceRowMax;
+
+// Per owner o (one block each): row o = [nblk, sub, block b's keys for o (at
+// most sub) ...], need[o] = the largest slice times the blocks (the chunk
+// size that would have held it: the next batch's capacity), *ovf when a
+// slice overflowed.
+__global__ __launch_bounds__(256) void route_counts(const uint32_t *dcnt, uint32_t nblk,
+                                                    uint32_t n, uint32_t sub, uint32_t *rows,
+                                                    uint32_t *need, uint64_t *ovf) {
+  __shared__ uint32_t mx[256];
+  const uint32_t o = blockIdx.x;
+  uint32_t *row = rows + (size_t)o * kSliceRow;
+  uint32_t m = 0;
+  for (uint32_t b = threadIdx.x; b < nblk; b += blockDim.x) {
+    const uint32_t v = dcnt[(size_t)b * n + o];
+    m = max(m, v);
+    row[2 + b] = min(v, sub);
+  }
+  if (threadIdx.x == 0) {
+    row[0] = nblk;
+    row[1] = sub;
+  }
+  mx[threadIdx.x] = m;
+  __syncthreads();
+  for (uint32_t h = 128; h; h >>= 1) {
+    if (threadIdx.x < h) mx[threadIdx.x] = max(mx[threadIdx.x], mx[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    need[o] = mx[0] * nblk;
+    if (mx[0] > sub) *ovf = 1;
+  }
+}
+
+// Exact exchange, per owner o (one block each): exclusive scan over blocks of
+// dcnt[.][o], offsets inside the owner's chunk (route_base adds the chunk's
+// start), dtot[o] the owner's total.
 __global__ __launch_bounds__(256) void route_scan(const uint32_t *dcnt, uint32_t nblk,
                                                   uint32_t n, uint32_t *dbase,
-                                                  uint32_t *dtot, uint32_t cap,
-                                                  uint64_t *ovf) {
+                                                  uint32_t *dtot) {
   __shared__ uint32_t part[256];
   const uint32_t o = blockIdx.x;
   const uint32_t per = (nblk + 255) / 256;
@@ -1158,10 +1204,9 @@ __global__ __launch_bounds__(256) void route_scan(const uint32_t *dcnt, uint32_t
       acc += v;
     }
     dtot[o] = acc;
-    if (cap && acc > cap) *ovf = 1;
   }
   __syncthreads();
-  uint32_t acc = part[threadIdx.x] + o * cap;
+  uint32_t acc = part[threadIdx.x];
   for (uint32_t b = b0; b < b1; b++) {
     dbase[(size_t)b * n + o] = acc;
     acc += dcnt[(size_t)b * n + o];
@@ -1180,19 +1225,20 @@ __global__ void route_base(uint32_t *dbase, const uint32_t *dtot, uint32_t nblk,
   }
 }
 
-// One block per source block: its slices into the send buffer (cap: only
-// the entries inside their owner's padded chunk).
-__global__ __launch_bounds__(256) void route_pack(const uint4 *desc, const uint32_t *dcnt,
-                                                  const uint32_t *dbase, uint32_t n,
-                                                  uint32_t range, uint32_t cap,
-                                                  uint4 *sendk) {
+// Exact exchange: one block per source block, its slices packed tight into
+// `out` (a slice's first `sub` keys from its padded slot, the rest from desc).
+__global__ __launch_bounds__(256) void route_pack(const uint4 *desc, const uint4 *padded,
+                                                  const uint32_t *dcnt, const uint32_t *dbase,
+                                                  uint32_t n, uint32_t range, uint32_t cap,
+                                                  uint32_t sub, uint4 *out) {
   const uint32_t b = blockIdx.x;
   for (uint32_t o = 0; o < n; o++) {
-    uint32_t cnt = dcnt[(size_t)b * n + o];
+    const uint32_t cnt = dcnt[(size_t)b * n + o];
     const uint32_t base = dbase[(size_t)b * n + o];
-    if (cap) cnt = min(cnt, (uint32_t)max(0, (int)((o + 1) * cap) - (int)base));
     const uint4 *src = desc + ((size_t)b * n + o) * range;
-    for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) sendk[base + k] = src[k];
+    const uint4 *pad = padded + (size_t)o * cap + (size_t)b * sub;
+    for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x)
+      out[base + k] = k < sub ? pad[k] : src[k];
   }
 }
 
@@ -1207,10 +1253,11 @@ __global__ __launch_bounds__(256) void route_pack(const uint4 *desc, const uint3
 // (wave_gather64) and the branch-free match; a key whose home bucket holds
 // three other keys walks on bucket by bucket (rare). Answers the index or
 // kNone (a new flow: the ingest rank queues the packet for phase B).
-// Padded exchange (cap > 0): n keys arrived as ranks x cap, peer q's first
-// rcnt[q] valid; no work when any rank overflowed (*ovf, published as
+// Padded exchange (cap > 0): n keys arrived as ranks x cap, peer q's chunk
+// one slice per block of its pass 1, the first rcnt row q's count of each
+// slice valid (route_counts); no work when any rank overflowed (*ovf, published as
 // ctl->route_ovf for the host). This rank's own keys (q == self) are read
-// where they were packed (`own_keys`, the send buffer, same layout) and
+// where pass 1 wrote them (`own_keys`, the send buffer, same layout) and
 // answered in place (`own_reply`, the answers' receive buffer): the
 // exchanges skip the rank's own chunk. cap == 0: n keys, all valid.
 __global__ __launch_bounds__(256, 4) void nat_own_probe(TableDev t, const uint32_t *crc_tab,
@@ -1234,8 +1281,16 @@ __global__ __launch_bounds__(256, 4) void nat_own_probe(TableDev t, const uint32
   const uint32_t tiles = (n + 63) / 64;
   const uint32_t per_b = (tiles + gridDim.x - 1) / gridDim.x;
   const uint32_t tend = min(tiles, blockIdx.x * per_b + per_b);
+  // key j of the padded exchange: peer q = j / cap, its pass-1 block b's
+  // slice (peer q's row of slice counts: [blocks, sub, counts]), slot k;
+  // valid when k < that slice's count
   auto valid_at = [&](uint32_t j) {
-    return j < n && (!cap || j % cap < rcnt[j / cap]);
+    if (j >= n) return false;
+    if (!cap) return true;
+    const uint32_t q = j / cap, l = j - q * cap;
+    const uint32_t *row = rcnt + (size_t)q * kSliceRow;
+    const uint32_t sub = row[1], b = l / sub;
+    return b < row[0] && l - b * sub < row[2 + b];
   };
   auto own = [&](uint32_t j) { return cap && j / cap == self; };
   // Software-pipelined over the wave's tiles: in the iteration for tile t
@@ -1340,9 +1395,11 @@ __device__ __forceinline__ uint32_t route_answer(const NatArgs &a, uint32_t p,
                                                  uint32_t rt) {
   const uint32_t o = (rt >> 24) & 63, k = rt & 0xFFFFFFu;
   const uint32_t blk = (p - a.own.first) / a.own.range;
-  const uint32_t at = a.own.dbase[(size_t)blk * a.own.n + o] + k;
-  if (a.own.cap && (at - o * a.own.cap >= a.own.cap || *a.own.ovf)) return kNoReply;
-  return a.own.rreply[at];
+  if (a.own.cap) {  // padded (no rank overflowed a slice: every k < sub)
+    if (*a.own.ovf) return kNoReply;
+    return a.own.rreply[(size_t)o * a.own.cap + (size_t)blk * a.own.sub + k];
+  }
+  return a.own.rreply[a.own.dbase[(size_t)blk * a.own.n + o] + k];
 }
 
 // Pass 2 for 64-byte slots: the same coalesced tiles as pass 1; routed
@@ -1551,25 +1608,30 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   }
   if (ph->range1 >= (1u << 24) - 1) return VP_ENOTSUP;
   const uint32_t C = std::max<uint32_t>(1, c->own_cap);  // keys per peer (padded)
+  const uint32_t sub = std::max<uint32_t>(1, C / ph->grid1);  // keys per block slice
+  if (ph->grid1 > kSliceRowMax) return VP_ENOTSUP;
   const size_t slices = (size_t)ph->grid1 * n;
   VP_TRY(grow_dev(&w.desc, &w.desc_n, slices * ph->range1, c->stream));
   VP_TRY(grow_dev(&w.dcnt, &w.dcnt_n, slices, c->stream));
   VP_TRY(grow_dev(&w.dbase, &w.dbase_n, slices, c->stream));
   VP_TRY(grow_dev(&w.dtot, &w.dtot_n, kMaxDest, c->stream));
+  VP_TRY(grow_dev(&w.dneed, &w.dneed_n, kMaxDest, c->stream));
+  VP_TRY(grow_dev(&w.cnt_t, &w.cnt_t_n, (size_t)n * kSliceRow, c->stream));
+  VP_TRY(grow_dev(&w.rcnt_t, &w.rcnt_t_n, (size_t)n * kSliceRow, c->stream));
   VP_TRY(grow_dev(&w.route, &w.route_n, b->n, c->stream));
   VP_TRY(grow_dev(&w.sendk, &w.sendk_n, (size_t)n * C, c->stream));
   VP_TRY(grow_dev(&w.recvk, &w.recvk_n, (size_t)n * C, c->stream));
   VP_TRY(grow_dev(&w.reply, &w.reply_n, (size_t)n * C, c->stream));
   VP_TRY(grow_dev(&w.rreply, &w.rreply_n, (size_t)n * C, c->stream));
-  if (!w.rcnt) VP_HIP(hipMalloc((void **)&w.rcnt, 4 * kMaxDest));
   if (!w.ovf64) VP_HIP(hipMalloc((void **)&w.ovf64, 8));
   if (!w.h_tot) VP_HIP(hipHostMalloc((void **)&w.h_tot, 4 * kMaxDest, hipHostMallocDefault));
   static const uint32_t route_all = [] {
     const char *e = getenv("VIGPATH_ROUTE_ALL");
     return e && atoi(e) ? 1u : 0u;
   }();
-  a.own = Route{n, r, w.desc, w.dcnt, w.route, nullptr, first, ph->range1, w.dbase,
-                w.rreply, C, w.ovf64, route_all};
+  a.own = Route{n,       r,        w.desc, w.dcnt,    w.route, nullptr,
+                first,   ph->range1, w.dbase, w.rreply, C,      w.ovf64,
+                route_all, w.sendk, sub};
 
   // (counters still zero after a segment that appended nothing, and the
   // overflow flag after an exchange that fit: no reset launches)
@@ -1595,25 +1657,24 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   }
   VP_HIP(ev_record(c->ktime, c->ev1, c->stream));
   pm.mark();
-  // C1 over the padded exchange, no host round trip: owner o's keys go to
-  // [o C, (o + 1) C) of the send buffer, the per-owner counts cross in their
-  // own small all-to-all, and a count past C (any rank: allreduced) leaves
-  // the routed packets to the exact exchange below
-  route_scan<<<n, 256, 0, c->stream>>>(w.dcnt, ph->grid1, n, w.dbase, w.dtot, C,
-                                       w.ovf64);
-  route_pack<<<ph->grid1, 256, 0, c->stream>>>(w.desc, w.dcnt, w.dbase, n, ph->range1, C,
-                                               w.sendk);
+  // C1 over the padded exchange, no host round trip: pass 1 wrote owner o's
+  // keys into [o C, (o + 1) C) of the send buffer, one slice of `sub` per
+  // block; the per-block counts cross in their own small all-to-all, and a
+  // slice past `sub` (any rank: allreduced) leaves the routed packets to the
+  // exact exchange below
+  route_counts<<<n, 256, 0, c->stream>>>(w.dcnt, ph->grid1, n, sub, w.cnt_t, w.dneed,
+                                         w.ovf64);
   VP_HIP(hipGetLastError());
-  // (this rank's own chunk stays where route_pack put it: the probe reads
-  // it from sendk and answers it into rreply, no self copies)
-  std::vector<size_t> s4(n, 4), sk(n, 16ull * C), sr(n, 4ull * C);
-  VP_TRY(m.alltoallv_dev(c, w.dtot, s4.data(), w.rcnt, s4.data()));
+  // (this rank's own chunk stays where pass 1 put it: the probe reads it
+  // from sendk and answers it into rreply, no self copies)
+  std::vector<size_t> sc(n, 4ull * kSliceRow), sk(n, 16ull * C), sr(n, 4ull * C);
+  VP_TRY(m.alltoallv_dev(c, w.cnt_t, sc.data(), w.rcnt_t, sc.data()));
   VP_TRY(m.allreduce_max_u64_dev(c, w.ovf64, 1));
   pm.mark();
   VP_TRY(m.alltoallv_dev(c, w.sendk, sk.data(), w.recvk, sk.data(), true));
   pm.mark();
   nat_own_probe<<<resident_grid((const void *)nat_own_probe, ((uint64_t)n * C + 255) / 256), 256,
-                  0, c->stream>>>(tbl_dev(t), c->crc_tab, w.recvk, n * C, C, w.rcnt, w.ovf64,
+                  0, c->stream>>>(tbl_dev(t), c->crc_tab, w.recvk, n * C, C, w.rcnt_t, w.ovf64,
                                   t.ctl, w.reply, r, w.sendk, w.rreply);
   VP_HIP(hipGetLastError());
   pm.mark();
@@ -1641,7 +1702,7 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   VP_TRY(pass2());
   VP_HIP(ev_record(c->ktime, c->ev3, c->stream));
   pm.mark();
-  VP_TRY(tbl_fold_read_ctl(c, t, ph->bp, w.log, p0, p1, now, seq0, w.dtot));
+  VP_TRY(tbl_fold_read_ctl(c, t, ph->bp, w.log, p0, p1, now, seq0, w.dneed));
   pm.mark();
   pm.finish(c, m.r, np);
   uint32_t maxsend = 0;  // for the next batch's capacity (run_batch_sharded)
@@ -1658,8 +1719,7 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   // pass 2 answered none of the routed packets; the exact exchange does,
   // with the sizes learned on the host, then the fold again (pass 1's own
   // touches fold twice, to the same stamps).
-  route_scan<<<n, 256, 0, c->stream>>>(w.dcnt, ph->grid1, n, w.dbase, w.dtot, 0,
-                                       nullptr);
+  route_scan<<<n, 256, 0, c->stream>>>(w.dcnt, ph->grid1, n, w.dbase, w.dtot);
   route_base<<<grid_for(slices), 256, 0, c->stream>>>(w.dbase, w.dtot, ph->grid1, n);
   VP_HIP(hipGetLastError());
   VP_HIP(hipMemcpyAsync(w.h_tot, w.dtot, 4ull * n, hipMemcpyDeviceToHost, c->stream));
@@ -1676,16 +1736,16 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
     fr[q] = 4ull * M[(size_t)q * n + r];  // answers go back the way keys came
     fa[q] = 4ull * M[(size_t)r * n + q];
   }
-  VP_TRY(grow_dev(&w.sendk, &w.sendk_n, S, c->stream));
+  VP_TRY(grow_dev(&w.xsend, &w.xsend_n, S, c->stream));
   VP_TRY(grow_dev(&w.rreply, &w.rreply_n, S, c->stream));
   VP_TRY(grow_dev(&w.recvk, &w.recvk_n, R, c->stream));
   VP_TRY(grow_dev(&w.reply, &w.reply_n, R, c->stream));
   a.own.rreply = w.rreply;
   a.own.cap = 0;
-  route_pack<<<ph->grid1, 256, 0, c->stream>>>(w.desc, w.dcnt, w.dbase, n, ph->range1, 0,
-                                               w.sendk);
+  route_pack<<<ph->grid1, 256, 0, c->stream>>>(w.desc, w.sendk, w.dcnt, w.dbase, n, ph->range1,
+                                               C, sub, w.xsend);
   VP_HIP(hipGetLastError());
-  VP_TRY(m.alltoallv_dev(c, w.sendk, ek.data(), w.recvk, er.data()));
+  VP_TRY(m.alltoallv_dev(c, w.xsend, ek.data(), w.recvk, er.data()));
   nat_own_probe<<<resident_grid((const void *)nat_own_probe, (std::max<uint64_t>(R, 1) + 255) / 256),
                   256, 0, c->stream>>>(tbl_dev(t), c->crc_tab, w.recvk, (uint32_t)R, 0, nullptr,
                                        nullptr, t.ctl, w.reply, kNone, nullptr, nullptr);
@@ -1694,7 +1754,7 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   VP_HIP(ev_record(c->ktime, c->ev2, c->stream));
   VP_TRY(pass2());
   VP_HIP(ev_record(c->ktime, c->ev3, c->stream));
-  VP_TRY(tbl_fold_read_ctl(c, t, ph->bp, w.log, p0, p1, now, seq0, w.dtot));
+  VP_TRY(tbl_fold_read_ctl(c, t, ph->bp, w.log, p0, p1, now, seq0, w.dneed));
   VP_HIP(ev_ms(c->ktime, c->ev2, c->ev3, &k2));
   ph->ms += k2;
   return 0;

@@ -195,7 +195,8 @@ static void free_all(vp_ctx *c) {
                   c->st_bk,  c->st_val,  c->be_rec,   c->cht,   c->dmacw,
                   w.sbuf,    w.rbuf,     c->pol_size, c->pol_time,
                   c->pol_cnt, c->pol_off, c->pol_runs, w.desc, w.dcnt, w.dbase, w.dtot,
-                  w.route,   w.sendk,    w.recvk,  w.reply,  w.rreply};
+                  w.route,   w.sendk,    w.recvk,  w.reply,  w.rreply,
+                  w.cnt_t,   w.rcnt_t,   w.dneed,  w.xsend};
   for (void *p : ptrs) hipFree(p);
   if (w.h_tot) hipHostFree(w.h_tot);
   if (w.h_frames) hipHostFree(w.h_frames);
