@@ -1608,7 +1608,8 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   }
   if (ph->range1 >= (1u << 24) - 1) return VP_ENOTSUP;
   const uint32_t C = std::max<uint32_t>(1, c->own_cap);  // keys per peer (padded)
-  const uint32_t sub = std::max<uint32_t>(1, C / ph->grid1);  // keys per block slice
+  uint32_t sub = std::max<uint32_t>(1, C / ph->grid1);  // keys per block slice
+  if (sub >= 64) sub &= ~63u;  // (whole 64-key probe tiles per slice)
   if (ph->grid1 > kSliceRowMax) return VP_ENOTSUP;
   const size_t slices = (size_t)ph->grid1 * n;
   VP_TRY(grow_dev(&w.desc, &w.desc_n, slices * ph->range1, c->stream));
