@@ -1,6 +1,7 @@
 #!/bin/bash
 # round 4 session l: viglb storing 48 bytes of rewritten UDP frames
-# (VIGPATH_LB_WB48=1) against the whole 64: tests, rate, PMC traffic
+# (VIGPATH_LB_WB48=1) against the whole 64: tests, rate, PMC traffic;
+# kernel traces of the random-key and churn workloads
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -19,3 +20,5 @@ for i in 1 2; do
 done
 VIGPATH_LB_WB48=1 step pmcw 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/r04l_lb48_write -- python3 tools/bench_nf.py --only lb --no-cpu --steps 3
 VIGPATH_LB_WB48=1 step pmcf 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/r04l_lb48_fetch -- python3 tools/bench_nf.py --only lb --no-cpu --steps 3
+step trace_random 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r04l_random_kt -- python3 tools/bench_extra.py nat_random_keys
+step trace_churn 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r04l_churn_kt -- python3 tools/bench_extra.py nat_churn
