@@ -128,7 +128,6 @@ struct LbArgs {
   // log their touches themselves and are applied after the fold as late
   // touches (lb_segment)
   bool binned;
-  uint32_t udp_mask;  // chunks stored back for a rewritten UDP frame (0x7: bytes 0-47)
 };
 
 // cht_find_preferred_available_backend: bucket = (u64)hash % height, the
@@ -386,7 +385,7 @@ __global__ __launch_bounds__(256, 4) void lb_classify64(LbArgs a, uint32_t n_all
         // dst address, MACs and checksums change bytes 0-47 (and the TCP
         // checksum 50-51): the whole 64-byte slot is stored back, since a
         // partial-line write costs more than a whole one
-        return rw ? (proto == 17 ? a.udp_mask : 0xFu) : 0u;
+        return rw ? 0xFu : 0u;
       },
       bins, TileQueue{}, cur);
 }
@@ -671,10 +670,6 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
         bp.on ? bp.grid : resident_grid((const void *)lb_classify64, (tiles + 3) / 4);
     LbArgs a64 = a;
     a64.binned = bp.on;
-    a64.udp_mask = [] {  // (diagnostics: VIGPATH_LB_WB48=1 stores 48 bytes of UDP frames)
-      const char *e = getenv("VIGPATH_LB_WB48");
-      return e && atoi(e) ? 0x7u : 0xFu;
-    }();
     lb_classify64<<<grid, 256, 0, c->stream>>>(a64, b->n, bp.bins);
   } else {
     lb_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
