@@ -127,6 +127,7 @@ struct FlowTable {
   uint32_t lin_ok = 0;
   bool lin_tried = false;
   uint64_t nb_nominal = 0;  // buckets of the CRC-bit layouts
+  uint64_t nb_base = 0;     // the power of two >= cap (one bucket per index)
   uint32_t *slot_of = nullptr;
   uint32_t *hash_of = nullptr;
   uint64_t *ts = nullptr;

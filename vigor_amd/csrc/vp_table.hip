@@ -163,16 +163,18 @@ static uint64_t tbl_entries(const FlowTable &t) {
 
 int tbl_alloc(vp_ctx *c, FlowTable &t, uint32_t cap) {
   (void)c;
-  // one bucket (3 entries) per index: load <= 1/3, so a random key set puts
-  // ~2 % of its keys past their home bucket (~13 % at load 2/3, each one a
-  // reprobe); 64 B of HBM per index. Tombstones purged at 0.85.
+  // two buckets (3 entries each) per index: load <= 1/6, so a random key
+  // set puts ~0.2 % of its keys past their home bucket (~2.3 % at load 1/3,
+  // ~13 % at 2/3, each one a reprobe: DESIGN.md §5.1, random keys 0.80 ->
+  // 0.66 ms per step); 128 B of HBM per index (the allocation-order layout,
+  // §4, rebuilds at 32 B). Tombstones purged at 0.85.
   uint64_t nb = 64;
   while (nb < cap) nb <<= 1;
-  if (const char *sp = getenv("VIGPATH_SPARSE")) {  // diagnostics: 2^k x buckets
-    const int k = atoi(sp);
-    if (k > 0) nb <<= std::min(k, 3);
-    if (k < 0) nb = std::max<uint64_t>(64, nb >> std::min(-k, 3));
-  }
+  t.nb_base = nb;
+  int k = 1;
+  if (const char *sp = getenv("VIGPATH_SPARSE")) k = atoi(sp);  // (tests: 2^k x buckets)
+  if (k > 0) nb <<= std::min(k, 3);
+  if (k < 0) nb = std::max<uint64_t>(64, nb >> std::min(-k, 3));
   t.bmask = (uint32_t)(nb - 1);
   t.nb_nominal = nb;
   t.cap = cap;
@@ -390,7 +392,7 @@ int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
   // first chance for the allocation-order layout (below), whatever the
   // current layout's clustering: it replaces it
   if (t.lin_ok && !t.lin_tried && !t.own_n && t.mix != kMixLin &&
-      2ull * t.h_ctl.n_live > (uint64_t)t.bmask + 1) {
+      2ull * t.h_ctl.n_live > t.nb_base) {
     VP_TRY(tbl_try_linear(c, t));
     if (t.mix == kMixLin) {
       VP_HIP(hipMemsetAsync(&t.ctl->max_disp, 0, 4, c->stream));
