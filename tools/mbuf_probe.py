@@ -35,8 +35,6 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--modes", default="gpu",
                     help="VIGPATH_MBUF_MODE values: gpu (zero-copy), host (host threads gather)")
-    ap.add_argument("--lines", action="store_true",
-                    help="VIGPATH_MBUF_LINES=1: write back whole 64-byte lines (diagnostics)")
     ap.add_argument("--pools", default="pinned",
                     help="pinned (page-locked 4 KB pages), huge (2 MB THP, registered)")
     args = ap.parse_args()
@@ -81,7 +79,6 @@ def main():
                 for blk, mode in [(b, m) for b in args.blocks.split(",")
                                   for m in args.modes.split(",")]:
                     os.environ["VIGPATH_MBUF_MODE"] = mode
-                    os.environ["VIGPATH_MBUF_LINES"] = "1" if args.lines else "0"
                     os.environ["VIGPATH_HOST_CHUNK"] = ch
                     os.environ["VIGPATH_MBUF_BLOCKS"] = blk
                     call = nat.mbuf_step(ptrs, lens, ind, out)
@@ -102,7 +99,7 @@ def main():
                     assert (out == 1).all()
                     el = sum(times) / len(times)
                     print(json.dumps({"pool": kind, "layout": var, "chunk": int(ch), "blocks": int(blk),
-                                      "mode": mode, "lines": args.lines,
+                                      "mode": mode,
                                       "threads": os.environ.get("VIGPATH_MBUF_THREADS", "8"),
                                       "ms_per_call": round(el * 1e3, 3),
                                       "mpps": round(B / el / 1e6, 1)}), flush=True)

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256) void mbuf_scatter(const uint64_t *ptr, const u
                                                    const uint16_t *in_dev,
                                                    const uint16_t *out, uint32_t n, MapTab m,
                                                    const uint8_t *slots, uint32_t slot,
-                                                   uint32_t wb, uint32_t lines) {
+                                                   uint32_t wb) {
   const uint32_t q = threadIdx.x & 3;
   const uint32_t ng = (gridDim.x * blockDim.x) >> 2;
   for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 2; i < n; i += ng) {
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(256) void mbuf_scatter(const uint64_t *ptr, const u
     const uint32_t L = len[i];
     uint8_t *f = map_frame(m, ptr[i], L);
     if (!f) continue;
-    const uint32_t bytes = lines ? wb : min(L, wb);  // (lines: diagnostics, whole 64-byte lines)
+    const uint32_t bytes = min(L, wb);
     const uint4 *s = reinterpret_cast<const uint4 *>(slots + (size_t)i * slot);
     for (uint32_t c = q; 16 * c < bytes; c += 4) host_st(f + 16 * c, min(16u, bytes - 16 * c), s[c]);
   }
@@ -510,8 +510,6 @@ static int mbuf_pipeline(vp_ctx *c, const vp_mbuf_batch *b) {
     return 0;
   };
   hipStream_t ws = w.dstream;  // (on the gather stream instead: 10-15 % slower, r04f)
-  const char *le = getenv("VIGPATH_MBUF_LINES");  // diagnostics: write back whole 64-byte lines
-  const bool lines = le && atoi(le);
   auto issue_scatter = [&](uint32_t k) -> int {
     if (staged[k]) return 0;
     const uint32_t i = k % S, m = cnt(k);
@@ -522,7 +520,7 @@ static int mbuf_pipeline(vp_ctx *c, const vp_mbuf_batch *b) {
           w.mb_ptr + (size_t)i * ch, w.mb_len + (size_t)i * ch, w.mb_in + (size_t)i * ch,
           w.mb_out + (size_t)i * ch, m, mt,
           wslot[k] ? w.mb_full : w.mb_slots + (size_t)i * ch * 64, wslot[k] ? wslot[k] : 64,
-          wb, lines && !wslot[k] ? 1u : 0u);
+          wb);
       VP_HIP(hipGetLastError());
     }
     VP_HIP(hipMemcpyAsync(hout(k), w.mb_out + (size_t)i * ch, 2ull * m, hipMemcpyDeviceToHost,
