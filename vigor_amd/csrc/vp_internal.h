@@ -162,6 +162,7 @@ struct Workspace {
   uint32_t *defer = nullptr;
   uint32_t *reprobe = nullptr;  // packets whose probe continues past the home bucket
   uint32_t *reprobe_cnt = nullptr;  // per classify block (TileQueue)
+  uint32_t *missq = nullptr;  // phase-A misses per classify block (the reprobe slices' layout)
   uint32_t *mkey = nullptr;  // 4 words per miss
   uint32_t *mhash = nullptr;
   uint32_t *first = nullptr;

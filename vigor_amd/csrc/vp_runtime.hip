@@ -91,7 +91,7 @@ static void ws_release(Workspace &w) {
                   w.first, w.rank,        w.rep,   w.assign, w.scratch,
                   w.log,   w.iota,        w.skey,  w.sval,
                   w.log2,  w.defer_sorted, w.aux,  w.aux_sorted, w.rlist, w.hbl,
-                  w.unow,  w.reprobe,     w.reprobe_cnt, w.ovf_q, w.ovf_cnt};
+                  w.unow,  w.reprobe,     w.reprobe_cnt, w.ovf_q, w.ovf_cnt, w.missq};
   for (void *p : ptrs) hipFree(p);
   w.miss = w.miss_sorted = w.defer = w.mkey = w.mhash = w.first = w.rank =
       w.rep = w.assign = w.scratch = w.log = w.iota = w.skey = w.sval = nullptr;
@@ -99,6 +99,7 @@ static void ws_release(Workspace &w) {
   w.unow = nullptr;
   w.reprobe = w.reprobe_cnt = nullptr;
   w.ovf_q = w.ovf_cnt = nullptr;
+  w.missq = nullptr;
   w.cap_n = 0;
 }
 
@@ -116,6 +117,7 @@ int ws_reserve(vp_ctx *c, uint32_t n) {
   VP_TRY(dalloc(&w.reprobe, cap + 128));  // per-block slices end on tile bounds
   VP_TRY(dalloc(&w.reprobe_cnt, 4096));   // >= any resident grid
   VP_TRY(dalloc(&w.ovf_q, cap + 128));     // (the same slices as reprobe)
+  VP_TRY(dalloc(&w.missq, cap + 128));
   VP_TRY(dalloc(&w.ovf_cnt, 4096));
   VP_TRY(dalloc(&w.mkey, 4ull * cap));
   VP_TRY(dalloc(&w.mhash, cap));
