@@ -1085,23 +1085,53 @@ static NatTileKernel nat_tile_kernel(uint32_t slot, bool hdr_tail = false) {
 
 // ------------------------------------------------------------- phase B --
 
-// FlowId keys and hashes of the queued misses (frames still unmodified).
-__global__ void nat_miss_keys(NatArgs a, const uint32_t *list, uint32_t n,
-                              uint32_t *mkey, uint32_t *mhash) {
+// The first 64 bytes of slot p as a register frame (slots that are a
+// multiple of 16 bytes, at least 64: every coalesced slot size).
+__device__ __forceinline__ bool nat_slot_regs(const NatArgs &a, uint32_t p, RFrame &f) {
+  if (a.slot < 64 || (a.slot & 15)) return false;
+  const uint4 *fp = reinterpret_cast<const uint4 *>(a.frames + (size_t)p * a.slot);
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) {
+    const uint4 v = fp[k];
+    f.w[4 * k] = v.x;
+    f.w[4 * k + 1] = v.y;
+    f.w[4 * k + 2] = v.z;
+    f.w[4 * k + 3] = v.w;
+  }
+  return true;
+}
+
+// FlowId keys and hashes of the queued misses (frames still unmodified):
+// register frames with the tile kernels' field reads and the batched hash
+// from the LDS tables, the generic byte path for any other frame.
+__global__ __launch_bounds__(256) void nat_miss_keys(NatArgs a, const uint32_t *list,
+                                                     uint32_t n, uint32_t *mkey,
+                                                     uint32_t *mhash) {
+  __shared__ uint32_t T[kNatTabWords];
+  load_nat_tables(T, a);
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
        j += gridDim.x * blockDim.x) {
     const uint32_t p = list[j];
-    GFrame f{a.frames + (size_t)p * a.slot, a.slot};
-    const L34 h = parse_l34(f, a.len[p]);
-    const uint32_t proto = f.r8(h.ip + 9), in = a.in_dev[p];
-    const uint32_t sp = f.r16(h.l4), dp = f.r16(h.l4 + 2);
-    const uint32_t sip = f.r32(h.ip + 12), dip = f.r32(h.ip + 16);
-    uint32_t *k = mkey + 4 * (size_t)j;
-    k[0] = sp | (dp << 16);
-    k[1] = sip;
-    k[2] = dip;
-    k[3] = in | (proto << 16);
-    mhash[j] = flowid_hash(a.crc_tab, sp, dp, sip, dip, in, proto);
+    const uint32_t in = a.in_dev[p], len = a.len[p];
+    uint32_t proto, sp, dp, sip, dip;
+    RFrame r;
+    if (nat_slot_regs(a, p, r) && nat_reg_ok(r, len, 0xFFFFu)) {
+      proto = r.w[5] >> 24;
+      sp = r.w[8] >> 16;
+      dp = r.w[9] & 0xFFFF;
+      sip = r.u32at2(26);
+      dip = r.u32at2(30);
+    } else {
+      GFrame f{a.frames + (size_t)p * a.slot, a.slot};
+      const L34 h = parse_l34(f, len);
+      proto = f.r8(h.ip + 9);
+      sp = f.r16(h.l4);
+      dp = f.r16(h.l4 + 2);
+      sip = f.r32(h.ip + 12);
+      dip = f.r32(h.ip + 16);
+    }
+    reinterpret_cast<uint4 *>(mkey)[j] = make_uint4(sp | (dp << 16), sip, dip, in | (proto << 16));
+    mhash[j] = flowid_hash_batched(T, sp, dp, sip, dip, in, proto);
   }
 }
 
@@ -1117,10 +1147,14 @@ __device__ void nat_write_lan(const NatArgs &a, uint32_t p, uint32_t idx) {
   a.out[p] = a.wan;
 }
 
-// Every miss: the index its first sighting got (or drop: table full).
-__global__ void nat_miss_finish(NatArgs a, const uint32_t *list, uint32_t n,
-                                const uint32_t *scratch, const uint32_t *rep,
-                                const uint32_t *assign) {
+// Every miss: the index its first sighting got (or drop: table full). A
+// register-path frame of a 64-byte slot is rewritten as the tile kernels
+// rewrite a hit (four 16-byte loads and stores); any other takes the byte
+// path.
+__global__ __launch_bounds__(256) void nat_miss_finish(NatArgs a, const uint32_t *list,
+                                                       uint32_t n, const uint32_t *scratch,
+                                                       const uint32_t *rep,
+                                                       const uint32_t *assign) {
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
        j += gridDim.x * blockDim.x) {
     const uint32_t p = list[j];
@@ -1128,6 +1162,23 @@ __global__ void nat_miss_finish(NatArgs a, const uint32_t *list, uint32_t n,
     a.log[p] = idx;
     if (idx == kNone) {  // nat_main.c:87-91
       a.out[p] = a.in_dev[p];
+      continue;
+    }
+    RFrame f;
+    if (a.slot == 64 && nat_slot_regs(a, p, f) &&
+        nat_lan_fast_ok(a, f, a.in_dev[p], a.len[p], nat_lim64(a))) {
+      const uint32_t proto = f.w[5] >> 24;
+      f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
+      f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
+      fast_checksums(f, proto, bswap16((uint16_t)(f.w[4] & 0xFFFF)), nat_tail(a, p));
+      f.w[0] = a.wan_macw0;
+      f.w[1] = a.wan_macw1;
+      f.w[2] = a.wan_macw2;
+      uint4 *fp = reinterpret_cast<uint4 *>(a.frames + (size_t)p * 64);
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++)
+        fp[k] = make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
+      a.out[p] = a.wan;
       continue;
     }
     nat_write_lan(a, p, idx);
