@@ -276,7 +276,7 @@ __global__ void nk_dedup(NkArgs m) {
       if (old == kEmpty) break;
       const uint32_t *ko = m.mkey + 4 * (size_t)old;
       if (m.mhash[old] == m.mhash[j] && key_eq(ko, kj)) {
-        atomicMin(&m.scratch[s], j);
+        if (j < old) atomicMin(&m.scratch[s], j);  // (a later packet holds the slot)
         break;
       }
       s = (s + 1) & m.smask;
@@ -1083,7 +1083,10 @@ int tbl_reprobe_stamp(vp_ctx *c, FlowTable &t, const uint32_t *list,
 
 // ---------------------------------------------------------------- expiry --
 
-__global__ void tbl_min_ts(TableDev t) {
+// (One global atomic per block: with one per wave the 8192 waves of a 1M-index
+// table queued on a single address, ≈ 95 µs; round 4.)
+__global__ __launch_bounds__(256) void tbl_min_ts(TableDev t) {
+  __shared__ unsigned long long wbest[4];
   unsigned long long best = ~0ull;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.cap;
        i += gridDim.x * blockDim.x)
@@ -1092,15 +1095,19 @@ __global__ void tbl_min_ts(TableDev t) {
     unsigned long long v = __shfl_xor(best, o);
     best = v < best ? v : best;
   }
-  if (__lane_id() == 0 && best != ~0ull)
-    atomicMin((unsigned long long *)&t.ctl->min_ts, best);
+  if (__lane_id() == 0) wbest[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t w = 1; w < blockDim.x / 64; w++) best = wbest[w] < best ? wbest[w] : best;
+    if (best != ~0ull) atomicMin((unsigned long long *)&t.ctl->min_ts, best);
+  }
 }
 
 int tbl_exact_floor(vp_ctx *c, FlowTable &t) {
   const uint64_t all = ~0ull;
   VP_HIP(hipMemcpyAsync(&t.ctl->min_ts, &all, 8, hipMemcpyHostToDevice,
                         c->stream));
-  tbl_min_ts<<<grid_for(t.cap), 256, 0, c->stream>>>(tbl_dev(t));
+  tbl_min_ts<<<grid_for(t.cap, 256, 512), 256, 0, c->stream>>>(tbl_dev(t));
   VP_HIP(hipGetLastError());
   VP_TRY(read_ctl(c, t));
   t.ts_floor = t.h_ctl.min_ts;
@@ -1110,12 +1117,27 @@ int tbl_exact_floor(vp_ctx *c, FlowTable &t) {
 // Every allocated index with ts < cutoff: the set expire_items_single_map
 // frees (LRU order is (ts, last-touch) order, so the loop stops exactly at
 // the first stamp >= cutoff).
-__global__ void exp_collect(TableDev t, int64_t cutoff, uint64_t *ekey,
-                            uint32_t *eidx) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.cap;
-       i += gridDim.x * blockDim.x) {
-    const bool take = t.slot_of[i] != kNone && (int64_t)t.ts[i] < cutoff;
-    const uint32_t k = wave_append(&t.ctl->exp_count, take);
+// Two passes over the block's contiguous range of indices: count, one global
+// atomic for the block's base, then append behind it (the set is sorted
+// afterwards: its order here does not matter).
+__global__ __launch_bounds__(256) void exp_collect(TableDev t, int64_t cutoff, uint64_t *ekey,
+                                                   uint32_t *eidx) {
+  __shared__ uint32_t cnt, base;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  const uint32_t per = (t.cap + gridDim.x - 1) / gridDim.x;
+  const uint32_t i0 = blockIdx.x * per, i1 = min(t.cap, i0 + per);
+  auto take_at = [&](uint32_t i) { return t.slot_of[i] != kNone && (int64_t)t.ts[i] < cutoff; };
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) wave_append(&cnt, take_at(i));
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    base = cnt ? atomicAdd(&t.ctl->exp_count, cnt) : 0u;
+    cnt = 0;
+  }
+  __syncthreads();
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const bool take = take_at(i);
+    const uint32_t k = base + wave_append(&cnt, take);
     if (take) {
       eidx[k] = i;
       ekey[k] = t.tseq[i];
@@ -1133,7 +1155,10 @@ __global__ void exp_gather_ts(const uint32_t *eidx, uint32_t n, const uint64_t *
 // Free in LRU order: the oldest is pushed first, so the youngest expired
 // index ends on top (double-chain-impl.c:1968-1981); erase the keys.
 // (Owner mode: every rank frees the index; only the key's owner erases it.)
-__global__ void exp_apply(TableDev t, const uint32_t *eidx, uint32_t n) {
+__global__ __launch_bounds__(256) void exp_apply(TableDev t, const uint32_t *eidx, uint32_t n) {
+  __shared__ uint32_t tombs;
+  if (threadIdx.x == 0) tombs = 0;
+  __syncthreads();
   const uint32_t top = t.ctl->stack_top;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
        j += gridDim.x * blockDim.x) {
@@ -1143,9 +1168,10 @@ __global__ void exp_apply(TableDev t, const uint32_t *eidx, uint32_t n) {
     const bool own = e < kElsewhere;
     if (own) t.bk[e >> 2].idx[e & 3] = kTomb;
     t.slot_of[idx] = kNone;
-    const uint32_t k = wave_append(&t.ctl->n_tomb, own);
-    (void)k;
+    wave_append(&tombs, own);  // (counted per block, one global atomic)
   }
+  __syncthreads();
+  if (threadIdx.x == 0 && tombs) atomicAdd(&t.ctl->n_tomb, tombs);
 }
 
 __global__ void exp_commit(Ctl *ctl, uint32_t n, uint32_t n_tomb_before) {
@@ -1240,8 +1266,8 @@ int tbl_owner_reserve(vp_ctx *c, FlowTable &t, uint32_t n) {
 
 int tbl_expire(vp_ctx *c, FlowTable &t, int64_t cutoff, uint32_t *n_out) {
   VP_HIP(hipMemsetAsync(&t.ctl->exp_count, 0, 4, c->stream));
-  exp_collect<<<grid_for(t.cap), 256, 0, c->stream>>>(tbl_dev(t), cutoff, t.ekey,
-                                                      t.eidx);
+  exp_collect<<<grid_for(t.cap, 256, 512), 256, 0, c->stream>>>(tbl_dev(t), cutoff, t.ekey,
+                                                                t.eidx);
   VP_HIP(hipGetLastError());
   VP_TRY(read_ctl(c, t));
   const uint32_t k = t.h_ctl.exp_count;
