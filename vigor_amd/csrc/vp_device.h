@@ -283,7 +283,8 @@ constexpr uint32_t kCurReprobe = kMaxBins;       // LDS cursor of the reprobe qu
 constexpr uint32_t kCurOverflow = kMaxBins + 1;  // LDS cursor of the overflow queue
 constexpr uint32_t kCurDest = kMaxBins + 2;      // LDS cursors per owner rank (owner mode)
 constexpr uint32_t kMaxDest = 64;                // = kMaxRanks (vp_internal.h)
-constexpr uint32_t kCurs = kCurDest + kMaxDest;
+constexpr uint32_t kCurMiss = kCurDest + kMaxDest;  // LDS cursor of vignat's miss slice
+constexpr uint32_t kCurs = kCurMiss + 1;
 // finish() may set touch = kReprobe instead of an index: the packet leaves
 // the wave and is queued on the block's reprobe slice (TileQueue).
 constexpr uint32_t kReprobe = 0xFFFFFFFDu;

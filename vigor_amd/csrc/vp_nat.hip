@@ -159,24 +159,12 @@ struct NatArgs {
   // longer frames, tail[p] = the raw sum of frame p's bytes [64, end) the L4
   // checksum covers (0 where nothing lies past 64); null otherwise.
   const uint32_t *tail;
-  // 64-byte tiles (nat_tiles): phase-A misses go to the block's slice of mq
-  // (LDS cursor mq_cur) and are appended to `miss` once per block at its end,
-  // not by one global atomic per wave (a churn batch has misses in every
-  // wave); null elsewhere
+  // 64-byte tiles (nat_tiles): the lean tiles' phase-A misses go to the
+  // block's slice of mq (LDS cursor kCurMiss) and are appended to `miss` once
+  // per block at its end, not by one global atomic per wave (a churn batch
+  // has misses in every wave); null elsewhere
   uint32_t *mq;
-  uint32_t *mq_cur;
-  uint32_t mq_range;  // packets per block (the slice stride)
 };
-
-// Queue packet p for phase B (a LAN miss); under divergence like wave_append.
-__device__ __forceinline__ void miss_append(const NatArgs &a, uint32_t p) {
-  if (a.mq_cur) {
-    const uint32_t k = wave_append(a.mq_cur, true);
-    a.mq[(size_t)blockIdx.x * a.mq_range + k] = p;
-  } else {
-    a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
-  }
-}
 
 // The register path's total_length bound for 64-byte slots (every L4 byte in
 // the slot), or any total_length for header slots with tail sums.
@@ -268,7 +256,7 @@ __device__ uint32_t nat_generic_a(const NatArgs &a, const uint32_t *T,
     }
     const uint32_t idx = tbl_probe(a.t, hh, key);
     if (idx == kNone) {
-      miss_append(a, p);
+      a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
       log_put(a.log, p, kNone);  // phase B writes the real entry
       return kNone;
     }
@@ -413,7 +401,7 @@ __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
       return false;
     }
     if (idx == kNone) {  // new flow, or not yet visible: phase B
-      miss_append(a, p);
+      a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
       log_put(a.log, p, kNone);  // phase B writes the real entry
       return false;
     }
@@ -612,9 +600,8 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   __shared__ uint32_t T[kNatTabWords];
   __shared__ uint4 stage[4][256];
   __shared__ uint32_t cur[kCurs];
-  __shared__ uint32_t mcur, mbase;
+  __shared__ uint32_t mbase;
   for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
-  if (threadIdx.x == 0) mcur = 0;
   a.own.cur = cur + kCurDest;
   load_nat_tables(T, a);  // (its barrier also covers cur)
   uint4 *S = stage[threadIdx.x >> 6];
@@ -677,8 +664,15 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   uint32_t tile = rb * per_b + wv;
   const uint32_t tend = min(tiles, rb * per_b + per_b), tstep = 4;
   const uint32_t range0 = first + rb * per_b * 64;  // this block's first packet
-  a.mq_cur = a.mq ? &mcur : nullptr;
-  a.mq_range = per_b * 64;
+  // a lean tile's misses (wave-uniform call)
+  auto miss_put = [&](bool miss) {
+    if (a.mq) {
+      const uint32_t k = group_reserve(cur, kCurMiss, miss);
+      if (miss) a.mq[(size_t)rb * per_b * 64 + k] = tile * 64 + first + lane;
+    } else if (miss) {
+      a.miss[wave_append(&a.t.ctl->miss_count, true)] = first + tile * 64 + lane;
+    }
+  };
   // (wide slots: the headers of the wave's own tile at its start; a prefetch
   // of the next tile's would keep 16 registers the tail sums need)
   if (G == 0 && tile < tend) fetch(tile);
@@ -778,7 +772,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
         const bool hit = done & (idx != kNone);
         if (__ballot(!hit)) {  // misses (phase B) and full home buckets (reprobes)
           const bool miss = done & !hit;
-          if (miss) miss_append(a, p);
+          miss_put(miss);
           const uint32_t k = group_reserve(cur, kCurReprobe, !done);
           if (!done) rq.ent[(size_t)rb * per_b * 64 + k] = p;
           if (!hit) log_put(a.log, p, kNone);
@@ -869,7 +863,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       const bool hit = done & (idx != kNone);
       if (__ballot(!hit)) {  // misses (phase B) and full home buckets (reprobes)
         const bool miss = done & !hit;
-        if (miss) miss_append(a, p);
+        miss_put(miss);
         const uint32_t k = group_reserve(cur, kCurReprobe, !done);
         if (!done) rq.ent[(size_t)rb * per_b * 64 + k] = p;
         if (!hit) log_put(a.log, p, kNone);
@@ -930,7 +924,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
         bool done;
         const uint32_t idx = bucket_match_sel(row, key, &done);
         t1 = !done ? kReprobe : idx;  // kNone: a new flow, phase B
-        if (done & (idx == kNone)) miss_append(a, p);
+        miss_put(done & (idx == kNone));
         if (done & (idx != kNone)) {
           f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
           f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
@@ -1029,11 +1023,11 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
     rq.cnt[rb] = c;
     if (c) atomicAdd(rq.total, c);
   }
-  if (a.mq_cur) {  // the block's misses onto the phase-B list (one atomic)
-    const uint32_t c = mcur;
+  if (a.mq) {  // the block's lean-tile misses onto the phase-B list (one atomic)
+    const uint32_t c = cur[kCurMiss];
     if (threadIdx.x == 0 && c) mbase = atomicAdd(&a.t.ctl->miss_count, c);
     __syncthreads();
-    const uint32_t *src = a.mq + (size_t)rb * a.mq_range;
+    const uint32_t *src = a.mq + (size_t)rb * per_b * 64;
     for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) a.miss[mbase + i] = src[i];
   }
   route_publish(a, cur + kCurDest);
@@ -1518,7 +1512,7 @@ __global__ __launch_bounds__(256, 4) void nat_remote64(NatArgs a, uint32_t n_all
           return 0u;
         }
         if (P.idx == kNone) {  // a new flow (or not yet visible): phase B
-          miss_append(a, p);
+          a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
           log_put(a.log, p, kNone);
           return 0u;
         }
@@ -1546,7 +1540,7 @@ __global__ void nat_remote_lane(NatArgs a) {
     if (idx == kNoReply) continue;  // the exact exchange answers it
     a.log[p] = idx;
     if (idx == kNone) {
-      miss_append(a, p);
+      a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
       continue;
     }
     nat_write_lan(a, p, idx);
