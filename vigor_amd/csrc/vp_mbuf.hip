@@ -105,27 +105,23 @@ __device__ __forceinline__ void host_st(uint8_t *d, uint32_t nb, uint4 v) {
   }
 }
 
-// Frames of the chunk in one contiguous range per block. Pass 1, four lanes
-// per frame (lane q: bytes [16q, 16q + 16) of the header; 16 frames per
-// instruction): header slot = the frame's bytes [0, min(len, 64)), zeros
-// after. TAIL, pass 2 over the same frames, eight lanes per frame (each
-// instruction reads 128 contiguous bytes of a frame: half the PCIe read
-// requests of four lanes): tail[i] = raw sum (vp_device.h
-// sum16x4, the checksum's arithmetic) of bytes [64, min(len, 14 +
-// total_length)) of an IPv4 IHL-5 frame, else 0 (pass 1 leaves that end in
-// tail[i]). Every wave ORs its flags into *flags once. rule kRuleNoOpt: an
-// IPv4 frame with options longer than 64 bytes sets kMbWhole (its L4 header,
-// and so its rewrite, may lie past byte 64).
+// Frames of the chunk, four lanes each (lane q: bytes [16q, 16q + 16) of the
+// header), grid-stride; every wave ORs its flags into *flags once.
+// Header slot: the frame's bytes [0, min(len, 64)), zeros after. TAIL:
+// tail[i] = raw sum (vp_device.h sum16x4, the checksum's arithmetic) of bytes
+// [64, min(len, 14 + total_length)) of an IPv4 IHL-5 frame, else 0 -- four
+// lanes per frame, each a chunk of every 64 bytes, four loads in flight.
+// rule kRuleNoOpt: an IPv4 frame with options longer than 64 bytes sets
+// kMbWhole (its L4 header, and so its rewrite, may lie past byte 64).
 template <bool TAIL>
 __global__ __launch_bounds__(256) void mbuf_gather_hdr(const uint64_t *ptr, const uint16_t *len,
                                                       uint32_t n, MapTab m, uint32_t rule,
                                                       uint8_t *slots, uint32_t *tail,
                                                       uint32_t *flags) {
   const uint32_t lane = threadIdx.x & 63, q = lane & 3, lead = lane & ~3u;
-  const uint32_t per = (n + gridDim.x - 1) / gridDim.x;
-  const uint32_t i0 = blockIdx.x * per, i1 = min(n, i0 + per);
+  const uint32_t ng = (gridDim.x * blockDim.x) >> 2;
   uint32_t fl = 0;
-  for (uint32_t i = i0 + (threadIdx.x >> 2); i < i1; i += blockDim.x >> 2) {
+  for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 2; i < n; i += ng) {
     const uint32_t L = len[i];
     const uint8_t *f = map_frame(m, ptr[i], L);
     const uint4 v = f ? host_ld16(f, 16 * q, L) : make_uint4(0, 0, 0, 0);
@@ -137,31 +133,22 @@ __global__ __launch_bounds__(256) void mbuf_gather_hdr(const uint64_t *ptr, cons
     const bool ip = (w3 & 0xFFFF) == 0x0008;
     const uint32_t ihl = (w3 >> 16) & 0x0F;
     if (f && rule == kRuleNoOpt && L > 64 && ip && ihl > 5) fl |= kMbWhole;
-    if (TAIL && q == 0)
-      tail[i] = f && ip && ihl == 5 ? min(L, 14u + bswap16((uint16_t)(w4 & 0xFFFF))) : 0u;
-  }
-  const uint64_t b1 = __ballot(fl & kMbWhole), b2 = __ballot(fl & kMbUnmapped);
-  if (lane == 0 && (b1 | b2)) atomicOr(flags, (b1 ? kMbWhole : 0u) | (b2 ? kMbUnmapped : 0u));
-  if constexpr (TAIL) {
-    __syncthreads();  // (the ends this block's pass 1 wrote)
-    const uint32_t q8 = lane & 7;
-    for (uint32_t i = i0 + (threadIdx.x >> 3); i < i1; i += blockDim.x >> 3) {
-      const uint32_t end = tail[i];
+    if constexpr (TAIL) {
+      uint32_t end = 0;
+      if (f && ip && ihl == 5) end = min(L, 14u + bswap16((uint16_t)(w4 & 0xFFFF)));
       uint32_t s = 0;
-      if (end > 64) {  // (frames past 64 bytes only; `end` <= len: mapped)
-        const uint8_t *f = map_frame(m, ptr[i], end);
-        for (uint32_t c = 4 + q8; 16 * c < end; c += 32) {
-          const uint4 x0 = host_ld16(f, 16 * c, end), x1 = host_ld16(f, 16 * (c + 8), end),
-                      x2 = host_ld16(f, 16 * (c + 16), end), x3 = host_ld16(f, 16 * (c + 24), end);
-          s = sum16x4(x3, sum16x4(x2, sum16x4(x1, sum16x4(x0, s))));
-        }
+      for (uint32_t c = 4 + q; 16 * c < end; c += 16) {
+        const uint4 x0 = host_ld16(f, 16 * c, end), x1 = host_ld16(f, 16 * (c + 4), end),
+                    x2 = host_ld16(f, 16 * (c + 8), end), x3 = host_ld16(f, 16 * (c + 12), end);
+        s = sum16x4(x3, sum16x4(x2, sum16x4(x1, sum16x4(x0, s))));
       }
       s += (uint32_t)__shfl_xor((int)s, 1);
       s += (uint32_t)__shfl_xor((int)s, 2);
-      s += (uint32_t)__shfl_xor((int)s, 4);
-      if (q8 == 0) tail[i] = s;
+      if (q == 0) tail[i] = s;
     }
   }
+  const uint64_t b1 = __ballot(fl & kMbWhole), b2 = __ballot(fl & kMbUnmapped);
+  if (lane == 0 && (b1 | b2)) atomicOr(flags, (b1 ? kMbWhole : 0u) | (b2 ? kMbUnmapped : 0u));
 }
 
 // Whole frames into `slot`-byte slots (zeros past each frame), four lanes
