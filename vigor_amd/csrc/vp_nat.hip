@@ -169,7 +169,6 @@ struct NatArgs {
   // run before the host learns phase A's counts (tbl_fold_read_ctl)
   PubArgs pub;
   uint32_t *arrive;  // blocks done (the last one resets it)
-  uint32_t pub_mode;  // (diagnostics, VIGPATH_PUB_MODE: 0 fences, 1 no block fences, 2 + relaxed epoch)
 };
 
 // The register path's total_length bound for 64-byte slots (every L4 byte in
@@ -1040,11 +1039,11 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   if (a.pub.pub) {  // the last block to finish publishes the control block
     __syncthreads();  // (every wave's counter updates of this block are done)
     if (threadIdx.x == 0) {
-      if (a.pub_mode == 0) __threadfence();
+      __threadfence();
       if (atomicAdd(a.arrive, 1u) == gridDim.x - 1) {
-        if (a.pub_mode == 0) __threadfence();  // (the other blocks' updates)
+        __threadfence();  // (the other blocks' updates, released before their arrival)
         *a.arrive = 0;
-        ctl_publish(a.pub, a.pub_mode == 2);
+        ctl_publish(a.pub);
       }
     }
   }
@@ -1915,12 +1914,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     if (tiles64) {
       NatArgs a64 = a;
       if (bp.on) a64.log = nullptr;  // touches go to the bins only
-      static const int pub_mode = [] {
-        const char *e = getenv("VIGPATH_PUB_MODE");
-        return e ? atoi(e) : 0;
-      }();
-      if (bp.on && !c->comm && pub_mode != 3) {
-        a64.pub_mode = (uint32_t)pub_mode;
+      if (bp.on && !c->comm) {
         cl_epoch = ++t.pub_epoch;
         a64.pub = PubArgs{t.d_pub, t.ctl, cl_epoch, nullptr, nullptr, 0, 0};
         a64.arrive = t.arrive;
@@ -1945,11 +1939,8 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // applied on top of it afterwards as late touches (tbl_late_touches: last
   // toucher still wins).
   hostprof(2);
-  static const bool defer = [] {
-    const char *e = getenv("VIGPATH_DEFER");
-    return !e || atoi(e);
-  }();
-  VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, seq0, nullptr, cl_epoch, defer));
+  VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, seq0, nullptr, cl_epoch,
+                           /*may_defer=*/true));
   hostprof(4);
   VP_HIP(ev_ms(c->ktime, c->ev0, c->ev1, &ph.ms));
   hostprof(5);

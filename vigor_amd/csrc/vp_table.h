@@ -66,7 +66,7 @@ struct PubArgs {
   uint32_t n0, n1;
 };
 static_assert(sizeof(Ctl) % 8 == 0, "Ctl is published as 8-byte words");
-__device__ __forceinline__ void ctl_publish(const PubArgs &a, bool relaxed = false) {
+__device__ __forceinline__ void ctl_publish(const PubArgs &a) {
   if (!a.pub) return;
   constexpr uint32_t kW = sizeof(Ctl) / 8;
   const uint64_t *s = reinterpret_cast<const uint64_t *>(a.ctl);
@@ -83,12 +83,6 @@ __device__ __forceinline__ void ctl_publish(const PubArgs &a, bool relaxed = fal
     __hip_atomic_store(&a.pub->xtra[i],
                        __hip_atomic_load(s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  if (relaxed) {  // (no L2 write-back: the data stores went to the host page;
-                  // wait for them, then the epoch, in PCIe's posted-write order)
-    __builtin_amdgcn_s_waitcnt(0);
-    __hip_atomic_store(&a.pub->epoch, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return;
   }
   __hip_atomic_store(&a.pub->epoch, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
