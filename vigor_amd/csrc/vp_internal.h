@@ -110,17 +110,6 @@ struct CtlPub {
   uint32_t epoch;
 };
 
-// One batch's touch bins as the fold reads them (vp_table.hip bins_reduce):
-// a steady-state vignat batch may leave its fold to the next one (the
-// stamps are then stale-low until folded; every reader folds first).
-struct FoldSet {
-  const uint32_t *ent = nullptr, *cnt = nullptr;
-  uint32_t nsrc = 0, cap = 0, pbits = 0, range = 0, p0 = 0;
-  const int64_t *arr = nullptr;  // the batch's time array, or affine now0 + p step
-  int64_t now0 = 0, step = 0;
-  uint64_t seq_base = 0;
-};
-
 // One device table (see vp_table.h).
 struct FlowTable {
   Bucket *bk = nullptr;
@@ -153,11 +142,6 @@ struct FlowTable {
   CtlPub *d_pub = nullptr;         // (its device address)
   uint32_t pub_epoch = 0;          // last epoch asked of the fold
   uint32_t *ttotal = nullptr;  // touch-reduce entry count (device)
-  uint32_t *arrive = nullptr;  // classify blocks done (the last one publishes the control block)
-  // a steady batch's fold left for the next one (tbl_fold_flush)
-  bool pend_on = false;
-  FoldSet pend;
-  uint32_t pend_bbits = 0, pend_L = 0;
   uint64_t ts_floor = UINT64_MAX;  // lower bound of min ts over live indices
   // the segment counters (miss_count .. reprobe_count) are known to be zero on
   // the device: the next segment needs no reset (vignat steady state)
@@ -201,11 +185,6 @@ struct Workspace {
   uint32_t *hist = nullptr, *hoff = nullptr;  // touch-reduce (chunk x span)
   uint64_t hist_cap = 0;
   uint32_t *bins_ent = nullptr, *bins_cnt = nullptr;  // touch bins (TouchBins)
-  // the second set of bins (a deferred fold's bins stay while the next batch
-  // fills these), and which set the next plan takes
-  uint32_t *bins_ent2 = nullptr, *bins_cnt2 = nullptr;
-  size_t bins_ent2_n = 0, bins_cnt2_n = 0;
-  uint32_t bins_buf = 0;
   uint32_t *ovf_q = nullptr, *ovf_cnt = nullptr;  // overflowed touches per block
   // owner mode: per-block slices of descriptors by owner rank, their counts
   // and send offsets, per-packet routes, the exchanged keys and replies

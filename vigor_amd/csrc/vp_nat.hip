@@ -164,11 +164,6 @@ struct NatArgs {
   // per block at its end, not by one global atomic per wave (a churn batch
   // has misses in every wave); null elsewhere
   uint32_t *mq;
-  // one GPU, touch bins: the launch's last block to finish publishes the
-  // control block to the host page (pub.pub null: off), so the fold need not
-  // run before the host learns phase A's counts (tbl_fold_read_ctl)
-  PubArgs pub;
-  uint32_t *arrive;  // blocks done (the last one resets it)
 };
 
 // The register path's total_length bound for 64-byte slots (every L4 byte in
@@ -1036,17 +1031,6 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
     for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) a.miss[mbase + i] = src[i];
   }
   route_publish(a, cur + kCurDest);
-  if (a.pub.pub) {  // the last block to finish publishes the control block
-    __syncthreads();  // (every wave's counter updates of this block are done)
-    if (threadIdx.x == 0) {
-      __threadfence();
-      if (atomicAdd(a.arrive, 1u) == gridDim.x - 1) {
-        __threadfence();  // (the other blocks' updates, released before their arrival)
-        *a.arrive = 0;
-        ctl_publish(a.pub);
-      }
-    }
-  }
 }
 
 __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_all,
@@ -1909,16 +1893,10 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
   t.ctl_clean = false;
   hostprof(1);
-  uint32_t cl_epoch = 0;  // the classify launch publishes the control block
   if (p1 > p0) {  // (the launch's own timestamps in ev0 / ev1)
     if (tiles64) {
       NatArgs a64 = a;
       if (bp.on) a64.log = nullptr;  // touches go to the bins only
-      if (bp.on && !c->comm) {
-        cl_epoch = ++t.pub_epoch;
-        a64.pub = PubArgs{t.d_pub, t.ctl, cl_epoch, nullptr, nullptr, 0, 0};
-        a64.arrive = t.arrive;
-      }
       if (c->ktime) {
         VP_HIP(launch_timed(tk, grid64, 256, c->stream, c->ev0, c->ev1, a64,
                             (uint32_t)b->n, bp.bins, rq));
@@ -1939,8 +1917,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // applied on top of it afterwards as late touches (tbl_late_touches: last
   // toucher still wins).
   hostprof(2);
-  VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, seq0, nullptr, cl_epoch,
-                           /*may_defer=*/true));
+  VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, seq0));
   hostprof(4);
   VP_HIP(ev_ms(c->ktime, c->ev0, c->ev1, &ph.ms));
   hostprof(5);

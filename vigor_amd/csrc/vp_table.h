@@ -257,17 +257,9 @@ int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
 // Multi-GPU: also gathers the ranks' segment counters (Workspace::h_gath;
 // owner mode: + this rank's `sends`, its key count per owner).
 int tbl_wait_pub(vp_ctx *c, FlowTable &t, uint32_t epoch);
-// cl_epoch != 0: the classify launch's last block published the control
-// block with that epoch (vp_nat.hip nat_tiles); then, one GPU, a batch whose
-// phase A left nothing behind (no misses, deferred WAN packets, reprobes or
-// overflowed bin slices) and whose time is affine may leave its fold to the
-// next batch's (may_defer: one pending fold per table; tbl_fold_flush).
 int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_t *log,
                       uint32_t p0, uint32_t p1, const NowSpec &now, uint64_t seq_base,
-                      const uint32_t *sends = nullptr, uint32_t cl_epoch = 0,
-                      bool may_defer = false);
-// The table's deferred fold, if any (before anything reads or writes stamps).
-int tbl_fold_flush(vp_ctx *c, FlowTable &t);
+                      const uint32_t *sends = nullptr);
 
 // Exact min ts over allocated indices -> t.ts_floor (~0 if none).
 int tbl_exact_floor(vp_ctx *c, FlowTable &t);

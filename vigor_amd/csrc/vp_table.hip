@@ -195,8 +195,6 @@ int tbl_alloc(vp_ctx *c, FlowTable &t, uint32_t cap) {
   memset(t.h_pub, 0, sizeof(CtlPub));
   VP_HIP(hipHostGetDevicePointer((void **)&t.d_pub, t.h_pub, 0));
   VP_TRY(dalloc(&t.ttotal, 1));
-  VP_TRY(dalloc(&t.arrive, 1));
-  VP_HIP(hipMemset(t.arrive, 0, sizeof(uint32_t)));
   VP_TRY(dalloc(&t.ekey, cap));
   VP_TRY(dalloc(&t.ekey2, cap));
   VP_TRY(dalloc(&t.eidx, cap));
@@ -217,7 +215,6 @@ void tbl_free(FlowTable &t) {
                   t.ekey2, t.eidx,    t.eidx2};
   for (void *p : ptrs) hipFree(p);
   hipFree(t.ttotal);
-  hipFree(t.arrive);
   hipFree(t.lin);
   hipFree(t.kv);
   if (t.h_pin) hipHostFree(t.h_pin);
@@ -817,19 +814,12 @@ int tbl_touch_reduce(vp_ctx *c, FlowTable &t, const uint32_t *log, uint32_t p0,
 // packet (one write while classifying, one read here).
 constexpr uint32_t kBinLocalMax = 16384;  // in-bin indices held in LDS
 
-// Up to two batches' bins in one launch (a deferred fold and the batch after
-// it): the LDS key of a touch is its batch in bit 31 above 1 + its position in
-// that batch's launch, so the later batch's touches win, as last toucher.
-struct FoldSets {
-  FoldSet s[2];
-  uint32_t n;
-};
-
 template <uint32_t kU>  // 64-entry chunks in flight per wave
-__global__ __launch_bounds__(1024) void touch_bins_reduce(FoldSets fs, uint32_t bbits,
-                                                          uint32_t L, uint32_t tcap,
-                                                          uint64_t *ts, uint64_t *tseq,
-                                                          PubArgs pub) {
+__global__ __launch_bounds__(1024) void touch_bins_reduce(
+    const uint32_t *ent, const uint32_t *cnt, uint32_t nsrc, uint32_t cap,
+    uint32_t pbits, uint32_t bbits, uint32_t range, uint32_t L, uint32_t tcap,
+    uint32_t p0, NowSpec now, uint64_t seq_base, uint64_t *ts, uint64_t *tseq,
+    PubArgs pub) {
   // 1 + position in the launch, 0 = none; L words of dynamic LDS (16 KB at
   // 1M flows: the 256 bin blocks spread over all CUs, where a 64 KB static
   // array let only two blocks share a CU and left half of them idle)
@@ -839,45 +829,40 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(FoldSets fs, uint32_t 
   for (uint32_t i = threadIdx.x; i < L; i += blockDim.x) last[i] = 0;
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  for (uint32_t si = 0; si < fs.n; si++) {
-    const FoldSet &S = fs.s[si];
-    const uint32_t *ent = S.ent, *cnt = S.cnt;
-    const uint32_t nsrc = S.nsrc, cap = S.cap, pbits = S.pbits, range = S.range;
-    const uint32_t pmask = (1u << pbits) - 1, tag = si << 31;
-    // wave w takes slices w, w + nw, ...; 64 of them per round, their sizes
-    // loaded by one instruction (lane l <-> slice w + l * nw). The round's
-    // slices are one list of 64-entry chunks (chunk t of the list belongs to
-    // the lane whose exclusive prefix of chunk counts covers t), read kU
-    // chunks at a time whatever the slices' lengths.
-    for (uint32_t r0 = threadIdx.x >> 6; r0 < nsrc; r0 += 64 * nw) {
-      const uint32_t my = r0 + lane * nw;
-      const uint32_t nv = my < nsrc ? cnt[(size_t)bin * nsrc + my] : 0;
-      const uint32_t ch = (nv + 63) >> 6;
-      uint32_t inc = ch;  // inclusive prefix over the wave
+  const uint32_t pmask = (1u << pbits) - 1;
+  // wave w takes slices w, w + nw, ...; 64 of them per round, their sizes
+  // loaded by one instruction (lane l <-> slice w + l * nw). The round's
+  // slices are one list of 64-entry chunks (chunk t of the list belongs to
+  // the lane whose exclusive prefix of chunk counts covers t), read kU chunks
+  // at a time whatever the slices' lengths.
+  for (uint32_t r0 = threadIdx.x >> 6; r0 < nsrc; r0 += 64 * nw) {
+    const uint32_t my = r0 + lane * nw;
+    const uint32_t nv = my < nsrc ? cnt[(size_t)bin * nsrc + my] : 0;
+    const uint32_t ch = (nv + 63) >> 6;
+    uint32_t inc = ch;  // inclusive prefix over the wave
 #pragma unroll
-      for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)inc, o);
-        if (lane >= o) inc += t;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const uint32_t t = (uint32_t)__shfl_up((int)inc, o);
+      if (lane >= o) inc += t;
+    }
+    const uint32_t exc = inc - ch;
+    const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
+    for (uint32_t t0 = 0; t0 < total; t0 += kU) {
+      uint32_t e[kU], lim[kU], base[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; u++) {
+        const uint32_t t = t0 + u;
+        const uint64_t own = __ballot(exc <= t && t < inc);  // (none past the list)
+        const uint32_t l = own ? (uint32_t)__ffsll((unsigned long long)own) - 1 : 0u;
+        const uint32_t k = (t - __builtin_amdgcn_readlane(exc, l)) << 6;
+        const uint32_t sb = r0 + l * nw;
+        lim[u] = own ? __builtin_amdgcn_readlane(nv, l) - k : 0u;
+        base[u] = sb * range + 1;
+        e[u] = lane < lim[u] ? ent[((size_t)bin * nsrc + sb) * cap + k + lane] : 0u;
       }
-      const uint32_t exc = inc - ch;
-      const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
-      for (uint32_t t0 = 0; t0 < total; t0 += kU) {
-        uint32_t e[kU], lim[kU], base[kU];
 #pragma unroll
-        for (uint32_t u = 0; u < kU; u++) {
-          const uint32_t t = t0 + u;
-          const uint64_t own = __ballot(exc <= t && t < inc);  // (none past the list)
-          const uint32_t l = own ? (uint32_t)__ffsll((unsigned long long)own) - 1 : 0u;
-          const uint32_t k = (t - __builtin_amdgcn_readlane(exc, l)) << 6;
-          const uint32_t sb = r0 + l * nw;
-          lim[u] = own ? __builtin_amdgcn_readlane(nv, l) - k : 0u;
-          base[u] = tag | (sb * range + 1);
-          e[u] = lane < lim[u] ? ent[((size_t)bin * nsrc + sb) * cap + k + lane] : 0u;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++)
-          if (lane < lim[u]) atomicMax(&last[e[u] >> pbits], base[u] + (e[u] & pmask));
-      }
+      for (uint32_t u = 0; u < kU; u++)
+        if (lane < lim[u]) atomicMax(&last[e[u] >> pbits], base[u] + (e[u] & pmask));
     }
   }
   __syncthreads();
@@ -885,10 +870,9 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(FoldSets fs, uint32_t 
     const uint32_t v = last[l];
     const uint32_t i = bin_index(bin, l, bbits);
     if (!v || i >= tcap) continue;
-    const FoldSet &S = fs.s[v >> 31];
-    const uint32_t p = S.p0 + (v & 0x7FFFFFFFu) - 1;
-    ts[i] = (uint64_t)(S.arr ? S.arr[p] : S.now0 + (int64_t)p * S.step);
-    tseq[i] = S.seq_base + p;
+    const uint32_t p = p0 + v - 1;
+    ts[i] = (uint64_t)now.at(p);
+    tseq[i] = seq_base + p;
   }
 }
 
@@ -924,90 +908,48 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   const uint32_t cap =
       std::max<uint32_t>(((2 * range / nbins + 32) + 15) & ~15u, 2 * kBinRun);
   const size_t ne = (size_t)grid * nbins * cap, nc = (size_t)grid * nbins;
-  // the set the fold of an earlier batch may still need is the other one
-  uint32_t **ent = w.bins_buf ? &w.bins_ent2 : &w.bins_ent;
-  uint32_t **cnt = w.bins_buf ? &w.bins_cnt2 : &w.bins_cnt;
-  size_t *ent_n = w.bins_buf ? &w.bins_ent2_n : &w.bins_ent_n;
-  size_t *cnt_n = w.bins_buf ? &w.bins_cnt2_n : &w.bins_cnt_n;
-  if (ne > *ent_n) {
+  if (ne > w.bins_ent_n) {
     VP_HIP(hipStreamSynchronize(c->stream));
-    hipFree(*ent);
-    *ent = nullptr;
-    *ent_n = 0;
-    VP_TRY(dalloc(ent, ne));
-    *ent_n = ne;
+    hipFree(w.bins_ent);
+    w.bins_ent = nullptr;
+    w.bins_ent_n = 0;
+    VP_TRY(dalloc(&w.bins_ent, ne));
+    w.bins_ent_n = ne;
   }
-  if (nc > *cnt_n) {
+  if (nc > w.bins_cnt_n) {
     VP_HIP(hipStreamSynchronize(c->stream));
-    hipFree(*cnt);
-    *cnt = nullptr;
-    *cnt_n = 0;
-    VP_TRY(dalloc(cnt, nc));
-    *cnt_n = nc;
+    hipFree(w.bins_cnt);
+    w.bins_cnt = nullptr;
+    w.bins_cnt_n = 0;
+    VP_TRY(dalloc(&w.bins_cnt, nc));
+    w.bins_cnt_n = nc;
   }
   plan->on = true;  // (the segment's counter reset clears touch_ovf)
   plan->grid = grid;
   plan->range = range;
   plan->L = L;
-  plan->bins = TouchBins{*ent, *cnt, &t.ctl->touch_ovf, w.ovf_q,
+  plan->bins = TouchBins{w.bins_ent, w.bins_cnt, &t.ctl->touch_ovf, w.ovf_q,
                          w.ovf_cnt, w.log, cap, pbits, bbits, grid};
-  return 0;
-}
-
-static FoldSet fold_set(const BinsPlan &plan, uint32_t p0, const NowSpec &now,
-                        uint64_t seq_base) {
-  FoldSet f;
-  f.ent = plan.bins.ent;
-  f.cnt = plan.bins.cnt;
-  f.nsrc = plan.grid;
-  f.cap = plan.bins.cap;
-  f.pbits = plan.bins.pbits;
-  f.range = plan.range;
-  f.p0 = p0;
-  f.arr = now.arr;
-  f.now0 = now.now0;
-  f.step = now.step;
-  f.seq_base = seq_base;
-  return f;
-}
-
-// The fold of `cur` (if any) and of the table's deferred batch (if any), in
-// one launch; the deferred one first (its touches are the earlier ones).
-static int bins_reduce_sets(vp_ctx *c, FlowTable &t, const FoldSet *cur, uint32_t bbits,
-                            uint32_t L, PubArgs pub) {
-  // chunks in flight per fold wave (VIGPATH_FOLD_U: 8, 16 or 32; 16 and 32
-  // measured no faster than 8, r03k, r04f)
-  static const uint32_t fold_u = [] {
-    const char *e = getenv("VIGPATH_FOLD_U");
-    const int v = e ? atoi(e) : 0;
-    return v == 16 || v == 32 ? (uint32_t)v : 8u;
-  }();
-  FoldSets fs{};
-  if (t.pend_on) {
-    fs.s[fs.n++] = t.pend;
-    bbits = t.pend_bbits;
-    L = t.pend_L;
-    t.pend_on = false;
-  }
-  if (cur) fs.s[fs.n++] = *cur;
-  if (!fs.n) return 0;
-  auto *fold = fold_u == 8 ? touch_bins_reduce<8> : fold_u == 32 ? touch_bins_reduce<32>
-                                                                 : touch_bins_reduce<16>;
-  fold<<<1u << bbits, 1024, 4u * L, c->stream>>>(fs, bbits, L, t.cap, t.ts, t.tseq, pub);
-  VP_HIP(hipGetLastError());
   return 0;
 }
 
 static int bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
                        const NowSpec &now, uint64_t seq_base, PubArgs pub) {
-  const FoldSet cur = fold_set(plan, p0, now, seq_base);
-  return bins_reduce_sets(c, t, &cur, plan.bins.bbits, plan.L, pub);
-}
-
-// A deferred fold, before anything reads or writes the stamps.
-int tbl_fold_flush(vp_ctx *c, FlowTable &t) {
-  if (!t.pend_on) return 0;
-  return bins_reduce_sets(c, t, nullptr, 0, 0, PubArgs{});
+  // chunks in flight per fold wave (VIGPATH_FOLD_U: 8, 16 or 32; 16 and 32
+  // measured no faster than 8, r03k)
+  static const uint32_t fold_u = [] {
+    const char *e = getenv("VIGPATH_FOLD_U");
+    const int v = e ? atoi(e) : 0;
+    return v == 16 || v == 32 ? (uint32_t)v : 8u;
+  }();
+  auto *fold = fold_u == 8 ? touch_bins_reduce<8> : fold_u == 32 ? touch_bins_reduce<32>
+                                                                 : touch_bins_reduce<16>;
+  fold<<<1u << plan.bins.bbits, 1024, 4u * plan.L, c->stream>>>(
+      plan.bins.ent, plan.bins.cnt, plan.grid, plan.bins.cap, plan.bins.pbits,
+      plan.bins.bbits, plan.range, plan.L, t.cap, p0, now, seq_base, t.ts, t.tseq,
+      pub);
+  VP_HIP(hipGetLastError());
+  return 0;
 }
 
 int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
@@ -1048,25 +990,9 @@ int tbl_wait_pub(vp_ctx *c, FlowTable &t, uint32_t epoch) {
 
 int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_t *log,
                       uint32_t p0, uint32_t p1, const NowSpec &now, uint64_t seq_base,
-                      const uint32_t *sends, uint32_t cl_epoch, bool may_defer) {
+                      const uint32_t *sends) {
   Workspace &w = c->ws;
   const uint32_t nr = c->comm ? (uint32_t)c->comm->n : 0u;
-  if (cl_epoch && bp.on && !nr) {  // the classify published the block
-    VP_TRY(tbl_wait_pub(c, t, cl_epoch));
-    const Ctl &h = t.h_ctl;
-    const bool steady = !h.miss_count && !h.defer_count && !h.touch_ovf && !h.reprobe_count;
-    const FoldSet cur = fold_set(bp, p0, now, seq_base);
-    if (steady && may_defer && !t.pend_on && !now.arr) {
-      t.pend = cur;  // folded with the next batch's bins, or flushed
-      t.pend_bbits = bp.bins.bbits;
-      t.pend_L = bp.L;
-      t.pend_on = true;
-      w.bins_buf ^= 1u;  // (the next plan fills the other set)
-      return 0;
-    }
-    return bins_reduce_sets(c, t, &cur, bp.bins.bbits, bp.L, PubArgs{});
-  }
-  VP_TRY(tbl_fold_flush(c, t));  // (a deferred fold goes first)
   const uint32_t ns = sends ? nr : 0u;
   w.gath_ok = false;
   if (nr) {
@@ -1443,7 +1369,6 @@ int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
       FlowTable &t = *tabs[i].t;
       const int64_t cut = tabs[i].cutoff(c, ta);
       if (cut <= (int64_t)lim(i)) continue;
-      VP_TRY(tbl_fold_flush(c, t));  // (stamps read below)
       VP_TRY(tbl_exact_floor(c, t));
       if (t.ts_floor != ~0ull && (int64_t)t.ts_floor < cut) {
         VP_TRY(tbl_expire(c, t, cut, nullptr));
@@ -1643,8 +1568,6 @@ static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
   c->last_launches = 0;
   for (float &x : c->stage_ms) x = 0.f;
   c->stage_n = 0;
-  for (int i = 0; i < ntabs; i++)  // (a fold deferred before the attach)
-    VP_TRY(tbl_fold_flush(c, *tabs[i].t));
   // 1. every rank's slice size, time range and floors (one small gather);
   //    errors are decided from the gathered data so all ranks agree
   RankInfo me{};
@@ -1812,7 +1735,6 @@ __global__ void dump_k(TableDev t, uint8_t *alloc, int64_t *ts, uint32_t *keys) 
 
 int tbl_dump(vp_ctx *c, FlowTable &t, uint8_t *alloc, int64_t *ts,
              uint32_t *keys) {
-  VP_TRY(tbl_fold_flush(c, t));
   const uint32_t cap = t.cap;
   uint8_t *d_alloc = nullptr;
   int64_t *d_ts = nullptr;
