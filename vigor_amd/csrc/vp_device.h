@@ -303,7 +303,14 @@ struct TouchBins {
   uint32_t *olog;  // olog[p] = index of an overflowed touch
   uint32_t cap, pbits, bbits;
   uint32_t nsrc;  // classify blocks (the launch's grid)
+  // run entries (runs != 0): a wave whose 64 packets touch the 64
+  // consecutive indices of one bin run records them as one word in its
+  // block's row of rtab ([block][bin], kept whole in the L2 as the block
+  // fills it), flagged in the bin's count (kBinRunFlag); one per block and bin
+  uint32_t *rtab;
+  uint32_t runs;
 };
+constexpr uint32_t kBinRunFlag = 0x80000000u;
 
 // Touch-log entry of packet p; `log` is null in the classify kernels that
 // bin their touches.
@@ -334,9 +341,28 @@ __device__ __forceinline__ void bins_put(const TouchBins &bins, uint32_t *cur,
                                          uint32_t rb, uint32_t range, uint32_t range0,
                                          uint32_t p, uint32_t touch) {
   if (!bins.ent) return;
+  if (bins.runs) {  // the whole wave one run of 64 indices: one word
+    const uint32_t lane = __lane_id();
+    const uint32_t t0 = __builtin_amdgcn_readfirstlane(touch);
+    const uint32_t q0 = __builtin_amdgcn_readfirstlane(p);
+    const bool in_run = t0 != kNone && (t0 & (kBinRun - 1)) == 0 && touch == t0 + lane &&
+                        p == q0 + lane;
+    if (__ballot(in_run) == ~0ull) {
+      const uint32_t b0 = bin_of(t0, bins.bbits);
+      uint32_t old = 0;
+      if (lane == 0) old = atomicOr(&cur[b0], kBinRunFlag);
+      if (!(__builtin_amdgcn_readfirstlane(old) & kBinRunFlag)) {
+        if (lane == 0)
+          bins.rtab[((size_t)rb << bins.bbits) + b0] =
+              ((bin_local(t0, bins.bbits) >> kBinRunBits) << 20) | (q0 - range0);
+        return;
+      }
+      // (the block's run slot of this bin is taken: the touches one by one)
+    }
+  }
   const bool v = touch != kNone;
   const uint32_t b = v ? bin_of(touch, bins.bbits) : 0;
-  const uint32_t k = group_reserve(cur, b, v);
+  const uint32_t k = group_reserve(cur, b, v) & ~kBinRunFlag;
   const bool fits = k < bins.cap;
   if (v && fits)
     bins.ent[((size_t)b * bins.nsrc + rb) * bins.cap + k] =
@@ -355,8 +381,8 @@ __device__ __forceinline__ void bins_publish(const TouchBins &bins, const uint32
                                              uint32_t rb) {
   if (!bins.ent) return;
   for (uint32_t b = threadIdx.x; b < (1u << bins.bbits); b += blockDim.x) {
-    const uint32_t c = cur[b];
-    bins.cnt[(size_t)b * bins.nsrc + rb] = c < bins.cap ? c : bins.cap;
+    const uint32_t c = cur[b] & ~kBinRunFlag;
+    bins.cnt[(size_t)b * bins.nsrc + rb] = (c < bins.cap ? c : bins.cap) | (cur[b] & kBinRunFlag);
   }
   if (threadIdx.x == 0) {
     const uint32_t o = cur[kOvf];

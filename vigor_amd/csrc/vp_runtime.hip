@@ -192,7 +192,7 @@ static void free_all(vp_ctx *c) {
     if (w.mb_ev_out[i]) hipEventDestroy(w.mb_ev_out[i]);
   }
   void *ptrs[] = {w.hist, w.hoff, w.cub_tmp, w.d_frames, w.d_len,    w.d_in,
-                  w.bins_ent, w.bins_cnt,
+                  w.bins_ent, w.bins_cnt, w.bins_rtab,
                   w.d_out,   w.d_now,    c->crc_tab, c->macw,
                   c->st_bk,  c->st_val,  c->be_rec,   c->cht,   c->dmacw,
                   w.sbuf,    w.rbuf,     c->pol_size, c->pol_time,

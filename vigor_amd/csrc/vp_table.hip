@@ -819,7 +819,7 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
     const uint32_t *ent, const uint32_t *cnt, uint32_t nsrc, uint32_t cap,
     uint32_t pbits, uint32_t bbits, uint32_t range, uint32_t L, uint32_t tcap,
     uint32_t p0, NowSpec now, uint64_t seq_base, uint64_t *ts, uint64_t *tseq,
-    PubArgs pub) {
+    PubArgs pub, const uint32_t *rtab) {
   // 1 + position in the launch, 0 = none; L words of dynamic LDS (16 KB at
   // 1M flows: the 256 bin blocks spread over all CUs, where a 64 KB static
   // array let only two blocks share a CU and left half of them idle)
@@ -837,7 +837,11 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
   // at a time whatever the slices' lengths.
   for (uint32_t r0 = threadIdx.x >> 6; r0 < nsrc; r0 += 64 * nw) {
     const uint32_t my = r0 + lane * nw;
-    const uint32_t nv = my < nsrc ? cnt[(size_t)bin * nsrc + my] : 0;
+    const uint32_t raw = my < nsrc ? cnt[(size_t)bin * nsrc + my] : 0;
+    const uint32_t nv = raw & ~kBinRunFlag;
+    // the slice's run word (one load per lane, all in flight together)
+    const bool run = (raw & kBinRunFlag) != 0;
+    const uint32_t re = run ? rtab[((size_t)my << bbits) + bin] : 0u;
     const uint32_t ch = (nv + 63) >> 6;
     uint32_t inc = ch;  // inclusive prefix over the wave
 #pragma unroll
@@ -863,6 +867,12 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
 #pragma unroll
       for (uint32_t u = 0; u < kU; u++)
         if (lane < lim[u]) atomicMax(&last[e[u] >> pbits], base[u] + (e[u] & pmask));
+    }
+    for (uint64_t m = __ballot(run); m; m &= m - 1) {  // a run: 64 touches, one per lane
+      const uint32_t l = (uint32_t)__ffsll((unsigned long long)m) - 1;
+      const uint32_t e = __builtin_amdgcn_readlane(re, l);
+      const uint32_t sb = r0 + l * nw;
+      atomicMax(&last[((e >> 20) << kBinRunBits) + lane], sb * range + 1 + (e & 0xFFFFFu) + lane);
     }
   }
   __syncthreads();
@@ -928,8 +938,23 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   plan->grid = grid;
   plan->range = range;
   plan->L = L;
+  // run words: one per block and bin, positions below 2^20 within a block
+  const size_t nr = (size_t)grid << bbits;
+  if (nr > w.bins_rtab_n) {
+    VP_HIP(hipStreamSynchronize(c->stream));
+    hipFree(w.bins_rtab);
+    w.bins_rtab = nullptr;
+    w.bins_rtab_n = 0;
+    VP_TRY(dalloc(&w.bins_rtab, nr));
+    w.bins_rtab_n = nr;
+  }
+  static const uint32_t runs_env = [] {  // (VIGPATH_BIN_RUNS=0: off, for A/B)
+    const char *e = getenv("VIGPATH_BIN_RUNS");
+    return e ? (uint32_t)atoi(e) : 1u;
+  }();
+  const uint32_t runs = runs_env && range <= (1u << 20) && (L >> kBinRunBits) < (1u << 12);
   plan->bins = TouchBins{w.bins_ent, w.bins_cnt, &t.ctl->touch_ovf, w.ovf_q,
-                         w.ovf_cnt, w.log, cap, pbits, bbits, grid};
+                         w.ovf_cnt, w.log, cap, pbits, bbits, grid, w.bins_rtab, runs};
   return 0;
 }
 
@@ -947,7 +972,7 @@ static int bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p
   fold<<<1u << plan.bins.bbits, 1024, 4u * plan.L, c->stream>>>(
       plan.bins.ent, plan.bins.cnt, plan.grid, plan.bins.cap, plan.bins.pbits,
       plan.bins.bbits, plan.range, plan.L, t.cap, p0, now, seq_base, t.ts, t.tseq,
-      pub);
+      pub, plan.bins.rtab);
   VP_HIP(hipGetLastError());
   return 0;
 }
