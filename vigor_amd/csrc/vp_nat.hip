@@ -593,7 +593,7 @@ __device__ __forceinline__ uint32_t dense128_tail(const uint4 d[8]) {
 // phase B or the reprobe walk are stored unchanged). Any other tile runs
 // nat_issue / nat_finish per lane. Owner mode's pass 1 has a lean tile of its
 // own (keys of other ranks routed, this rank's looked up).
-template <uint32_t G, uint32_t H = 1, bool D = false, bool X = false, bool P = false>
+template <uint32_t G, uint32_t H = 1, bool D = false, bool X = false>
 __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins bins,
                                           TileQueue rq) {
   static_assert(!X || G == 0, "header slots (X) are 64-byte slots");
@@ -676,21 +676,6 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   // (wide slots: the headers of the wave's own tile at its start; a prefetch
   // of the next tile's would keep 16 registers the tail sums need)
   if (G == 0 && tile < tend) fetch(tile);
-  // P (128-byte slots, two waves per SIMD): the next tile's 8 KiB is loaded
-  // into dn while this tile's rows are fetched and it is finished
-  uint4 dn[(D && P) ? 8 : 1];
-  auto fetch_dense = [&](uint32_t tl) {
-    const uint32_t tb = first + tl * 64;
-    const uint8_t *g8 = a.frames + (size_t)tb * 128u;
-    const uint32_t bytes = min(64u, n_all - tb) * 128u;
-#pragma unroll
-    for (uint32_t j = 0; j < ((D && P) ? 8u : 0u); j++)
-      dn[j] = buf_ld16(g8, bytes, (64 * j + lane) * 16);
-    const uint32_t pp = tb + lane;
-    m_in = pp < n_all ? a.in_dev[pp] : 0u;
-    m_len = pp < n_all ? a.len[pp] : 0u;
-  };
-  if (D && P && tile < tend) fetch_dense(tile);
   for (; tile < tend; tile += tstep) {
     const uint32_t tb = first + tile * 64;
     uint8_t *g8 = a.frames + (size_t)tb * slot;
@@ -701,17 +686,12 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       // 128-byte slots: the tile's 8 KiB as eight 1 KiB-contiguous loads,
       // header chunks (part < 4 of a slot) into the frame image, the tail
       // chunks summed from registers below (dense128_tail): one round trip
-      if constexpr (P) {
+      const uint32_t bytes = min(64u, n_all - tb) * 128u;
 #pragma unroll
-        for (uint32_t j = 0; j < 8; j++) d8[j] = dn[(D && P) ? j : 0];
-      } else {
-        const uint32_t bytes = min(64u, n_all - tb) * 128u;
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++) d8[j] = buf_ld16(g8, bytes, (64 * j + lane) * 16);
-        const uint32_t pp = tb + lane;
-        m_in = pp < n_all ? a.in_dev[pp] : 0u;
-        m_len = pp < n_all ? a.len[pp] : 0u;
-      }
+      for (uint32_t j = 0; j < 8; j++) d8[j] = buf_ld16(g8, bytes, (64 * j + lane) * 16);
+      const uint32_t pp = tb + lane;
+      m_in = pp < n_all ? a.in_dev[pp] : 0u;
+      m_len = pp < n_all ? a.len[pp] : 0u;
 #pragma unroll
       for (uint32_t j = 0; j < 8; j++)
         if ((lane & 7) < 4) S[chunk_swz(4 * (8 * j + (lane >> 3)) + (lane & 3))] = d8[j];
@@ -773,8 +753,6 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
         const uint32_t rw = __shfl(rowid, 16 * j + (lane >> 2));
         q[j] = rw != kNone ? rows[4 * (size_t)rw + (lane & 3)] : make_uint4(0, 0, 0, 0);
       }
-      if constexpr (D && P)
-        if (tile + tstep < tend) fetch_dense(tile + tstep);
       if constexpr (!D) tail = tile_tail_sums<G, H>(g8, slot, tbytes, end);
       reread();
       wave_lds_sync();
@@ -1084,24 +1062,13 @@ __global__ __launch_bounds__(256, 4) void nat_classify128(NatArgs a, uint32_t n_
                                                          TouchBins bins, TileQueue rq) {
   nat_tiles<4, 1, true>(a, n_all, bins, rq);
 }
-// ... with the next tile prefetched, two waves per SIMD (VIGPATH_128P=1)
-__global__ __launch_bounds__(256, 2) void nat_classify128p(NatArgs a, uint32_t n_all,
-                                                          TouchBins bins, TileQueue rq) {
-  nat_tiles<4, 1, true, false, true>(a, n_all, bins, rq);
-}
 
 // The classify kernel for a slot: 64 bytes, or the wide kernel whose G is the
 // tail's 16-byte chunks (slot - 64) / 16 rounded up to a power of two, at most 16.
 typedef void (*NatTileKernel)(NatArgs, uint32_t, TouchBins, TileQueue);
 static NatTileKernel nat_tile_kernel(uint32_t slot, bool hdr_tail = false) {
   if (slot == 64) return hdr_tail ? nat_classify64x : nat_classify64;
-  if (slot == 128) {
-    static const bool pf = [] {
-      const char *e = getenv("VIGPATH_128P");
-      return e && atoi(e);
-    }();
-    return pf ? nat_classify128p : nat_classify128;
-  }
+  if (slot == 128) return nat_classify128;
   const uint32_t nch = (slot - 64) / 16;
   if (nch <= 1) return nat_classify_wide<1>;
   if (nch <= 2) return nat_classify_wide<2>;
