@@ -839,9 +839,10 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
     const uint32_t my = r0 + lane * nw;
     const uint32_t raw = my < nsrc ? cnt[(size_t)bin * nsrc + my] : 0;
     const uint32_t nv = raw & ~kBinRunFlag;
-    // the slice's run word (one load per lane, all in flight together)
+    // the slice's run word, loaded beside the count (one round trip; a word
+    // whose flag is clear is stale and ignored)
+    const uint32_t re = my < nsrc ? rtab[((size_t)my << bbits) + bin] : 0u;
     const bool run = (raw & kBinRunFlag) != 0;
-    const uint32_t re = run ? rtab[((size_t)my << bbits) + bin] : 0u;
     const uint32_t ch = (nv + 63) >> 6;
     uint32_t inc = ch;  // inclusive prefix over the wave
 #pragma unroll
