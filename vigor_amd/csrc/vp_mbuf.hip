@@ -375,6 +375,169 @@ struct CtxTailGuard {
   }
 };
 
+static int mbuf_pipeline(vp_ctx *c, const vp_mbuf_batch *b) {
+  Workspace &w = c->ws;
+  CtxTailGuard guard{c};
+  const MbufPlan pl = mbuf_plan(c);
+  const uint32_t n = b->n;
+  // one device call per batch on a multi-GPU context (vp_process_device is a
+  // collective there), on whole-frame slots (owner mode has no header slots)
+  const bool one = c->comm != nullptr;
+  const bool header = pl.header && !one;
+  uint32_t ch = 1u << 20;
+  if (const char *e = getenv("VIGPATH_HOST_CHUNK")) ch = std::max(1, atoi(e));
+  if (one || ch > n) ch = std::max<uint32_t>(n, 1);
+  const uint32_t K = one ? 1 : (n + ch - 1) / ch;
+  constexpr uint32_t S = Workspace::kMbufSets;
+  VP_TRY(mbuf_reserve(c, ch));
+  const MapTab mt = map_tab(c);
+  const bool pin_ptr = host_pinned(b->frames), pin_len = host_pinned(b->len),
+             pin_in = host_pinned(b->in_dev), pin_out = host_pinned(b->out_dev),
+             pin_now = b->now && host_pinned(b->now);
+  const uint32_t G = mbuf_blocks();
+  auto cnt = [&](uint32_t k) { return std::min(ch, n - k * ch); };
+  auto hm = [&](uint32_t k, size_t at) { return w.h_mbmeta + (size_t)(k % S) * 22 * ch + at * ch; };
+  // a per-packet array's chunk k: the caller's page-locked memory itself, or
+  // a staged copy in the set's pinned block (`at`: offset in units of ch)
+  auto src = [&](const void *arr, bool pinned, size_t esz, size_t at, uint32_t k) {
+    const uint8_t *a = static_cast<const uint8_t *>(arr) + (size_t)k * ch * esz;
+    if (pinned) return a;
+    memcpy(hm(k, at), a, esz * cnt(k));
+    return static_cast<const uint8_t *>(hm(k, at));
+  };
+  auto hout = [&](uint32_t k) {
+    return pin_out ? b->out_dev + (size_t)k * ch : reinterpret_cast<uint16_t *>(hm(k, 20));
+  };
+  std::vector<uint32_t> wslot(K, 0);  // 0: header slots; else whole-frame slot bytes
+  std::vector<uint8_t> staged(K, 0);  // processed through the host (staged_range)
+  std::vector<uint8_t> retired(K, 0);
+  auto retire = [&](uint32_t k) -> int {
+    if (retired[k]) return 0;
+    retired[k] = 1;
+    if (staged[k]) return 0;
+    VP_HIP(hipEventSynchronize(w.mb_ev_out[k % S]));
+    if (!pin_out) memcpy(b->out_dev + (size_t)k * ch, hm(k, 20), 2ull * cnt(k));
+    return 0;
+  };
+  auto issue_gather = [&](uint32_t k) -> int {
+    const uint32_t i = k % S, m = cnt(k);
+    if (k >= S) VP_TRY(retire(k - S));  // frees the set's pinned staging
+    // the set's device buffers: free once chunk k - S's write-back read them
+    if (k >= S && !staged[k - S]) VP_HIP(hipStreamWaitEvent(w.cstream, w.mb_ev_out[i], 0));
+    VP_HIP(hipMemcpyAsync(w.mb_ptr + (size_t)i * ch, src(b->frames, pin_ptr, 8, 0, k), 8ull * m,
+                          hipMemcpyHostToDevice, w.cstream));
+    VP_HIP(hipMemcpyAsync(w.mb_len + (size_t)i * ch, src(b->len, pin_len, 2, 8, k), 2ull * m,
+                          hipMemcpyHostToDevice, w.cstream));
+    VP_HIP(hipMemcpyAsync(w.mb_in + (size_t)i * ch, src(b->in_dev, pin_in, 2, 10, k), 2ull * m,
+                          hipMemcpyHostToDevice, w.cstream));
+    if (b->now)
+      VP_HIP(hipMemcpyAsync(w.mb_now + (size_t)i * ch, src(b->now, pin_now, 8, 12, k), 8ull * m,
+                            hipMemcpyHostToDevice, w.cstream));
+    VP_HIP(hipMemsetAsync(w.mb_flags + i, 0, 4, w.cstream));
+    if (header && m) {
+      auto *kern = pl.tail ? mbuf_gather_hdr<true> : mbuf_gather_hdr<false>;
+      kern<<<std::min<uint32_t>(G, (m + 63) / 64), 256, 0, w.cstream>>>(
+          w.mb_ptr + (size_t)i * ch, w.mb_len + (size_t)i * ch, m, mt, pl.rule,
+          w.mb_slots + (size_t)i * ch * 64, w.mb_tail + (size_t)i * ch, w.mb_flags + i);
+      VP_HIP(hipGetLastError());
+    }
+    VP_HIP(hipMemcpyAsync(w.h_mbflags + i, w.mb_flags + i, 4, hipMemcpyDeviceToHost,
+                          w.cstream));
+    VP_HIP(hipEventRecord(w.mb_ev_in[i], w.cstream));
+    return 0;
+  };
+  int32_t last_full = -1;  // the last chunk on whole-frame slots (mb_full's user)
+  auto process = [&](uint32_t k) -> int {
+    const uint32_t i = k % S, m = cnt(k);
+    VP_HIP(event_poll(w.mb_ev_in[i]));
+    uint32_t fl = header ? w.h_mbflags[i] : kMbWhole;
+    vp_dev_batch db{};
+    db.n = m;
+    db.len = w.mb_len + (size_t)i * ch;
+    db.in_dev = w.mb_in + (size_t)i * ch;
+    db.now = b->now ? w.mb_now + (size_t)i * ch : nullptr;
+    db.now0 = b->now0 + (int64_t)k * ch * b->now_step;
+    db.now_step = b->now_step;
+    db.out_dev = w.mb_out + (size_t)i * ch;
+    VP_HIP(hipStreamWaitEvent(c->stream, w.mb_ev_in[i], 0));
+    if (fl & kMbWhole) {  // whole-frame slots: the chunk's longest frame
+      uint32_t maxlen = 64;
+      for (uint32_t j = 0; j < m; j++) maxlen = std::max<uint32_t>(maxlen, b->len[(size_t)k * ch + j]);
+      const uint32_t slot = (maxlen + 15) & ~15u;
+      if ((size_t)m * slot > w.mb_full_bytes) {
+        VP_HIP(hipDeviceSynchronize());
+        hipFree(w.mb_full);
+        w.mb_full = nullptr;
+        w.mb_full_bytes = 0;
+        VP_HIP(hipMalloc((void **)&w.mb_full, (size_t)std::max<uint32_t>(m, 1) * slot));
+        w.mb_full_bytes = (size_t)std::max<uint32_t>(m, 1) * slot;
+      } else if (last_full >= 0 && !staged[last_full]) {  // its write-back read mb_full
+        VP_HIP(hipStreamWaitEvent(c->stream, w.mb_ev_out[last_full % S], 0));
+      }
+      if (m) {
+        mbuf_gather_full<<<std::min<uint32_t>(G, (m + 63) / 64), 256, 0, c->stream>>>(
+            w.mb_ptr + (size_t)i * ch, db.len, m, mt, w.mb_full, slot, w.mb_flags + i);
+        VP_HIP(hipGetLastError());
+      }
+      if (!header) {  // (the header gather did not look: the unmapped flag now)
+        VP_HIP(hipMemcpyAsync(w.h_mbflags + i, w.mb_flags + i, 4, hipMemcpyDeviceToHost,
+                              c->stream));
+        VP_HIP(stream_wait(c->stream));
+        fl |= w.h_mbflags[i];
+      }
+      if (!(fl & kMbUnmapped)) {
+        db.frames = w.mb_full;
+        db.slot = slot;
+        wslot[k] = slot;
+        last_full = (int32_t)k;
+      }
+    } else {
+      db.frames = w.mb_slots + (size_t)i * ch * 64;
+      db.slot = 64;
+      c->hdr_tail = pl.tail ? w.mb_tail + (size_t)i * ch : nullptr;
+    }
+    if (fl & kMbUnmapped) {  // a frame outside the registered memory
+      c->hdr_tail = nullptr;
+      staged[k] = 1;
+      return staged_range(c, b, k * ch, m);
+    }
+    c->host_now = b->now ? b->now + (size_t)k * ch : nullptr;
+    const int rc = vp_process_device(c, &db, nullptr);
+    c->hdr_tail = nullptr;
+    c->host_now = nullptr;
+    VP_TRY(rc);
+    VP_HIP(hipEventRecord(w.mb_ev_done[i], c->stream));
+    return 0;
+  };
+  hipStream_t ws = w.dstream;  // (on the gather stream instead: 10-15 % slower, r04f)
+  auto issue_scatter = [&](uint32_t k) -> int {
+    if (staged[k]) return 0;
+    const uint32_t i = k % S, m = cnt(k);
+    VP_HIP(hipStreamWaitEvent(ws, w.mb_ev_done[i], 0));
+    const uint32_t wb = wslot[k] ? pl.wb_full : pl.wb_hdr;
+    if (wb && m) {
+      mbuf_scatter<<<std::min<uint32_t>(G, (m + 63) / 64), 256, 0, ws>>>(
+          w.mb_ptr + (size_t)i * ch, w.mb_len + (size_t)i * ch, w.mb_in + (size_t)i * ch,
+          w.mb_out + (size_t)i * ch, m, mt,
+          wslot[k] ? w.mb_full : w.mb_slots + (size_t)i * ch * 64, wslot[k] ? wslot[k] : 64,
+          wb);
+      VP_HIP(hipGetLastError());
+    }
+    VP_HIP(hipMemcpyAsync(hout(k), w.mb_out + (size_t)i * ch, 2ull * m, hipMemcpyDeviceToHost,
+                          ws));
+    VP_HIP(hipEventRecord(w.mb_ev_out[i], ws));
+    return 0;
+  };
+  for (uint32_t k = 0; k < std::min<uint32_t>(K, 2); k++) VP_TRY(issue_gather(k));
+  for (uint32_t k = 0; k < K; k++) {
+    if (k + 2 < K) VP_TRY(issue_gather(k + 2));
+    VP_TRY(process(k));
+    VP_TRY(issue_scatter(k));
+  }
+  for (uint32_t k = 0; k < K; k++) VP_TRY(retire(k));
+  return 0;
+}
+
 // ------------------------------------------------------ host-gather mode --
 // The same batch with the host's cores doing the scattered part: worker
 // threads copy every frame's first 64 bytes (and, for vignat, the raw sum of
@@ -489,220 +652,6 @@ static inline uint32_t host_gather_one(const uint8_t *f, uint32_t L, uint8_t *d,
     *tail = s;
   }
   return pl.rule == kRuleNoOpt && L > 64 && ip && ihl > 5 ? kMbWhole : 0u;
-}
-
-// The tail sum of one host frame of L bytes (host_gather_one's arithmetic)
-// without its header slot: 0 unless it is an IPv4 IHL-5 frame longer than 64.
-static inline uint32_t host_tail(const uint8_t *f, uint32_t L) {
-  if (L <= 64 || f[12] != 0x08 || f[13] != 0x00 || (f[14] & 0x0F) != 5) return 0;
-  const uint32_t end = std::min<uint32_t>(L, 14u + ((uint32_t)f[16] << 8 | f[17]));
-  uint32_t s = 0, o = 64;
-  for (; o + 1 < end; o += 2) s += (uint32_t)f[o] | (uint32_t)f[o + 1] << 8;
-  if (o < end) s += f[o];
-  return s;
-}
-
-static int mbuf_pipeline(vp_ctx *c, const vp_mbuf_batch *b) {
-  Workspace &w = c->ws;
-  CtxTailGuard guard{c};
-  const MbufPlan pl = mbuf_plan(c);
-  const uint32_t n = b->n;
-  // one device call per batch on a multi-GPU context (vp_process_device is a
-  // collective there), on whole-frame slots (owner mode has no header slots)
-  const bool one = c->comm != nullptr;
-  const bool header = pl.header && !one;
-  uint32_t ch = 1u << 20;
-  if (const char *e = getenv("VIGPATH_HOST_CHUNK")) ch = std::max(1, atoi(e));
-  if (one || ch > n) ch = std::max<uint32_t>(n, 1);
-  const uint32_t K = one ? 1 : (n + ch - 1) / ch;
-  constexpr uint32_t S = Workspace::kMbufSets;
-  VP_TRY(mbuf_reserve(c, ch));
-  const MapTab mt = map_tab(c);
-  const bool pin_ptr = host_pinned(b->frames), pin_len = host_pinned(b->len),
-             pin_in = host_pinned(b->in_dev), pin_out = host_pinned(b->out_dev),
-             pin_now = b->now && host_pinned(b->now);
-  const uint32_t G = mbuf_blocks();
-  // vignat's tail sums of frames longer than 64 bytes from the host's cores
-  // (the frames' bytes past 64 then never cross PCIe, and the GPU's read
-  // requests stay one per frame; VIGPATH_MBUF_TAILS=gpu: the gather kernel
-  // reads and sums them)
-  const char *te = getenv("VIGPATH_MBUF_TAILS");
-  const bool host_tails = header && pl.tail && !(te && !strcmp(te, "gpu"));
-  if (host_tails && ch > w.mb_hcap) {
-    VP_HIP(hipDeviceSynchronize());
-    if (w.h_mbslots) hipHostFree(w.h_mbslots);
-    if (w.h_mbtail) hipHostFree(w.h_mbtail);
-    w.h_mbslots = nullptr;
-    w.h_mbtail = nullptr;
-    w.mb_hcap = 0;
-    VP_HIP(hipHostMalloc((void **)&w.h_mbslots, 64ull * S * ch, hipHostMallocDefault));
-    VP_HIP(hipHostMalloc((void **)&w.h_mbtail, 4ull * S * ch, hipHostMallocDefault));
-    w.mb_hcap = ch;
-  }
-  auto cnt = [&](uint32_t k) { return std::min(ch, n - k * ch); };
-  auto hm = [&](uint32_t k, size_t at) { return w.h_mbmeta + (size_t)(k % S) * 22 * ch + at * ch; };
-  // a per-packet array's chunk k: the caller's page-locked memory itself, or
-  // a staged copy in the set's pinned block (`at`: offset in units of ch)
-  auto src = [&](const void *arr, bool pinned, size_t esz, size_t at, uint32_t k) {
-    const uint8_t *a = static_cast<const uint8_t *>(arr) + (size_t)k * ch * esz;
-    if (pinned) return a;
-    memcpy(hm(k, at), a, esz * cnt(k));
-    return static_cast<const uint8_t *>(hm(k, at));
-  };
-  auto hout = [&](uint32_t k) {
-    return pin_out ? b->out_dev + (size_t)k * ch : reinterpret_cast<uint16_t *>(hm(k, 20));
-  };
-  std::vector<uint32_t> wslot(K, 0);  // 0: header slots; else whole-frame slot bytes
-  std::vector<uint8_t> staged(K, 0);  // processed through the host (staged_range)
-  std::vector<uint8_t> retired(K, 0);
-  auto retire = [&](uint32_t k) -> int {
-    if (retired[k]) return 0;
-    retired[k] = 1;
-    if (staged[k]) return 0;
-    VP_HIP(hipEventSynchronize(w.mb_ev_out[k % S]));
-    if (!pin_out) memcpy(b->out_dev + (size_t)k * ch, hm(k, 20), 2ull * cnt(k));
-    return 0;
-  };
-  auto issue_gather = [&](uint32_t k) -> int {
-    const uint32_t i = k % S, m = cnt(k);
-    if (k >= S) VP_TRY(retire(k - S));  // frees the set's pinned staging
-    // the set's device buffers: free once chunk k - S's write-back read them
-    if (k >= S && !staged[k - S]) VP_HIP(hipStreamWaitEvent(w.cstream, w.mb_ev_out[i], 0));
-    VP_HIP(hipMemcpyAsync(w.mb_ptr + (size_t)i * ch, src(b->frames, pin_ptr, 8, 0, k), 8ull * m,
-                          hipMemcpyHostToDevice, w.cstream));
-    VP_HIP(hipMemcpyAsync(w.mb_len + (size_t)i * ch, src(b->len, pin_len, 2, 8, k), 2ull * m,
-                          hipMemcpyHostToDevice, w.cstream));
-    VP_HIP(hipMemcpyAsync(w.mb_in + (size_t)i * ch, src(b->in_dev, pin_in, 2, 10, k), 2ull * m,
-                          hipMemcpyHostToDevice, w.cstream));
-    if (b->now)
-      VP_HIP(hipMemcpyAsync(w.mb_now + (size_t)i * ch, src(b->now, pin_now, 8, 12, k), 8ull * m,
-                            hipMemcpyHostToDevice, w.cstream));
-    VP_HIP(hipMemsetAsync(w.mb_flags + i, 0, 4, w.cstream));
-    if (host_tails && m) {  // (the set's pinned tails: chunk k - S's copy is done)
-      uint32_t *ht = w.h_mbtail + (size_t)i * ch;
-      const uint32_t k0 = k * ch;
-      HostPool &hp = host_pool();
-      const uint32_t parts = 4 * hp.size();
-      std::atomic<uint32_t> any{0};
-      hp.run(parts, [&](uint32_t part) {
-        const uint32_t lo = (uint32_t)((uint64_t)m * part / parts),
-                       hi = (uint32_t)((uint64_t)m * (part + 1) / parts);
-        uint32_t long_ = 0;
-        for (uint32_t j = lo; j < hi; j++) {
-          const uint32_t L = b->len[k0 + j];
-          ht[j] = L > 64 ? host_tail(b->frames[k0 + j], L) : 0u;
-          long_ |= L > 64;
-        }
-        if (long_) any.store(1);
-      });
-      if (any.load())
-        VP_HIP(hipMemcpyAsync(w.mb_tail + (size_t)i * ch, ht, 4ull * m, hipMemcpyHostToDevice,
-                              w.cstream));
-      else
-        VP_HIP(hipMemsetAsync(w.mb_tail + (size_t)i * ch, 0, 4ull * m, w.cstream));
-    }
-    if (header && m) {
-      auto *kern = pl.tail && !host_tails ? mbuf_gather_hdr<true> : mbuf_gather_hdr<false>;
-      kern<<<std::min<uint32_t>(G, (m + 63) / 64), 256, 0, w.cstream>>>(
-          w.mb_ptr + (size_t)i * ch, w.mb_len + (size_t)i * ch, m, mt, pl.rule,
-          w.mb_slots + (size_t)i * ch * 64, w.mb_tail + (size_t)i * ch, w.mb_flags + i);
-      VP_HIP(hipGetLastError());
-    }
-    VP_HIP(hipMemcpyAsync(w.h_mbflags + i, w.mb_flags + i, 4, hipMemcpyDeviceToHost,
-                          w.cstream));
-    VP_HIP(hipEventRecord(w.mb_ev_in[i], w.cstream));
-    return 0;
-  };
-  int32_t last_full = -1;  // the last chunk on whole-frame slots (mb_full's user)
-  auto process = [&](uint32_t k) -> int {
-    const uint32_t i = k % S, m = cnt(k);
-    VP_HIP(event_poll(w.mb_ev_in[i]));
-    uint32_t fl = header ? w.h_mbflags[i] : kMbWhole;
-    vp_dev_batch db{};
-    db.n = m;
-    db.len = w.mb_len + (size_t)i * ch;
-    db.in_dev = w.mb_in + (size_t)i * ch;
-    db.now = b->now ? w.mb_now + (size_t)i * ch : nullptr;
-    db.now0 = b->now0 + (int64_t)k * ch * b->now_step;
-    db.now_step = b->now_step;
-    db.out_dev = w.mb_out + (size_t)i * ch;
-    VP_HIP(hipStreamWaitEvent(c->stream, w.mb_ev_in[i], 0));
-    if (fl & kMbWhole) {  // whole-frame slots: the chunk's longest frame
-      uint32_t maxlen = 64;
-      for (uint32_t j = 0; j < m; j++) maxlen = std::max<uint32_t>(maxlen, b->len[(size_t)k * ch + j]);
-      const uint32_t slot = (maxlen + 15) & ~15u;
-      if ((size_t)m * slot > w.mb_full_bytes) {
-        VP_HIP(hipDeviceSynchronize());
-        hipFree(w.mb_full);
-        w.mb_full = nullptr;
-        w.mb_full_bytes = 0;
-        VP_HIP(hipMalloc((void **)&w.mb_full, (size_t)std::max<uint32_t>(m, 1) * slot));
-        w.mb_full_bytes = (size_t)std::max<uint32_t>(m, 1) * slot;
-      } else if (last_full >= 0 && !staged[last_full]) {  // its write-back read mb_full
-        VP_HIP(hipStreamWaitEvent(c->stream, w.mb_ev_out[last_full % S], 0));
-      }
-      if (m) {
-        mbuf_gather_full<<<std::min<uint32_t>(G, (m + 63) / 64), 256, 0, c->stream>>>(
-            w.mb_ptr + (size_t)i * ch, db.len, m, mt, w.mb_full, slot, w.mb_flags + i);
-        VP_HIP(hipGetLastError());
-      }
-      if (!header) {  // (the header gather did not look: the unmapped flag now)
-        VP_HIP(hipMemcpyAsync(w.h_mbflags + i, w.mb_flags + i, 4, hipMemcpyDeviceToHost,
-                              c->stream));
-        VP_HIP(stream_wait(c->stream));
-        fl |= w.h_mbflags[i];
-      }
-      if (!(fl & kMbUnmapped)) {
-        db.frames = w.mb_full;
-        db.slot = slot;
-        wslot[k] = slot;
-        last_full = (int32_t)k;
-      }
-    } else {
-      db.frames = w.mb_slots + (size_t)i * ch * 64;
-      db.slot = 64;
-      c->hdr_tail = pl.tail ? w.mb_tail + (size_t)i * ch : nullptr;
-    }
-    if (fl & kMbUnmapped) {  // a frame outside the registered memory
-      c->hdr_tail = nullptr;
-      staged[k] = 1;
-      return staged_range(c, b, k * ch, m);
-    }
-    c->host_now = b->now ? b->now + (size_t)k * ch : nullptr;
-    const int rc = vp_process_device(c, &db, nullptr);
-    c->hdr_tail = nullptr;
-    c->host_now = nullptr;
-    VP_TRY(rc);
-    VP_HIP(hipEventRecord(w.mb_ev_done[i], c->stream));
-    return 0;
-  };
-  hipStream_t ws = w.dstream;  // (on the gather stream instead: 10-15 % slower, r04f)
-  auto issue_scatter = [&](uint32_t k) -> int {
-    if (staged[k]) return 0;
-    const uint32_t i = k % S, m = cnt(k);
-    VP_HIP(hipStreamWaitEvent(ws, w.mb_ev_done[i], 0));
-    const uint32_t wb = wslot[k] ? pl.wb_full : pl.wb_hdr;
-    if (wb && m) {
-      mbuf_scatter<<<std::min<uint32_t>(G, (m + 63) / 64), 256, 0, ws>>>(
-          w.mb_ptr + (size_t)i * ch, w.mb_len + (size_t)i * ch, w.mb_in + (size_t)i * ch,
-          w.mb_out + (size_t)i * ch, m, mt,
-          wslot[k] ? w.mb_full : w.mb_slots + (size_t)i * ch * 64, wslot[k] ? wslot[k] : 64,
-          wb);
-      VP_HIP(hipGetLastError());
-    }
-    VP_HIP(hipMemcpyAsync(hout(k), w.mb_out + (size_t)i * ch, 2ull * m, hipMemcpyDeviceToHost,
-                          ws));
-    VP_HIP(hipEventRecord(w.mb_ev_out[i], ws));
-    return 0;
-  };
-  for (uint32_t k = 0; k < std::min<uint32_t>(K, 2); k++) VP_TRY(issue_gather(k));
-  for (uint32_t k = 0; k < K; k++) {
-    if (k + 2 < K) VP_TRY(issue_gather(k + 2));
-    VP_TRY(process(k));
-    VP_TRY(issue_scatter(k));
-  }
-  for (uint32_t k = 0; k < K; k++) VP_TRY(retire(k));
-  return 0;
 }
 
 static int mbuf_host_pipeline(vp_ctx *c, const vp_mbuf_batch *b, const MbufPlan &pl) {
