@@ -1378,9 +1378,25 @@ __global__ __launch_bounds__(256, 4) void nat_own_probe(TableDev t, const uint32
   auto load = [&](uint32_t tl) {
     Tile x{false, make_uint4(0, 0, 0, 0)};
     if (tl < tend) {
-      const uint32_t j = tl * 64 + lane;
-      x.act = valid_at(j);
-      if (x.act) x.k = (own(j) ? own_keys + j : keys + j)[0];
+      const uint32_t j0 = tl * 64, j = j0 + lane;
+      if (cap && (cap & 63) == 0) {
+        // the tile's peer and slice, once per tile (scalar): with chunks and
+        // slices of whole tiles a tile lies in one slice
+        const uint32_t q = j0 / cap, l0 = j0 - q * cap;
+        const uint32_t *row = rcnt + (size_t)q * kSliceRow;
+        const uint32_t sub = row[1];
+        if ((sub & 63) == 0) {
+          const uint32_t b = l0 / sub, k0 = l0 - b * sub;
+          const uint32_t c = b < row[0] ? row[2 + b] : 0u;
+          x.act = j < n && k0 + lane < c;
+        } else {
+          x.act = valid_at(j);
+        }
+        if (x.act) x.k = (q == self ? own_keys + j : keys + j)[0];
+      } else {
+        x.act = valid_at(j);
+        if (x.act) x.k = (own(j) ? own_keys + j : keys + j)[0];
+      }
     }
     return x;
   };
