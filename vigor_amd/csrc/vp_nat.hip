@@ -1949,7 +1949,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     VP_HIP(hipGetLastError());
     VP_TRY(tbl_reprobe_stamp(c, t, w.reprobe, rcnt, nre, range, nblk, w.log, now,
                              seq0));
-    VP_TRY(tbl_read_ctl_pub(c, t));  // the walk may have found new flows
+    VP_TRY(read_ctl(c, t));  // the walk may have found new flows
   }
   const bool ovf = bp.on && t.h_ctl.touch_ovf != 0;
   if (ovf)  // touches that found their bin slice full, logged alone

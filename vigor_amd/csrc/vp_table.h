@@ -257,9 +257,6 @@ int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
 // Multi-GPU: also gathers the ranks' segment counters (Workspace::h_gath;
 // owner mode: + this rank's `sends`, its key count per owner).
 int tbl_wait_pub(vp_ctx *c, FlowTable &t, uint32_t epoch);
-// t.h_ctl as of the work enqueued so far, published by a one-thread launch
-// (read_ctl's result without a copy launch or a stream query).
-int tbl_read_ctl_pub(vp_ctx *c, FlowTable &t);
 int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_t *log,
                       uint32_t p0, uint32_t p1, const NowSpec &now, uint64_t seq_base,
                       const uint32_t *sends = nullptr);

@@ -996,21 +996,6 @@ int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
 // block, and owner mode adds this rank's key count per owner (`sends`): the
 // host learns all of it with the one wait it makes anyway (union_sizes,
 // DESIGN.md §6).
-// One thread publishes the control block as of the work enqueued so far.
-__global__ void ctl_publish_k(PubArgs pub) {
-  if (threadIdx.x == 0) ctl_publish(pub);
-}
-
-// The control block behind the work enqueued so far, published into the
-// host page by a one-thread launch and polled (no copy launch, no stream
-// query): the reprobe walk's counts in a steady random-key step.
-int tbl_read_ctl_pub(vp_ctx *c, FlowTable &t) {
-  const uint32_t epoch = ++t.pub_epoch;
-  ctl_publish_k<<<1, 64, 0, c->stream>>>(PubArgs{t.d_pub, t.ctl, epoch, nullptr, nullptr, 0, 0});
-  VP_HIP(hipGetLastError());
-  return tbl_wait_pub(c, t, epoch);
-}
-
 // Wait for the control block a kernel published with `epoch` (ctl_publish)
 // and copy it to t.h_ctl; a stream that ends (or fails) without it is an
 // error.
