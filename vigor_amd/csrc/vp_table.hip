@@ -823,10 +823,15 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
   // 1 + position in the launch, 0 = none; L words of dynamic LDS (16 KB at
   // 1M flows: the 256 bin blocks spread over all CUs, where a 64 KB static
   // array let only two blocks share a CU and left half of them idle)
+  // Behind it, one word per 64-index group of the bin: the largest base
+  // (1 + position of lane 0) of the run words that cover the group, so a run
+  // costs one lane's atomic instead of 64 (its lane j touched index 64 g + j
+  // at base + j, the same winner for all 64).
   extern __shared__ uint32_t last[];
+  uint32_t *grp = last + L;
   const uint32_t bin = blockIdx.x;
   if (bin == 0 && threadIdx.x == 0) ctl_publish(pub);
-  for (uint32_t i = threadIdx.x; i < L; i += blockDim.x) last[i] = 0;
+  for (uint32_t i = threadIdx.x; i < L + (L >> kBinRunBits); i += blockDim.x) last[i] = 0;
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const uint32_t pmask = (1u << pbits) - 1;
@@ -869,16 +874,12 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
       for (uint32_t u = 0; u < kU; u++)
         if (lane < lim[u]) atomicMax(&last[e[u] >> pbits], base[u] + (e[u] & pmask));
     }
-    for (uint64_t m = __ballot(run); m; m &= m - 1) {  // a run: 64 touches, one per lane
-      const uint32_t l = (uint32_t)__ffsll((unsigned long long)m) - 1;
-      const uint32_t e = __builtin_amdgcn_readlane(re, l);
-      const uint32_t sb = r0 + l * nw;
-      atomicMax(&last[((e >> 20) << kBinRunBits) + lane], sb * range + 1 + (e & 0xFFFFFu) + lane);
-    }
+    if (run) atomicMax(&grp[re >> 20], my * range + 1 + (re & 0xFFFFFu));
   }
   __syncthreads();
   for (uint32_t l = threadIdx.x; l < L; l += blockDim.x) {
-    const uint32_t v = last[l];
+    const uint32_t g = grp[l >> kBinRunBits];
+    const uint32_t v = max(last[l], g ? g + (l & (kBinRun - 1)) : 0u);
     const uint32_t i = bin_index(bin, l, bbits);
     if (!v || i >= tcap) continue;
     const uint32_t p = p0 + v - 1;
@@ -970,7 +971,7 @@ static int bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p
   }();
   auto *fold = fold_u == 8 ? touch_bins_reduce<8> : fold_u == 32 ? touch_bins_reduce<32>
                                                                  : touch_bins_reduce<16>;
-  fold<<<1u << plan.bins.bbits, 1024, 4u * plan.L, c->stream>>>(
+  fold<<<1u << plan.bins.bbits, 1024, 4u * (plan.L + (plan.L >> kBinRunBits)), c->stream>>>(
       plan.bins.ent, plan.bins.cnt, plan.grid, plan.bins.cap, plan.bins.pbits,
       plan.bins.bbits, plan.range, plan.L, t.cap, p0, now, seq_base, t.ts, t.tseq,
       pub, plan.bins.rtab);
