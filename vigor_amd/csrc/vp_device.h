@@ -192,14 +192,6 @@ __device__ __forceinline__ void tile_st(uint4 *g, uint32_t c, uint4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)(c * 16), 0, 16);
 }
 
-// A packet's u16 out-port at out[p], written through (sc1, as tile_st) so
-// the port array does not sit dirty in the L2s for the kernel's end to
-// write back. `out` is uniform (one buffer resource in scalar registers).
-__device__ __forceinline__ void out_st16(uint16_t *out, uint32_t p, uint32_t v) {
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7FFFFFFF, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, rs, (int)(2 * p), 0, 16);
-}
-
 // Stores of the wide-slot classify tiles: 16 bytes at byte `off` of the tile
 // at g (64 slots, `bytes` in all), write-through like tile_st.
 __device__ __forceinline__ void tile_st_at(uint8_t *g, uint32_t bytes, uint32_t off,

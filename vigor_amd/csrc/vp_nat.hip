@@ -883,7 +883,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
         f.w[0] = a.wan_macw0;
         f.w[1] = a.wan_macw1;
         f.w[2] = a.wan_macw2;
-        out_st16(a.out, p, a.wan);
+        a.out[p] = (uint16_t)a.wan;
       }
       store_all = true;
     } else if (lean_own && __ballot(mine && nat_lan_fast_ok(a, f, in, ln)) == ~0ull) {
