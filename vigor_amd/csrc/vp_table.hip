@@ -905,7 +905,12 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   const uint32_t per_b = (tiles + grid - 1) / grid;
   const uint32_t range = per_b * 64;
   // the fewest bins (>= 256) whose in-bin index range fits the fold's LDS
-  uint32_t bbits = 8;
+  static const uint32_t bbits_min = [] {  // (VIGPATH_BIN_BITS: more bins, for A/B)
+    const char *e = getenv("VIGPATH_BIN_BITS");
+    const int v = e ? atoi(e) : 8;
+    return v >= 8 && v <= 10 ? (uint32_t)v : 8u;
+  }();
+  uint32_t bbits = bbits_min;
   auto in_bin = [&](uint32_t bb) {  // in-bin index range for 2^bb bins
     return (((uint64_t)t.cap + ((uint64_t)kBinRun << bb) - 1) >> (kBinRunBits + bb))
            << kBinRunBits;
