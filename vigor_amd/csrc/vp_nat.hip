@@ -866,14 +866,18 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
       bool done;
       uint32_t idx = bucket_match_sel(row, key, &done);
-      if (__ballot(!done)) {  // a full home bucket: the next one, in the lane
-        // (the walk's second step, tbl_probe_from; random keys leave ~0.2 %
-        // of their packets here every batch, whose reprobe launch and
-        // control-block read-back this spares)
-        if (!done) {
-          const uint4 *q = rows + 4 * (size_t)((b + 1) & a.t.bmask);
-          const uint4 r2[4] = {q[0], q[1], q[2], q[3]};
-          idx = bucket_match_sel(r2, key, &done);
+      if (__ballot(!done)) {  // a full home bucket: the walk on, in the lane
+        // (tbl_probe_from; random keys leave ~0.2 % of their packets here
+        // every batch, whose reprobe launch and control-block read-back this
+        // spares; the loop is wave-uniform, a lane past its end queues)
+        uint32_t nb = b;
+        for (uint32_t st = 0; st < a.t.bmask && __ballot(!done); st++) {
+          if (!done) {
+            nb = (nb + 1) & a.t.bmask;
+            const uint4 *q = rows + 4 * (size_t)nb;
+            const uint4 r2[4] = {q[0], q[1], q[2], q[3]};
+            idx = bucket_match_sel(r2, key, &done);
+          }
         }
       }
       const bool hit = done & (idx != kNone);
