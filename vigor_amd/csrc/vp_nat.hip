@@ -1124,6 +1124,55 @@ __device__ __forceinline__ bool nat_slot_regs(const NatArgs &a, uint32_t p, RFra
   return true;
 }
 
+// The first 64 bytes of the 64-byte slots of the wave's lanes' packets
+// (p == kNone: zeros), four lanes per frame, so each load instruction reads
+// 16 frames of 64 contiguous bytes instead of 64 scattered 16-byte pieces;
+// the wave's LDS tile S hands each lane its frame (the tiles' layout, chunk
+// c = part c % 4 of the frame of lane c / 4). Wave-uniform call.
+__device__ __forceinline__ void gather_slots64(const uint8_t *frames, uint32_t p, uint4 *S,
+                                               RFrame &f) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint4 q[4];
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t ps = (uint32_t)__shfl((int)p, (int)(16 * j + (lane >> 2)));
+    q[j] = ps != kNone ? reinterpret_cast<const uint4 *>(frames + (size_t)ps * 64)[lane & 3]
+                       : make_uint4(0, 0, 0, 0);
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = q[j];
+  wave_lds_sync();
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) {
+    const uint4 v = S[chunk_swz(4 * lane + k)];
+    f.w[4 * k] = v.x;
+    f.w[4 * k + 1] = v.y;
+    f.w[4 * k + 2] = v.z;
+    f.w[4 * k + 3] = v.w;
+  }
+}
+// ... and back: the frames of the lanes with `st` stored whole, four lanes
+// per frame (wave-uniform call).
+__device__ __forceinline__ void scatter_slots64(uint8_t *frames, uint32_t p, bool st, uint4 *S,
+                                                const RFrame &f) {
+  const uint32_t lane = threadIdx.x & 63;
+  wave_lds_sync();
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++)
+    S[chunk_swz(4 * lane + k)] =
+        make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
+  wave_lds_sync();
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t src = 16 * j + (lane >> 2);
+    const uint32_t ps = (uint32_t)__shfl((int)p, (int)src);
+    const bool ok = __shfl((int)st, (int)src) != 0;
+    if (ok) reinterpret_cast<uint4 *>(frames + (size_t)ps * 64)[lane & 3] = S[chunk_swz(64 * j + lane)];
+  }
+  wave_lds_sync();
+}
+
 // FlowId keys and hashes of the queued misses (frames still unmodified):
 // register frames with the tile kernels' field reads and the batched hash
 // from the LDS tables, the generic byte path for any other frame.
@@ -1131,14 +1180,28 @@ __global__ __launch_bounds__(256) void nat_miss_keys(NatArgs a, const uint32_t *
                                                      uint32_t n, uint32_t *mkey,
                                                      uint32_t *mhash) {
   __shared__ uint32_t T[kNatTabWords];
+  __shared__ uint4 stage[4][256];
   load_nat_tables(T, a);
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
-       j += gridDim.x * blockDim.x) {
-    const uint32_t p = list[j];
-    const uint32_t in = a.in_dev[p], len = a.len[p];
-    uint32_t proto, sp, dp, sip, dip;
+  uint4 *S = stage[threadIdx.x >> 6];
+  const uint32_t lane = threadIdx.x & 63;
+  // (the loop is wave-uniform: the 64-byte-slot gather is cooperative)
+  for (uint32_t j0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); j0 < n;
+       j0 += gridDim.x * blockDim.x) {
+    const uint32_t j = j0 + lane;
+    const bool v = j < n;
+    const uint32_t p = v ? list[j] : kNone;
+    const uint32_t in = v ? a.in_dev[p] : 0u, len = v ? a.len[p] : 0u;
     RFrame r;
-    if (nat_slot_regs(a, p, r) && nat_reg_ok(r, len, 0xFFFFu)) {
+    bool reg;
+    if (a.slot == 64) {
+      gather_slots64(a.frames, p, S, r);
+      reg = true;
+    } else {
+      reg = v && nat_slot_regs(a, p, r);
+    }
+    if (!v) continue;
+    uint32_t proto, sp, dp, sip, dip;
+    if (reg && nat_reg_ok(r, len, 0xFFFFu)) {
       proto = r.w[5] >> 24;
       sp = r.w[8] >> 16;
       dp = r.w[9] & 0xFFFF;
@@ -1172,39 +1235,46 @@ __device__ void nat_write_lan(const NatArgs &a, uint32_t p, uint32_t idx) {
 
 // Every miss: the index its first sighting got (or drop: table full). A
 // register-path frame of a 64-byte slot is rewritten as the tile kernels
-// rewrite a hit (four 16-byte loads and stores); any other takes the byte
-// path.
+// rewrite a hit (gathered and stored four lanes per frame); any other takes
+// the byte path.
 __global__ __launch_bounds__(256) void nat_miss_finish(NatArgs a, const uint32_t *list,
                                                        uint32_t n, const uint32_t *scratch,
                                                        const uint32_t *rep,
                                                        const uint32_t *assign) {
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
-       j += gridDim.x * blockDim.x) {
-    const uint32_t p = list[j];
-    const uint32_t idx = assign[scratch[rep[j]]];
-    a.log[p] = idx;
-    if (idx == kNone) {  // nat_main.c:87-91
-      a.out[p] = a.in_dev[p];
-      continue;
+  __shared__ uint4 stage[4][256];
+  uint4 *S = stage[threadIdx.x >> 6];
+  const uint32_t lane = threadIdx.x & 63;
+  // (the loop is wave-uniform: the 64-byte-slot gather and store are
+  // cooperative)
+  for (uint32_t j0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); j0 < n;
+       j0 += gridDim.x * blockDim.x) {
+    const uint32_t j = j0 + lane;
+    const bool v = j < n;
+    const uint32_t p = v ? list[j] : kNone;
+    const uint32_t idx = v ? assign[scratch[rep[j]]] : kNone;
+    if (v) {
+      a.log[p] = idx;
+      if (idx == kNone) a.out[p] = a.in_dev[p];  // nat_main.c:87-91
     }
-    RFrame f;
-    if (a.slot == 64 && nat_slot_regs(a, p, f) &&
-        nat_lan_fast_ok(a, f, a.in_dev[p], a.len[p], nat_lim64(a))) {
-      const uint32_t proto = f.w[5] >> 24;
-      f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
-      f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
-      fast_checksums(f, proto, bswap16((uint16_t)(f.w[4] & 0xFFFF)), nat_tail(a, p));
-      f.w[0] = a.wan_macw0;
-      f.w[1] = a.wan_macw1;
-      f.w[2] = a.wan_macw2;
-      uint4 *fp = reinterpret_cast<uint4 *>(a.frames + (size_t)p * 64);
-#pragma unroll
-      for (uint32_t k = 0; k < 4; k++)
-        fp[k] = make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
-      a.out[p] = a.wan;
-      continue;
+    const bool live = v && idx != kNone;
+    bool fast = false;
+    if (a.slot == 64) {
+      RFrame f;
+      gather_slots64(a.frames, live ? p : kNone, S, f);
+      fast = live && nat_lan_fast_ok(a, f, a.in_dev[p], a.len[p], nat_lim64(a));
+      if (fast) {
+        const uint32_t proto = f.w[5] >> 24;
+        f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
+        f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
+        fast_checksums(f, proto, bswap16((uint16_t)(f.w[4] & 0xFFFF)), nat_tail(a, p));
+        f.w[0] = a.wan_macw0;
+        f.w[1] = a.wan_macw1;
+        f.w[2] = a.wan_macw2;
+        a.out[p] = a.wan;
+      }
+      scatter_slots64(a.frames, p, fast, S, f);
     }
-    nat_write_lan(a, p, idx);
+    if (live && !fast) nat_write_lan(a, p, idx);
   }
 }
 
