@@ -346,7 +346,7 @@ static int bridge_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // the classify launch bins its touches when it can (TouchBins; no touch
   // log then), else logs them and the log is folded
   BinsPlan bp{};
-  VP_TRY(tbl_bins_plan(c, t, (const void *)bridge_classify, p0, p1, &bp));
+  VP_TRY(tbl_bins_plan(c, t, (const void *)bridge_classify, p0, p1, &bp, 4, 8));
   const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
   const uint32_t grid = bp.on ? bp.grid : resident_grid((const void *)bridge_classify,
                                                         (tiles + 3) / 4);

@@ -305,12 +305,15 @@ struct TouchBins {
   uint32_t nsrc;  // classify blocks (the launch's grid)
   // run entries (runs != 0): a wave whose 64 packets touch the 64
   // consecutive indices of one bin run records them as one word in its
-  // block's row of rtab ([block][bin], kept whole in the L2 as the block
-  // fills it), flagged in the bin's count (kBinRunFlag); one per block and bin
+  // block's row of rtab ([block][bin][2], kept whole in the L2 as the block
+  // fills it), flagged in the bin's count (kBinRunFlag, kBinRunFlag2); two
+  // per block and bin
   uint32_t *rtab;
   uint32_t runs;
 };
-constexpr uint32_t kBinRunFlag = 0x80000000u;
+constexpr uint32_t kBinRunFlag = 0x80000000u;   // run word 0 of the block's bin
+constexpr uint32_t kBinRunFlag2 = 0x40000000u;  // run word 1
+constexpr uint32_t kBinRunFlags = kBinRunFlag | kBinRunFlag2;
 
 // Touch-log entry of packet p; `log` is null in the classify kernels that
 // bin their touches.
@@ -349,20 +352,26 @@ __device__ __forceinline__ void bins_put(const TouchBins &bins, uint32_t *cur,
                         p == q0 + lane;
     if (__ballot(in_run) == ~0ull) {
       const uint32_t b0 = bin_of(t0, bins.bbits);
-      uint32_t old = 0;
-      if (lane == 0) old = atomicOr(&cur[b0], kBinRunFlag);
-      if (!(__builtin_amdgcn_readfirstlane(old) & kBinRunFlag)) {
+      uint32_t slot = 2;
+      if (lane == 0) {
+        if (!(atomicOr(&cur[b0], kBinRunFlag) & kBinRunFlag))
+          slot = 0;
+        else if (!(atomicOr(&cur[b0], kBinRunFlag2) & kBinRunFlag2))
+          slot = 1;
+      }
+      slot = __builtin_amdgcn_readfirstlane(slot);
+      if (slot < 2) {
         if (lane == 0)
-          bins.rtab[((size_t)rb << bins.bbits) + b0] =
+          bins.rtab[((((size_t)rb << bins.bbits) + b0) << 1) + slot] =
               ((bin_local(t0, bins.bbits) >> kBinRunBits) << 20) | (q0 - range0);
         return;
       }
-      // (the block's run slot of this bin is taken: the touches one by one)
+      // (the block's run slots of this bin are taken: the touches one by one)
     }
   }
   const bool v = touch != kNone;
   const uint32_t b = v ? bin_of(touch, bins.bbits) : 0;
-  const uint32_t k = group_reserve(cur, b, v) & ~kBinRunFlag;
+  const uint32_t k = group_reserve(cur, b, v) & ~kBinRunFlags;
   const bool fits = k < bins.cap;
   if (v && fits)
     bins.ent[((size_t)b * bins.nsrc + rb) * bins.cap + k] =
@@ -381,8 +390,8 @@ __device__ __forceinline__ void bins_publish(const TouchBins &bins, const uint32
                                              uint32_t rb) {
   if (!bins.ent) return;
   for (uint32_t b = threadIdx.x; b < (1u << bins.bbits); b += blockDim.x) {
-    const uint32_t c = cur[b] & ~kBinRunFlag;
-    bins.cnt[(size_t)b * bins.nsrc + rb] = (c < bins.cap ? c : bins.cap) | (cur[b] & kBinRunFlag);
+    const uint32_t c = cur[b] & ~kBinRunFlags;
+    bins.cnt[(size_t)b * bins.nsrc + rb] = (c < bins.cap ? c : bins.cap) | (cur[b] & kBinRunFlags);
   }
   if (threadIdx.x == 0) {
     const uint32_t o = cur[kOvf];

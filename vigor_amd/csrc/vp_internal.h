@@ -185,7 +185,7 @@ struct Workspace {
   uint32_t *hist = nullptr, *hoff = nullptr;  // touch-reduce (chunk x span)
   uint64_t hist_cap = 0;
   uint32_t *bins_ent = nullptr, *bins_cnt = nullptr;  // touch bins (TouchBins)
-  uint32_t *bins_rtab = nullptr;  // their run words ([block][bin])
+  uint32_t *bins_rtab = nullptr;  // their run words ([block][bin][2])
   size_t bins_rtab_n = 0;
   uint32_t *ovf_q = nullptr, *ovf_cnt = nullptr;  // overflowed touches per block
   // owner mode: per-block slices of descriptors by owner rank, their counts

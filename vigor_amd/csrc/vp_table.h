@@ -231,10 +231,13 @@ int tbl_touch_reduce(vp_ctx *c, FlowTable &t, const uint32_t *log, uint32_t p0,
 struct BinsPlan {
   bool on;
   uint32_t grid, range, L;
+  uint32_t sbits;  // 2^sbits fold blocks per bin, each L >> sbits indices
   TouchBins bins;
 };
+// min_bits: at least 2^min_bits bins (vigbridge keeps 256: measured 1.7 %
+// slower at 128, tools/sessions/gpu_r04bc.sh).
 int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
-                  uint32_t p1, BinsPlan *plan, uint32_t waves = 4);
+                  uint32_t p1, BinsPlan *plan, uint32_t waves = 4, uint32_t min_bits = 0);
 // ts of the indices the reprobe kernels touched (after their tseq atomicMax;
 // the queue as in reprobe_slices, vp_device.h).
 int tbl_reprobe_stamp(vp_ctx *c, FlowTable &t, const uint32_t *list,

@@ -819,7 +819,7 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
     const uint32_t *ent, const uint32_t *cnt, uint32_t nsrc, uint32_t cap,
     uint32_t pbits, uint32_t bbits, uint32_t range, uint32_t L, uint32_t tcap,
     uint32_t p0, NowSpec now, uint64_t seq_base, uint64_t *ts, uint64_t *tseq,
-    PubArgs pub, const uint32_t *rtab) {
+    PubArgs pub, const uint32_t *rtab, uint32_t sbits) {
   // 1 + position in the launch, 0 = none; L words of dynamic LDS (16 KB at
   // 1M flows: the 256 bin blocks spread over all CUs, where a 64 KB static
   // array let only two blocks share a CU and left half of them idle)
@@ -827,11 +827,15 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
   // (1 + position of lane 0) of the run words that cover the group, so a run
   // costs one lane's atomic instead of 64 (its lane j touched index 64 g + j
   // at base + j, the same winner for all 64).
+  // With 2^sbits blocks per bin (fewer bins than fold blocks), block
+  // (bin, part) keeps in-bin indices [lo, lo + Lp) and skips the rest of the
+  // bin's entries and runs (each part reads them all).
   extern __shared__ uint32_t last[];
-  uint32_t *grp = last + L;
-  const uint32_t bin = blockIdx.x;
-  if (bin == 0 && threadIdx.x == 0) ctl_publish(pub);
-  for (uint32_t i = threadIdx.x; i < L + (L >> kBinRunBits); i += blockDim.x) last[i] = 0;
+  const uint32_t Lp = L >> sbits;
+  uint32_t *grp = last + Lp;
+  const uint32_t bin = blockIdx.x >> sbits, lo = (blockIdx.x & ((1u << sbits) - 1)) * Lp;
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctl_publish(pub);
+  for (uint32_t i = threadIdx.x; i < Lp + (Lp >> kBinRunBits); i += blockDim.x) last[i] = 0;
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const uint32_t pmask = (1u << pbits) - 1;
@@ -843,11 +847,12 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
   for (uint32_t r0 = threadIdx.x >> 6; r0 < nsrc; r0 += 64 * nw) {
     const uint32_t my = r0 + lane * nw;
     const uint32_t raw = my < nsrc ? cnt[(size_t)bin * nsrc + my] : 0;
-    const uint32_t nv = raw & ~kBinRunFlag;
-    // the slice's run word, loaded beside the count (one round trip; a word
+    const uint32_t nv = raw & ~kBinRunFlags;
+    // the slice's run words, loaded beside the count (one round trip; a word
     // whose flag is clear is stale and ignored)
-    const uint32_t re = my < nsrc ? rtab[((size_t)my << bbits) + bin] : 0u;
-    const bool run = (raw & kBinRunFlag) != 0;
+    const size_t ri = (((size_t)my << bbits) + bin) << 1;
+    const uint32_t re = my < nsrc ? rtab[ri] : 0u, re2 = my < nsrc ? rtab[ri + 1] : 0u;
+    const bool run = (raw & kBinRunFlag) != 0, run2 = (raw & kBinRunFlag2) != 0;
     const uint32_t ch = (nv + 63) >> 6;
     uint32_t inc = ch;  // inclusive prefix over the wave
 #pragma unroll
@@ -872,15 +877,19 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
       }
 #pragma unroll
       for (uint32_t u = 0; u < kU; u++)
-        if (lane < lim[u]) atomicMax(&last[e[u] >> pbits], base[u] + (e[u] & pmask));
+        if (lane < lim[u] && (e[u] >> pbits) - lo < Lp)
+          atomicMax(&last[(e[u] >> pbits) - lo], base[u] + (e[u] & pmask));
     }
-    if (run) atomicMax(&grp[re >> 20], my * range + 1 + (re & 0xFFFFFu));
+    if (run && ((re >> 20) << kBinRunBits) - lo < Lp)
+      atomicMax(&grp[(re >> 20) - (lo >> kBinRunBits)], my * range + 1 + (re & 0xFFFFFu));
+    if (run2 && ((re2 >> 20) << kBinRunBits) - lo < Lp)
+      atomicMax(&grp[(re2 >> 20) - (lo >> kBinRunBits)], my * range + 1 + (re2 & 0xFFFFFu));
   }
   __syncthreads();
-  for (uint32_t l = threadIdx.x; l < L; l += blockDim.x) {
+  for (uint32_t l = threadIdx.x; l < Lp; l += blockDim.x) {
     const uint32_t g = grp[l >> kBinRunBits];
     const uint32_t v = max(last[l], g ? g + (l & (kBinRun - 1)) : 0u);
-    const uint32_t i = bin_index(bin, l, bbits);
+    const uint32_t i = bin_index(bin, lo + l, bbits);
     if (!v || i >= tcap) continue;
     const uint32_t p = p0 + v - 1;
     ts[i] = (uint64_t)now.at(p);
@@ -895,7 +904,7 @@ static uint32_t ceil_log2(uint64_t v) {
 }
 
 int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
-                  uint32_t p1, BinsPlan *plan, uint32_t waves) {
+                  uint32_t p1, BinsPlan *plan, uint32_t waves, uint32_t min_bits) {
   Workspace &w = c->ws;
   *plan = BinsPlan{};
   const char *env = getenv("VIGPATH_TOUCH_BINS");  // diagnostics: 0 = off
@@ -904,22 +913,30 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   const uint32_t grid = resident_grid(kernel, (tiles + waves - 1) / waves, 64 * (int)waves);
   const uint32_t per_b = (tiles + grid - 1) / grid;
   const uint32_t range = per_b * 64;
-  // the fewest bins (>= 256) whose in-bin index range fits the fold's LDS
-  static const uint32_t bbits_min = [] {  // (VIGPATH_BIN_BITS: more bins, for A/B)
+  // The fewest bins (>= 2^bbits_min) whose in-bin index range fits the
+  // fold's LDS, and at least 256 fold blocks whatever the bin count (2^sbits
+  // per bin). A block keeps one partly written line per bin slice: at 256
+  // bins, 32 MB over the chip, as much as all the L2s, which shuffled
+  // touches (no runs) pay for (tools/sessions/gpu_r04ba.sh);
+  // two run words per block and bin keep round robin whole at 128.
+  static const uint32_t bbits_min = [] {  // (VIGPATH_BIN_BITS, for A/B)
     const char *e = getenv("VIGPATH_BIN_BITS");
-    const int v = e ? atoi(e) : 8;
-    return v >= 8 && v <= 10 ? (uint32_t)v : 8u;
+    const int v = e ? atoi(e) : 7;
+    return v >= 6 && v <= 10 ? (uint32_t)v : 7u;
   }();
-  uint32_t bbits = bbits_min;
-  auto in_bin = [&](uint32_t bb) {  // in-bin index range for 2^bb bins
-    return (((uint64_t)t.cap + ((uint64_t)kBinRun << bb) - 1) >> (kBinRunBits + bb))
-           << kBinRunBits;
+  auto split = [](uint32_t bb) { return bb < 8 ? 8 - bb : 0u; };
+  auto in_bin = [&](uint32_t bb) {  // in-bin index range for 2^bb bins: a
+    // whole number of runs per fold block
+    const uint32_t q = kBinRunBits + split(bb);
+    return (((uint64_t)t.cap + ((uint64_t)1 << (q + bb)) - 1) >> (q + bb)) << q;
   };
-  while (bbits < 10 && in_bin(bbits) > kBinLocalMax) bbits++;
+  uint32_t bbits = std::max(bbits_min, std::min<uint32_t>(min_bits, 10));
+  while (bbits < 10 && (in_bin(bbits) >> split(bbits)) > kBinLocalMax) bbits++;
+  const uint32_t sbits = split(bbits);
   const uint32_t nbins = 1u << bbits;
   const uint32_t L = (uint32_t)in_bin(bbits);
   const uint32_t pbits = std::max<uint32_t>(1, ceil_log2(range));
-  if (L > kBinLocalMax || ceil_log2(L) + pbits > 32) return 0;
+  if ((L >> sbits) > kBinLocalMax || ceil_log2(L) + pbits > 32) return 0;
   // twice a uniform share of a block's packets per bin, and at least two
   // waves' worth (a wave touching 64 consecutive indices fills one bin)
   const uint32_t cap =
@@ -945,8 +962,9 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   plan->grid = grid;
   plan->range = range;
   plan->L = L;
-  // run words: one per block and bin, positions below 2^20 within a block
-  const size_t nr = (size_t)grid << bbits;
+  plan->sbits = sbits;
+  // run words: two per block and bin, positions below 2^20 within a block
+  const size_t nr = ((size_t)grid << bbits) * 2;
   if (nr > w.bins_rtab_n) {
     VP_HIP(hipStreamSynchronize(c->stream));
     hipFree(w.bins_rtab);
@@ -976,10 +994,11 @@ static int bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p
   }();
   auto *fold = fold_u == 8 ? touch_bins_reduce<8> : fold_u == 32 ? touch_bins_reduce<32>
                                                                  : touch_bins_reduce<16>;
-  fold<<<1u << plan.bins.bbits, 1024, 4u * (plan.L + (plan.L >> kBinRunBits)), c->stream>>>(
-      plan.bins.ent, plan.bins.cnt, plan.grid, plan.bins.cap, plan.bins.pbits,
-      plan.bins.bbits, plan.range, plan.L, t.cap, p0, now, seq_base, t.ts, t.tseq,
-      pub, plan.bins.rtab);
+  const uint32_t Lp = plan.L >> plan.sbits;
+  fold<<<1u << (plan.bins.bbits + plan.sbits), 1024, 4u * (Lp + (Lp >> kBinRunBits)),
+         c->stream>>>(plan.bins.ent, plan.bins.cnt, plan.grid, plan.bins.cap, plan.bins.pbits,
+                      plan.bins.bbits, plan.range, plan.L, t.cap, p0, now, seq_base, t.ts,
+                      t.tseq, pub, plan.bins.rtab, plan.sbits);
   VP_HIP(hipGetLastError());
   return 0;
 }
