@@ -235,9 +235,11 @@ def test_touch_bins_steady_state(n_flows, order):
 def test_multiplicative_home_buckets_reprobe(order, slot, monkeypatch):
     """With the multiplicative home-bucket spread (VIGPATH_MIX=1, the layout
     the table rebuilds into for clustering key sets) a full home bucket is
-    common at load 0.65: those packets leave the classify wave and finish in
-    nat_reprobe (per-block slices for 64-byte tiles, one list for the
-    per-lane path of wider slots). Outputs and state equal the oracle's."""
+    common at load 0.65. A lean 64-byte tile (every lane a fast LAN packet)
+    walks the probe path on in the lane; the other tiles' packets leave the
+    classify wave and finish in nat_reprobe (per-block slices for 64-byte
+    tiles, one list for the per-lane path of wider slots). Outputs and state
+    equal the oracle's either way."""
     monkeypatch.setenv("VIGPATH_MIX", "1")
     monkeypatch.setenv("VIGPATH_SPARSE", "-1")  # load 2/3: many reprobes
     monkeypatch.setenv("VIGPATH_LIN", "0")  # (no allocation-order layout)
