@@ -546,6 +546,28 @@ __device__ __forceinline__ uint32_t bucket_match_sel(const uint4 *row,
   return m0 ? ix.x : e0 ? kNone : m1 ? ix.y : e1 ? kNone : m2 ? ix.z : kNone;
 }
 
+// A lean tile's probe walk on from a full home bucket b, in the lane
+// (tbl_probe_from's order; lanes with !*done walk, `idx` is the home
+// bucket's answer). Random keys leave ~0.2 % of their packets here every
+// batch, whose reprobe launch and control-block read-back this spares; the
+// loop is wave-uniform and bounded by the table size (a lane past it
+// queues for nat_reprobe).
+__device__ __forceinline__ uint32_t lean_walk(const NatArgs &a, const uint4 *rows, uint32_t b,
+                                              const uint32_t key[4], uint32_t idx, bool *done) {
+  if (__ballot(!*done)) {
+    uint32_t nb = b;
+    for (uint32_t st = 0; st < a.t.bmask && __ballot(!*done); st++) {
+      if (!*done) {
+        nb = (nb + 1) & a.t.bmask;
+        const uint4 *q = rows + 4 * (size_t)nb;
+        const uint4 r2[4] = {q[0], q[1], q[2], q[3]};
+        idx = bucket_match_sel(r2, key, done);
+      }
+    }
+  }
+  return idx;
+}
+
 // 128-byte slots: the tail sums of the wave's tile from the registers the
 // dense fetch left (d[j] = chunk 64 j + lane: frame 8 j + lane / 8, part
 // lane % 8; parts 4-7 are the bytes 64-127 the L4 sum may cover), right
@@ -768,6 +790,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
         const uint32_t key[4] = {(f.w[8] >> 16) | ((f.w[9] & 0xFFFF) << 16), f.u32at2(26),
                                  f.u32at2(30), in | (proto << 16)};
         bool done;
+        // (no walk in the lane here: it costs the wide kernels scratch)
         const uint32_t idx = bucket_match_sel(row, key, &done);
         const bool hit = done & (idx != kNone);
         if (__ballot(!hit)) {  // misses (phase B) and full home buckets (reprobes)
@@ -865,21 +888,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       for (uint32_t k = 0; k < 4; k++) row[k] = S[chunk_swz(4 * lane + k)];
       const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
       bool done;
-      uint32_t idx = bucket_match_sel(row, key, &done);
-      if (__ballot(!done)) {  // a full home bucket: the walk on, in the lane
-        // (tbl_probe_from; random keys leave ~0.2 % of their packets here
-        // every batch, whose reprobe launch and control-block read-back this
-        // spares; the loop is wave-uniform, a lane past its end queues)
-        uint32_t nb = b;
-        for (uint32_t st = 0; st < a.t.bmask && __ballot(!done); st++) {
-          if (!done) {
-            nb = (nb + 1) & a.t.bmask;
-            const uint4 *q = rows + 4 * (size_t)nb;
-            const uint4 r2[4] = {q[0], q[1], q[2], q[3]};
-            idx = bucket_match_sel(r2, key, &done);
-          }
-        }
-      }
+      const uint32_t idx = lean_walk(a, rows, b, key, bucket_match_sel(row, key, &done), &done);
       const bool hit = done & (idx != kNone);
       if (__ballot(!hit)) {  // misses (phase B) and longer walks (reprobes)
         const bool miss = done & !hit;
