@@ -582,11 +582,13 @@ def cpu_model() -> str:
 
 
 def timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank, first, steps,
-                order="rr", host_comm=False, stages=None):
+                order="rr", host_comm=False, stages=None, wd=None, label="timed"):
     """Fill one buffer per step (batches first .. first + steps - 1 of this
     rank's slices, `order`), then time exactly `steps` prepared
     vp_process_device calls between barriers + synchronisations. Returns
-    (elapsed s, max over ranks; [(kernel ms, launches)] per step; buffers)."""
+    (elapsed s, max over ranks; [(kernel ms, launches)] per step; buffers).
+    wd: the N > 1 watchdog (vigor_amd.watchdog), one marker per step."""
+    mark = wd.stage if wd is not None else (lambda name: None)
     def gstart(k):  # global position of this rank's slice of global batch k
         return (k * world + rank) * B
     bufs = []
@@ -597,16 +599,19 @@ def timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank, first, 
     calls = [nat.device_step(b, lens, in_dev, out, slot) for b in bufs]
     torch.cuda.synchronize()
     kms = []
+    mark("%s: barrier" % label)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(steps):
+        mark("%s: step %d/%d" % (label, k + 1, steps))
         calls[k](T.NOW0 + gstart(first + k), 1)
         kms.append(nat.last_kernel_ms())
         if stages is not None:  # owner mode's phase-A stages (timing pass)
             for name, ms in nat.last_stage_ms().items():
                 stages[name] = stages.get(name, 0.0) + ms / steps
+    mark("%s: end barrier" % label)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -688,6 +693,24 @@ def main():
     host_comm = os.environ.get("VIGPATH_COMM", "rccl") == "host"
     if host_comm:
         local = 0
+    # N > 1: flushed stage markers on every rank, and a watchdog that aborts
+    # the collectives, prints a partial line and exits 3 after
+    # VIGPATH_WATCHDOG_S seconds (default 240) without a new stage
+    # (vigor_amd/watchdog.py); VIGPATH_STALL="rank:ms:call" rehearses it
+    wd = None
+    nat_ref = []  # the context the watchdog aborts
+    if world > 1 or "VIGPATH_WATCHDOG_S" in os.environ:  # (one rank: rehearsals)
+        from vigor_amd.watchdog import Watchdog
+        wd = Watchdog(rank, world, float(os.environ.get("VIGPATH_WATCHDOG_S", "240")),
+                      partial={"metric": METRIC, "unit": "Mpps", "higher_is_better": True,
+                               "steps": args.steps, "warmup": args.warmup,
+                               "config": {"shard_mode": args.shard_mode,
+                                          "transport": "gloo (host)" if host_comm
+                                          else "RCCL/xGMI"}},
+                      abort=lambda: [n.L.vp_comm_abort(n.h) for n in nat_ref if n.h.value])
+        wd.start()
+        wd.stage("comm init (%s)" % ("gloo" if host_comm else "nccl"))
+    mark = wd.stage if wd is not None else (lambda name: None)
     if world > 1:
         if host_comm:
             dist.init_process_group("gloo")
@@ -708,12 +731,15 @@ def main():
         if args.route_all and world == 1:  # the owner pipeline on one GPU
             import ctypes
             from vigor_amd import shard
+            nat_ref.append(nat)
             os.environ["VIGPATH_ROUTE_ALL"] = "1"
             uid = (ctypes.c_uint8 * 128).from_buffer_copy(shard.rccl_unique_id())
             vigor_amd._check(nat.L.vp_attach_rccl(nat.h, uid, 1, 0), "vp_attach_rccl", nat.L)
             shard.set_mode(nat, "owner")
         if world > 1:  # one vignat over all ranks
             from vigor_amd import shard
+            mark("attach %s" % mode)
+            nat_ref.append(nat)
             if host_comm:
                 shard.attach_torch(nat, rank, world, mode=mode)
             else:
@@ -727,6 +753,7 @@ def main():
         wbuf = torch.empty(B * slot, dtype=torch.uint8, device=dev)
         rate = None
         for w in range(args.warmup):
+            mark("warm-up batch %d/%d" % (w + 1, args.warmup))
             bank.fill(wbuf, (w * world + rank) * B)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -744,7 +771,8 @@ def main():
     # the headline pass: no per-launch timing events (they cost a step about
     # 6 us of kernel-boundary time)
     elapsed, _, bufs = timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world,
-                                   rank, args.warmup, args.steps, args.order, host_comm)
+                                   rank, args.warmup, args.steps, args.order, host_comm,
+                                   wd=wd, label="timed")
     # the last timed batch, byte for byte, against the reference's output of
     # the same batch (after timing; the golden exists for the default shape);
     # wider slots: a size-independent check of a sample (checksums verify)
@@ -771,10 +799,11 @@ def main():
     stages = {} if owner_run else None
     el_k, kms, bufs = timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank,
                                   args.warmup + args.steps, args.steps, args.order, host_comm,
-                                  stages)
+                                  stages, wd=wd, label="kernel timing")
     del bufs
     stages_max = None
     if stages and world > 1:  # the slowest rank per stage
+        mark("stage times all-reduce")
         names = sorted(stages)
         t = torch.tensor([stages[k] for k in names], dtype=torch.float64,
                          device="cpu" if host_comm else dev)
@@ -856,16 +885,21 @@ def main():
     if world > 1 and not args.no_extra:
         # the other dictionary placement, same workload
         other = "replicated" if mode == "owner" else "owner"
+        mark("other shard mode: %s" % other)
+        nat_ref.clear()
         nat.close()
         nat2 = make_nat(other)
         warm(nat2)
         el3, kms3, bufs3 = timed_steps(nat2, bank, dev, lens, in_dev, out, B, slot, world,
-                                       rank, args.warmup, args.steps, "rr", host_comm)
+                                       rank, args.warmup, args.steps, "rr", host_comm,
+                                       wd=wd, label="other mode")
         del bufs3
         extra["other_shard_mode"] = {
             "mode": other, "value": round(B * args.steps * world / el3 / 1e6, 2),
             "unit": "Mpps", "ms_per_step": round(el3 / args.steps * 1e3, 4)}
+        nat_ref.clear()
         nat2.close()
+    mark("report")
     if rank == 0:
         cpu = None
         if not args.no_cpu and world == 1 and slot == SLOT:
@@ -929,9 +963,15 @@ def main():
                           "mean per step on rank 0; that pass's step: %.4f ms"
                           % (el_k / args.steps * 1e3)}
         line.update(extra)
+        if wd is not None:
+            line["stages_done"] = len(wd.done) + 1
         print(json.dumps(line), flush=True)
     if world > 1:
+        mark("destroy process group")
         dist.destroy_process_group()
+    if wd is not None:
+        wd.stage("done")
+        wd.stop()
 
 
 if __name__ == "__main__":

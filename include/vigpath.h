@@ -176,7 +176,9 @@ int vp_unregister_host(vp_ctx *ctx, void *base);
  * in_dev[i] its port; every frame is rewritten in place and out_dev[i] gets
  * nf_process's return value, as calling nf_process on every packet in order
  * would (nf.c:150-176). Time: now[i], or now0 + i * now_step when now is
- * NULL (nf.c stamps one polling sweep with one current_time(), nf.c:56).
+ * NULL (nf.c's per-packet loop stamps a polling sweep over the devices with
+ * one current_time(), nf.c:56: now_step 0; its batched loop stamps every
+ * packet, nf.c:197: a time array, or now_step > 0).
  * Frames inside memory registered with vp_register_host are read and written
  * by the GPU in place, in pipelined chunks: per frame the
  * first 64 bytes and, for vignat, the bytes its L4 checksum covers cross
@@ -265,6 +267,15 @@ int vp_shard_mode(vp_ctx *ctx, int mode);
 /* Collective: merge the ranks' timestamps so vp_nat_dump is exact on every
  * rank (the dictionary and allocator are identical everywhere already). */
 int vp_sync_state(vp_ctx *ctx);
+
+/* Abort this rank's collectives (not collective itself; any thread, also
+ * while another thread is inside a vp_* call on the context): the RCCL
+ * communicator is aborted (ncclCommAbort), so a rank waiting for a peer that
+ * never comes returns instead of spinning; every later vp_* call on the
+ * context that needs the ranks fails with VP_EIO. Host transports
+ * (vp_attach_comm) have nothing to abort: returns 0. For watchdogs
+ * (bench.py --gpus N); the context may only be destroyed afterwards. */
+int vp_comm_abort(vp_ctx *ctx);
 
 /* ------------------------------------------------------- observability -- */
 

@@ -21,8 +21,10 @@ struct Comm {
   virtual int allreduce_max_u64_dev(vp_ctx *c, uint64_t *buf, size_t count) = 0;
   // personalised exchange of device buffers: sbytes[q] bytes to rank q
   // (chunks consecutive in rank order), rbytes[q] bytes from rank q;
-  // skip_self: this rank's own chunk is not copied (the caller reads it from
-  // `send` where it lies; RCCL transport, the host transport copies it anyway)
+  // skip_self: this rank's own chunk is not copied into `recv` by either
+  // transport (the caller reads it from `send` where it lies)
+  // abandon every collective of this rank (vp_comm_abort; any thread)
+  virtual int abort() { return 0; }
   virtual int alltoallv_dev(vp_ctx *c, const void *send, const size_t *sbytes,
                             void *recv, const size_t *rbytes, bool skip_self = false) = 0;
 };

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -33,9 +34,22 @@ struct RcclComm : Comm {
   uint8_t *hstage = nullptr;
   size_t hstage_bytes = 0;
   ~RcclComm() override {
-    if (comm) ncclCommDestroy(comm);
+    // (an aborted communicator is gone: ncclCommAbort freed it)
+    if (comm && !aborted.load()) ncclCommDestroy(comm);
     if (stage) hipFree(stage);
     if (hstage) hipHostFree(hstage);
+  }
+  std::atomic<bool> aborted{false};
+  int live() const {
+    if (!aborted.load()) return 0;
+    state_fail("RCCL communicator aborted (vp_comm_abort)");
+    return VP_EIO;
+  }
+  int abort() override {
+    bool was = false;
+    if (!comm || !aborted.compare_exchange_strong(was, true)) return 0;
+    VP_NCCL(ncclCommAbort(comm));
+    return 0;
   }
   int reserve_host(size_t bytes) {
     if (bytes <= hstage_bytes) return 0;
@@ -56,6 +70,7 @@ struct RcclComm : Comm {
     return 0;
   }
   int allgather_host(vp_ctx *c, const void *send, void *recv, size_t bytes) override {
+    VP_TRY(live());
     VP_TRY(reserve(bytes * (n + 1)));
     VP_TRY(reserve_host(bytes * (n + 1)));
     uint8_t *s = static_cast<uint8_t *>(stage), *h = hstage;
@@ -69,10 +84,12 @@ struct RcclComm : Comm {
     return 0;
   }
   int allgather_dev(vp_ctx *c, const void *send, void *recv, size_t bytes) override {
+    VP_TRY(live());
     VP_NCCL(ncclAllGather(send, recv, bytes, ncclUint8, comm, c->stream));
     return 0;
   }
   int allreduce_max_u64_dev(vp_ctx *c, uint64_t *buf, size_t count) override {
+    VP_TRY(live());
     VP_NCCL(ncclAllReduce(buf, buf, count, ncclUint64, ncclMax, comm, c->stream));
     return 0;
   }
@@ -80,6 +97,7 @@ struct RcclComm : Comm {
   // xGMI link at once
   int alltoallv_dev(vp_ctx *c, const void *send, const size_t *sbytes, void *recv,
                     const size_t *rbytes, bool skip_self) override {
+    VP_TRY(live());
     const uint8_t *s = static_cast<const uint8_t *>(send);
     uint8_t *d = static_cast<uint8_t *>(recv);
     size_t so = 0, ro = 0;
@@ -252,6 +270,12 @@ int vp_shard_mode(vp_ctx *c, int mode) {
   VP_TRY(tbl_set_owner(c, c->ft, (uint32_t)c->comm->n, (uint32_t)c->comm->r));
   c->shard_mode = mode;
   return 0;
+}
+
+int vp_comm_abort(vp_ctx *c) {
+  if (!c) return VP_EINVAL;
+  if (!c->comm) return 0;
+  return c->comm->abort();
 }
 
 int vp_sync_state(vp_ctx *c) {

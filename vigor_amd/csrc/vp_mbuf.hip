@@ -792,7 +792,10 @@ extern "C" {
 
 int vp_register_host(vp_ctx *c, void *base, size_t bytes) {
   if (!c || !base || !bytes) return VP_EINVAL;
-  if (c->hmaps.size() >= (size_t)kMaxHostMaps) return VP_ENOMEM;
+  if (c->hmaps.size() >= (size_t)kMaxHostMaps) {
+    state_fail("vp_register_host: at most %d registered host ranges per context", kMaxHostMaps);
+    return VP_ENOMEM;
+  }
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
   const uint64_t hb = reinterpret_cast<uint64_t>(base);
   for (const HostMap &h : c->hmaps)

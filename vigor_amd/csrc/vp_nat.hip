@@ -549,14 +549,18 @@ __device__ __forceinline__ uint32_t bucket_match_sel(const uint4 *row,
 // A lean tile's probe walk on from a full home bucket b, in the lane
 // (tbl_probe_from's order; lanes with !*done walk, `idx` is the home
 // bucket's answer). Random keys leave ~0.2 % of their packets here every
-// batch, whose reprobe launch and control-block read-back this spares; the
-// loop is wave-uniform and bounded by the table size (a lane past it
-// queues for nat_reprobe).
+// batch, whose reprobe launch and control-block read-back this spares. The
+// loop is wave-uniform, so one long path would stall all 64 lanes: it stops
+// after kLeanWalk buckets past home (tombstone-heavy tables, the
+// multiplicative spread at high load), and a lane still !*done then queues
+// for nat_reprobe, which walks the whole path.
+constexpr uint32_t kLeanWalk = 4;
 __device__ __forceinline__ uint32_t lean_walk(const NatArgs &a, const uint4 *rows, uint32_t b,
                                               const uint32_t key[4], uint32_t idx, bool *done) {
   if (__ballot(!*done)) {
     uint32_t nb = b;
-    for (uint32_t st = 0; st < a.t.bmask && __ballot(!*done); st++) {
+    const uint32_t steps = min(a.t.bmask, kLeanWalk);
+    for (uint32_t st = 0; st < steps && __ballot(!*done); st++) {
       if (!*done) {
         nb = (nb + 1) & a.t.bmask;
         const uint4 *q = rows + 4 * (size_t)nb;

@@ -9,6 +9,7 @@
 
 #include <cstddef>
 #include <hipcub/hipcub.hpp>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -163,16 +164,21 @@ static uint64_t tbl_entries(const FlowTable &t) {
 
 int tbl_alloc(vp_ctx *c, FlowTable &t, uint32_t cap) {
   (void)c;
-  // two buckets (3 entries each) per index: load <= 1/6, so a random key
-  // set puts ~0.2 % of its keys past their home bucket (~2.3 % at load 1/3,
-  // ~13 % at 2/3, each one a reprobe: DESIGN.md §5.1, random keys 0.80 ->
-  // 0.66 ms per step); 128 B of HBM per index (the allocation-order layout,
-  // §4, rebuilds at 32 B). Tombstones purged at 0.85.
+  // Every NF's flow table (vignat, vigfw, vigpol flows, vigbridge MACs, viglb
+  // flows and backends) gets two buckets (3 entries each) per index: load
+  // <= 1/6, so a random key set puts ~0.2 % of its keys past their home
+  // bucket (~2.3 % at load 1/3, ~13 % at 2/3, each one a reprobe: DESIGN.md
+  // §4-5.1, random keys 0.80 -> 0.66 ms per step). 128 B of HBM per index,
+  // 128 MB at 1M flows of 288 GB; the allocation-order layout (§4) rebuilds
+  // at 32 B. Tombstones purged at 0.85 of one bucket per index
+  // (tbl_check_tombs).
   uint64_t nb = 64;
   while (nb < cap) nb <<= 1;
   t.nb_base = nb;
   int k = 1;
-  if (const char *sp = getenv("VIGPATH_SPARSE")) k = atoi(sp);  // (tests: 2^k x buckets)
+  // (VIGPATH_SPARSE=k: 2^k buckets per index, k in -3..3; the tests use it to
+  // force high loads and full home buckets)
+  if (const char *sp = getenv("VIGPATH_SPARSE")) k = atoi(sp);
   if (k > 0) nb <<= std::min(k, 3);
   if (k < 0) nb = std::max<uint64_t>(64, nb >> std::min(-k, 3));
   t.bmask = (uint32_t)(nb - 1);
@@ -1342,9 +1348,14 @@ int tbl_expire(vp_ctx *c, FlowTable &t, int64_t cutoff, uint32_t *n_out) {
   return tbl_check_tombs(c, t);
 }
 
+// Tombstones are purged (a rebuild) when they and the live entries fill 85 %
+// of the entries of one bucket per index (nb_base), or of the table when it
+// is smaller (the allocation-order layout): the spread tables' second bucket
+// per index is headroom for short probe paths, not room for tombstones.
 int tbl_check_tombs(vp_ctx *c, FlowTable &t) {
   VP_TRY(read_ctl(c, t));
-  if ((uint64_t)t.h_ctl.n_tomb + t.h_ctl.sh_live > tbl_entries(t) * 85 / 100)
+  const uint64_t base = std::min<uint64_t>(tbl_entries(t), t.nb_base * kBucketEntries);
+  if ((uint64_t)t.h_ctl.n_tomb + t.h_ctl.sh_live > base * 85 / 100)
     return tbl_rebuild(c, t);
   return 0;
 }
@@ -1611,9 +1622,27 @@ __global__ void union_stamp(const uint32_t *first, const uint32_t *assign,
   }
 }
 
+// VIGPATH_STALL="rank:ms:call" (watchdog rehearsals, bench.py): rank `rank`
+// sleeps `ms` at the start of its `call`-th multi-GPU batch (0-based), while
+// its peers wait for it inside the batch's first collective.
+static void maybe_stall(int rank) {
+  static int calls = 0;
+  static const struct S { int r, ms, call; } st = [] {
+    S v{-1, 0, 0};
+    if (const char *e = getenv("VIGPATH_STALL")) sscanf(e, "%d:%d:%d", &v.r, &v.ms, &v.call);
+    return v;
+  }();
+  if (st.r == rank && calls++ == st.call) {
+    fprintf(stderr, "vigpath: rank %d stalls %d ms in batch %d (VIGPATH_STALL)\n", rank, st.ms,
+            st.call);
+    usleep((useconds_t)st.ms * 1000u);
+  }
+}
+
 static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
                              ExpiringTable *tabs, int ntabs, SegmentFn seg) {
   Comm &m = *c->comm;
+  maybe_stall(m.r);
   const uint32_t n = b->n;
   c->last_ms = 0.f;
   c->last_launches = 0;
