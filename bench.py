@@ -555,6 +555,43 @@ def bench_nat_churn(dev, B, steps, golden, state=None):
     return r
 
 
+def per_packet_drop_in(packets: int = 20000, flows: int = 1024, batches=(0, 32, 1024)):
+    """north_star's "drops into nf.c's main loop unchanged", timed: host/nf_loop
+    (nf.c:143-216 restated over a trace file, linked against
+    libvignat_nf.so) with every packet through nf_process one at a time
+    (batch 0: nf.c:150-176, VIGOR_BATCH_SIZE == 1), and through the batched
+    form (vp_process_batch, nf.c:178-215) for comparison. The trace: `flows`
+    flows allocated by an untimed warm-up (--warm), then `packets` steady
+    hits round robin, each with its own time stamp. Host frames in pageable
+    memory, as nf.c's mbuf data would be to a library that did not register
+    the pool. Returns {batch: {us_per_packet, kpps}}."""
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "host", "nf_loop")
+    n = flows + packets
+    fr, ln, dv, now = T.nat_lan_trace(n, flows)
+    res = {}
+    with tempfile.TemporaryDirectory() as d:
+        tin, tout = os.path.join(d, "t.in"), os.path.join(d, "t.out")
+        with open(tin, "wb") as f:
+            f.write(b"VPTR" + np.array([n, SLOT], np.uint32).tobytes())
+            f.write(dv.astype(np.uint16).tobytes() + ln.astype(np.uint16).tobytes())
+            f.write(now.astype(np.int64).tobytes() + fr.tobytes())
+        for bt in batches:
+            cmd = [exe, tin, tout, "--warm", str(flows)] + (["--batch", str(bt)] if bt else [])
+            r = subprocess.run(cmd + ["--"] + NAT_ARGS + ["--max-flows", str(flows)],
+                               capture_output=True, text=True, timeout=300)
+            if r.returncode != 0:
+                raise RuntimeError("nf_loop failed: %s" % r.stderr[-500:])
+            line = [x for x in r.stderr.splitlines() if x.startswith("timed ")][-1]
+            us = float(line.split(",")[1].split()[0])
+            res["per_packet" if bt == 0 else "batch_%d" % bt] = {
+                "us_per_packet": round(us, 3), "kpps": round(1e3 / us, 2)}
+            out = np.frombuffer(open(tout, "rb").read(), np.uint16, n, 12)
+            assert (out[flows:] == 1).all()  # every steady packet out on the WAN port
+    return res
+
+
 def launch_ranks(n: int) -> int:
     """--gpus N > 1 without a torch.distributed environment: start one rank
     per GPU as child processes (torch.distributed.run), before anything here
@@ -623,6 +660,35 @@ def timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank, first, 
     # every packet hit (steady state) and went out on the WAN port
     assert int((out != 1).sum().item()) == 0
     return elapsed, kms, bufs
+
+
+def shape_ceiling(L, B, slot, dev, reps=10):
+    """vp_probe_slots over a scratch batch of B slots: (read+write ms, read
+    ms) per pass, each the mean of `reps` launches timed like the classify
+    kernel (its dispatch's own timestamps)."""
+    import ctypes
+    buf = torch.zeros(B * slot, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    out = []
+    for store in (1, 0):
+        ms = ctypes.c_float()
+        vigor_amd._check(L.vp_probe_slots(ctypes.c_void_p(buf.data_ptr()), B, slot, store, reps,
+                                          ctypes.byref(ms)), "vp_probe_slots", L)
+        out.append(float(ms.value))
+    del buf
+    torch.cuda.empty_cache()
+    return out
+
+
+def ceiling_fields(ceiling, kernel_s, step_s):
+    rw, rd = ceiling
+    return {"shape_ceiling_ms": round(rw, 4), "shape_read_ms": round(rd, 4),
+            "kernel_over_ceiling": round(kernel_s * 1e3 / rw, 4),
+            "step_over_ceiling": round(step_s * 1e3 / rw, 4),
+            "shape_ceiling_source": "vp_probe_slots on this box: nat_classify64's grid and "
+                                    "1 KiB access shape, every slot read and written back "
+                                    "whole (write-through), no other work; shape_read_ms "
+                                    "the same without the stores"}
 
 
 def kernel_rate(kms, B, steps, alg_bytes):
@@ -810,6 +876,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         stages_max = {k: float(v) for k, v in zip(names, t.tolist())}
     per_launch_s, pkts_per_launch, achieved = kernel_rate(kms, B, args.steps, alg_bytes)
+    # the classify tile's memory-shape ceiling on this box (vp_probe_slots:
+    # the same grid and 1 KiB access shape, every slot read and written back
+    # whole, nothing else), beside the kernel it bounds
+    ceiling = None
+    if world == 1 and slot in (64, 128) and not args.route_all:
+        mark("shape ceiling probe")
+        ceiling = shape_ceiling(nat.L, B, slot, dev)
     traffic = None  # PMC bytes of the same kernel (profiles/, per launch)
     tpath = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE)
     if (os.path.exists(tpath) and B == 1 << 24 and args.flows == 1 << 20
@@ -847,6 +920,7 @@ def main():
         del bufs2
         pl2, pk2, ach2 = kernel_rate(kms2, B, args.steps, alg_bytes)
         extra["secondary_order"] = {
+            "kernel_over_ceiling": round(pl2 * 1e3 / ceiling[0], 4) if ceiling else None,
             "order": "uniform (flow = splitmix64(0x5EED, p) mod N)",
             "value": round(B * args.steps / el2 / 1e6, 2), "unit": "Mpps",
             "ms_per_step": round(el2 / args.steps * 1e3, 4),
@@ -870,6 +944,12 @@ def main():
         extra["end_to_end_mbuf"] = end_to_end_mbuf(nat, bank, dev, base)
         extra["end_to_end_mbuf_imix"] = end_to_end_mbuf(nat, bank, dev,
                                                         base + 4 * MBUF_BATCH, imix=True)
+        pp = per_packet_drop_in()
+        pp.update({"path": "host/nf_loop (nf.c's loop) over libvignat_nf.so: nf_process "
+                           "per packet (vp_process_batch of 1), and the batched loop for "
+                           "comparison; frames in pageable host memory",
+                   "packets": 20000, "flows": 1024})
+        extra["per_packet_drop_in"] = pp
     if (world == 1 and not args.no_extra and slot == SLOT and args.order == "rr"
             and not args.route_all and args.flows == 1 << 20):
         nat.close()
@@ -882,6 +962,10 @@ def main():
         extra["nat_random_keys"] = bench_nat_random(dev, B, steps_x, gold.get("random"))
         extra["nat_churn"] = bench_nat_churn(dev, B, steps_x, gold.get("churn"),
                                              gold.get("churn_state"))
+        if ceiling:  # (the same 64-byte read+write shape bounds every classify kernel)
+            for k in ("config3_bridge", "config4_lb", "nat_random_keys", "nat_churn"):
+                extra[k]["kernel_over_ceiling"] = round(
+                    extra[k]["kernel_ms_per_launch"] / ceiling[0], 4)
     if world > 1 and not args.no_extra:
         # the other dictionary placement, same workload
         other = "replicated" if mode == "owner" else "owner"
@@ -946,6 +1030,8 @@ def main():
                                           "on its stream; that pass: %.4f ms per step"
                                           % (args.steps, el_k / args.steps * 1e3),
                          "alg_bytes_per_packet": alg_bytes,
+                         **(ceiling_fields(ceiling, per_launch_s, elapsed / args.steps)
+                            if ceiling else {}),
                          "kernel_mpps": round(pkts_per_launch / per_launch_s
                                               / 1e6, 1)},
             "cpu_baseline": cpu,

@@ -11,7 +11,10 @@
  * against our libvignat_nf.so. With --batch B it instead hands B packets at
  * a time to vp_process_batch (the batched form, nf.c:178-215).
  *
- * usage: nf_loop <trace.in> <trace.out> [--batch B] -- <NF options>
+ * usage: nf_loop <trace.in> <trace.out> [--batch B] [--warm W] -- <NF options>
+ * --warm W: the first W packets run first, untimed; the rest are timed and
+ * the rate is printed on stderr ("timed P packets: S s, U us/packet, K Kpps":
+ * the per-packet cost of the drop-in).
  * trace.in:  "VPTR" u32 n u32 slot, u16 in_dev[n], u16 len[n], i64 now[n],
  *            u8 frames[n*slot]
  * trace.out: "VPTO" u32 n u32 slot, u16 out_dev[n], u8 frames[n*slot],
@@ -32,6 +35,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../include/vigpath.h"
 
@@ -57,12 +61,14 @@ int main(int argc, char **argv) {
     fprintf(stderr, "usage: %s in out [--batch B] -- NF options\n", argv[0]);
     return 2;
   }
-  uint32_t batch = 0;
+  uint32_t batch = 0, warm = 0;
   int nf_argc = 1;
   char **nf_argv = argv + 2; /* argv[2] stands in for the program name */
   for (int i = 3; i < argc; i++) {
     if (!strcmp(argv[i], "--batch") && i + 1 < argc) {
       batch = (uint32_t)atoi(argv[++i]);
+    } else if (!strcmp(argv[i], "--warm") && i + 1 < argc) {
+      warm = (uint32_t)atoi(argv[++i]);
     } else if (!strcmp(argv[i], "--")) {
       nf_argv = argv + i;
       nf_argc = argc - i;
@@ -94,14 +100,28 @@ int main(int argc, char **argv) {
   }
   uint16_t *out = calloc(n ? n : 1, 2);
   uint64_t drops = 0, floods = 0, tx = 0;
+  if (warm > n) warm = n;
+  struct timespec t0 = {0, 0}, t1;
   if (batch == 0) {
-    for (uint32_t i = 0; i < n; i++) /* nf.c:150-176 */
+    for (uint32_t i = 0; i < n; i++) { /* nf.c:150-176 */
+      if (i == warm) clock_gettime(CLOCK_MONOTONIC, &t0);
       out[i] = (uint16_t)nf_process(in_dev[i], frames + (size_t)i * slot, len[i],
                                     now[i]);
+    }
   } else {
     extern vp_ctx *vp_nf_context(void);
     uint8_t **ptrs = malloc(sizeof(uint8_t *) * batch);
-    for (uint32_t a = 0; a < n; a += batch) {
+    for (uint32_t a = 0; a < warm; a += batch) {  /* untimed */
+      uint32_t m = warm - a < batch ? warm - a : batch;
+      for (uint32_t i = 0; i < m; i++) ptrs[i] = frames + (size_t)(a + i) * slot;
+      if (vp_process_batch(vp_nf_context(), m, in_dev + a, ptrs, len + a,
+                           now + a, out + a) != VP_OK) {
+        fprintf(stderr, "vp_process_batch failed\n");
+        return 1;
+      }
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (uint32_t a = warm; a < n; a += batch) {
       uint32_t m = n - a < batch ? n - a : batch;
       for (uint32_t i = 0; i < m; i++) ptrs[i] = frames + (size_t)(a + i) * slot;
       if (vp_process_batch(vp_nf_context(), m, in_dev + a, ptrs, len + a,
@@ -111,6 +131,12 @@ int main(int argc, char **argv) {
       }
     }
     free(ptrs);
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  if (n > warm) {
+    const double el = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    fprintf(stderr, "timed %u packets: %.6f s, %.3f us/packet, %.2f Kpps\n", n - warm, el,
+            1e6 * el / (n - warm), (n - warm) / el / 1e3);
   }
   const char *nd = getenv("VIGPATH_NB_DEVICES");
   const uint32_t nb_devices = nd ? (uint32_t)atoi(nd) : 2u;

@@ -350,9 +350,19 @@ int vp_last_kernel_ms(vp_ctx *ctx, float *ms, int *launches);
  * its segments, from HIP events between the stages: ms[0] pass 1 (classify,
  * keys routed), ms[1] offsets (counts all-to-all, overflow all-reduce),
  * ms[2] keys all-to-all, ms[3] owner probe, ms[4] answers all-to-all,
- * ms[5] pass 2 (routed packets rewritten, touches binned), ms[6] fold.
- * *stages = 7, or 0 when nothing was recorded. ms must hold 7 floats. */
+ * ms[5] pass 2 (routed packets rewritten, touches binned), ms[6] fold;
+ * the chunked pipeline records ms[7], its chunks' passes,
+ * exchanges and probes together (they overlap), and ms[6] only. *stages = 7
+ * or 8, or 0 when nothing was recorded. ms must hold 8 floats. */
 int vp_last_stage_ms(vp_ctx *ctx, float *ms, int *stages);
+
+/* Diagnostics (bench.py): the memory-shape ceiling of the classify tile --
+ * n slots of `slot` (64 or 128) bytes at `frames` (device memory, n a
+ * multiple of 64) streamed with nat_classify64's grid and access shape, each
+ * slot read and, store != 0, written back unchanged (write-through). *ms =
+ * the mean duration of `reps` launches, each timed by its own dispatch's
+ * timestamps. DESIGN.md §5.1. */
+int vp_probe_slots(void *frames, uint32_t n, uint32_t slot, int store, int reps, float *ms);
 
 /* Build identification (e.g. "vigpath gfx950"). */
 const char *vp_version(void);

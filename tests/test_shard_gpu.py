@@ -53,6 +53,7 @@ def _worker(rank, world, port, spec, outdir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     if spec.get("own_cap"):  # owner mode: force the padded exchange's capacity
         os.environ["VIGPATH_OWN_CAP"] = str(spec["own_cap"])
+    os.environ.update(spec.get("env", {}))  # (e.g. the chunked pipeline's geometry)
     import vigor_amd
     from gpuh import run_gpu
     from vigor_amd import shard
@@ -173,6 +174,74 @@ def test_owner_padded_exchange_overflow(world, spec):
     packets alone and the exact exchange answers them; the results are
     still the single NF's."""
     check_sharded(dict(spec, mode="owner"), world)
+
+
+# The chunked owner pipeline (DESIGN.md §6) in chunks of 4 blocks x 4 tiles
+# (1024 packets) instead of the resident grid x 2^20 packets: batches of
+# thousands of packets take many chunks, alternating the two buffer sets.
+CHUNKS = {"VIGPATH_OWN_BLOCKS": "4", "VIGPATH_OWN_CHUNK": "1024"}
+
+
+@pytest.mark.parametrize("world,spec", [
+    (2, dict(SPECS[0][1], env=CHUNKS)),
+    (3, dict(SPECS[1][1], env=CHUNKS)),
+    (4, dict(SPECS[3][1], env=CHUNKS)),
+    (2, dict(SPECS[4][1], env=CHUNKS)),
+    (2, dict(SPECS[0][1], env=CHUNKS, own_cap=64)),
+    (4, dict(SPECS[3][1], env=CHUNKS, own_cap=40)),
+])
+def test_owner_chunked_pipeline(world, spec):
+    """Owner mode through the chunked pipeline with many chunks per segment
+    (pass 1 / exchange / probe / pass 2 per chunk on two streams, touch bins
+    over virtual blocks), with and without slices that overflow (the
+    leftover exchange and the second, stamp-raising fold): the single NF's
+    results."""
+    check_sharded(dict(spec, mode="owner"), world)
+
+
+def _worker_route_all(outdir, env, n, cuts):
+    """One rank with a one-rank RCCL communicator, every LAN key routed
+    through the exchange to itself (bench.py --route-all), in chunks."""
+    os.environ.update(env)
+    os.environ["VIGPATH_ROUTE_ALL"] = "1"
+    import ctypes as C
+    import vigor_amd
+    from gpuh import check_batches
+    from vigor_amd import shard
+    args = ["--wan", "1", "--expire", "60000000", "--starting-port", "0",
+            "--max-flows", "4096", "--extip", "192.168.4.2", "--eth-dest",
+            "0," + END_MACS[0].hex(":"), "--eth-dest", "1," + END_MACS[1].hex(":")]
+    nat = vigor_amd.Nat(vigor_amd.nat_config_from_args(args, 2, DEV_MACS), gpu=0)
+    uid = (C.c_uint8 * 128).from_buffer_copy(shard.rccl_unique_id())
+    assert nat.L.vp_attach_rccl(nat.h, uid, 1, 0) == 0
+    shard.set_mode(nat, "owner")
+    rng = np.random.default_rng(11)
+    fr, ln, dv, now = mixed_nat_trace(rng, n, 3000, max_idx=4096)
+    cfg = orc.nat_cfg(wan=1, start_port=0, ext_ip=T.ip4(192, 168, 4, 2),
+                      expire_us=60_000_000, max_flows=4096, device_macs=DEV_MACS,
+                      endpoint_macs=END_MACS)
+    o = orc.Oracle("nat", cfg)
+    check_batches(nat, o, fr, ln, dv, now, 64, cuts)
+    oa, ots, ok = o.nat_dump(4096)
+    ga, gts, gk = nat.dump()
+    np.testing.assert_array_equal(ga, oa)
+    np.testing.assert_array_equal(gts[oa == 1], ots[oa == 1])
+    np.testing.assert_array_equal(gk[oa == 1], ok[oa == 1])
+    open(os.path.join(outdir, "ok"), "w").write("ok")
+
+
+@pytest.mark.parametrize("env", [dict(CHUNKS), dict(CHUNKS, VIGPATH_OWN_CAP="96")])
+def test_owner_route_all_chunked_rccl(env):
+    """bench.py --route-all's configuration (one rank, a real RCCL
+    communicator, every key through the exchange) in many chunks, with and
+    without overflowing slices: bit-exact with the oracle."""
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        p = ctx.Process(target=_worker_route_all, args=(d, env, 30_000, [6400, 19_200]))
+        p.start()
+        p.join(timeout=300)
+        assert p.exitcode == 0
+        assert os.path.exists(os.path.join(d, "ok"))
 
 
 def check_sharded(spec, world):

@@ -126,7 +126,7 @@ EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_fw_create",
            "vp_attach_comm", "vp_shard_mode", "vp_sync_state", "vp_live_count",
            "vp_kernel_timing", "vp_last_kernel_ms", "vp_version", "vp_table_stats_get",
            "vp_last_error", "vp_register_host", "vp_unregister_host", "vp_process_mbufs",
-           "vp_last_stage_ms", "vp_comm_abort"]
+           "vp_last_stage_ms", "vp_comm_abort", "vp_probe_slots"]
 
 _libs = {}
 
@@ -199,6 +199,9 @@ def lib(path: str | None = None):
     L.vp_sync_state.restype = C.c_int
     L.vp_comm_abort.argtypes = [C.c_void_p]
     L.vp_comm_abort.restype = C.c_int
+    L.vp_probe_slots.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int,
+                                 C.POINTER(C.c_float)]
+    L.vp_probe_slots.restype = C.c_int
     L.vp_live_count.argtypes = [C.c_void_p]
     L.vp_live_count.restype = C.c_int64
     L.vp_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float),

@@ -25,8 +25,11 @@ struct Comm {
   // transport (the caller reads it from `send` where it lies)
   // abandon every collective of this rank (vp_comm_abort; any thread)
   virtual int abort() { return 0; }
+  // (on stream `s`, default the context's: the chunked owner pipeline runs its
+  // exchanges on a stream of their own)
   virtual int alltoallv_dev(vp_ctx *c, const void *send, const size_t *sbytes,
-                            void *recv, const size_t *rbytes, bool skip_self = false) = 0;
+                            void *recv, const size_t *rbytes, bool skip_self = false,
+                            hipStream_t s = nullptr) = 0;
 };
 
 }  // namespace vp

@@ -96,8 +96,9 @@ struct RcclComm : Comm {
   // one grouped send/recv per peer: every pair of GPUs talks over its own
   // xGMI link at once
   int alltoallv_dev(vp_ctx *c, const void *send, const size_t *sbytes, void *recv,
-                    const size_t *rbytes, bool skip_self) override {
+                    const size_t *rbytes, bool skip_self, hipStream_t st) override {
     VP_TRY(live());
+    if (!st) st = c->stream;
     const uint8_t *s = static_cast<const uint8_t *>(send);
     uint8_t *d = static_cast<uint8_t *>(recv);
     size_t so = 0, ro = 0;
@@ -111,19 +112,19 @@ struct RcclComm : Comm {
     if (sbytes[r] != rbytes[r]) return VP_EINVAL;
     if (sbytes[r] && !skip_self)
       VP_HIP(hipMemcpyAsync(d + roff[r], s + soff[r], sbytes[r],
-                            hipMemcpyDeviceToDevice, c->stream));
+                            hipMemcpyDeviceToDevice, st));
     VP_NCCL(ncclGroupStart());
     for (int q = 0; q < n; q++) {
       if (q == r) continue;
       if (sbytes[q]) {
-        ncclResult_t e = ncclSend(s + soff[q], sbytes[q], ncclUint8, q, comm, c->stream);
+        ncclResult_t e = ncclSend(s + soff[q], sbytes[q], ncclUint8, q, comm, st);
         if (e != ncclSuccess) {
           ncclGroupEnd();
           return nccl_fail(e, "ncclSend");
         }
       }
       if (rbytes[q]) {
-        ncclResult_t e = ncclRecv(d + roff[q], rbytes[q], ncclUint8, q, comm, c->stream);
+        ncclResult_t e = ncclRecv(d + roff[q], rbytes[q], ncclUint8, q, comm, st);
         if (e != ncclSuccess) {
           ncclGroupEnd();
           return nccl_fail(e, "ncclRecv");
@@ -174,18 +175,19 @@ struct HostComm : Comm {
     return 0;
   }
   int alltoallv_dev(vp_ctx *c, const void *send, const size_t *sbytes, void *recv,
-                    const size_t *rbytes, bool skip_self) override {
+                    const size_t *rbytes, bool skip_self, hipStream_t st) override {
     if (!ops.alltoallv) return VP_ENOTSUP;
-    size_t st = 0, rt = 0, r0 = 0;  // r0: where this rank's own chunk lands in recv
+    if (!st) st = c->stream;
+    size_t sn = 0, rt = 0, r0 = 0;  // r0: where this rank's own chunk lands in recv
     for (int q = 0; q < n; q++) {
       if (q == r) r0 = rt;
-      st += sbytes[q];
+      sn += sbytes[q];
       rt += rbytes[q];
     }
-    hs.resize(st ? st : 1);
+    hs.resize(sn ? sn : 1);
     hr.resize(rt ? rt : 1);
-    if (st) VP_HIP(hipMemcpyAsync(hs.data(), send, st, hipMemcpyDeviceToHost, c->stream));
-    VP_HIP(hipStreamSynchronize(c->stream));
+    if (sn) VP_HIP(hipMemcpyAsync(hs.data(), send, sn, hipMemcpyDeviceToHost, st));
+    VP_HIP(hipStreamSynchronize(st));
     if (ops.alltoallv(ops.user, hs.data(), sbytes, hr.data(), rbytes))
       return comm_fail("alltoallv");
     // (skip_self: the callback moved every chunk, the own one is not copied
@@ -193,11 +195,11 @@ struct HostComm : Comm {
     const size_t own = skip_self ? rbytes[r] : 0;
     uint8_t *d = static_cast<uint8_t *>(recv);
     if (r0)
-      VP_HIP(hipMemcpyAsync(d, hr.data(), r0, hipMemcpyHostToDevice, c->stream));
+      VP_HIP(hipMemcpyAsync(d, hr.data(), r0, hipMemcpyHostToDevice, st));
     if (rt > r0 + own)
       VP_HIP(hipMemcpyAsync(d + r0 + own, hr.data() + r0 + own, rt - r0 - own,
-                            hipMemcpyHostToDevice, c->stream));
-    VP_HIP(hipStreamSynchronize(c->stream));
+                            hipMemcpyHostToDevice, st));
+    VP_HIP(hipStreamSynchronize(st));
     return 0;
   }
 };

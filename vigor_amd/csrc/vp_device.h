@@ -434,6 +434,10 @@ __device__ __forceinline__ void bins_publish(const TouchBins &bins, const uint32
 // XCD-aware range order, as every block streams its own DRAM
 // pages and its packets' table rows stay near each other in its XCD's L2.
 // `cur` is kCurs LDS counters, zeroed by the kernel before its barrier.
+// Virtual blocks (vper != 0; the chunked owner pipeline, vp_nat.hip): the
+// launch is blocks vb0 .. vb0 + gridDim.x - 1 of a grid whose every block
+// owns vper tiles of [p0, p1); the per-block slices (bins, rq) are indexed by
+// the virtual block.
 template <uint32_t kOvf = kCurOverflow, class Issue, class Finish>
 __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
                                                const uint16_t *len,
@@ -444,7 +448,8 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
                                                Finish finish,
                                                const TouchBins &bins,
                                                const TileQueue &rq,
-                                               uint32_t *cur) {
+                                               uint32_t *cur, uint32_t vb0 = 0,
+                                               uint32_t vper = 0) {
   // (the wave index as a scalar: the tile stores' buffer resources are
   // provably uniform, no waterfall loops)
   const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -465,8 +470,8 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
     m_in = p < n_all ? in_dev[p] : 0u;
     m_len = p < n_all ? len[p] : 0u;
   };
-  const uint32_t rb = blockIdx.x;
-  const uint32_t per_b = (tiles + gridDim.x - 1) / gridDim.x;
+  const uint32_t rb = vb0 + blockIdx.x;
+  const uint32_t per_b = vper ? vper : (tiles + gridDim.x - 1) / gridDim.x;
   uint32_t tile = rb * per_b + wv;
   const uint32_t tend = min(tiles, rb * per_b + per_b), tstep = 4;
   const uint32_t range0 = first + rb * per_b * 64;  // this block's first packet

@@ -65,9 +65,10 @@ hipError_t launch_timed(void (*k)(P...), dim3 grid, dim3 block, hipStream_t s,
 }
 
 // Owner-mode phase A stages (vp_last_stage_ms).
-constexpr int kStages = 7;
+constexpr int kStages = 8;
 inline constexpr const char *kStageNames[kStages] = {
-    "pass1", "offsets", "a2a_keys", "probe", "a2a_answers", "pass2", "fold"};
+    "pass1", "offsets", "a2a_keys", "probe", "a2a_answers", "pass2", "fold", "pipeline"};
+constexpr int kStageFold = 6, kStagePipeline = 7;
 
 struct Comm;  // vp_comm.hip: collectives between the ranks of one NF
 constexpr int kMaxRanks = 64;
@@ -84,6 +85,10 @@ struct Ctl {
   uint32_t defer_count;    // }
   uint32_t touch_ovf;      // } a touch-bin slice overflowed (TouchBins)
   uint32_t reprobe_count;  // } home bucket full of other keys (vp_nat.hip)
+  uint32_t route_ovf;   // } owner mode: some rank's keys for an owner exceeded the
+                        //   padded exchange's capacity (the unchunked pipeline:
+                        //   all ranks agree, allreduced; the chunked one: this
+                        //   rank's own slices, gathered before the fold)
   uint32_t exp_count;
   uint32_t tomb_reused;
   uint64_t min_ts;
@@ -93,8 +98,6 @@ struct Ctl {
   uint32_t disp_count;  // inserts that passed their home bucket (since rebuild)
   uint32_t sh_live;     // entries in this rank's buckets (= n_live unless owner mode)
   uint32_t own_new;     // owner mode: union keys this rank will insert (upper bound)
-  uint32_t route_ovf;   // owner mode: some rank's keys for an owner exceeded the
-                        // padded exchange's capacity (all ranks agree: allreduced)
   uint32_t pad_;
 };
 
@@ -103,7 +106,7 @@ struct Ctl {
 // Multi-GPU: the fold also publishes every rank's segment counters
 // (miss, defer, touch_ovf, reprobe: gathered on the device before the fold)
 // and, owner mode, this rank's key count per owner.
-constexpr int kPubGath = 4;  // words per rank
+constexpr int kPubGath = 5;  // words per rank (miss_count .. route_ovf)
 struct CtlPub {
   Ctl ctl;
   uint32_t xtra[(kPubGath + 1) * 64];
@@ -211,6 +214,16 @@ struct Workspace {
   size_t xsend_n = 0;
   uint64_t *ovf64 = nullptr;
   bool ovf64_clean = false;  // ovf64 is zero (the last exchange did not overflow)
+  // the chunked owner pipeline (vp_nat.hip nat_phase_a_owner_chunked): the
+  // exchange stream, and per chunk parity the events "pass 1 done" and
+  // "answers back"; a second set of the padded exchange's buffers
+  hipStream_t xstream = nullptr;
+  hipEvent_t ev_p1[2] = {}, ev_ans[2] = {};
+  uint4 *sendk2 = nullptr, *recvk2 = nullptr;
+  uint32_t *reply2 = nullptr, *rreply2 = nullptr;
+  size_t sendk2_n = 0, recvk2_n = 0, reply2_n = 0, rreply2_n = 0;
+  uint32_t *lcnt = nullptr;  // leftover exchange: keys past each slice
+  size_t lcnt_n = 0;
   // multi-GPU: the ranks' segment counters gathered on the device before a
   // fold (kPubGath words each) and their host copy (gath_ok: this segment's)
   uint32_t *gath = nullptr;
@@ -328,6 +341,10 @@ struct vp_ctx {
   vp::Comm *comm = nullptr;
   int shard_mode = 0;  // VP_SHARD_REPLICATED / VP_SHARD_OWNER
   uint32_t off = 0;
+  // the current segment's global packet range (run_batch_sharded): every rank
+  // derives every rank's part of it from rank_n (the chunked owner pipeline's
+  // chunk count is the same everywhere)
+  uint64_t seg_g0 = 0, seg_g1 = 0;
   // owner mode: keys per peer the padded exchange carries in this batch (0:
   // exact exchange), and this rank's largest per-owner key count last seen
   uint32_t own_cap = 0;

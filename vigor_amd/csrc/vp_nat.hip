@@ -109,6 +109,21 @@ __device__ __forceinline__ uint32_t flowid_hash_batched(const uint32_t *T, uint3
 // routed packets from the owners' replies.
 constexpr uint32_t kRouteBit = 0x80000000u;
 constexpr uint32_t kRouted = 0xFFFFFFFBu;  // touch: the packet was routed
+// Exchange modes (Route::mode):
+//   kOwnPadded    one pass 1 / exchange / pass 2 per segment over the padded
+//                 exchange, the slice counts exchanged beside the keys and a
+//                 slice overflow allreduced (every rank then takes the exact
+//                 exchange; cap == 0: the exact exchange itself);
+//   kOwnChunked   the chunked pipeline (nat_phase_a_owner_chunked): one
+//                 padded exchange per chunk of the segment, on a stream of its
+//                 own beside the passes; a block closes its key slices with
+//                 sentinel keys (the owner needs no counts), a key past its
+//                 slice sets this rank's *lovf and waits;
+//   kOwnLeftover  after any rank's *lovf: the exact exchange of the keys
+//                 past their slices only (pass 2 finishes just those packets).
+enum : uint32_t { kOwnPadded = 0, kOwnChunked = 1, kOwnLeftover = 2 };
+constexpr uint32_t kKeySentinelW = 0xFFFFFFFFu;  // key.w of an empty slot (a routed
+                                                 // key's is in_dev | proto << 16)
 struct Route {
   uint32_t n, r;          // ranks, this rank (n == 0: single table)
   uint4 *desc;            // [block][n][range] keys by owner
@@ -132,8 +147,12 @@ struct Route {
   // sub; pass 1 writes them there itself, past sub into desc)
   uint4 *sendk;
   uint32_t sub;
+  uint32_t mode;   // kOwnPadded / kOwnChunked / kOwnLeftover
+  uint32_t *lovf;  // kOwnChunked: this rank's slice-overflow flag (Ctl::route_ovf)
+  uint32_t *need;  // kOwnChunked: per owner, the largest slice of any block (atomicMax)
 };
 constexpr uint32_t kNoReply = 0xFFFFFFFAu;  // route_answer: not answered in this pass
+constexpr uint32_t kAnswered = 0xFFFFFFF9u;  // route_answer: answered by an earlier pass
 
 struct NatArgs {
   uint8_t *frames;
@@ -164,6 +183,10 @@ struct NatArgs {
   // per block at its end, not by one global atomic per wave (a churn batch
   // has misses in every wave); null elsewhere
   uint32_t *mq;
+  // virtual blocks (vper != 0, the chunked owner pipeline): this launch is
+  // blocks vb0 .. vb0 + gridDim.x - 1 of a segment-wide grid whose blocks own
+  // vper tiles each (frames64_tiles, vp_device.h)
+  uint32_t vb0, vper;
 };
 
 // The register path's total_length bound for 64-byte slots (every L4 byte in
@@ -175,19 +198,44 @@ __device__ __forceinline__ uint32_t nat_tail(const NatArgs &a, uint32_t p) {
   return a.tail ? a.tail[p] : 0u;
 }
 
+// Lanes with `v` reserve consecutive slots of counter ctr[ch] (LDS): one
+// atomic per distinct counter in the wave (a wave's routed keys go to few
+// owners; one atomic per lane serialised a wave 64 deep on one counter).
+// Returns the lane's slot.
+__device__ __forceinline__ uint32_t multi_reserve(uint32_t *ctr, uint32_t ch, bool v) {
+  uint64_t pend = __ballot(v);
+  uint32_t res = 0;
+  const uint32_t lane = __lane_id();
+  while (pend) {
+    const uint32_t lead = (uint32_t)__ffsll((unsigned long long)pend) - 1;
+    const uint32_t lc = (uint32_t)__shfl((int)ch, (int)lead);
+    const uint64_t same = __ballot(v && ch == lc) & pend;
+    uint32_t base = 0;
+    if (lane == lead) base = atomicAdd(&ctr[lc], (uint32_t)__popcll(same));
+    base = (uint32_t)__shfl((int)base, (int)lead);
+    if ((same >> lane) & 1ull) res = base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+    pend &= ~same;
+  }
+  return res;
+}
+
 // Owner mode: hand the LAN packet with key `key` (hash h) to its owner if
-// that is another rank. Returns true when routed.
+// that is another rank. Returns true when routed. (Lanes that do not call
+// it take no part in the reservation: it runs on the calling lanes.)
 __device__ __forceinline__ bool nat_route(const NatArgs &a, uint32_t p, uint32_t h,
                                           const uint32_t key[4]) {
   if (!a.own.n) return false;
   const uint32_t o = owner_of(h, a.own.n);
-  if (o == a.own.r && !a.own.all) return false;
-  const uint32_t k = atomicAdd(&a.own.cur[o], 1u);
+  const bool go = o != a.own.r || a.own.all;
+  const uint32_t k = multi_reserve(a.own.cur, o, go);
+  if (!go) return false;
   const uint4 v = make_uint4(key[0], key[1], key[2], key[3]);
-  if (k < a.own.sub)  // (the padded exchange's own slice: no packing pass)
+  if (k < a.own.sub) {  // (the padded exchange's own slice: no packing pass)
     a.own.sendk[(size_t)o * a.own.cap + (size_t)blockIdx.x * a.own.sub + k] = v;
-  else
-    a.own.desc[((size_t)blockIdx.x * a.own.n + o) * a.own.range + k] = v;
+  } else {
+    a.own.desc[((size_t)(a.vb0 + blockIdx.x) * a.own.n + o) * a.own.range + k] = v;
+    if (a.own.mode == kOwnChunked) atomicOr(a.own.lovf, 1u);  // (rare: skew)
+  }
   a.own.route[p] = kRouteBit | (o << 24) | k;
   return true;
 }
@@ -443,12 +491,24 @@ __device__ __forceinline__ uint32_t route_note(const NatArgs &a, uint32_t p,
   return touch == kReprobe ? kReprobe : kNone;  // pass 2 bins the touches
 }
 
-// Owner mode: publish this block's key count per owner (after a barrier).
-__device__ __forceinline__ void route_publish(const NatArgs &a, const uint32_t *cur) {
+// Owner mode: publish (virtual) block rb's key count per owner (after a
+// barrier); the chunked pipeline also closes each of the block's slices with
+// sentinel keys and raises need[o] to its slice's count.
+__device__ __forceinline__ void route_publish(const NatArgs &a, const uint32_t *cur,
+                                              uint32_t rb) {
   if (!a.own.n) return;
   __syncthreads();
-  for (uint32_t o = threadIdx.x; o < a.own.n; o += blockDim.x)
-    a.own.dcnt[(size_t)blockIdx.x * a.own.n + o] = cur[o];
+  for (uint32_t o = threadIdx.x; o < a.own.n; o += blockDim.x) {
+    a.own.dcnt[(size_t)rb * a.own.n + o] = cur[o];
+    if (a.own.mode == kOwnChunked && cur[o]) atomicMax(&a.own.need[o], cur[o]);
+  }
+  if (a.own.mode != kOwnChunked) return;
+  const uint4 none = make_uint4(0u, 0u, 0u, kKeySentinelW);
+  for (uint32_t o = 0; o < a.own.n; o++) {
+    uint4 *sl = a.own.sendk + (size_t)o * a.own.cap + (size_t)blockIdx.x * a.own.sub;
+    for (uint32_t j = min(cur[o], a.own.sub) + threadIdx.x; j < a.own.sub; j += blockDim.x)
+      sl[j] = none;
+  }
 }
 
 // One packet, its slot's first 64 bytes in registers (any slot size; frames
@@ -498,7 +558,7 @@ __global__ __launch_bounds__(256) void nat_classify(NatArgs a) {
     const uint32_t b0 = a.own.first + blockIdx.x * a.own.range;
     const uint32_t b1 = min(a.p1, b0 + a.own.range);
     for (uint32_t p = b0 + threadIdx.x; p < b1; p += blockDim.x) nat_lane(a, T, p);
-    route_publish(a, dcur);
+    route_publish(a, dcur, blockIdx.x);
     return;
   }
   const uint32_t stride = gridDim.x * blockDim.x;
@@ -685,8 +745,8 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
     m_in = p < n_all ? a.in_dev[p] : 0u;
     m_len = p < n_all ? a.len[p] : 0u;
   };
-  const uint32_t rb = blockIdx.x;
-  const uint32_t per_b = (tiles + gridDim.x - 1) / gridDim.x;
+  const uint32_t rb = a.vb0 + blockIdx.x;  // (virtual blocks: the chunked pipeline)
+  const uint32_t per_b = a.vper ? a.vper : (tiles + gridDim.x - 1) / gridDim.x;
   uint32_t tile = rb * per_b + wv;
   const uint32_t tend = min(tiles, rb * per_b + per_b), tstep = 4;
   const uint32_t range0 = first + rb * per_b * 64;  // this block's first packet
@@ -969,7 +1029,10 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
           m = true;
         }
       }
-      touch = route_note(a, p, t1);  // (the touch log is off in owner pass 1)
+      // (the touch log is off in owner pass 1 when pass 2 bins; an unaligned
+      // segment folds the log: every packet's entry, pass 2 writes the routed)
+      log_put(a.log, p, t1 == kRouted || t1 == kReprobe ? kNone : t1);
+      touch = route_note(a, p, t1);
       {  // queue on this block's reprobe slice
         const bool v = touch == kReprobe;
         const uint32_t k = group_reserve(cur, kCurReprobe, v);
@@ -1063,7 +1126,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
     const uint32_t *src = a.mq + (size_t)rb * per_b * 64;
     for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) a.miss[mbase + i] = src[i];
   }
-  route_publish(a, cur + kCurDest);
+  route_publish(a, cur + kCurDest, rb);
 }
 
 __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_all,
@@ -1427,6 +1490,26 @@ __global__ __launch_bounds__(256) void route_pack(const uint4 *desc, const uint4
   }
 }
 
+// Leftover exchange (the chunked pipeline, after a slice overflowed): per
+// (virtual block, owner) the keys past the slice's `sub`, and those keys
+// packed tight from desc (route_scan / route_base give the offsets).
+__global__ void route_left(const uint32_t *dcnt, uint32_t m, uint32_t sub, uint32_t *lcnt) {
+  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < m; x += gridDim.x * blockDim.x)
+    lcnt[x] = dcnt[x] > sub ? dcnt[x] - sub : 0u;
+}
+__global__ __launch_bounds__(256) void route_pack_left(const uint4 *desc, const uint32_t *dcnt,
+                                                       const uint32_t *dbase, uint32_t n,
+                                                       uint32_t range, uint32_t sub,
+                                                       uint4 *out) {
+  const uint32_t b = blockIdx.x;
+  for (uint32_t o = 0; o < n; o++) {
+    const uint32_t cnt = dcnt[(size_t)b * n + o];
+    const uint32_t base = dbase[(size_t)b * n + o];
+    const uint4 *src = desc + ((size_t)b * n + o) * range;
+    for (uint32_t k = sub + threadIdx.x; k < cnt; k += blockDim.x) out[base + k - sub] = src[k];
+  }
+}
+
 // The owner side of C1: map_get (find_key, map-impl-pow2.c:629-732) of every
 // received FlowId in this rank's buckets. Tiles of 64 keys per wave (one
 // 1 KiB load; the next tile's keys in flight while this one is matched), a
@@ -1454,8 +1537,10 @@ __global__ __launch_bounds__(256, 4) void nat_own_probe(TableDev t, const uint32
                                                         uint32_t *own_reply) {
   __shared__ uint32_t T[kNatTabWords];
   __shared__ uint4 stage[4][256];
-  const bool skip = cap && *ovf;
-  if (blockIdx.x == 0 && threadIdx.x == 0) ctl->route_ovf = skip ? 1u : 0u;
+  // (sentinel slices, the chunked pipeline: rcnt and ovf null; the rank's
+  // own flag is pass 1's)
+  const bool skip = cap && ovf && *ovf;
+  if (ovf && blockIdx.x == 0 && threadIdx.x == 0) ctl->route_ovf = skip ? 1u : 0u;
   if (skip) return;
   if (t.mix == kMixLin)
     for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) T[kCrcWords + i] = t.lin[i];
@@ -1491,7 +1576,12 @@ __global__ __launch_bounds__(256, 4) void nat_own_probe(TableDev t, const uint32
     Tile x{false, make_uint4(0, 0, 0, 0)};
     if (tl < tend) {
       const uint32_t j0 = tl * 64, j = j0 + lane;
-      if (cap && (cap & 63) == 0) {
+      if (cap && !rcnt) {  // sentinel slices: every slot loaded, empty ones marked
+        if (j < n) {
+          x.k = (own(j) ? own_keys + j : keys + j)[0];
+          x.act = x.k.w != kKeySentinelW;
+        }
+      } else if (cap && (cap & 63) == 0) {
         // the tile's peer and slice, once per tile (scalar): with chunks and
         // slices of whole tiles a tile lies in one slice
         const uint32_t q = j0 / cap, l0 = j0 - q * cap;
@@ -1591,11 +1681,19 @@ __device__ __forceinline__ void nat_lan_fast(const NatArgs &a, RFrame &f, uint32
   a.out[p] = a.wan;
 }
 
-// The answer for packet p's route (kRouteBit set), or kNoReply.
+// The answer for packet p's route (kRouteBit set), kNoReply (the exact
+// exchange's) or kAnswered (an earlier pass 2 finished it).
 __device__ __forceinline__ uint32_t route_answer(const NatArgs &a, uint32_t p,
                                                  uint32_t rt) {
   const uint32_t o = (rt >> 24) & 63, k = rt & 0xFFFFFFu;
   const uint32_t blk = (p - a.own.first) / a.own.range;
+  if (a.own.mode == kOwnChunked)  // this chunk's replies; the launch's blocks
+    return k < a.own.sub                                   // are its slices
+               ? a.own.rreply[(size_t)o * a.own.cap + (size_t)(blk - a.vb0) * a.own.sub + k]
+               : kNoReply;
+  if (a.own.mode == kOwnLeftover)  // the exact exchange of the keys past their slices
+    return k < a.own.sub ? kAnswered
+                         : a.own.rreply[a.own.dbase[(size_t)blk * a.own.n + o] + k - a.own.sub];
   if (a.own.cap) {  // padded (no rank overflowed a slice: every k < sub)
     if (*a.own.ovf) return kNoReply;
     return a.own.rreply[(size_t)o * a.own.cap + (size_t)blk * a.own.sub + k];
@@ -1624,11 +1722,13 @@ __global__ __launch_bounds__(256, 4) void nat_remote64(NatArgs a, uint32_t n_all
         const uint32_t rt = a.own.route[p];
         if (rt == kNone) return P;
         if (!(rt & kRouteBit)) {
+          if (a.own.mode == kOwnLeftover) return P;  // (binned by the first pass 2)
           P.kind = 1;  // pass 1's own touch
           P.idx = rt;
         } else {
           P.idx = route_answer(a, p, rt);
-          P.kind = P.idx == kNoReply ? 0 : 2;  // (no reply: the exact exchange's)
+          // (no reply: the exact exchange's; answered: an earlier pass 2's)
+          P.kind = P.idx == kNoReply || P.idx == kAnswered ? 0 : 2;
         }
         return P;
       },
@@ -1636,6 +1736,7 @@ __global__ __launch_bounds__(256, 4) void nat_remote64(NatArgs a, uint32_t n_all
           uint32_t len, uint32_t &touch) -> uint32_t {
         if (P.kind == 0) return 0u;
         if (P.kind == 1) {
+          log_put(a.log, p, P.idx);  // (the lean pass-1 tile logs nothing)
           touch = P.idx;
           return 0u;
         }
@@ -1655,7 +1756,7 @@ __global__ __launch_bounds__(256, 4) void nat_remote64(NatArgs a, uint32_t n_all
         nat_lan_fast(a, f, p, P.idx);
         return 0xFu;  // the whole slot: whole-line writes
       },
-      bins, TileQueue{}, cur);
+      bins, TileQueue{}, cur, a.vb0, a.vper);
 }
 
 // Pass 2, any slot size: routed packets only, one lane each (byte path).
@@ -1665,7 +1766,7 @@ __global__ void nat_remote_lane(NatArgs a) {
     const uint32_t rt = a.own.route[p];
     if (rt == kNone || !(rt & kRouteBit)) continue;
     const uint32_t idx = route_answer(a, p, rt);
-    if (idx == kNoReply) continue;  // the exact exchange answers it
+    if (idx == kNoReply || idx == kAnswered) continue;  // the exact exchange's
     a.log[p] = idx;
     if (idx == kNone) {
       a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
@@ -1753,6 +1854,7 @@ struct PhaseA {
 // VIGPATH_PHASES=1 also prints them per segment on stderr (diagnostics).
 struct PhaseMarks {
   hipEvent_t ev[kStages + 1] = {};
+  int id[kStages + 1] = {};  // the stage that ends at mark i
   int n = 0;
   bool on = false, print_on = false;
   PhaseMarks(hipStream_t s, bool timing) : stream(s) {
@@ -1766,8 +1868,11 @@ struct PhaseMarks {
     if (on)
       for (auto &x : ev) (void)hipEventDestroy(x);
   }
-  void mark() {
-    if (on && n <= kStages) (void)hipEventRecord(ev[n++], stream);
+  // (stage: the one this mark ends; default the next in kStageNames order)
+  void mark(int stage = -1) {
+    if (!on || n > kStages) return;
+    id[n] = stage >= 0 ? stage : n - 1;
+    (void)hipEventRecord(ev[n++], stream);
   }
   void finish(vp_ctx *c, int rank, uint32_t np) {
     if (!on || n < 2) return;
@@ -1776,10 +1881,10 @@ struct PhaseMarks {
     for (int i = 1; i < n; i++) {
       float ms = 0.f;
       (void)hipEventElapsedTime(&ms, ev[i - 1], ev[i]);
-      c->stage_ms[i - 1] += ms;
-      if (print_on) fprintf(stderr, " %s %.3f", kStageNames[i - 1], ms);
+      c->stage_ms[id[i]] += ms;
+      c->stage_n = std::max(c->stage_n, id[i] + 1);
+      if (print_on) fprintf(stderr, " %s %.3f", kStageNames[id[i]], ms);
     }
-    c->stage_n = std::max(c->stage_n, n - 1);
     if (print_on) fprintf(stderr, " ms\n");
   }
   hipStream_t stream;
@@ -1963,6 +2068,285 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   return 0;
 }
 
+// ------------------------------------------------ chunked owner pipeline --
+// (off by default, nat_own_chunk_packets) The segment's tiles
+// are cut into K chunks of G blocks x vper
+// tiles. Chunk k runs pass 1 on the context's stream S; its keys cross, are
+// answered by nat_own_probe and come back on the exchange stream X while S
+// runs pass 1 of chunk k + 1; then S runs chunk k's pass 2, whose frame
+// reads find chunk k's frames still in the Infinity Cache (read by its pass 1
+// one chunk earlier; a chunk of 2^20 packets is 64 MB of the 256 MB), as do
+// the keys, routes and answers. Per chunk the exchange is the keys'
+// all-to-all, the probe and the answers' all-to-all: a block closes its
+// slices with sentinel keys, so no counts cross, and a key past its slice
+// raises this rank's overflow flag, gathered before the fold (no allreduce
+// per chunk). Two buffer sets alternate between chunks. Every rank runs the
+// same K (computed from every rank's part of the segment), so the exchanges
+// match. After the fold, if any rank overflowed, the keys past their slices
+// take the exact exchange (route_left / route_pack_left), a pass 2 over the
+// leftovers and a second fold that only raises stamps (BinsPlan::maxmode).
+struct OwnChunks {
+  uint32_t K = 0;     // chunks (0: the unchunked pipeline)
+  uint32_t G = 0;     // blocks per chunk launch
+  uint32_t vper = 0;  // tiles per (virtual) block
+};
+
+// Blocks per chunk launch: the resident grid of both passes (VIGPATH_OWN_BLOCKS
+// lowers it: tests cut small batches into many chunks).
+static uint32_t own_grid() {
+  static const uint32_t g = std::min(resident_grid((const void *)nat_classify64, 1u << 30),
+                                     resident_grid((const void *)nat_remote64, 1u << 30));
+  const char *e = getenv("VIGPATH_OWN_BLOCKS");
+  const uint32_t v = e ? (uint32_t)atoi(e) : 0u;
+  return v ? std::min(v, g) : g;
+}
+
+// Packets per chunk (VIGPATH_OWN_CHUNK; 0, the default: the unchunked
+// pipeline), rounded up to whole blocks of whole tiles. Off by default: on
+// one MI355X (bench.py --route-all) chunks of 2^19-2^21 packets made the
+// owner step 1.39-2.43 ms against 1.04 unchunked -- each chunk's launches
+// pay their ramp, tail and per-block table loads, pass 2 did not get faster
+// from the Infinity Cache, and a probe beside a pass 2 slows both (DESIGN.md
+// §6.1, profiles/r05de_owner_chunked_traces.txt). (Read per call: the tests
+// change it.)
+uint32_t nat_own_chunk_packets() {
+  const char *e = getenv("VIGPATH_OWN_CHUNK");
+  const uint64_t want = e ? strtoull(e, nullptr, 10) : 0;
+  if (!want) return 0u;
+  const uint64_t G = own_grid();
+  const uint64_t vper = std::max<uint64_t>(1, (want / 64 + G - 1) / G);
+  return (uint32_t)std::min<uint64_t>(vper * G * 64, 1ull << 30);
+}
+
+// The same decision on every rank: 64-byte slots with coalesced tiles, and
+// every rank's part of the segment starting on a tile (touch bins); K = the
+// most chunks any rank's part needs.
+static OwnChunks own_chunks_plan(vp_ctx *c, const vp_dev_batch *b) {
+  OwnChunks oc;
+  const uint32_t pk = nat_own_chunk_packets();
+  if (!pk || b->slot != 64 || !c->coalesced_io || c->rank_n.empty()) return oc;
+  const uint32_t G = own_grid();
+  const uint32_t vper = pk / 64 / G;
+  uint64_t off = 0, K = 0;
+  for (uint32_t q = 0; q < c->rank_n.size(); q++) {
+    const uint64_t n = c->rank_n[q];
+    const uint64_t l0 = std::min(std::max(c->seg_g0, off), off + n) - off;
+    const uint64_t l1 = std::min(std::max(c->seg_g1, off), off + n) - off;
+    off += n;
+    if (l1 <= l0) continue;
+    if (l0 & 63) return oc;  // (a cut inside a tile: no touch bins there)
+    const uint64_t tiles = (l1 - l0 + 63) / 64;
+    const uint64_t vg = (tiles + vper - 1) / vper;
+    K = std::max<uint64_t>(K, (vg + G - 1) / G);
+  }
+  oc.K = (uint32_t)K;
+  oc.G = G;
+  oc.vper = vper;
+  return oc;
+}
+
+static int nat_phase_a_owner_chunked(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
+                                     const NowSpec &now, uint32_t p0, uint32_t p1,
+                                     uint64_t seq0, const OwnChunks &oc, PhaseA *ph) {
+  FlowTable &t = c->ft;
+  Workspace &w = c->ws;
+  Comm &m = *c->comm;
+  const uint32_t n = (uint32_t)m.n, r = (uint32_t)m.r;
+  const uint32_t np = p1 - p0;
+  const uint32_t G = oc.G, vper = oc.vper, K = oc.K;
+  const uint32_t tiles = np ? (p1 - p0 + 63) / 64 : 0;
+  const uint32_t vg = (tiles + vper - 1) / vper;  // this rank's virtual blocks
+  ph->tiles64 = np != 0;
+  ph->grid1 = std::max<uint32_t>(vg, 1);
+  ph->range1 = vper * 64;
+  if (np) {
+    VP_TRY(tbl_bins_plan(c, t, (const void *)nat_remote64, p0, p1, &ph->bp, 4, 0, vper));
+    if (!ph->bp.on || ph->bp.grid != vg || ph->bp.range != vper * 64)
+      return state_fail("chunked owner pipeline: no touch bins for [%u, %u)", p0, p1);
+  }
+  const uint32_t C = std::max<uint32_t>(1, c->own_cap);  // keys per peer and chunk
+  // keys per block slice: C over the blocks a chunk launch of this rank has
+  // (the sender's layout alone: owners find the keys by their sentinels)
+  uint32_t sub = std::max<uint32_t>(1, C / std::max<uint32_t>(1, std::min(G, vg)));
+  if (sub >= 64) sub &= ~63u;  // (whole 64-key probe tiles per slice)
+  const size_t slices = (size_t)std::max<uint32_t>(vg, 1) * n;
+  VP_TRY(grow_dev(&w.desc, &w.desc_n, slices * ph->range1, c->stream));
+  VP_TRY(grow_dev(&w.dcnt, &w.dcnt_n, slices, c->stream));
+  if (!vg) VP_HIP(hipMemsetAsync(w.dcnt, 0, 4ull * n, c->stream));  // (leftovers: none)
+  VP_TRY(grow_dev(&w.dbase, &w.dbase_n, slices, c->stream));
+  VP_TRY(grow_dev(&w.dtot, &w.dtot_n, kMaxDest, c->stream));
+  VP_TRY(grow_dev(&w.dneed, &w.dneed_n, kMaxDest, c->stream));
+  VP_TRY(grow_dev(&w.route, &w.route_n, b->n, c->stream));
+  uint4 *sk[2], *rk[2];
+  uint32_t *rp[2], *rr[2];
+  VP_TRY(grow_dev(&w.sendk, &w.sendk_n, (size_t)n * C, c->stream));
+  VP_TRY(grow_dev(&w.recvk, &w.recvk_n, (size_t)n * C, c->stream));
+  VP_TRY(grow_dev(&w.reply, &w.reply_n, (size_t)n * C, c->stream));
+  VP_TRY(grow_dev(&w.rreply, &w.rreply_n, (size_t)n * C, c->stream));
+  VP_TRY(grow_dev(&w.sendk2, &w.sendk2_n, (size_t)n * C, c->stream));
+  VP_TRY(grow_dev(&w.recvk2, &w.recvk2_n, (size_t)n * C, c->stream));
+  VP_TRY(grow_dev(&w.reply2, &w.reply2_n, (size_t)n * C, c->stream));
+  VP_TRY(grow_dev(&w.rreply2, &w.rreply2_n, (size_t)n * C, c->stream));
+  sk[0] = w.sendk, sk[1] = w.sendk2, rk[0] = w.recvk, rk[1] = w.recvk2;
+  rp[0] = w.reply, rp[1] = w.reply2, rr[0] = w.rreply, rr[1] = w.rreply2;
+  if (!w.h_tot) VP_HIP(hipHostMalloc((void **)&w.h_tot, 4 * kMaxDest, hipHostMallocDefault));
+  if (!w.xstream) {
+    VP_HIP(hipStreamCreateWithFlags(&w.xstream, hipStreamNonBlocking));
+    for (int i = 0; i < 2; i++) {
+      VP_HIP(hipEventCreateWithFlags(&w.ev_p1[i], hipEventDisableTiming));
+      VP_HIP(hipEventCreateWithFlags(&w.ev_ans[i], hipEventDisableTiming));
+    }
+  }
+  static const bool one_stream = [] {  // (diagnostics: no overlap between the streams)
+    const char *e = getenv("VIGPATH_OWN_ONESTREAM");
+    return e && atoi(e);
+  }();
+  hipStream_t S = c->stream, X = one_stream ? c->stream : w.xstream;
+  static const uint32_t route_all = [] {
+    const char *e = getenv("VIGPATH_ROUTE_ALL");
+    return e && atoi(e) ? 1u : 0u;
+  }();
+  const uint32_t first = p0 & ~63u;
+  a.own = Route{n,       r,          w.desc, w.dcnt,    w.route, nullptr,
+                first,   ph->range1, w.dbase, nullptr,  C,       nullptr,
+                route_all, nullptr,  sub,    kOwnChunked, &t.ctl->route_ovf, w.dneed};
+  // (miss .. route_ovf; the per-owner slice maxima)
+  if (!t.ctl_clean) VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 20, S));
+  t.ctl_clean = false;
+  VP_HIP(hipMemsetAsync(w.dneed, 0, 4ull * n, S));
+  VP_HIP(ev_record(c->ktime, c->ev0, S));
+  PhaseMarks pm(S, c->ktime);
+  pm.mark();
+  const uint32_t gp = resident_grid((const void *)nat_own_probe, ((uint64_t)n * C + 255) / 256);
+  std::vector<size_t> sz(n, 16ull * C), sa(n, 4ull * C);
+  auto blocks = [&](uint32_t k) {  // this rank's blocks of chunk k
+    const uint32_t b0 = k * G;
+    return b0 < vg ? std::min(G, vg - b0) : 0u;
+  };
+  auto pass2 = [&](uint32_t k) -> int {
+    const uint32_t nb = blocks(k);
+    if (!nb) return 0;
+    NatArgs a2 = a;
+    a2.log = nullptr;  // (pass 2 bins every touch)
+    a2.vb0 = k * G;
+    a2.vper = vper;
+    a2.own.rreply = rr[k & 1];
+    nat_remote64<<<nb, 256, 0, S>>>(a2, b->n, ph->bp.bins);
+    VP_HIP(hipGetLastError());
+    return 0;
+  };
+  for (uint32_t k = 0; k < K; k++) {
+    const uint32_t i = k & 1;
+    // pass 1 of chunk k (its buffer set was last used by chunk k - 2)
+    if (k >= 2) VP_HIP(hipStreamWaitEvent(S, w.ev_ans[i], 0));
+    const uint32_t nb = blocks(k);
+    if (nb) {
+      NatArgs a1 = a;
+      a1.tileq = 1;
+      a1.mq = w.missq;
+      a1.log = nullptr;  // pass 2 bins every touch
+      a1.vb0 = k * G;
+      a1.vper = vper;
+      a1.own.sendk = sk[i];
+      nat_classify64<<<nb, 256, 0, S>>>(
+          a1, b->n, TouchBins{}, TileQueue{w.reprobe, w.reprobe_cnt, &t.ctl->reprobe_count});
+      VP_HIP(hipGetLastError());
+    } else {  // (no packets of this rank in chunk k: empty slices)
+      VP_HIP(hipMemsetAsync(sk[i], 0xFF, 16ull * n * C, S));
+    }
+    VP_HIP(hipEventRecord(w.ev_p1[i], S));
+    // chunk k's exchange on X: keys out, answered by their owners, back
+    VP_HIP(hipStreamWaitEvent(X, w.ev_p1[i], 0));
+    VP_TRY(m.alltoallv_dev(c, sk[i], sz.data(), rk[i], sz.data(), true, X));
+    nat_own_probe<<<gp, 256, 0, X>>>(tbl_dev(t), c->crc_tab, rk[i], n * C, C, nullptr, nullptr,
+                                     t.ctl, rp[i], r, sk[i], rr[i]);
+    VP_HIP(hipGetLastError());
+    VP_TRY(m.alltoallv_dev(c, rp[i], sa.data(), rr[i], sa.data(), true, X));
+    VP_HIP(hipEventRecord(w.ev_ans[i], X));
+    // pass 2 of chunk k - 1 behind pass 1 of chunk k
+    if (k >= 1) {
+      VP_HIP(hipStreamWaitEvent(S, w.ev_ans[i ^ 1], 0));
+      VP_TRY(pass2(k - 1));
+    }
+  }
+  if (K) {
+    VP_HIP(hipStreamWaitEvent(S, w.ev_ans[(K - 1) & 1], 0));
+    VP_TRY(pass2(K - 1));
+  }
+  VP_HIP(ev_record(c->ktime, c->ev3, S));
+  pm.mark(kStagePipeline);
+  VP_TRY(tbl_fold_read_ctl(c, t, ph->bp, nullptr, p0, p1, now, seq0, w.dneed));
+  pm.mark(kStageFold);
+  pm.finish(c, m.r, np);
+  uint32_t maxsend = 0;  // the next batch's capacity per chunk (run_batch_sharded)
+  for (uint32_t o = 0; o < n; o++)
+    if (o != r || route_all) maxsend = std::max(maxsend, w.h_gath[kPubGath * n + o]);
+  c->own_maxsend = maxsend * G;
+  float k1 = 0.f;
+  VP_HIP(ev_ms(c->ktime, c->ev0, c->ev3, &k1));
+  ph->ms = k1;
+  bool any = false;
+  for (uint32_t q = 0; q < n; q++) any |= w.h_gath[kPubGath * q + 4] != 0;
+  if (!any) return 0;
+  // Leftovers (some rank's slice overflowed): the exact exchange of every
+  // rank's keys past their slices, pass 2 over those packets, a second fold
+  VP_TRY(grow_dev(&w.lcnt, &w.lcnt_n, slices, S));
+  route_left<<<grid_for(slices), 256, 0, S>>>(w.dcnt, (uint32_t)slices, sub, w.lcnt);
+  route_scan<<<n, 256, 0, S>>>(w.lcnt, ph->grid1, n, w.dbase, w.dtot);
+  route_base<<<grid_for(slices), 256, 0, S>>>(w.dbase, w.dtot, ph->grid1, n);
+  VP_HIP(hipGetLastError());
+  VP_HIP(hipMemcpyAsync(w.h_tot, w.dtot, 4ull * n, hipMemcpyDeviceToHost, S));
+  VP_HIP(stream_wait(S));
+  std::vector<uint32_t> M((size_t)n * n);  // M[q * n + o] = keys rank q sends to owner o
+  VP_TRY(m.allgather_host(c, w.h_tot, M.data(), 4ull * n));
+  uint64_t Ssum = 0, R = 0;
+  std::vector<size_t> ek(n), er(n), fr(n), fa(n);
+  for (uint32_t q = 0; q < n; q++) {
+    Ssum += M[(size_t)r * n + q];
+    R += M[(size_t)q * n + r];
+    ek[q] = 16ull * M[(size_t)r * n + q];
+    er[q] = 16ull * M[(size_t)q * n + r];
+    fr[q] = 4ull * M[(size_t)q * n + r];  // answers go back the way keys came
+    fa[q] = 4ull * M[(size_t)r * n + q];
+  }
+  VP_TRY(grow_dev(&w.xsend, &w.xsend_n, Ssum, S));
+  VP_TRY(grow_dev(&w.rreply, &w.rreply_n, Ssum, S));
+  VP_TRY(grow_dev(&w.recvk, &w.recvk_n, R, S));
+  VP_TRY(grow_dev(&w.reply, &w.reply_n, R, S));
+  if (vg)
+    route_pack_left<<<vg, 256, 0, S>>>(w.desc, w.dcnt, w.dbase, n, ph->range1, sub, w.xsend);
+  VP_HIP(hipGetLastError());
+  VP_TRY(m.alltoallv_dev(c, w.xsend, ek.data(), w.recvk, er.data()));
+  nat_own_probe<<<resident_grid((const void *)nat_own_probe, (std::max<uint64_t>(R, 1) + 255) / 256),
+                  256, 0, S>>>(tbl_dev(t), c->crc_tab, w.recvk, (uint32_t)R, 0, nullptr,
+                               nullptr, t.ctl, w.reply, kNone, nullptr, nullptr);
+  VP_HIP(hipGetLastError());
+  VP_TRY(m.alltoallv_dev(c, w.reply, fr.data(), w.rreply, fa.data()));
+  // The first pass 2's touches that found their bin slice full sit on the
+  // blocks' overflow queues, which the leftover pass 2 rewrites: apply them
+  // now (late touches commute: tseq atomicMax, then the winner's ts).
+  if (t.h_ctl.touch_ovf)
+    VP_TRY(tbl_late_touches(c, t, ph->bp.bins.oent, ph->bp.bins.ocnt, 0, ph->bp.range,
+                            ph->bp.grid, w.log, now, seq0));
+  if (vg) {  // (the touch bins are rewritten by these blocks: leftover touches only)
+    NatArgs a2 = a;
+    a2.log = nullptr;
+    a2.vb0 = 0;
+    a2.vper = vper;
+    a2.own.mode = kOwnLeftover;
+    a2.own.rreply = w.rreply;
+    nat_remote64<<<vg, 256, 0, S>>>(a2, b->n, ph->bp.bins);
+    VP_HIP(hipGetLastError());
+  }
+  BinsPlan again = ph->bp;
+  again.maxmode = true;
+  VP_TRY(tbl_fold_read_ctl(c, t, again, nullptr, p0, p1, now, seq0, w.dneed));
+  // (the flag is this segment's: a next segment whose counters need no reset
+  // must not find it set)
+  VP_HIP(hipMemsetAsync(&t.ctl->route_ovf, 0, 4, S));
+  return 0;
+}
+
 static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
                        uint32_t p0, uint32_t p1, float *ms, int *launches,
                        uint32_t *allocated) {
@@ -1998,7 +2382,13 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   const bool owner = c->shard_mode == VP_SHARD_OWNER && c->comm;
   if (owner && a.tail) return VP_ENOTSUP;  // (vp_mbuf.hip never asks for it)
   PhaseA ph{};
-  if (owner) VP_TRY(nat_phase_a_owner(c, b, a, now, p0, p1, seq0, &ph));
+  if (owner) {
+    const OwnChunks oc = own_chunks_plan(c, b);
+    if (oc.K)
+      VP_TRY(nat_phase_a_owner_chunked(c, b, a, now, p0, p1, seq0, oc, &ph));
+    else
+      VP_TRY(nat_phase_a_owner(c, b, a, now, p0, p1, seq0, &ph));
+  }
   // tiles of 64 packets (64-byte slots, or wider ones: nat_tiles): the
   // classify launch also bins its touches (TouchBins) and queues reprobes
   // per block (TileQueue)

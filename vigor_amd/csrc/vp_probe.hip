@@ -1,0 +1,99 @@
+// Memory-shape ceiling of the 64-byte classify tile (vp_probe_slots,
+// include/vigpath.h): the same persistent grid and access shape as
+// nat_classify64 -- 4 blocks of 256 threads per CU, each block a contiguous
+// range of 64-slot tiles, its four waves interleaved over it, every load and
+// store instruction 1 KiB contiguous through a buffer resource, write-through
+// (sc1) stores as the tile stores -- with none of its work: each slot is read
+// and (store != 0) written back in place. bench.py times it on the box it
+// measures the classify kernel on, so the kernel's distance from the fastest
+// possible pass over its bytes is a driver-measured number.
+// (tools/slot_probe.hip is the stand-alone form with more variants.)
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "vp_internal.h"
+
+namespace vp {
+
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+// N = 16-byte chunks per slot; ST: store the slot back
+template <uint32_t N, bool ST>
+__global__ __launch_bounds__(256, 4) void probe_slots(uint4 *buf, uint32_t tiles,
+                                                      uint32_t *sink) {
+  const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t per_b = (tiles + gridDim.x - 1) / gridDim.x;
+  const uint32_t tend = min(tiles, blockIdx.x * per_b + per_b);
+  v4u acc = {0, 0, 0, 0};
+  for (uint32_t tile = blockIdx.x * per_b + wv; tile < tend; tile += 4) {
+    uint4 *g = buf + (size_t)tile * 64 * N;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(g, 0, 64 * N * 16, 0x00020000);
+    v4u d[N];
+#pragma unroll
+    for (uint32_t j = 0; j < N; j++)
+      d[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((64 * j + lane) * 16), 0, 0);
+#pragma unroll
+    for (uint32_t j = 0; j < N; j++) acc += d[j];
+    if constexpr (ST) {
+#pragma unroll
+      for (uint32_t j = 0; j < N; j++)  // (the bytes as read: the buffer is unchanged)
+        __builtin_amdgcn_raw_buffer_store_b128(d[j], rs, (int)((64 * j + lane) * 16), 0, 16);
+    }
+  }
+  // (keeps the loads; never true for a buffer the caller filled with frames)
+  if (acc.x == 0x9E3779B9u && acc.y == 0x7F4A7C15u) sink[0] = acc.z;
+}
+
+}  // namespace vp
+
+using namespace vp;
+
+extern "C" int vp_probe_slots(void *frames, uint32_t n, uint32_t slot, int store, int reps,
+                              float *ms) {
+  if (!frames || !ms || reps < 1 || (n & 63) || n == 0 || (slot != 64 && slot != 128) ||
+      ((uintptr_t)frames & 15))
+    return VP_EINVAL;
+  auto k = slot == 64 ? (store ? probe_slots<4, true> : probe_slots<4, false>)
+                      : (store ? probe_slots<8, true> : probe_slots<8, false>);
+  int dev = 0, cus = 0, per = 0;
+  VP_HIP(hipGetDevice(&dev));
+  VP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  VP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)k, 256, 0));
+  const uint32_t grid = (uint32_t)(cus * (per > 4 ? 4 : per));
+  hipStream_t s = nullptr;
+  hipEvent_t a = nullptr, b = nullptr;
+  uint32_t *sink = nullptr;
+  int rc = 0;
+  float t = 0.f;
+  auto fail = [&](hipError_t e, int line) { return hip_fail(e, "vp_probe_slots", __FILE__, line); };
+  hipError_t e;
+  if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess) return fail(e, __LINE__);
+  if ((e = hipEventCreate(&a)) != hipSuccess || (e = hipEventCreate(&b)) != hipSuccess ||
+      (e = hipMalloc((void **)&sink, 16)) != hipSuccess) {
+    rc = fail(e, __LINE__);
+    goto out;
+  }
+  for (int i = 0; i < 2; i++) k<<<grid, 256, 0, s>>>((uint4 *)frames, n / 64, sink);  // warm
+  // each launch timed by its own dispatch's timestamps, as the classify
+  // kernel is (launch_timed, vp_internal.h)
+  for (int i = 0; i < reps; i++) {
+    float one = 0.f;
+    if ((e = launch_timed(k, dim3(grid), dim3(256), s, a, b, (uint4 *)frames, n / 64, sink)) !=
+            hipSuccess ||
+        (e = hipEventSynchronize(b)) != hipSuccess ||
+        (e = hipEventElapsedTime(&one, a, b)) != hipSuccess) {
+      rc = fail(e, __LINE__);
+      goto out;
+    }
+    t += one;
+  }
+  *ms = t / (float)reps;
+out:
+  if (s) hipStreamSynchronize(s);
+  if (sink) hipFree(sink);
+  if (a) hipEventDestroy(a);
+  if (b) hipEventDestroy(b);
+  if (s) hipStreamDestroy(s);
+  return rc;
+}

@@ -115,10 +115,13 @@ int ws_reserve(vp_ctx *c, uint32_t n) {
   VP_TRY(dalloc(&w.miss_sorted, cap));
   VP_TRY(dalloc(&w.defer, cap));
   VP_TRY(dalloc(&w.reprobe, cap + 128));  // per-block slices end on tile bounds
-  VP_TRY(dalloc(&w.reprobe_cnt, 4096));   // >= any resident grid
+  // per classify block: >= any resident grid, and the chunked owner
+  // pipeline's virtual blocks (at least one tile each)
+  const size_t nblk = std::max<size_t>(4096, cap / 64 + 64);
+  VP_TRY(dalloc(&w.reprobe_cnt, nblk));
   VP_TRY(dalloc(&w.ovf_q, cap + 128));     // (the same slices as reprobe)
   VP_TRY(dalloc(&w.missq, cap + 128));
-  VP_TRY(dalloc(&w.ovf_cnt, 4096));
+  VP_TRY(dalloc(&w.ovf_cnt, nblk));
   VP_TRY(dalloc(&w.mkey, 4ull * cap));
   VP_TRY(dalloc(&w.mhash, cap));
   VP_TRY(dalloc(&w.first, cap));
@@ -198,8 +201,17 @@ static void free_all(vp_ctx *c) {
                   w.sbuf,    w.rbuf,     c->pol_size, c->pol_time,
                   c->pol_cnt, c->pol_off, c->pol_runs, w.desc, w.dcnt, w.dbase, w.dtot,
                   w.route,   w.sendk,    w.recvk,  w.reply,  w.rreply,
-                  w.cnt_t,   w.rcnt_t,   w.dneed,  w.xsend};
+                  w.cnt_t,   w.rcnt_t,   w.dneed,  w.xsend, w.sendk2, w.recvk2,
+                  w.reply2,  w.rreply2,  w.lcnt};
   for (void *p : ptrs) hipFree(p);
+  for (int i = 0; i < 2; i++) {
+    if (w.ev_p1[i]) hipEventDestroy(w.ev_p1[i]);
+    if (w.ev_ans[i]) hipEventDestroy(w.ev_ans[i]);
+  }
+  if (w.xstream) {
+    hipStreamSynchronize(w.xstream);
+    hipStreamDestroy(w.xstream);
+  }
   if (w.h_tot) hipHostFree(w.h_tot);
   if (w.h_frames) hipHostFree(w.h_frames);
   if (w.h_meta) hipHostFree(w.h_meta);

@@ -233,11 +233,18 @@ struct BinsPlan {
   uint32_t grid, range, L;
   uint32_t sbits;  // 2^sbits fold blocks per bin, each L >> sbits indices
   TouchBins bins;
+  // a second fold of a segment whose first fold ran already (the owner
+  // pipeline's leftover exchange): an index's stamp is only raised (its
+  // touches here may precede the ones folded first)
+  bool maxmode;
 };
 // min_bits: at least 2^min_bits bins (vigbridge keeps 256: measured 1.7 %
 // slower at 128, tools/sessions/gpu_r04bc.sh).
+// vper: virtual blocks of vper tiles each (the chunked owner pipeline's
+// launches, frames64_tiles) instead of the kernel's resident grid.
 int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
-                  uint32_t p1, BinsPlan *plan, uint32_t waves = 4, uint32_t min_bits = 0);
+                  uint32_t p1, BinsPlan *plan, uint32_t waves = 4, uint32_t min_bits = 0,
+                  uint32_t vper = 0);
 // ts of the indices the reprobe kernels touched (after their tseq atomicMax;
 // the queue as in reprobe_slices, vp_device.h).
 int tbl_reprobe_stamp(vp_ctx *c, FlowTable &t, const uint32_t *list,
@@ -330,6 +337,9 @@ uint32_t grid_for(uint64_t n, uint32_t block = 256, uint32_t max_blocks = 2048);
 // larger grid leaves the blocks that do not fit to run after the first wave
 // of blocks, as a tail at lower occupancy.
 uint32_t resident_grid(const void *kernel, uint64_t work_blocks, int threads = 256);
+// vignat owner mode: packets per chunk of the chunked pipeline (0: off;
+// vp_nat.hip)
+uint32_t nat_own_chunk_packets();
 uint32_t next_pow2(uint64_t v);
 int cub_reserve(vp_ctx *c, size_t bytes);
 

@@ -825,7 +825,7 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
     const uint32_t *ent, const uint32_t *cnt, uint32_t nsrc, uint32_t cap,
     uint32_t pbits, uint32_t bbits, uint32_t range, uint32_t L, uint32_t tcap,
     uint32_t p0, NowSpec now, uint64_t seq_base, uint64_t *ts, uint64_t *tseq,
-    PubArgs pub, const uint32_t *rtab, uint32_t sbits) {
+    PubArgs pub, const uint32_t *rtab, uint32_t sbits, uint32_t maxmode) {
   // 1 + position in the launch, 0 = none; L words of dynamic LDS (16 KB at
   // 1M flows: the 256 bin blocks spread over all CUs, where a 64 KB static
   // array let only two blocks share a CU and left half of them idle)
@@ -898,6 +898,9 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
     const uint32_t i = bin_index(bin, lo + l, bbits);
     if (!v || i >= tcap) continue;
     const uint32_t p = p0 + v - 1;
+    // (maxmode: a second fold of the same segment, BinsPlan::maxmode; one
+    // thread per index, so the compare needs no atomic)
+    if (maxmode && tseq[i] >= seq_base + p) continue;
     ts[i] = (uint64_t)now.at(p);
     tseq[i] = seq_base + p;
   }
@@ -910,14 +913,17 @@ static uint32_t ceil_log2(uint64_t v) {
 }
 
 int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
-                  uint32_t p1, BinsPlan *plan, uint32_t waves, uint32_t min_bits) {
+                  uint32_t p1, BinsPlan *plan, uint32_t waves, uint32_t min_bits,
+                  uint32_t vper) {
   Workspace &w = c->ws;
   *plan = BinsPlan{};
   const char *env = getenv("VIGPATH_TOUCH_BINS");  // diagnostics: 0 = off
   if ((env && !atoi(env)) || (p0 & 63) || p1 <= p0) return 0;
   const uint32_t tiles = (p1 - p0 + 63) / 64;
-  const uint32_t grid = resident_grid(kernel, (tiles + waves - 1) / waves, 64 * (int)waves);
-  const uint32_t per_b = (tiles + grid - 1) / grid;
+  const uint32_t grid = vper ? (tiles + vper - 1) / vper
+                            : resident_grid(kernel, (tiles + waves - 1) / waves,
+                                            64 * (int)waves);
+  const uint32_t per_b = vper ? vper : (tiles + grid - 1) / grid;
   const uint32_t range = per_b * 64;
   // The fewest bins (>= 2^bbits_min) whose in-bin index range fits the
   // fold's LDS, and at least 256 fold blocks whatever the bin count (2^sbits
@@ -1004,7 +1010,7 @@ static int bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p
   fold<<<1u << (plan.bins.bbits + plan.sbits), 1024, 4u * (Lp + (Lp >> kBinRunBits)),
          c->stream>>>(plan.bins.ent, plan.bins.cnt, plan.grid, plan.bins.cap, plan.bins.pbits,
                       plan.bins.bbits, plan.range, plan.L, t.cap, p0, now, seq_base, t.ts,
-                      t.tseq, pub, plan.bins.rtab, plan.sbits);
+                      t.tseq, pub, plan.bins.rtab, plan.sbits, plan.maxmode ? 1u : 0u);
   VP_HIP(hipGetLastError());
   return 0;
 }
@@ -1054,8 +1060,8 @@ int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_
   w.gath_ok = false;
   if (nr) {
     if (!w.gath) VP_TRY(dalloc(&w.gath, (size_t)kPubGath * kMaxRanks));
-    static_assert(offsetof(Ctl, reprobe_count) - offsetof(Ctl, miss_count) ==
-                      4 * (kPubGath - 1), "miss_count .. reprobe_count contiguous");
+    static_assert(offsetof(Ctl, route_ovf) - offsetof(Ctl, miss_count) ==
+                      4 * (kPubGath - 1), "miss_count .. route_ovf contiguous");
     VP_TRY(c->comm->allgather_dev(c, &t.ctl->miss_count, w.gath, 4 * kPubGath));
   }
   if (!bp.on) {
@@ -1684,12 +1690,17 @@ static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
     // (a rank that has sent nothing yet: its slice's uniform share per owner;
     // a skewed first batch takes the exact exchange once, and no rank pins
     // ranks x slice entries of exchange buffers)
+    // (the chunked pipeline, vp_nat.hip: keys per peer and chunk, so a rank's
+    // part counts at most one chunk)
+    const uint64_t pk = c->shard_mode == VP_SHARD_OWNER && b->slot == 64
+                            ? nat_own_chunk_packets() : 0;
+    auto part = [&](uint64_t x) { return pk ? std::min<uint64_t>(x, pk) : x; };
     uint64_t maxs = 0, maxn = 0;
     for (int r = 0; r < m.n; r++) {
-      maxn = std::max<uint64_t>(maxn, (uint64_t)all[r].n);
+      maxn = std::max<uint64_t>(maxn, part((uint64_t)all[r].n));
       maxs = std::max<uint64_t>(maxs, all[r].maxsend
                                           ? all[r].maxsend
-                                          : ((uint64_t)all[r].n + m.n - 1) / m.n);
+                                          : (part((uint64_t)all[r].n) + m.n - 1) / m.n);
     }
     uint64_t C = (maxs + maxs / 8 + 256 + 255) & ~255ull;
     if (const char *e = getenv("VIGPATH_OWN_CAP")) C = strtoull(e, nullptr, 10);  // tests
@@ -1775,6 +1786,8 @@ static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
         }
     }
     // 4. this rank's part of [A, B1); collectives inside run on every rank
+    c->seg_g0 = A;
+    c->seg_g1 = B1;
     const uint32_t lp0 = (uint32_t)(std::min<uint64_t>(std::max<uint64_t>(A, off), off + (uint64_t)n) - off);
     const uint32_t lp1 = (uint32_t)(std::min<uint64_t>(std::max<uint64_t>(B1, off), off + (uint64_t)n) - off);
     uint32_t allocated = 0;

@@ -97,14 +97,20 @@ class NfBase:
         self._ck(self.L.vp_last_kernel_ms(self.h, rms, rk), "vp_last_kernel_ms")
         return ms.value, k.value
 
-    STAGES = ("pass1", "offsets", "a2a_keys", "probe", "a2a_answers", "pass2", "fold")
+    STAGES = ("pass1", "offsets", "a2a_keys", "probe", "a2a_answers", "pass2", "fold",
+              "pipeline")
 
     def last_stage_ms(self) -> dict:
         """vp_last_stage_ms: owner mode with kernel timing on, the last
-        call's phase-A stage times (ms) by stage name ({} if none)."""
-        ms, k = (C.c_float * 7)(), C.c_int()
+        call's phase-A stage times (ms) by stage name ({} if none); the
+        chunked pipeline reports "pipeline" (its overlapped chunks) and
+        "fold" only."""
+        ms, k = (C.c_float * 8)(), C.c_int()
         self._ck(self.L.vp_last_stage_ms(self.h, ms, C.byref(k)), "vp_last_stage_ms")
-        return {self.STAGES[i]: ms[i] for i in range(k.value)}
+        d = {self.STAGES[i]: ms[i] for i in range(k.value)}
+        if d.get("pipeline"):
+            d = {"pipeline": d["pipeline"], "fold": d["fold"]}
+        return d
 
     def table_stats(self, table: int = 0) -> dict:
         """vp_table_stats_get: live / shard_live / tombstones / buckets /
