@@ -167,6 +167,18 @@ struct Workspace {
   uint32_t *reprobe_cnt = nullptr;  // per classify block (TileQueue)
   uint32_t *missq = nullptr;  // phase-A misses per classify block (the reprobe slices' layout)
   uint32_t *mkey = nullptr;  // 4 words per miss
+  uint32_t *pairs = nullptr;  // tbl_touch_reduce's scattered (position, index) words
+  // tbl_new_keys_unsorted: the tagged key set (3 x u64 per slot, never
+  // reset: a slot of an older tag is empty), its tag, first-sighting bits
+  // per position and their scan, the first sightings' miss ordinals and
+  // their count; phase A's per-block key slices (beside missq)
+  unsigned long long *nkset = nullptr;
+  size_t nkset_n = 0;
+  uint32_t nk_tag = 0;
+  uint32_t *nkbits = nullptr, *nkpre = nullptr, *nkfirst = nullptr, *nkcnt = nullptr;
+  size_t nkbits_n = 0, nkfirst_n = 0;
+  uint4 *mkq = nullptr;
+  uint32_t *mhq = nullptr;
   uint32_t *mhash = nullptr;
   uint32_t *first = nullptr;
   uint32_t *rank = nullptr;

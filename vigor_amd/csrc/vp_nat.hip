@@ -187,7 +187,25 @@ struct NatArgs {
   // blocks vb0 .. vb0 + gridDim.x - 1 of a segment-wide grid whose blocks own
   // vper tiles each (frames64_tiles, vp_device.h)
   uint32_t vb0, vper;
+  // one GPU (tbl_new_keys_unsorted): every queued miss also leaves its FlowId
+  // and hash, miss[k] <-> mkey[k] / mhash[k] (the lean tiles through their
+  // block's slices mkq / mhq beside mq); null: positions only
+  uint4 *mkey;
+  uint32_t *mhash;
+  uint4 *mkq;
+  uint32_t *mhq;
 };
+
+// Queue packet p (FlowId key, hash h) as a phase-B miss.
+__device__ __forceinline__ void miss_add(const NatArgs &a, uint32_t p, const uint32_t key[4],
+                                         uint32_t h) {
+  const uint32_t k = wave_append(&a.t.ctl->miss_count, true);
+  a.miss[k] = p;
+  if (a.mkey) {
+    a.mkey[k] = make_uint4(key[0], key[1], key[2], key[3]);
+    a.mhash[k] = h;
+  }
+}
 
 // The register path's total_length bound for 64-byte slots (every L4 byte in
 // the slot), or any total_length for header slots with tail sums.
@@ -304,7 +322,7 @@ __device__ uint32_t nat_generic_a(const NatArgs &a, const uint32_t *T,
     }
     const uint32_t idx = tbl_probe(a.t, hh, key);
     if (idx == kNone) {
-      a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
+      miss_add(a, p, key, hh);
       log_put(a.log, p, kNone);  // phase B writes the real entry
       return kNone;
     }
@@ -333,7 +351,7 @@ struct NatPend {
   uint32_t kind;
   uint32_t row;  // LAN: home bucket, gathered by frames64_tiles; else kNone
   uint32_t b;    // LAN: home bucket; WAN: flow index
-  uint32_t s;    // WAN: slot_of[index]
+  uint32_t s;    // WAN: slot_of[index]; LAN: the FlowId hash
 };
 
 // `lim`: the longest total_length the register path takes (50: the L4 bytes
@@ -388,6 +406,7 @@ __device__ __forceinline__ NatPend nat_issue(const NatArgs &a, const uint32_t *T
     P.kind = kPendLan;
     P.b = home_bucket(hh, a.t.bmask, a.t.mix, nat_lin(T));
     P.row = P.b;
+    P.s = hh;
   }
   return P;
 }
@@ -449,7 +468,7 @@ __device__ __forceinline__ bool nat_finish(const NatArgs &a, const uint32_t *T,
       return false;
     }
     if (idx == kNone) {  // new flow, or not yet visible: phase B
-      a.miss[wave_append(&a.t.ctl->miss_count, true)] = p;
+      miss_add(a, p, key, P.s);
       log_put(a.log, p, kNone);  // phase B writes the real entry
       return false;
     }
@@ -750,13 +769,19 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   uint32_t tile = rb * per_b + wv;
   const uint32_t tend = min(tiles, rb * per_b + per_b), tstep = 4;
   const uint32_t range0 = first + rb * per_b * 64;  // this block's first packet
-  // a lean tile's misses (wave-uniform call)
-  auto miss_put = [&](bool miss) {
+  // a lean tile's misses (wave-uniform call), with their FlowIds and hashes
+  // when phase B takes them unsorted (a.mkq)
+  auto miss_put = [&](bool miss, const uint32_t key[4], uint32_t h) {
     if (a.mq) {
       const uint32_t k = group_reserve(cur, kCurMiss, miss);
-      if (miss) a.mq[(size_t)rb * per_b * 64 + k] = tile * 64 + first + lane;
+      const size_t at = (size_t)rb * per_b * 64 + k;
+      if (miss) a.mq[at] = tile * 64 + first + lane;
+      if (miss && a.mkq) {
+        a.mkq[at] = make_uint4(key[0], key[1], key[2], key[3]);
+        a.mhq[at] = h;
+      }
     } else if (miss) {
-      a.miss[wave_append(&a.t.ctl->miss_count, true)] = first + tile * 64 + lane;
+      miss_add(a, first + tile * 64 + lane, key, h);
     }
   };
   // (wide slots: the headers of the wave's own tile at its start; a prefetch
@@ -859,7 +884,11 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
         const bool hit = done & (idx != kNone);
         if (__ballot(!hit)) {  // misses (phase B) and full home buckets (reprobes)
           const bool miss = done & !hit;
-          miss_put(miss);
+          // (the hash again, not kept across the tail sums: registers)
+          const uint32_t lh = a.mkq ? flowid_hash_batched(T, key[0] & 0xFFFF, key[0] >> 16,
+                                                          key[1], key[2], in, proto)
+                                    : 0u;
+          miss_put(miss, key, lh);
           const uint32_t k = group_reserve(cur, kCurReprobe, !done);
           if (!done) rq.ent[(size_t)rb * per_b * 64 + k] = p;
           if (!hit) log_put(a.log, p, kNone);
@@ -923,8 +952,8 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       // checksum arithmetic, which keeps more requests in flight (PR;
       // 64-byte slots 0.4-0.6 % faster, 128-byte slots no change: r04ah/ai)
       if constexpr (PR) __builtin_amdgcn_s_setprio(1);
-      const uint32_t b = home_bucket(flowid_hash_batched(T, sp, dp, sip, dip, in, proto),
-                                     a.t.bmask, a.t.mix, nat_lin(T));
+      const uint32_t lh = flowid_hash_batched(T, sp, dp, sip, dip, in, proto);
+      const uint32_t b = home_bucket(lh, a.t.bmask, a.t.mix, nat_lin(T));
       // lane L fetches part L % 4 of the row of packet 16 j + L / 4: the four
       // row numbers come in by ds_bpermute, issued together and waited for
       // once; named registers (an array here stays in scratch memory)
@@ -956,7 +985,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       const bool hit = done & (idx != kNone);
       if (__ballot(!hit)) {  // misses (phase B) and longer walks (reprobes)
         const bool miss = done & !hit;
-        miss_put(miss);
+        miss_put(miss, key, lh);
         const uint32_t k = group_reserve(cur, kCurReprobe, !done);
         if (!done) rq.ent[(size_t)rb * per_b * 64 + k] = p;
         if (!hit) log_put(a.log, p, kNone);
@@ -1017,7 +1046,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
         bool done;
         const uint32_t idx = bucket_match_sel(row, key, &done);
         t1 = !done ? kReprobe : idx;  // kNone: a new flow, phase B
-        miss_put(done & (idx == kNone));
+        miss_put(done & (idx == kNone), key, h);
         if (done & (idx != kNone)) {
           f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
           f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
@@ -1123,8 +1152,14 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
     const uint32_t c = cur[kCurMiss];
     if (threadIdx.x == 0 && c) mbase = atomicAdd(&a.t.ctl->miss_count, c);
     __syncthreads();
-    const uint32_t *src = a.mq + (size_t)rb * per_b * 64;
-    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) a.miss[mbase + i] = src[i];
+    const size_t s0 = (size_t)rb * per_b * 64;
+    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) {
+      a.miss[mbase + i] = a.mq[s0 + i];
+      if (a.mkq) {
+        a.mkey[mbase + i] = a.mkq[s0 + i];
+        a.mhash[mbase + i] = a.mhq[s0 + i];
+      }
+    }
   }
   route_publish(a, cur + kCurDest, rb);
 }
@@ -1313,10 +1348,13 @@ __device__ void nat_write_lan(const NatArgs &a, uint32_t p, uint32_t idx) {
 // register-path frame of a 64-byte slot is rewritten as the tile kernels
 // rewrite a hit (gathered and stored four lanes per frame); any other takes
 // the byte path.
+// (nkord: tbl_new_keys_unsorted's key set, whose slot word carries the
+// index; then no touch-log entries: the set stamped the new flows itself)
 __global__ __launch_bounds__(256) void nat_miss_finish(NatArgs a, const uint32_t *list,
                                                        uint32_t n, const uint32_t *scratch,
                                                        const uint32_t *rep,
-                                                       const uint32_t *assign) {
+                                                       const uint32_t *assign,
+                                                       const unsigned long long *nkord) {
   __shared__ uint4 stage[4][256];
   uint4 *S = stage[threadIdx.x >> 6];
   const uint32_t lane = threadIdx.x & 63;
@@ -1327,9 +1365,9 @@ __global__ __launch_bounds__(256) void nat_miss_finish(NatArgs a, const uint32_t
     const uint32_t j = j0 + lane;
     const bool v = j < n;
     const uint32_t p = v ? list[j] : kNone;
-    const uint32_t idx = v ? assign[scratch[rep[j]]] : kNone;
+    const uint32_t idx = !v ? kNone : nkord ? (uint32_t)nkord[rep[j]] : assign[scratch[rep[j]]];
     if (v) {
-      a.log[p] = idx;
+      if (!nkord) a.log[p] = idx;
       if (idx == kNone) a.out[p] = a.in_dev[p];  // nat_main.c:87-91
     }
     const bool live = v && idx != kNone;
@@ -2347,6 +2385,8 @@ static int nat_phase_a_owner_chunked(vp_ctx *c, const vp_dev_batch *b, NatArgs &
   return 0;
 }
 
+void build_flowid_tables(std::vector<uint32_t> &tab);
+
 static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
                        uint32_t p0, uint32_t p1, float *ms, int *launches,
                        uint32_t *allocated) {
@@ -2378,6 +2418,20 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.start_port = c->nat.start_port;
   a.n_dev = c->nat.n_devices;
   a.tail = c->hdr_tail;  // (vp_process_mbufs' header slots; null otherwise)
+  // one GPU: phase B takes the misses unsorted, with the keys phase A leaves
+  // (tbl_new_keys_unsorted; VIGPATH_NK_SORTED=1: the sorted path, for A/B);
+  // multi-GPU ranks allocate the union in global order (sorted)
+  static const bool nk_sorted = [] {
+    const char *e = getenv("VIGPATH_NK_SORTED");
+    return e && atoi(e);
+  }();
+  const bool nku = !c->comm && !nk_sorted;
+  if (nku) {
+    a.mkey = reinterpret_cast<uint4 *>(w.mkey);
+    a.mhash = w.mhash;
+    a.mkq = w.mkq;
+    a.mhq = w.mhq;
+  }
 
   const bool owner = c->shard_mode == VP_SHARD_OWNER && c->comm;
   if (owner && a.tail) return VP_ENOTSUP;  // (vp_mbuf.hip never asks for it)
@@ -2463,7 +2517,56 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
 
   uint32_t union_n = nmiss, union_off = 0;  // this rank's misses in the union
   if (c->comm) VP_TRY(union_sizes(c, nmiss, &union_n, &union_off));
-  if (nmiss) {
+  auto nk_check = [&](const char *tag) -> int {  // (diagnostics: the miss records)
+    if (!getenv("VIGPATH_NK_CHECK")) return 0;
+    fprintf(stderr, "nkcheck %s\n", tag);
+    {
+      std::vector<uint32_t> pos(nmiss), hs(nmiss), ks(4ull * nmiss), tab;
+      VP_HIP(hipStreamSynchronize(c->stream));
+      VP_HIP(hipMemcpy(pos.data(), w.miss, 4ull * nmiss, hipMemcpyDeviceToHost));
+      VP_HIP(hipMemcpy(hs.data(), w.mhash, 4ull * nmiss, hipMemcpyDeviceToHost));
+      VP_HIP(hipMemcpy(ks.data(), w.mkey, 16ull * nmiss, hipMemcpyDeviceToHost));
+      build_flowid_tables(tab);
+      uint32_t bad = 0, out = 0;
+      for (uint32_t j = 0; j < nmiss; j++) {
+        const uint32_t *k = &ks[4 * j];
+        const uint32_t sp = k[0] & 0xFFFF, dp = k[0] >> 16, dv = k[3] & 0xFFFF, pr = (k[3] >> 16) & 0xFF;
+        const uint32_t b8[15] = {sp & 0xFF, sp >> 8, dp & 0xFF, dp >> 8, k[1] & 0xFF, (k[1] >> 8) & 0xFF,
+                                 (k[1] >> 16) & 0xFF, k[1] >> 24, k[2] & 0xFF, (k[2] >> 8) & 0xFF,
+                                 (k[2] >> 16) & 0xFF, k[2] >> 24, dv & 0xFF, dv >> 8, pr};
+        uint32_t h = 0;
+        for (int q = 0; q < 15; q++) h ^= tab[q * 256 + b8[q]];
+        if (h != hs[j]) {
+          if (bad < 5) {
+            uint8_t fr[64];
+            VP_HIP(hipMemcpy(fr, b->frames + (size_t)pos[j] * b->slot, 64, hipMemcpyDeviceToHost));
+            uint16_t ind = 0;
+            VP_HIP(hipMemcpy(&ind, b->in_dev + pos[j], 2, hipMemcpyDeviceToHost));
+            uint32_t fk0 = fr[34] | fr[35] << 8 | fr[36] << 16 | (uint32_t)fr[37] << 24;
+            uint32_t fk1 = fr[26] | fr[27] << 8 | fr[28] << 16 | (uint32_t)fr[29] << 24;
+            uint32_t fk2 = fr[30] | fr[31] << 8 | fr[32] << 16 | (uint32_t)fr[33] << 24;
+            uint32_t fk3 = ind | (uint32_t)fr[23] << 16;
+            fprintf(stderr, "nkcheck: miss %u pos %u hash %08x want %08x key %08x %08x %08x %08x frame %08x %08x %08x %08x ihl %u\n",
+                    j, pos[j], hs[j], h, k[0], k[1], k[2], k[3], fk0, fk1, fk2, fk3, fr[14] & 15);
+          }
+          bad++;
+        }
+        if (pos[j] < p0 || pos[j] >= p1) out++;
+      }
+      fprintf(stderr, "nkcheck: seg [%u,%u) misses %u bad hashes %u out of segment %u\n", p0, p1,
+              nmiss, bad, out);
+    }
+    return 0;
+  };
+  if (nmiss && nku) {  // (one GPU: no sort, no key gather, no late touches)
+    VP_TRY(nk_check("unsorted"));
+    VP_TRY(tbl_new_keys_unsorted(c, t, nmiss, p0, p1, now, c->seq));
+    a.t = tbl_dev(t);  // a rebuild may have moved the buckets
+    nat_miss_finish<<<grid_for(nmiss), 256, 0, c->stream>>>(a, w.miss, nmiss, nullptr, w.rep,
+                                                            nullptr, w.nkset);
+    VP_HIP(hipGetLastError());
+    *allocated |= 1u;
+  } else if (nmiss) {
     size_t need = 0;
     hipcub::DeviceRadixSort::SortKeys(nullptr, need, w.miss, w.miss_sorted,
                                       (int)nmiss, 0, 32, c->stream);
@@ -2474,8 +2577,9 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     nat_miss_keys<<<grid_for(nmiss), 256, 0, c->stream>>>(a, w.miss_sorted, nmiss,
                                                           w.mkey, w.mhash);
     VP_HIP(hipGetLastError());
+    if (!c->comm) VP_TRY(nk_check("sorted"));
   }
-  if (union_n) {
+  if (union_n && !nku) {
     if (c->comm) {  // every rank allocates the union in global packet order
       VP_TRY(union_exchange(c, nmiss, now));
       if (owner) VP_TRY(tbl_owner_reserve(c, t, union_n));
@@ -2490,7 +2594,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     }
     if (nmiss) {
       nat_miss_finish<<<grid_for(nmiss), 256, 0, c->stream>>>(
-          a, w.miss_sorted, nmiss, w.scratch, w.rep + union_off, w.assign);
+          a, w.miss_sorted, nmiss, w.scratch, w.rep + union_off, w.assign, nullptr);
       VP_HIP(hipGetLastError());
       VP_TRY(tbl_late_touches(c, t, w.miss_sorted, nullptr, nmiss, 256,
                               (nmiss + 255) / 256, w.log, now, seq0));
@@ -2503,7 +2607,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     VP_TRY(tbl_late_touches(c, t, w.defer, nullptr, ndefer, 256, (ndefer + 255) / 256,
                             w.log, now, seq0));
   }
-  if (union_n || ndefer) VP_TRY(read_ctl(c, t));
+  if ((union_n && !nku) || ndefer) VP_TRY(read_ctl(c, t));  // (unsorted: read already)
   // steady state (every packet a phase-A hit): the frames and ports are
   // complete (the control copy waited for phase A); only the fold of the
   // stamps may still run — unless it reads the caller's time array, which

@@ -91,7 +91,8 @@ static void ws_release(Workspace &w) {
                   w.first, w.rank,        w.rep,   w.assign, w.scratch,
                   w.log,   w.iota,        w.skey,  w.sval,
                   w.log2,  w.defer_sorted, w.aux,  w.aux_sorted, w.rlist, w.hbl,
-                  w.unow,  w.reprobe,     w.reprobe_cnt, w.ovf_q, w.ovf_cnt, w.missq};
+                  w.unow,  w.reprobe,     w.reprobe_cnt, w.ovf_q, w.ovf_cnt, w.missq,
+                  w.mkq,   w.mhq,    w.pairs};
   for (void *p : ptrs) hipFree(p);
   w.miss = w.miss_sorted = w.defer = w.mkey = w.mhash = w.first = w.rank =
       w.rep = w.assign = w.scratch = w.log = w.iota = w.skey = w.sval = nullptr;
@@ -100,6 +101,9 @@ static void ws_release(Workspace &w) {
   w.reprobe = w.reprobe_cnt = nullptr;
   w.ovf_q = w.ovf_cnt = nullptr;
   w.missq = nullptr;
+  w.mkq = nullptr;
+  w.mhq = nullptr;
+  w.pairs = nullptr;
   w.cap_n = 0;
 }
 
@@ -121,6 +125,9 @@ int ws_reserve(vp_ctx *c, uint32_t n) {
   VP_TRY(dalloc(&w.reprobe_cnt, nblk));
   VP_TRY(dalloc(&w.ovf_q, cap + 128));     // (the same slices as reprobe)
   VP_TRY(dalloc(&w.missq, cap + 128));
+  VP_TRY(dalloc(&w.mkq, cap + 128));  // (phase A's miss keys beside missq)
+  VP_TRY(dalloc(&w.mhq, cap + 128));
+  VP_TRY(dalloc(&w.pairs, cap));
   VP_TRY(dalloc(&w.ovf_cnt, nblk));
   VP_TRY(dalloc(&w.mkey, 4ull * cap));
   VP_TRY(dalloc(&w.mhash, cap));
@@ -202,7 +209,8 @@ static void free_all(vp_ctx *c) {
                   c->pol_cnt, c->pol_off, c->pol_runs, w.desc, w.dcnt, w.dbase, w.dtot,
                   w.route,   w.sendk,    w.recvk,  w.reply,  w.rreply,
                   w.cnt_t,   w.rcnt_t,   w.dneed,  w.xsend, w.sendk2, w.recvk2,
-                  w.reply2,  w.rreply2,  w.lcnt};
+                  w.reply2,  w.rreply2,  w.lcnt, w.nkset, w.nkbits, w.nkpre,
+                  w.nkfirst, w.nkcnt};
   for (void *p : ptrs) hipFree(p);
   for (int i = 0; i < 2; i++) {
     if (w.ev_p1[i]) hipEventDestroy(w.ev_p1[i]);

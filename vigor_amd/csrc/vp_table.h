@@ -186,6 +186,37 @@ __device__ __forceinline__ uint32_t tbl_probe(const TableDev &t, uint32_t h,
 }
 
 // Key words of an allocated index's entry.
+// Claim the first empty-or-erased entry on key hash h's probe path (the
+// map_put position; the key is known to be absent) and store key + index.
+// Returns the entry id. Concurrent claimers race on the index word only.
+__device__ inline uint32_t tbl_insert(const TableDev &t, uint32_t h, const uint32_t *k,
+                               uint32_t idx, bool *reused_tomb, uint32_t *disp) {
+  uint32_t b = home_bucket(h, t.bmask, t.mix, t.lin);
+  for (uint32_t d = 0;; d++) {
+    if (d == 1) *disp += 1;  // past the home bucket
+    if (d == 8) atomicMax(&t.ctl->max_disp, d);  // clustering signal
+    for (uint32_t e = 0; e < kBucketEntries; e++) {
+      uint32_t *w = &t.bk[b].idx[e];
+      uint32_t cur = __hip_atomic_load(w, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+      while (cur == kEmpty || cur == kTomb) {
+        const uint32_t old = atomicCAS(w, cur, idx);
+        if (old == cur) {
+          uint32_t *kk = t.bk[b].k[e];
+          kk[0] = k[0];
+          kk[1] = k[1];
+          kk[2] = k[2];
+          kk[3] = k[3];
+          *reused_tomb = cur == kTomb;
+          return (b << 2) | e;
+        }
+        cur = old;  // lost the race; look at this entry again
+      }
+    }
+    b = (b + 1) & t.bmask;
+  }
+}
+
 __device__ __forceinline__ uint4 tbl_key_of(const TableDev &t, uint32_t idx) {
   if (t.kv) return t.kv[idx];
   const uint32_t e = t.slot_of[idx];
@@ -216,6 +247,17 @@ TableDev tbl_dev(const FlowTable &t);
 // packet order, hand out dchain indices (free-list order) and insert the
 // keys. Afterwards ws.assign[j0] holds the index for first sighting j0 (or
 // kNone when the table was full) and scratch[rep[j]] = j0 for every j.
+// New flows of one segment on one GPU without sorting the misses (DESIGN.md
+// §5.1, churn): n misses in any order, w.miss[j] = packet position p0 <= p <
+// p1 with its FlowId in w.mkey[j] / hash w.mhash[j] (written by phase A).
+// Per distinct key: the first and last packet (a tagged hash set, no reset);
+// first sightings ranked in packet order by a bit per position; the r-th
+// takes the r-th free-list entry (dchain_allocate_new_index order), is
+// inserted, born at its first packet and stamped with its last. On return
+// the low word of w.nkset[w.rep[j]] is miss j's index (kNone: table full)
+// and h_ctl holds the counters.
+int tbl_new_keys_unsorted(vp_ctx *c, FlowTable &t, uint32_t n, uint32_t p0, uint32_t p1,
+                          const NowSpec &now, uint64_t seq_base);
 int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
                  uint32_t *n_new);
 

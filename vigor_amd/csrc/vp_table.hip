@@ -228,37 +228,6 @@ void tbl_free(FlowTable &t) {
   t = FlowTable{};
 }
 
-// Claim the first empty-or-erased entry on key hash h's probe path (the
-// map_put position; the key is known to be absent) and store key + index.
-// Returns the entry id. Concurrent claimers race on the index word only.
-__device__ uint32_t tbl_insert(const TableDev &t, uint32_t h, const uint32_t *k,
-                               uint32_t idx, bool *reused_tomb, uint32_t *disp) {
-  uint32_t b = home_bucket(h, t.bmask, t.mix, t.lin);
-  for (uint32_t d = 0;; d++) {
-    if (d == 1) *disp += 1;  // past the home bucket
-    if (d == 8) atomicMax(&t.ctl->max_disp, d);  // clustering signal
-    for (uint32_t e = 0; e < kBucketEntries; e++) {
-      uint32_t *w = &t.bk[b].idx[e];
-      uint32_t cur = __hip_atomic_load(w, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-      while (cur == kEmpty || cur == kTomb) {
-        const uint32_t old = atomicCAS(w, cur, idx);
-        if (old == cur) {
-          uint32_t *kk = t.bk[b].k[e];
-          kk[0] = k[0];
-          kk[1] = k[1];
-          kk[2] = k[2];
-          kk[3] = k[3];
-          *reused_tomb = cur == kTomb;
-          return (b << 2) | e;
-        }
-        cur = old;  // lost the race; look at this entry again
-      }
-    }
-    b = (b + 1) & t.bmask;
-  }
-}
-
 // ------------------------------------------------------------ new keys --
 
 struct NkArgs {
@@ -358,6 +327,218 @@ __global__ void nk_commit(NkArgs m) {
   c->new_count = used;
 }
 
+// ---------------------------------------------------- unsorted new keys --
+// (tbl_new_keys_unsorted, vp_table.h) Slot s of the key set: ord[s] = tag <<
+// 32 | a miss ordinal holding the key, fpos = tag << 32 | ~first position
+// (atomicMax keeps the earliest), lpos = tag << 32 | last position.
+struct NkuArgs {
+  TableDev t;
+  const uint32_t *pos;  // miss j's packet position
+  const uint4 *key;
+  const uint32_t *hash;
+  uint32_t n, smask;
+  unsigned long long *set;  // [3][smask + 1]
+  uint32_t tag;
+  uint32_t *rep, *bits, *pre, *first, *cnt;
+  uint32_t p0, nwords;
+  NowSpec now;
+  uint64_t seq_base;
+};
+
+__global__ void nku_dedup(NkuArgs m) {
+  const size_t S = (size_t)m.smask + 1;
+  unsigned long long *ord = m.set, *fp = m.set + S, *lp = m.set + 2 * S;
+  const unsigned long long tg = (unsigned long long)m.tag << 32;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m.n;
+       j += gridDim.x * blockDim.x) {
+    const uint4 kj = m.key[j];
+    const uint32_t h = m.hash[j];
+    uint32_t s = home_bucket(h, m.smask, kMixMul);
+    for (;;) {
+      unsigned long long cur = __hip_atomic_load(&ord[s], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+      if ((cur >> 32) != m.tag) {  // an empty slot (an older tag): claim it
+        const unsigned long long old = atomicCAS(&ord[s], cur, tg | j);
+        if (old == cur) break;
+        cur = old;  // (someone of this call took it: compare)
+      }
+      const uint32_t o = (uint32_t)cur;
+      const uint4 ko = m.key[o];
+      if (m.hash[o] == h && ko.x == kj.x && ko.y == kj.y && ko.z == kj.z && ko.w == kj.w) break;
+      s = (s + 1) & m.smask;
+    }
+    m.rep[j] = s;
+    const uint32_t p = m.pos[j];
+    atomicMax(&fp[s], tg | (unsigned long long)(~p));
+    atomicMax(&lp[s], tg | (unsigned long long)p);
+  }
+}
+
+// First sightings: one bit per segment position, and their miss ordinals.
+__global__ void nku_firsts(NkuArgs m) {
+  const size_t S = (size_t)m.smask + 1;
+  const unsigned long long *fp = m.set + S;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m.n;
+       j += gridDim.x * blockDim.x) {
+    const uint32_t p = m.pos[j];
+    bool f = (uint32_t)~(uint32_t)fp[m.rep[j]] == p;
+    // (one first sighting per position: a packet queued twice counts once)
+    if (f) {
+      const uint32_t bit = 1u << ((p - m.p0) & 31);
+      f = !(atomicOr(&m.bits[(p - m.p0) >> 5], bit) & bit);
+    }
+    const uint32_t k = wave_append(m.cnt, f);
+    if (f) m.first[k] = j;
+  }
+}
+
+__global__ void nku_popc(const uint32_t *bits, uint32_t n, uint32_t *out) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    out[i] = (uint32_t)__popc(bits[i]);
+}
+
+// dchain_allocate_new_index for each first sighting by its rank in packet
+// order, map_put of the key, birth at the first packet, stamps of the last.
+__global__ void nku_alloc(NkuArgs m) {
+  const TableDev &t = m.t;
+  const size_t S = (size_t)m.smask + 1;
+  const unsigned long long *lp = m.set + 2 * S;
+  const uint32_t stack_top = t.ctl->stack_top;
+  const uint32_t fresh = t.ctl->fresh_next;
+  const uint32_t free_total = stack_top + (t.cap - fresh);
+  const uint32_t K = *m.cnt;
+  uint32_t disp = 0, ins = 0;
+  for (uint32_t f = blockIdx.x * blockDim.x + threadIdx.x; f < K;
+       f += gridDim.x * blockDim.x) {
+    const uint32_t j = m.first[f];
+    const uint32_t p = m.pos[j], q = p - m.p0, s = m.rep[j];
+    const uint32_t r = m.pre[q >> 5] + (uint32_t)__popc(m.bits[q >> 5] & ((1u << (q & 31)) - 1u));
+    unsigned long long *ord = m.set;  // (the slot's word now carries the index)
+    const unsigned long long tg = (unsigned long long)m.tag << 32;
+    if (r >= free_total) {  // table full: nat_main.c:87-91
+      ord[s] = tg | kNone;
+      continue;
+    }
+    const uint32_t idx = r < stack_top ? t.stack[stack_top - 1 - r] : fresh + (r - stack_top);
+    const uint4 k4 = m.key[j];
+    const uint32_t key[4] = {k4.x, k4.y, k4.z, k4.w};
+    bool tomb = false;
+    const uint32_t e = tbl_insert(t, m.hash[j], key, idx, &tomb, &disp);
+    if (tomb) atomicAdd(&t.ctl->tomb_reused, 1u);
+    ins++;
+    t.slot_of[idx] = e;
+    t.hash_of[idx] = m.hash[j];
+    t.birth[idx] = m.seq_base + p;
+    const uint32_t last = (uint32_t)lp[s];  // the key's last packet: its stamps
+    t.ts[idx] = (uint64_t)m.now.at(last);
+    t.tseq[idx] = m.seq_base + last;
+    ord[s] = tg | idx;
+  }
+  for (uint32_t o = 32; o > 0; o >>= 1) {
+    disp += __shfl_xor(disp, o);
+    ins += __shfl_xor(ins, o);
+  }
+  if ((threadIdx.x & 63) == 0 && disp) atomicAdd(&t.ctl->disp_count, disp);
+  if ((threadIdx.x & 63) == 0 && ins) atomicAdd(&t.ctl->sh_live, ins);
+}
+
+__global__ void nku_commit(Ctl *c, uint32_t cap, const uint32_t *cnt) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint32_t K = *cnt;
+  const uint32_t free_total = c->stack_top + (cap - c->fresh_next);
+  const uint32_t used = K < free_total ? K : free_total;
+  if (used <= c->stack_top) {
+    c->stack_top -= used;
+  } else {
+    c->fresh_next += used - c->stack_top;
+    c->stack_top = 0;
+  }
+  c->n_live += used;
+  c->n_tomb -= c->tomb_reused;
+  c->tomb_reused = 0;
+  c->new_count = used;
+}
+
+static int tbl_after_new_keys(vp_ctx *c, FlowTable &t);
+
+int tbl_new_keys_unsorted(vp_ctx *c, FlowTable &t, uint32_t n, uint32_t p0, uint32_t p1,
+                          const NowSpec &now, uint64_t seq_base) {
+  Workspace &w = c->ws;
+  if (!n) return 0;
+  const uint64_t S = next_pow2(2ull * n);
+  const uint32_t nwords = (p1 - p0 + 31) / 32;
+  if (3 * S > w.nkset_n) {  // (zeroed once: tag 0 is never used)
+    VP_HIP(hipStreamSynchronize(c->stream));
+    hipFree(w.nkset);
+    w.nkset = nullptr;
+    w.nkset_n = 0;
+    VP_TRY(dalloc(&w.nkset, 3 * S));
+    VP_HIP(hipMemsetAsync(w.nkset, 0, 8 * 3 * S, c->stream));
+    w.nkset_n = 3 * S;
+    w.nk_tag = 0;
+  }
+  if (nwords + 1 > w.nkbits_n) {
+    VP_HIP(hipStreamSynchronize(c->stream));
+    for (uint32_t **p : {&w.nkbits, &w.nkpre}) {
+      hipFree(*p);
+      *p = nullptr;
+    }
+    w.nkbits_n = 0;
+    VP_TRY(dalloc(&w.nkbits, nwords + 1));
+    VP_TRY(dalloc(&w.nkpre, nwords + 1));
+    w.nkbits_n = nwords + 1;
+  }
+  if (n > w.nkfirst_n) {
+    VP_HIP(hipStreamSynchronize(c->stream));
+    hipFree(w.nkfirst);
+    w.nkfirst = nullptr;
+    w.nkfirst_n = 0;
+    VP_TRY(dalloc(&w.nkfirst, n));
+    w.nkfirst_n = n;
+  }
+  if (!w.nkcnt) VP_TRY(dalloc(&w.nkcnt, 1));
+  // the set's layout depends on its size: a new size starts a new tag space
+  // (the memory of an older, larger set holds only older tags)
+  if (++w.nk_tag == 0) {
+    VP_HIP(hipMemsetAsync(w.nkset, 0, 8 * w.nkset_n, c->stream));
+    w.nk_tag = 1;
+  }
+  NkuArgs m{};
+  m.t = tbl_dev(t);
+  m.pos = w.miss;
+  m.key = reinterpret_cast<const uint4 *>(w.mkey);
+  m.hash = w.mhash;
+  m.n = n;
+  m.smask = (uint32_t)(S - 1);
+  m.set = w.nkset;
+  m.tag = w.nk_tag;
+  m.rep = w.rep;
+  m.bits = w.nkbits;
+  m.pre = w.nkpre;
+  m.first = w.nkfirst;
+  m.cnt = w.nkcnt;
+  m.p0 = p0;
+  m.nwords = nwords;
+  m.now = now;
+  m.seq_base = seq_base;
+  size_t need = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, need, w.nkpre, w.nkpre, (int)nwords, c->stream);
+  VP_TRY(cub_reserve(c, need));
+  VP_HIP(hipMemsetAsync(w.nkbits, 0, 4ull * nwords, c->stream));
+  VP_HIP(hipMemsetAsync(w.nkcnt, 0, 4, c->stream));
+  const uint32_t g = grid_for(n);
+  nku_dedup<<<g, 256, 0, c->stream>>>(m);
+  nku_firsts<<<g, 256, 0, c->stream>>>(m);
+  nku_popc<<<grid_for(nwords), 256, 0, c->stream>>>(w.nkbits, nwords, w.nkpre);
+  VP_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub_tmp, w.cub_bytes, w.nkpre, w.nkpre,
+                                          (int)nwords, c->stream));
+  nku_alloc<<<g, 256, 0, c->stream>>>(m);
+  nku_commit<<<1, 64, 0, c->stream>>>(t.ctl, t.cap, w.nkcnt);
+  VP_HIP(hipGetLastError());
+  VP_TRY(read_ctl(c, t));
+  return tbl_after_new_keys(c, t);
+}
+
 int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
                  uint32_t *n_new) {
   Workspace &w = c->ws;
@@ -391,6 +572,11 @@ int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
   VP_HIP(hipGetLastError());
   VP_TRY(read_ctl(c, t));
   if (n_new) *n_new = t.h_ctl.new_count;
+  return tbl_after_new_keys(c, t);
+}
+
+// After new keys went in (h_ctl read back): the home-bucket layout checks.
+static int tbl_after_new_keys(vp_ctx *c, FlowTable &t) {
   // A linear layout is exact-structured for GF(2)-linear key sets: either
   // well spread or clustered (a long probe, or a tenth of the keys past
   // their home bucket). Clustered: choose another layout and rebuild.
@@ -789,7 +975,8 @@ int tbl_touch_reduce(vp_ctx *c, FlowTable &t, const uint32_t *log, uint32_t p0,
   hipcub::DeviceScan::ExclusiveSum(nullptr, need, w.hist, w.hoff, (int)nh, ts);
   VP_TRY(cub_reserve(c, need));
   uint32_t *hist = w.hist, *off = w.hoff;
-  uint32_t *pairs = w.mkey;  // 4 words per packet available, 1 used
+  // (a buffer of its own: phase A leaves one-GPU misses' keys in mkey)
+  uint32_t *pairs = w.pairs;
   touch_count<<<nspans, 256, lds, ts>>>(log + p0, n, span, cb, nchunks, nspans,
                                         hist);
   VP_HIP(hipcub::DeviceScan::ExclusiveSum(w.cub_tmp, w.cub_bytes, hist, off,
