@@ -369,8 +369,13 @@ __global__ void nku_dedup(NkuArgs m) {
     }
     m.rep[j] = s;
     const uint32_t p = m.pos[j];
-    atomicMax(&fp[s], tg | (unsigned long long)(~p));
-    atomicMax(&lp[s], tg | (unsigned long long)p);
+    // (read first: a key's packets mostly arrive after its earliest and
+    // before its latest was seen, and a load is cheaper than an atomic)
+    const unsigned long long f = tg | (unsigned long long)(~p), l = tg | (unsigned long long)p;
+    if (f > __hip_atomic_load(&fp[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(&fp[s], f);
+    if (l > __hip_atomic_load(&lp[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(&lp[s], l);
   }
 }
 
