@@ -313,8 +313,6 @@ int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_
                       uint32_t p0, uint32_t p1, const NowSpec &now, uint64_t seq_base,
                       const uint32_t *sends = nullptr);
 
-// Exact min ts over allocated indices -> t.ts_floor (~0 if none).
-int tbl_exact_floor(vp_ctx *c, FlowTable &t);
 
 // expire_items_single_map for cutoff: free every allocated index with
 // ts < cutoff in LRU order (ts, then tseq) onto the stack, erase its key.

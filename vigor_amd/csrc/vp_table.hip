@@ -1338,53 +1338,42 @@ int tbl_reprobe_stamp(vp_ctx *c, FlowTable &t, const uint32_t *list,
 
 // ---------------------------------------------------------------- expiry --
 
-// (One global atomic per block: with one per wave the 8192 waves of a 1M-index
-// table queued on a single address, ≈ 95 µs; round 4.)
-__global__ __launch_bounds__(256) void tbl_min_ts(TableDev t) {
-  __shared__ unsigned long long wbest[4];
-  unsigned long long best = ~0ull;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < t.cap;
-       i += gridDim.x * blockDim.x)
-    if (t.slot_of[i] != kNone && t.ts[i] < best) best = t.ts[i];
-  for (int o = 32; o > 0; o >>= 1) {
-    unsigned long long v = __shfl_xor(best, o);
-    best = v < best ? v : best;
-  }
-  if (__lane_id() == 0) wbest[threadIdx.x >> 6] = best;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (uint32_t w = 1; w < blockDim.x / 64; w++) best = wbest[w] < best ? wbest[w] : best;
-    if (best != ~0ull) atomicMin((unsigned long long *)&t.ctl->min_ts, best);
-  }
-}
-
-int tbl_exact_floor(vp_ctx *c, FlowTable &t) {
-  const uint64_t all = ~0ull;
-  VP_HIP(hipMemcpyAsync(&t.ctl->min_ts, &all, 8, hipMemcpyHostToDevice,
-                        c->stream));
-  tbl_min_ts<<<grid_for(t.cap, 256, 512), 256, 0, c->stream>>>(tbl_dev(t));
-  VP_HIP(hipGetLastError());
-  VP_TRY(read_ctl(c, t));
-  t.ts_floor = t.h_ctl.min_ts;
-  return 0;
-}
-
 // Every allocated index with ts < cutoff: the set expire_items_single_map
 // frees (LRU order is (ts, last-touch) order, so the loop stops exactly at
 // the first stamp >= cutoff).
 // Two passes over the block's contiguous range of indices: count, one global
 // atomic for the block's base, then append behind it (the set is sorted
 // afterwards: its order here does not matter).
+// The same pass also gives the exact floor after the expiry: the least ts of
+// the allocated indices that stay (atomicMin into ctl->min_ts, reset by the
+// caller), so no separate scan over the stamps and read-back follows.
 __global__ __launch_bounds__(256) void exp_collect(TableDev t, int64_t cutoff, uint64_t *ekey,
                                                    uint32_t *eidx) {
   __shared__ uint32_t cnt, base;
+  __shared__ unsigned long long wmin[4];
   if (threadIdx.x == 0) cnt = 0;
   __syncthreads();
   const uint32_t per = (t.cap + gridDim.x - 1) / gridDim.x;
   const uint32_t i0 = blockIdx.x * per, i1 = min(t.cap, i0 + per);
   auto take_at = [&](uint32_t i) { return t.slot_of[i] != kNone && (int64_t)t.ts[i] < cutoff; };
-  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) wave_append(&cnt, take_at(i));
+  unsigned long long low = ~0ull;
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const bool live = t.slot_of[i] != kNone;
+    const uint64_t ts = live ? t.ts[i] : ~0ull;
+    const bool take = live && (int64_t)ts < cutoff;
+    wave_append(&cnt, take);
+    if (live && !take && ts < low) low = ts;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long v = __shfl_xor(low, o);
+    low = v < low ? v : low;
+  }
+  if (__lane_id() == 0) wmin[threadIdx.x >> 6] = low;
   __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t w = 1; w < blockDim.x / 64; w++) low = wmin[w] < low ? wmin[w] : low;
+    if (low != ~0ull) atomicMin((unsigned long long *)&t.ctl->min_ts, low);
+  }
   if (threadIdx.x == 0) {
     base = cnt ? atomicAdd(&t.ctl->exp_count, cnt) : 0u;
     cnt = 0;
@@ -1398,13 +1387,6 @@ __global__ __launch_bounds__(256) void exp_collect(TableDev t, int64_t cutoff, u
       ekey[k] = t.tseq[i];
     }
   }
-}
-
-__global__ void exp_gather_ts(const uint32_t *eidx, uint32_t n, const uint64_t *ts,
-                              uint64_t *ekey) {
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
-       j += gridDim.x * blockDim.x)
-    ekey[j] = ts[eidx[j]];
 }
 
 // Free in LRU order: the oldest is pushed first, so the youngest expired
@@ -1519,31 +1501,46 @@ int tbl_owner_reserve(vp_ctx *c, FlowTable &t, uint32_t n) {
   return tbl_rebuild(c, t, nb);
 }
 
+// Expiry at `cutoff` (expire_items_single_map, expirator.c:110-218): every
+// allocated index with ts < cutoff is freed in LRU order, and t.ts_floor
+// becomes the exact least stamp of what stays. One scan (exp_collect, which
+// also finds that floor), one read-back, one sort. LRU order is (ts, tseq)
+// order, and a sort by tseq alone gives it: ts and tseq are the time and the
+// global sequence of the same (last) touch, and times never decrease along
+// the sequence (every batch's times are monotone and start at or after the
+// last), so tseq_a < tseq_b implies ts_a <= ts_b.
 int tbl_expire(vp_ctx *c, FlowTable &t, int64_t cutoff, uint32_t *n_out) {
   VP_HIP(hipMemsetAsync(&t.ctl->exp_count, 0, 4, c->stream));
+  VP_HIP(hipMemsetAsync(&t.ctl->min_ts, 0xFF, 8, c->stream));
   exp_collect<<<grid_for(t.cap, 256, 512), 256, 0, c->stream>>>(tbl_dev(t), cutoff, t.ekey,
                                                                 t.eidx);
   VP_HIP(hipGetLastError());
   VP_TRY(read_ctl(c, t));
   const uint32_t k = t.h_ctl.exp_count;
+  t.ts_floor = t.h_ctl.min_ts;  // (~0: nothing stays)
   if (n_out) *n_out = k;
   if (k == 0) return 0;
   size_t need = 0;
   hipcub::DeviceRadixSort::SortPairs(nullptr, need, t.ekey, t.ekey2, t.eidx,
                                      t.eidx2, (int)k, 0, 64, c->stream);
   VP_TRY(cub_reserve(c, need));
-  // 1) by last-touch sequence, 2) stable by timestamp
   VP_HIP(hipcub::DeviceRadixSort::SortPairs(c->ws.cub_tmp, c->ws.cub_bytes,
                                             t.ekey, t.ekey2, t.eidx, t.eidx2,
                                             (int)k, 0, 64, c->stream));
-  exp_gather_ts<<<grid_for(k), 256, 0, c->stream>>>(t.eidx2, k, t.ts, t.ekey);
-  VP_HIP(hipcub::DeviceRadixSort::SortPairs(c->ws.cub_tmp, c->ws.cub_bytes,
-                                            t.ekey, t.ekey2, t.eidx2, t.eidx,
-                                            (int)k, 0, 64, c->stream));
-  exp_apply<<<grid_for(k), 256, 0, c->stream>>>(tbl_dev(t), t.eidx, k);
+  exp_apply<<<grid_for(k), 256, 0, c->stream>>>(tbl_dev(t), t.eidx2, k);
   exp_commit<<<1, 64, 0, c->stream>>>(t.ctl, k, t.h_ctl.n_tomb);
   VP_HIP(hipGetLastError());
-  return tbl_check_tombs(c, t);
+  if (t.own_n) return tbl_check_tombs(c, t);  // (only the owners' erasures are tombs)
+  // one GPU: every expired index leaves a tombstone; the counters follow
+  // without a read-back
+  Ctl &h = t.h_ctl;
+  h.stack_top += k;
+  h.n_live -= k;
+  h.n_tomb += k;
+  h.sh_live -= k;
+  const uint64_t base = std::min<uint64_t>(tbl_entries(t), t.nb_base * kBucketEntries);
+  if ((uint64_t)h.n_tomb + h.sh_live > base * 85 / 100) return tbl_rebuild(c, t);
+  return 0;
 }
 
 // Tombstones are purged (a rebuild) when they and the live entries fill 85 %
@@ -1629,11 +1626,7 @@ int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
       FlowTable &t = *tabs[i].t;
       const int64_t cut = tabs[i].cutoff(c, ta);
       if (cut <= (int64_t)lim(i)) continue;
-      VP_TRY(tbl_exact_floor(c, t));
-      if (t.ts_floor != ~0ull && (int64_t)t.ts_floor < cut) {
-        VP_TRY(tbl_expire(c, t, cut, nullptr));
-        VP_TRY(tbl_exact_floor(c, t));
-      }
+      VP_TRY(tbl_expire(c, t, cut, nullptr));  // (and the exact floor after it)
     }
     uint32_t b1 = n;
     if (!safe(ne - 1)) {  // first unsafe packet (cutoffs are monotone in time)
@@ -1941,11 +1934,7 @@ static int run_batch_sharded(vp_ctx *c, const vp_dev_batch *b,
       const int64_t cut = tabs[i].cutoff(c, tA);
       if (cut <= (int64_t)std::min<uint64_t>(F[i], (uint64_t)tA)) continue;
       VP_TRY(sync_ts(c, t));
-      VP_TRY(tbl_exact_floor(c, t));
-      if (t.ts_floor != ~0ull && (int64_t)t.ts_floor < cut) {
-        VP_TRY(tbl_expire(c, t, cut, nullptr));
-        VP_TRY(tbl_exact_floor(c, t));
-      }
+      VP_TRY(tbl_expire(c, t, cut, nullptr));  // (and the exact floor after it)
       F[i] = t.ts_floor;
     }
     auto safe_t = [&](int64_t tp) {
