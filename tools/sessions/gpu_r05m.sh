@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5 session m: expiry in one scan (the floor found beside the expired
+# round 5 session m (rerun as m2: lean-tile misses stay in their slices; the rewrite before the counters come back): expiry in one scan (the floor found beside the expired
 # set), one read-back, one sort -- GPU tests (expiry-heavy ones included),
 # churn rate and trace
 cd "${GRAFT_REPO_ROOT:-/root/repo}"

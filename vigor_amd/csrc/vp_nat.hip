@@ -1153,13 +1153,9 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
     if (threadIdx.x == 0 && c) mbase = atomicAdd(&a.t.ctl->miss_count, c);
     __syncthreads();
     const size_t s0 = (size_t)rb * per_b * 64;
-    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) {
-      a.miss[mbase + i] = a.mq[s0 + i];
-      if (a.mkq) {
-        a.mkey[mbase + i] = a.mkq[s0 + i];
-        a.mhash[mbase + i] = a.mhq[s0 + i];
-      }
-    }
+    // (unsorted phase B: the slots themselves, kMissSlice, their keys stay)
+    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x)
+      a.miss[mbase + i] = a.mkq ? (uint32_t)(s0 + i) | kMissSlice : a.mq[s0 + i];
   }
   route_publish(a, cur + kCurDest, rb);
 }
@@ -1364,7 +1360,8 @@ __global__ __launch_bounds__(256) void nat_miss_finish(NatArgs a, const uint32_t
        j0 += gridDim.x * blockDim.x) {
     const uint32_t j = j0 + lane;
     const bool v = j < n;
-    const uint32_t p = v ? list[j] : kNone;
+    uint32_t p = v ? list[j] : kNone;
+    if (v && nkord && (p & kMissSlice)) p = a.mq[p & ~kMissSlice];  // (a lean tile's slot)
     const uint32_t idx = !v ? kNone : nkord ? (uint32_t)nkord[rep[j]] : assign[scratch[rep[j]]];
     if (v) {
       if (!nkord) a.log[p] = idx;
@@ -2385,8 +2382,6 @@ static int nat_phase_a_owner_chunked(vp_ctx *c, const vp_dev_batch *b, NatArgs &
   return 0;
 }
 
-void build_flowid_tables(std::vector<uint32_t> &tab);
-
 static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
                        uint32_t p0, uint32_t p1, float *ms, int *launches,
                        uint32_t *allocated) {
@@ -2517,54 +2512,15 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
 
   uint32_t union_n = nmiss, union_off = 0;  // this rank's misses in the union
   if (c->comm) VP_TRY(union_sizes(c, nmiss, &union_n, &union_off));
-  auto nk_check = [&](const char *tag) -> int {  // (diagnostics: the miss records)
-    if (!getenv("VIGPATH_NK_CHECK")) return 0;
-    fprintf(stderr, "nkcheck %s\n", tag);
-    {
-      std::vector<uint32_t> pos(nmiss), hs(nmiss), ks(4ull * nmiss), tab;
-      VP_HIP(hipStreamSynchronize(c->stream));
-      VP_HIP(hipMemcpy(pos.data(), w.miss, 4ull * nmiss, hipMemcpyDeviceToHost));
-      VP_HIP(hipMemcpy(hs.data(), w.mhash, 4ull * nmiss, hipMemcpyDeviceToHost));
-      VP_HIP(hipMemcpy(ks.data(), w.mkey, 16ull * nmiss, hipMemcpyDeviceToHost));
-      build_flowid_tables(tab);
-      uint32_t bad = 0, out = 0;
-      for (uint32_t j = 0; j < nmiss; j++) {
-        const uint32_t *k = &ks[4 * j];
-        const uint32_t sp = k[0] & 0xFFFF, dp = k[0] >> 16, dv = k[3] & 0xFFFF, pr = (k[3] >> 16) & 0xFF;
-        const uint32_t b8[15] = {sp & 0xFF, sp >> 8, dp & 0xFF, dp >> 8, k[1] & 0xFF, (k[1] >> 8) & 0xFF,
-                                 (k[1] >> 16) & 0xFF, k[1] >> 24, k[2] & 0xFF, (k[2] >> 8) & 0xFF,
-                                 (k[2] >> 16) & 0xFF, k[2] >> 24, dv & 0xFF, dv >> 8, pr};
-        uint32_t h = 0;
-        for (int q = 0; q < 15; q++) h ^= tab[q * 256 + b8[q]];
-        if (h != hs[j]) {
-          if (bad < 5) {
-            uint8_t fr[64];
-            VP_HIP(hipMemcpy(fr, b->frames + (size_t)pos[j] * b->slot, 64, hipMemcpyDeviceToHost));
-            uint16_t ind = 0;
-            VP_HIP(hipMemcpy(&ind, b->in_dev + pos[j], 2, hipMemcpyDeviceToHost));
-            uint32_t fk0 = fr[34] | fr[35] << 8 | fr[36] << 16 | (uint32_t)fr[37] << 24;
-            uint32_t fk1 = fr[26] | fr[27] << 8 | fr[28] << 16 | (uint32_t)fr[29] << 24;
-            uint32_t fk2 = fr[30] | fr[31] << 8 | fr[32] << 16 | (uint32_t)fr[33] << 24;
-            uint32_t fk3 = ind | (uint32_t)fr[23] << 16;
-            fprintf(stderr, "nkcheck: miss %u pos %u hash %08x want %08x key %08x %08x %08x %08x frame %08x %08x %08x %08x ihl %u\n",
-                    j, pos[j], hs[j], h, k[0], k[1], k[2], k[3], fk0, fk1, fk2, fk3, fr[14] & 15);
-          }
-          bad++;
-        }
-        if (pos[j] < p0 || pos[j] >= p1) out++;
-      }
-      fprintf(stderr, "nkcheck: seg [%u,%u) misses %u bad hashes %u out of segment %u\n", p0, p1,
-              nmiss, bad, out);
-    }
-    return 0;
-  };
   if (nmiss && nku) {  // (one GPU: no sort, no key gather, no late touches)
-    VP_TRY(nk_check("unsorted"));
     VP_TRY(tbl_new_keys_unsorted(c, t, nmiss, p0, p1, now, c->seq));
-    a.t = tbl_dev(t);  // a rebuild may have moved the buckets
+    // (the frames before the counters come back: the host's round trip hides
+    // behind the rewrite)
     nat_miss_finish<<<grid_for(nmiss), 256, 0, c->stream>>>(a, w.miss, nmiss, nullptr, w.rep,
                                                             nullptr, w.nkset);
     VP_HIP(hipGetLastError());
+    VP_TRY(tbl_new_keys_done(c, t));
+    a.t = tbl_dev(t);  // a rebuild may have moved the buckets
     *allocated |= 1u;
   } else if (nmiss) {
     size_t need = 0;
@@ -2577,7 +2533,6 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     nat_miss_keys<<<grid_for(nmiss), 256, 0, c->stream>>>(a, w.miss_sorted, nmiss,
                                                           w.mkey, w.mhash);
     VP_HIP(hipGetLastError());
-    if (!c->comm) VP_TRY(nk_check("sorted"));
   }
   if (union_n && !nku) {
     if (c->comm) {  // every rank allocates the union in global packet order

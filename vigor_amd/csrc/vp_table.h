@@ -234,6 +234,12 @@ __device__ __forceinline__ bool tbl_allocated_before(const TableDev &t,
 
 // New-key pipeline input: `n` misses with keys/hashes already in
 // ws.mkey/ws.mhash and positions (ascending) in `pos`.
+// tbl_new_keys_unsorted's miss list: an entry with this bit is the index of
+// a lean tile's slot in the classify blocks' slices (missq / mkq / mhq: its
+// position, FlowId and hash there, not copied at the block's end); any other
+// entry j is a position, its FlowId and hash at mkey[j] / mhash[j].
+constexpr uint32_t kMissSlice = 0x80000000u;
+
 struct NewKeys {
   uint32_t n;
   const uint32_t *pos;
@@ -256,8 +262,11 @@ TableDev tbl_dev(const FlowTable &t);
 // inserted, born at its first packet and stamped with its last. On return
 // the low word of w.nkset[w.rep[j]] is miss j's index (kNone: table full)
 // and h_ctl holds the counters.
+// Asynchronous: the kernels are queued; tbl_new_keys_done reads the counters
+// back and runs the layout checks (the caller queues its own work between).
 int tbl_new_keys_unsorted(vp_ctx *c, FlowTable &t, uint32_t n, uint32_t p0, uint32_t p1,
                           const NowSpec &now, uint64_t seq_base);
+int tbl_new_keys_done(vp_ctx *c, FlowTable &t);
 int tbl_new_keys(vp_ctx *c, FlowTable &t, const NewKeys &nk, uint64_t seq_base,
                  uint32_t *n_new);
 

@@ -333,9 +333,12 @@ __global__ void nk_commit(NkArgs m) {
 // (atomicMax keeps the earliest), lpos = tag << 32 | last position.
 struct NkuArgs {
   TableDev t;
-  const uint32_t *pos;  // miss j's packet position
+  const uint32_t *pos;  // miss j's entry: its packet position, or a slice slot
   const uint4 *key;
   const uint32_t *hash;
+  const uint32_t *sq;  // the classify blocks' miss slices (kMissSlice entries)
+  const uint4 *skey;
+  const uint32_t *shash;
   uint32_t n, smask;
   unsigned long long *set;  // [3][smask + 1]
   uint32_t tag;
@@ -345,14 +348,27 @@ struct NkuArgs {
   uint64_t seq_base;
 };
 
+__device__ __forceinline__ uint32_t nku_pos(const NkuArgs &m, uint32_t j) {
+  const uint32_t e = m.pos[j];
+  return e & kMissSlice ? m.sq[e & ~kMissSlice] : e;
+}
+__device__ __forceinline__ uint4 nku_key(const NkuArgs &m, uint32_t j) {
+  const uint32_t e = m.pos[j];
+  return e & kMissSlice ? m.skey[e & ~kMissSlice] : m.key[j];
+}
+__device__ __forceinline__ uint32_t nku_hash(const NkuArgs &m, uint32_t j) {
+  const uint32_t e = m.pos[j];
+  return e & kMissSlice ? m.shash[e & ~kMissSlice] : m.hash[j];
+}
+
 __global__ void nku_dedup(NkuArgs m) {
   const size_t S = (size_t)m.smask + 1;
   unsigned long long *ord = m.set, *fp = m.set + S, *lp = m.set + 2 * S;
   const unsigned long long tg = (unsigned long long)m.tag << 32;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m.n;
        j += gridDim.x * blockDim.x) {
-    const uint4 kj = m.key[j];
-    const uint32_t h = m.hash[j];
+    const uint4 kj = nku_key(m, j);
+    const uint32_t h = nku_hash(m, j);
     uint32_t s = home_bucket(h, m.smask, kMixMul);
     for (;;) {
       unsigned long long cur = __hip_atomic_load(&ord[s], __ATOMIC_RELAXED,
@@ -363,12 +379,13 @@ __global__ void nku_dedup(NkuArgs m) {
         cur = old;  // (someone of this call took it: compare)
       }
       const uint32_t o = (uint32_t)cur;
-      const uint4 ko = m.key[o];
-      if (m.hash[o] == h && ko.x == kj.x && ko.y == kj.y && ko.z == kj.z && ko.w == kj.w) break;
+      const uint4 ko = nku_key(m, o);
+      if (nku_hash(m, o) == h && ko.x == kj.x && ko.y == kj.y && ko.z == kj.z && ko.w == kj.w)
+        break;
       s = (s + 1) & m.smask;
     }
     m.rep[j] = s;
-    const uint32_t p = m.pos[j];
+    const uint32_t p = nku_pos(m, j);
     // (read first: a key's packets mostly arrive after its earliest and
     // before its latest was seen, and a load is cheaper than an atomic)
     const unsigned long long f = tg | (unsigned long long)(~p), l = tg | (unsigned long long)p;
@@ -385,7 +402,7 @@ __global__ void nku_firsts(NkuArgs m) {
   const unsigned long long *fp = m.set + S;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m.n;
        j += gridDim.x * blockDim.x) {
-    const uint32_t p = m.pos[j];
+    const uint32_t p = nku_pos(m, j);
     bool f = (uint32_t)~(uint32_t)fp[m.rep[j]] == p;
     // (one first sighting per position: a packet queued twice counts once)
     if (f) {
@@ -416,7 +433,7 @@ __global__ void nku_alloc(NkuArgs m) {
   for (uint32_t f = blockIdx.x * blockDim.x + threadIdx.x; f < K;
        f += gridDim.x * blockDim.x) {
     const uint32_t j = m.first[f];
-    const uint32_t p = m.pos[j], q = p - m.p0, s = m.rep[j];
+    const uint32_t p = nku_pos(m, j), q = p - m.p0, s = m.rep[j];
     const uint32_t r = m.pre[q >> 5] + (uint32_t)__popc(m.bits[q >> 5] & ((1u << (q & 31)) - 1u));
     unsigned long long *ord = m.set;  // (the slot's word now carries the index)
     const unsigned long long tg = (unsigned long long)m.tag << 32;
@@ -425,14 +442,15 @@ __global__ void nku_alloc(NkuArgs m) {
       continue;
     }
     const uint32_t idx = r < stack_top ? t.stack[stack_top - 1 - r] : fresh + (r - stack_top);
-    const uint4 k4 = m.key[j];
+    const uint4 k4 = nku_key(m, j);
+    const uint32_t hj = nku_hash(m, j);
     const uint32_t key[4] = {k4.x, k4.y, k4.z, k4.w};
     bool tomb = false;
-    const uint32_t e = tbl_insert(t, m.hash[j], key, idx, &tomb, &disp);
+    const uint32_t e = tbl_insert(t, hj, key, idx, &tomb, &disp);
     if (tomb) atomicAdd(&t.ctl->tomb_reused, 1u);
     ins++;
     t.slot_of[idx] = e;
-    t.hash_of[idx] = m.hash[j];
+    t.hash_of[idx] = hj;
     t.birth[idx] = m.seq_base + p;
     const uint32_t last = (uint32_t)lp[s];  // the key's last packet: its stamps
     t.ts[idx] = (uint64_t)m.now.at(last);
@@ -513,6 +531,9 @@ int tbl_new_keys_unsorted(vp_ctx *c, FlowTable &t, uint32_t n, uint32_t p0, uint
   m.pos = w.miss;
   m.key = reinterpret_cast<const uint4 *>(w.mkey);
   m.hash = w.mhash;
+  m.sq = w.missq;
+  m.skey = w.mkq;
+  m.shash = w.mhq;
   m.n = n;
   m.smask = (uint32_t)(S - 1);
   m.set = w.nkset;
@@ -540,6 +561,10 @@ int tbl_new_keys_unsorted(vp_ctx *c, FlowTable &t, uint32_t n, uint32_t p0, uint
   nku_alloc<<<g, 256, 0, c->stream>>>(m);
   nku_commit<<<1, 64, 0, c->stream>>>(t.ctl, t.cap, w.nkcnt);
   VP_HIP(hipGetLastError());
+  return 0;
+}
+
+int tbl_new_keys_done(vp_ctx *c, FlowTable &t) {
   VP_TRY(read_ctl(c, t));
   return tbl_after_new_keys(c, t);
 }
