@@ -587,6 +587,9 @@ def per_packet_drop_in(packets: int = 20000, flows: int = 1024, batches=(0, 32, 
             us = float(line.split(",")[1].split()[0])
             res["per_packet" if bt == 0 else "batch_%d" % bt] = {
                 "us_per_packet": round(us, 3), "kpps": round(1e3 / us, 2)}
+            prof = [x for x in r.stderr.splitlines() if x.startswith("vigpath serve")]
+            if prof:  # (VIGPATH_SERVE_PROF=1: vp_process_one's stage times)
+                res["per_packet" if bt == 0 else "batch_%d" % bt]["serve_prof"] = prof[-1]
             out = np.frombuffer(open(tout, "rb").read(), np.uint16, n, 12)
             assert (out[flows:] == 1).all()  # every steady packet out on the WAN port
     return res

@@ -206,6 +206,18 @@ int vp_process_batch(vp_ctx *ctx, uint32_t n, const uint16_t *in_dev,
                      uint8_t *const *frames, const uint16_t *len,
                      const int64_t *now, uint16_t *out_dev);
 
+/* One packet: nf_process (nf.h:14-15, called once per packet by nf.c:150-176;
+ * the nf.h shims' nf_process calls this). The frame is rewritten in place and
+ * the output port stored in *out_dev; same results as vp_process_batch with
+ * n = 1. vignat on one GPU serves it from a persistent kernel that polls a
+ * host-coherent mailbox (no launch per packet) while no flow expiry is due at
+ * `now`; otherwise, and for the other NFs, it is vp_process_batch with n = 1.
+ * The kernel leaves after VIGPATH_SERVE_IDLE_MS (default 20) without a
+ * packet, at any other call on the context, and at exit; VIGPATH_SERVE=0
+ * turns it off. */
+int vp_process_one(vp_ctx *ctx, uint16_t in_dev, uint8_t *frame, uint16_t len,
+                   int64_t now, uint16_t *out_dev);
+
 /* Host-resident contiguous batch (frames `slot` bytes apart). */
 int vp_process_host(vp_ctx *ctx, uint32_t n, const uint16_t *in_dev,
                     uint8_t *frames, uint32_t slot, const uint16_t *len,

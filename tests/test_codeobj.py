@@ -27,7 +27,7 @@ MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 # per-packet kernels of the steady state: no private segment at all
 NO_SCRATCH = ["bridge_classify", "lb_classify64", "fw_classify64", "pol_classify64",
               "nat_remote64", "nat_own_probe", "touch_bins_reduce",
-              "mbuf_gather_hdr", "mbuf_gather_full", "mbuf_scatter"]
+              "mbuf_gather_hdr", "mbuf_gather_full", "mbuf_scatter", "nat_serve"]
 # the vignat tile kernels keep a few register spills on the per-lane path,
 # outside the lean tile (bytes per lane); holding the 128-byte tile's tail
 # registers one phase longer once cost 200 bytes and 60 % of the kernel

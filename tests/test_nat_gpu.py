@@ -133,6 +133,54 @@ def test_per_packet_nf_process():
         assert bytes(b) == exp[i * 64:i * 64 + 60].tobytes()
 
 
+@pytest.mark.parametrize("seed,slot,max_flows,expire_us", [
+    (0, 64, 64, 60_000_000),   # LAN/WAN mix, malformed frames, the table fills
+    (1, 256, 128, 60_000_000),  # header edge cases (options, odd lengths) up to 256 B
+    (2, 64, 256, 7),           # expiry due often: the kernel and the batch path alternate
+    (3, 2048, 64, 60_000_000),  # long frames (up to 1514 B: the mailbox's whole frame)
+])
+def test_process_one_server(seed, slot, max_flows, expire_us):
+    """vp_process_one (nf_process of the nf.h shims): vignat's persistent
+    per-packet kernel, packet for packet against the oracle, with batch calls
+    and an idle exit (the kernel leaves, the next packet launches it again)
+    in between, and the flow state compared at the end. Each frame is its own
+    buffer of len bytes (as an mbuf's data), so the oracle's frames are
+    zeroed past len."""
+    import time
+    rng = np.random.default_rng(seed)
+    n = 600
+    if slot == 64:
+        fr, ln, dv, now = mixed_nat_trace(rng, n, 150, max_idx=max_flows)
+    else:
+        fr, ln, dv = edge_nat_trace(rng, n, 100, slot=slot, long_frames=True)
+        now = T.NOW0 + np.arange(n, dtype=np.int64) * 3
+    F = fr.reshape(n, slot).copy()
+    for i in range(n):
+        F[i, ln[i]:] = 0
+    exp = F.reshape(-1).copy()
+    nat, o = make_pair(max_flows=max_flows, expire_us=expire_us)
+    exp_out = o.run(exp, ln, dv, now, slot)
+    E = exp.reshape(n, slot)
+    i = 0
+    while i < n:
+        if i % 200 == 150:  # a batch call between single packets
+            k = 20
+            bufs = [bytearray(F[j, :ln[j]].tobytes()) for j in range(i, i + k)]
+            out = nat.process_mbufs(bufs, dv[i:i + k], now[i:i + k])
+            np.testing.assert_array_equal(out, exp_out[i:i + k])
+            for j in range(k):
+                assert bytes(bufs[j]) == E[i + j, :ln[i + j]].tobytes(), i + j
+            i += k
+            continue
+        if i == 300:
+            time.sleep(0.1)  # past the idle exit (VIGPATH_SERVE_IDLE_MS, 20)
+        b = bytearray(F[i, :ln[i]].tobytes())
+        assert nat.process(int(dv[i]), b, int(now[i])) == exp_out[i], i
+        assert bytes(b) == E[i, :ln[i]].tobytes(), i
+        i += 1
+    check_state(nat, o, max_flows)
+
+
 def test_config2_1m_flows_full_size():
     """BASELINE config 2 at its full table size (1M flows, cap 2^20): a
     warm-up batch creating every flow, then steady-state batches, checked

@@ -126,7 +126,7 @@ EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_fw_create",
            "vp_attach_comm", "vp_shard_mode", "vp_sync_state", "vp_live_count",
            "vp_kernel_timing", "vp_last_kernel_ms", "vp_version", "vp_table_stats_get",
            "vp_last_error", "vp_register_host", "vp_unregister_host", "vp_process_mbufs",
-           "vp_last_stage_ms", "vp_comm_abort", "vp_probe_slots"]
+           "vp_last_stage_ms", "vp_comm_abort", "vp_probe_slots", "vp_process_one"]
 
 _libs = {}
 
@@ -174,6 +174,9 @@ def lib(path: str | None = None):
                                    C.POINTER(C.c_void_p), C.c_void_p,
                                    C.c_void_p, C.c_void_p]
     L.vp_process_batch.restype = C.c_int
+    L.vp_process_one.argtypes = [C.c_void_p, C.c_uint16, C.c_void_p, C.c_uint16,
+                                 C.c_int64, C.POINTER(C.c_uint16)]
+    L.vp_process_one.restype = C.c_int
     L.vp_process_mbufs.argtypes = [C.c_void_p, C.POINTER(MbufBatchC)]
     L.vp_process_mbufs.restype = C.c_int
     L.vp_register_host.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]

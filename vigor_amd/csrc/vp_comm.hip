@@ -233,6 +233,7 @@ int vp_attach_rccl(vp_ctx *c, const uint8_t id[VP_COMM_ID_BYTES], int nranks,
   VP_TRY(attach_check(c, nranks, rank));
   if (!id) return VP_EINVAL;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  VP_TRY(serve_stop(c));
   ncclUniqueId u;
   memcpy(u.internal, id, VP_COMM_ID_BYTES);
   RcclComm *m = new RcclComm();
@@ -251,6 +252,7 @@ int vp_attach_rccl(vp_ctx *c, const uint8_t id[VP_COMM_ID_BYTES], int nranks,
 int vp_attach_comm(vp_ctx *c, const vp_comm_ops *ops, int nranks, int rank) {
   VP_TRY(attach_check(c, nranks, rank));
   if (!ops || !ops->allgather || !ops->allreduce_max_u64) return VP_EINVAL;
+  VP_TRY(serve_stop(c));
   HostComm *m = new HostComm();
   m->n = nranks;
   m->r = rank;
@@ -267,6 +269,7 @@ int vp_shard_mode(vp_ctx *c, int mode) {
   if (!c->comm || c->seq != 0 || c->shard_mode != VP_SHARD_REPLICATED) return VP_EINVAL;
   if (c->kind != KIND_NAT) return VP_ENOTSUP;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  VP_TRY(serve_stop(c));
   HostComm *h = dynamic_cast<HostComm *>(c->comm);
   if (h && !h->ops.alltoallv) return VP_EINVAL;
   VP_TRY(tbl_set_owner(c, c->ft, (uint32_t)c->comm->n, (uint32_t)c->comm->r));
@@ -284,6 +287,7 @@ int vp_sync_state(vp_ctx *c) {
   if (!c) return VP_EINVAL;
   if (!c->comm) return 0;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  VP_TRY(serve_stop(c));
   return sync_tables(c);
 }
 

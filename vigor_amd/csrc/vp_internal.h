@@ -295,6 +295,30 @@ struct HostMap {
 };
 constexpr int kMaxHostMaps = 16;
 
+// vp_process_one's mailbox (vp_nat.hip nat_serve): page-locked, host-coherent
+// memory the host and a persistent one-wave kernel poll. The host writes the
+// packet's time and frame, then the doorbell; the kernel rewrites the frame in
+// place, then sets the answer word.
+constexpr uint32_t kServeFrame = 2048;  // longest frame served (others: the batch path)
+constexpr uint32_t kServeLeave = 0xFFFFFFFFu;  // doorbell high word: leave
+struct ServeBox {
+  uint64_t bell;     // host: request number | (len | in_dev << 16) << 32
+  uint64_t ans;      // device: request number | (out | fresh << 16) << 32
+  uint64_t prof[8];  // device: wall-clock stamps of the last request (VIGPATH_SERVE_PROF)
+  alignas(16) int64_t now;  // host: the packet's time (read with the frame's first bytes)
+  uint64_t pad_;
+  uint8_t frame[kServeFrame];
+};
+// One packet through the persistent kernel (vignat, one GPU, no expiry due):
+// 0 done; 1 not eligible (the caller takes the batch path, the server is
+// stopped); < 0 an error.
+int nat_process_one(vp_ctx *c, uint16_t in_dev, uint8_t *frame, uint16_t len, int64_t now,
+                    uint16_t *out);
+// Stop the context's persistent kernel, if it runs (every other entry point
+// calls this first: the kernel owns the table while it runs).
+int serve_stop(vp_ctx *c);
+void serve_free(vp_ctx *c);
+
 }  // namespace vp
 
 struct vp_ctx {
@@ -371,4 +395,11 @@ struct vp_ctx {
   // during vp_process_mbufs: tail sums of the 64-byte header slots the
   // current device batch holds (vp_nat.hip NatArgs::tail), else null
   const uint32_t *hdr_tail = nullptr;
+  // vp_process_one (vp_nat.hip): the mailbox, whether nat_serve runs on
+  // `stream`, the last request number, and its idle exit (wall-clock ticks)
+  vp::ServeBox *sbox = nullptr;
+  bool srv_on = false;
+  uint32_t srv_req = 0;
+  uint64_t srv_idle = 0, srv_idle_ms = 1;
+  double srv_prof[10] = {};  // VIGPATH_SERVE_PROF: summed stage times (us), counts
 };

@@ -797,6 +797,7 @@ int vp_register_host(vp_ctx *c, void *base, size_t bytes) {
     return VP_ENOMEM;
   }
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  VP_TRY(serve_stop(c));
   const uint64_t hb = reinterpret_cast<uint64_t>(base);
   for (const HostMap &h : c->hmaps)
     if (hb < h.hend && hb + bytes > h.hbase) return VP_EINVAL;  // overlaps
@@ -847,6 +848,7 @@ int vp_register_host(vp_ctx *c, void *base, size_t bytes) {
 int vp_unregister_host(vp_ctx *c, void *base) {
   if (!c || !base) return VP_EINVAL;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  VP_TRY(serve_stop(c));
   const uint64_t hb = reinterpret_cast<uint64_t>(base);
   for (size_t i = 0; i < c->hmaps.size(); i++) {
     if (c->hmaps[i].hbase != hb) continue;
@@ -863,6 +865,7 @@ int vp_process_mbufs(vp_ctx *c, const vp_mbuf_batch *b) {
   if (b->n && (!b->frames || !b->len || !b->in_dev || !b->out_dev)) return VP_EINVAL;
   if (!b->now && (b->now_step < 0 || b->now0 < 0)) return VP_ENOTSUP;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  VP_TRY(serve_stop(c));
   if (b->n == 0 && !c->comm) return 0;
   const MbufPlan pl = mbuf_plan(c);
   if (pl.header && !c->comm && mbuf_mode_host()) return mbuf_host_pipeline(c, b, pl);

@@ -20,9 +20,11 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "vp_comm.h"
@@ -1847,6 +1849,263 @@ __global__ void nat_defer_finish(NatArgs a, const uint32_t *list, uint32_t n) {
   }
 }
 
+// ========================================================= one packet ==
+// nf.c's per-packet loop (nf.c:150-176) calls nf_process once per packet.
+// Through the batch path one packet costs a launch sequence and a host round
+// trip per call (≈68 µs); vp_process_one instead hands it to
+// nat_serve, one wave that stays resident and polls a host-coherent mailbox
+// (ServeBox, vp_internal.h): no launch per packet. The host serves through it
+// only while no expiry is due (nat_process_one), so the kernel restates
+// nat_main.c:22-109 without the expiry step.
+
+// flow_manager_get_internal / allocate_flow (nat_main.c:68-97) for one LAN
+// key at global sequence seq: its index, allocated when new (*fresh = 1), and
+// stamped; kNone when the table is full (drop).
+__device__ __forceinline__ uint32_t one_lan(const TableDev &t, uint32_t hh, const uint32_t key[4],
+                                            int64_t now, uint64_t seq, uint32_t *fresh) {
+  uint32_t idx = tbl_probe(t, hh, key);
+  if (idx == kNone) {  // dchain_allocate_new_index: the freed stack, then fresh
+    Ctl *c = t.ctl;
+    const uint32_t st = c->stack_top, fn = c->fresh_next;
+    if (st) {
+      idx = t.stack[st - 1];
+      c->stack_top = st - 1;
+    } else if (fn < t.cap) {
+      idx = fn;
+      c->fresh_next = fn + 1;
+    } else {
+      return kNone;  // nat_main.c:87-91
+    }
+    bool tomb = false;
+    uint32_t disp = 0;
+    const uint32_t e = tbl_insert(t, hh, key, idx, &tomb, &disp);
+    if (tomb) c->n_tomb -= 1;
+    c->n_live += 1;
+    c->sh_live += 1;
+    c->disp_count += disp;
+    t.slot_of[idx] = e;
+    t.hash_of[idx] = hh;
+    t.birth[idx] = seq;
+    *fresh = 1;
+  }
+  t.ts[idx] = (uint64_t)now;
+  t.tseq[idx] = seq;
+  return idx;
+}
+
+// flow_manager_get_external (nat_main.c:42-67) for external port dp: false
+// when no flow holds it; else the flow's key in *k, stamped (rejuvenated
+// before the anti-spoof check).
+__device__ __forceinline__ bool one_wan(const NatArgs &a, uint32_t dp, int64_t now,
+                                        uint64_t seq, uint4 *k) {
+  const TableDev &t = a.t;
+  const int idx = (int)dp - (int)a.start_port;
+  if (idx < 0 || idx >= (int)t.cap || t.slot_of[idx] == kNone) return false;
+  *k = tbl_key_of(t, (uint32_t)idx);
+  t.ts[idx] = (uint64_t)now;
+  t.tseq[idx] = seq;
+  return true;
+}
+
+// nat_main.c:30-106 for one frame, byte-addressed (f: its bytes, cap = its
+// length; IP options, odd headers): returns the output port.
+__device__ __forceinline__ uint32_t nat_one(const NatArgs &a, const uint32_t *T,
+                                            const GFrame &f, uint32_t in, uint32_t len,
+                                            int64_t now, uint64_t seq, uint32_t *fresh) {
+  const L34 h = parse_l34(f, len);
+  if (!h.ok) return in;  // nat_main.c:30-38
+  const uint32_t proto = f.r8(h.ip + 9);
+  const uint32_t sp = f.r16(h.l4), dp = f.r16(h.l4 + 2);
+  const uint32_t sip = f.r32(h.ip + 12), dip = f.r32(h.ip + 16);
+  uint32_t dst;
+  if (in == a.wan) {
+    uint4 k;
+    if (!one_wan(a, dp, now, seq, &k)) return in;
+    if ((k.z != sip) | ((k.x >> 16) != sp) | (((k.w >> 16) & 0xFF) != proto)) return in;
+    f.w32(h.ip + 16, k.y);
+    f.w16(h.l4 + 2, (uint16_t)(k.x & 0xFFFF));
+    dst = k.w & 0xFFFF;
+  } else {
+    const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
+    const uint32_t idx = one_lan(a.t, flowid_hash(T, sp, dp, sip, dip, in, proto), key, now,
+                                 seq, fresh);
+    if (idx == kNone) return in;
+    f.w32(h.ip + 12, a.ext_ip);
+    f.w16(h.l4, (uint16_t)(a.start_port + idx));
+    dst = a.wan;
+  }
+  set_checksums(f, h.ip, h.l4);  // (the whole frame is in f)
+  uint32_t mw[3];
+  macs_for(a, dst, mw);
+  set_macs(f, mw);
+  return dst;
+}
+
+// The same for a frame with a 20-byte IPv4 header, its first 64 bytes in
+// registers (nat_issue / nat_finish's register path; `tail` = the raw sum of
+// the L4 bytes past byte 64). kNone: not such a frame (nat_one takes it).
+__device__ __forceinline__ uint32_t nat_one_reg(const NatArgs &a, const uint32_t *T, RFrame &f,
+                                                uint32_t in, uint32_t len, uint32_t tail,
+                                                int64_t now, uint64_t seq, uint32_t *fresh,
+                                                bool prof, uint64_t &mk0, uint64_t &mk1) {
+  const uint32_t et = f.w[3] & 0xFFFF, ihl = (f.w[3] >> 16) & 0x0F;
+  if (!(et == 0x0008 && ihl == 5)) return kNone;
+  const uint32_t tl = bswap16((uint16_t)(f.w[4] & 0xFFFF));
+  const uint16_t unread = (uint16_t)(len - 14);
+  const uint32_t proto = f.w[5] >> 24;
+  if (!((unread >= 20) & (unread >= tl) & ((proto == 6) | (proto == 17)) &
+        ((uint32_t)(len - 34) >= 4u)))
+    return in;
+  const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
+  const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
+  uint32_t dst, mw[3];
+  if (in == a.wan) {
+    uint4 k;
+    if (!one_wan(a, dp, now, seq, &k)) return in;
+    if ((k.z != sip) | ((k.x >> 16) != sp) | (((k.w >> 16) & 0xFF) != proto)) return in;
+    f.set32at2(30, k.y);        // dst_addr = flow.src_ip
+    f.set16(36, k.x & 0xFFFF);  // dst_port = flow.src_port
+    dst = k.w & 0xFFFF;
+  } else {
+    const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
+    const uint32_t hh = flowid_hash(T, sp, dp, sip, dip, in, proto);
+    if (prof) mk0 = wall_clock64();
+    const uint32_t idx = one_lan(a.t, hh, key, now, seq, fresh);
+    if (prof) mk1 = wall_clock64();
+    if (idx == kNone) return in;
+    f.set32at2(26, a.ext_ip);
+    f.set16(34, (uint16_t)(a.start_port + idx));
+    dst = a.wan;
+  }
+  macs_for(a, dst, mw);
+  fast_checksums(f, proto, tl, tail);
+  f.w[0] = mw[0];
+  f.w[1] = mw[1];
+  f.w[2] = mw[2];
+  return dst;
+}
+
+// The server: one wave. It polls the doorbell (one PCIe read a turn); on a
+// request the frame and time cross PCIe into LDS together (16-byte
+// system-coherent loads, one per lane per 1 KiB), the wave sums the L4 bytes
+// past byte 64, lane 0 runs the packet, the frame goes back the same way,
+// and the answer word follows once every store has completed. Packets take
+// global sequence numbers seq, seq + 1, ... It leaves on the leave doorbell
+// or after `idle` wall-clock ticks without a request; a request posted as it
+// leaves finds the stream idle and the host launches it again
+// (nat_process_one). flags: bit 0, the stage clock (VIGPATH_SERVE_PROF).
+__global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64_t seq,
+                                                uint64_t idle, uint32_t flags) {
+  __shared__ uint32_t T[kNatTabWords];
+  __shared__ uint4 fr[kServeFrame / 16];
+  __shared__ int64_t now_s;
+  load_nat_tables(T, a);
+  const uint32_t lane = threadIdx.x;
+  const bool prof = flags & 1u;
+  uint32_t done = (uint32_t)__hip_atomic_load(&box->ans, __ATOMIC_ACQUIRE,
+                                              __HIP_MEMORY_SCOPE_SYSTEM);
+  done = __builtin_amdgcn_readfirstlane(done);
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  constexpr int kSys = 17;  // sc0 | sc1: system-coherent (bypasses the GPU caches)
+  // 16-byte chunk 0: the time; chunk 1 + i: the frame's chunk i
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(&box->now, 0, 16 + kServeFrame, 0x00020000);
+  uint64_t t0 = wall_clock64();
+  for (;;) {
+    const uint64_t bell =
+        __hip_atomic_load(&box->bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t req = __builtin_amdgcn_readfirstlane((uint32_t)bell);
+    if (req == done) {
+      if (wall_clock64() - t0 > idle) break;
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    // The frame and time are read with system-coherent loads issued after
+    // the doorbell's came back (the host wrote them before it), so no
+    // acquire fence: one would also drop the table's lines from the L2.
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(bell >> 32));
+    if (hi == kServeLeave) break;
+    const uint64_t s0 = wall_clock64();
+    const uint32_t len = min(hi & 0xFFFFu, kServeFrame), in = hi >> 16;
+    const uint32_t nch = (len + 15) / 16;
+    for (uint32_t i = lane; i <= nch; i += 64) {
+      const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16 * i), 0, kSys);
+      if (i == 0)
+        now_s = (int64_t)((uint64_t)v[0] | ((uint64_t)v[1] << 32));
+      else
+        fr[i - 1] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    __syncthreads();
+    // the L4 checksum's bytes past 64: [64, min(14 + total_length, len))
+    uint32_t tail = 0;
+    if (len > 64) {
+      const uint8_t *fb = reinterpret_cast<const uint8_t *>(fr);
+      const uint32_t tl = ((uint32_t)fb[16] << 8) | fb[17];
+      const uint32_t end = min(14 + tl, len);
+      for (uint32_t c = 64 + 16 * lane; c < end; c += 1024)
+        tail = sum16x4(chunk_keep(fr[c / 16], 0, (int)end - (int)c), tail);
+      for (int o = 32; o > 0; o >>= 1) tail += __shfl_xor(tail, o);
+    }
+    const uint64_t s1 = wall_clock64();
+    uint32_t res = 0;
+    uint64_t mk0 = 0, mk1 = 0, mk2 = 0;
+    if (lane == 0) {
+      uint32_t fresh = 0;
+      RFrame f;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint4 v = chunk_keep(fr[j], 0, (int)len - 16 * j);
+        f.w[4 * j] = v.x;
+        f.w[4 * j + 1] = v.y;
+        f.w[4 * j + 2] = v.z;
+        f.w[4 * j + 3] = v.w;
+      }
+      uint32_t out = nat_one_reg(a, T, f, in, len, tail, now_s, seq, &fresh, prof, mk0, mk1);
+      if (prof) mk2 = wall_clock64();
+      if (out == kNone) {
+        const GFrame g{reinterpret_cast<uint8_t *>(fr), len};
+        out = nat_one(a, T, g, in, len, now_s, seq, &fresh);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          fr[j] = make_uint4(f.w[4 * j], f.w[4 * j + 1], f.w[4 * j + 2], f.w[4 * j + 3]);
+      }
+      res = out | (fresh << 16);
+    }
+    __syncthreads();
+    const uint64_t s2 = wall_clock64();
+    for (uint32_t i = lane; i < nch; i += 64) {
+      const uint4 v = fr[i];
+      __builtin_amdgcn_raw_buffer_store_b128((v4u){v.x, v.y, v.z, v.w}, rs, (int)(16 * (i + 1)),
+                                             0, kSys);
+    }
+    if (lane == 0) {
+      if (prof) {
+        auto put = [&](int k, uint64_t v) {
+          __hip_atomic_store(&box->prof[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        };
+        put(0, t0);
+        put(1, s0);
+        put(2, s1);
+        put(3, mk0);
+        put(4, mk1);
+        put(5, mk2);
+        put(6, s2);
+        put(7, wall_clock64());
+      }
+      const uint64_t ans = (uint64_t)req | ((uint64_t)res << 32);
+      // every store of the wave complete first (its counter covers all
+      // lanes); no release fence, which would write back the whole L2
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (no compiler reordering either)
+      __builtin_amdgcn_s_waitcnt(0);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      __hip_atomic_store(&box->ans, ans, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    done = req;
+    seq += 1;
+    t0 = wall_clock64();
+  }
+}
+
 // =============================================================== host ==
 
 // nat_flowmanager.c:57-65: expiration_time (u32 us) * 1000 is computed in
@@ -2582,6 +2841,164 @@ int nat_process_device(vp_ctx *c, const vp_dev_batch *b) {
 
 int nat_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *keys) {
   return tbl_dump(c, c->ft, alloc, ts, reinterpret_cast<uint32_t *>(keys));
+}
+
+// ---------------------------------------------------- vp_process_one --
+// Contexts whose server may run: stopped at exit, before the runtime's own
+// teardown (the kernel would otherwise keep the stream busy until its idle
+// exit).
+static std::mutex g_srv_mu;
+static std::vector<vp_ctx *> g_srv;
+static void serve_stop_all() {
+  std::vector<vp_ctx *> v;
+  {
+    std::lock_guard<std::mutex> g(g_srv_mu);
+    v = g_srv;
+  }
+  for (vp_ctx *c : v) serve_stop(c);
+}
+
+static const bool g_srv_prof = [] {
+  const char *e = getenv("VIGPATH_SERVE_PROF");
+  return e && atoi(e);
+}();
+int serve_stop(vp_ctx *c) {
+  if (!c || !c->srv_on) return 0;
+  ServeBox *bx = c->sbox;
+  const uint32_t req = ++c->srv_req;
+  __atomic_store_n(&bx->bell, (uint64_t)req | ((uint64_t)kServeLeave << 32), __ATOMIC_RELEASE);
+  const hipError_t e = hipStreamSynchronize(c->stream);
+  // (the kernel is gone: the leave request counts as answered for the next one)
+  __atomic_store_n(&bx->ans, (uint64_t)req, __ATOMIC_RELEASE);
+  c->srv_on = false;
+  {
+    std::lock_guard<std::mutex> g(g_srv_mu);
+    g_srv.erase(std::remove(g_srv.begin(), g_srv.end(), c), g_srv.end());
+  }
+  if (g_srv_prof && c->srv_prof[5] > 0) {
+    const double n = c->srv_prof[5];
+    fprintf(stderr,
+            "vigpath serve: %.0f packets, us/packet: host call %.2f, bell->seen %.2f "
+            "(idle poll), load %.2f, packet %.2f (LAN: hash %.2f, table %.2f, rewrite %.2f), "
+            "store+answer %.2f\n",
+            n, c->srv_prof[0] / n, c->srv_prof[1] / n, c->srv_prof[2] / n, c->srv_prof[3] / n,
+            c->srv_prof[6] / std::max(1.0, c->srv_prof[9]),
+            c->srv_prof[7] / std::max(1.0, c->srv_prof[9]),
+            c->srv_prof[8] / std::max(1.0, c->srv_prof[9]), c->srv_prof[4] / n);
+    for (double &x : c->srv_prof) x = 0;
+  }
+  VP_HIP(e);
+  return 0;
+}
+
+void serve_free(vp_ctx *c) {
+  serve_stop(c);
+  if (c->sbox) hipHostFree(c->sbox);
+  c->sbox = nullptr;
+}
+
+static int serve_launch(vp_ctx *c) {
+  const FlowTable &t = c->ft;
+  NatArgs a{};
+  a.t = tbl_dev(t);
+  a.crc_tab = c->crc_tab;
+  a.macw = c->macw;
+  a.wan_macw0 = c->wan_macw[0];
+  a.wan_macw1 = c->wan_macw[1];
+  a.wan_macw2 = c->wan_macw[2];
+  a.ext_ip = c->nat.external_addr;
+  a.wan = c->nat.wan_device;
+  a.start_port = c->nat.start_port;
+  a.n_dev = c->nat.n_devices;
+  ServeBox *dbox = nullptr;
+  VP_HIP(hipHostGetDevicePointer((void **)&dbox, c->sbox, 0));
+  nat_serve<<<1, 64, 0, c->stream>>>(a, dbox, c->seq, c->srv_idle,
+                                     g_srv_prof ? 1u : 0u);
+  VP_HIP(hipGetLastError());
+  if (!c->srv_on) {
+    static std::once_flag once;
+    std::call_once(once, [] { atexit(serve_stop_all); });
+    std::lock_guard<std::mutex> g(g_srv_mu);
+    g_srv.push_back(c);
+  }
+  c->srv_on = true;
+  return 0;
+}
+
+int nat_process_one(vp_ctx *c, uint16_t in_dev, uint8_t *frame, uint16_t len, int64_t now,
+                    uint16_t *out) {
+  static const bool off = [] {
+    const char *e = getenv("VIGPATH_SERVE");
+    return e && !atoi(e);
+  }();
+  FlowTable &t = c->ft;
+  // no expiry due at this packet (run_batch's test for a segment of one)
+  const bool ok = !off && !c->comm && len <= kServeFrame && now >= 0 && now >= c->last_now &&
+                  nat_cutoff(c, now) <= (int64_t)std::min<uint64_t>(t.ts_floor, (uint64_t)now);
+  if (!ok) {
+    VP_TRY(serve_stop(c));
+    return 1;
+  }
+  if (!c->sbox) {
+    VP_HIP(hipHostMalloc((void **)&c->sbox, sizeof(ServeBox),
+                         hipHostMallocCoherent | hipHostMallocMapped));
+    memset(c->sbox, 0, sizeof(ServeBox));
+    c->srv_req = 0;
+    int khz = 0;
+    VP_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->gpu));
+    const char *e = getenv("VIGPATH_SERVE_IDLE_MS");
+    c->srv_idle_ms = e ? std::max(1, atoi(e)) : 20;
+    c->srv_idle = (uint64_t)std::max(khz, 1) * c->srv_idle_ms;
+  }
+  if (!c->srv_on) {
+    // the batch path may leave a timestamp fold running: the server is
+    // queued behind it on the same stream
+    VP_TRY(serve_launch(c));
+  }
+  ServeBox *bx = c->sbox;
+  const auto h0 = std::chrono::steady_clock::now();
+  bx->now = now;
+  memcpy(bx->frame, frame, len);
+  const uint32_t req = ++c->srv_req;
+  __atomic_store_n(&bx->bell, (uint64_t)req | ((uint64_t)(len | ((uint32_t)in_dev << 16)) << 32),
+                   __ATOMIC_RELEASE);
+  auto last = h0;
+  uint64_t ans;
+  while ((uint32_t)(ans = __atomic_load_n(&bx->ans, __ATOMIC_ACQUIRE)) != req) {
+    __builtin_ia32_pause();
+    const auto nw = std::chrono::steady_clock::now();
+    if (nw - last < std::chrono::microseconds(200)) continue;
+    last = nw;
+    // the kernel left (idle) before it saw the request: launch it again
+    const hipError_t q = hipStreamQuery(c->stream);
+    if (q == hipErrorNotReady) continue;
+    VP_HIP(q);
+    if ((uint32_t)__atomic_load_n(&bx->ans, __ATOMIC_ACQUIRE) == req) continue;
+    VP_TRY(serve_launch(c));
+  }
+  memcpy(frame, bx->frame, len);
+  *out = (uint16_t)(ans >> 32);
+  if ((ans >> 48) & 1u) t.ts_floor = std::min<uint64_t>(t.ts_floor, (uint64_t)now);
+  c->seq += 1;
+  c->last_now = now;
+  if (g_srv_prof) {  // (device stamps: wall clock ticks, 100 MHz)
+    const double us_tick = 1e3 / (double)(c->srv_idle / c->srv_idle_ms);
+    c->srv_prof[0] +=
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
+    const uint64_t *p = bx->prof;
+    c->srv_prof[1] += us_tick * (double)(p[1] - p[0]);
+    c->srv_prof[2] += us_tick * (double)(p[2] - p[1]);
+    if (p[3] && p[4]) {  // (register-path LAN packets: hash | table | rewrite)
+      c->srv_prof[6] += us_tick * (double)(p[3] - p[2]);
+      c->srv_prof[7] += us_tick * (double)(p[4] - p[3]);
+      c->srv_prof[8] += us_tick * (double)(p[5] - p[4]);
+      c->srv_prof[9] += 1;
+    }
+    c->srv_prof[3] += us_tick * (double)(p[6] - p[2]);
+    c->srv_prof[4] += us_tick * (double)(p[7] - p[6]);
+    c->srv_prof[5] += 1;
+  }
+  return 0;
 }
 
 void build_flowid_tables(std::vector<uint32_t> &tab) {

@@ -95,13 +95,13 @@ static void print_mac(const uint8_t *m) {
   printf("%02X:%02X:%02X:%02X:%02X:%02X", m[0], m[1], m[2], m[3], m[4], m[5]);
 }
 
-/* One packet through the batch C-ABI. The reference has no error path; a
- * device failure here aborts like nf.c's tx failure does (nf.c:167-172). */
+/* One packet through the C-ABI (vp_process_one). The reference has no error
+ * path; a device failure here aborts like nf.c's tx failure does
+ * (nf.c:167-172). */
 static int shim_process_one(uint16_t device, uint8_t *buffer,
                             uint16_t packet_length, vigor_time_t now) {
   uint16_t out = device;
-  uint8_t *frames[1] = {buffer};
-  int rc = vp_process_batch(g_ctx, 1, &device, frames, &packet_length, &now, &out);
+  int rc = vp_process_one(g_ctx, device, buffer, packet_length, now, &out);
   if (rc != VP_OK) {
     fprintf(stderr, "vigpath: nf_process failed (%d)\n", rc);
     abort();

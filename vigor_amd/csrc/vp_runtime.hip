@@ -182,6 +182,7 @@ static int ctx_common(vp_ctx *c, int gpu) {
 static void free_all(vp_ctx *c) {
   if (!c) return;
   hipSetDevice(c->gpu);
+  serve_free(c);  // (vp_process_one's kernel: stopped first)
   if (c->stream) hipStreamSynchronize(c->stream);
   tbl_free(c->ft);
   tbl_free(c->ft2);
@@ -648,6 +649,7 @@ int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
     vp::hostprof(0);
   }
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  VP_TRY(serve_stop(c));
   hipStream_t user = (hipStream_t)stream;
   hipEvent_t dep = nullptr;
   if (user && user != c->stream) {  // order after the caller's stream
@@ -690,6 +692,18 @@ int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
   return rc;
 }
 
+int vp_process_one(vp_ctx *c, uint16_t in_dev, uint8_t *frame, uint16_t len, int64_t now,
+                   uint16_t *out_dev) {
+  if (!c || !frame || !out_dev) return VP_EINVAL;
+  if (c->kind == KIND_NAT) {
+    if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+    const int rc = nat_process_one(c, in_dev, frame, len, now, out_dev);
+    if (rc <= 0) return rc;  // (1: not eligible, the batch path below)
+  }
+  uint8_t *frames[1] = {frame};
+  return vp_process_batch(c, 1, &in_dev, frames, &len, &now, out_dev);
+}
+
 int vp_process_host_batch(vp_ctx *c, const vp_host_batch *b) {
   if (!c || !b) return VP_EINVAL;
   if (b->n && (!b->in_dev || !b->frames || !b->len || !b->out_dev)) return VP_EINVAL;
@@ -697,6 +711,7 @@ int vp_process_host_batch(vp_ctx *c, const vp_host_batch *b) {
   if (b->slot < 64 || (b->slot & 15)) return VP_EINVAL;
   if (!b->now && (b->now_step < 0 || b->now0 < 0)) return VP_ENOTSUP;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  VP_TRY(serve_stop(c));
   return host_pipeline(c, b);
 }
 
@@ -718,6 +733,7 @@ int vp_process_host(vp_ctx *c, uint32_t n, const uint16_t *in_dev,
 int vp_nat_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *keys) {
   if (!c || c->kind != KIND_NAT || !alloc || !ts || !keys) return VP_EINVAL;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  VP_TRY(serve_stop(c));
   return nat_dump(c, alloc, ts, keys);
 }
 
@@ -726,6 +742,7 @@ int vp_bridge_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *macs,
   if (!c || c->kind != KIND_BRIDGE || !alloc || !ts || !macs || !port)
     return VP_EINVAL;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  VP_TRY(serve_stop(c));
   std::vector<uint32_t> keys(4ull * c->ft.cap);
   VP_TRY(tbl_dump(c, c->ft, alloc, ts, keys.data()));
   for (uint32_t i = 0; i < c->ft.cap; i++) {
@@ -742,6 +759,7 @@ int vp_fw_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint8_t *keys,
   if (!c || c->kind != KIND_FW || !alloc || !ts || !keys || !int_dev)
     return VP_EINVAL;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  VP_TRY(serve_stop(c));
   return fw_dump(c, alloc, ts, keys, int_dev);
 }
 
@@ -751,12 +769,14 @@ int vp_pol_dump(vp_ctx *c, uint8_t *alloc, int64_t *ts, uint32_t *keys,
       !bucket_time)
     return VP_EINVAL;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  VP_TRY(serve_stop(c));
   return pol_dump(c, alloc, ts, keys, bucket_size, bucket_time);
 }
 
 int64_t vp_live_count(vp_ctx *c) {
   if (!c) return VP_EINVAL;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  VP_TRY(serve_stop(c));
   if (hipStreamSynchronize(c->stream) != hipSuccess) return VP_EIO;
   Ctl h{};
   if (hipMemcpy(&h, c->ft.ctl, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)
@@ -777,6 +797,7 @@ int vp_lb_dump(vp_ctx *c, uint8_t *f_alloc, int64_t *f_ts, uint8_t *f_keys,
       !b_alloc || !b_ts || !b_ip || !b_mac || !b_nic)
     return VP_EINVAL;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  VP_TRY(serve_stop(c));
   return lb_dump(c, f_alloc, f_ts, f_keys, f_backend, b_alloc, b_ts, b_ip, b_mac,
                  b_nic);
 }
@@ -785,6 +806,7 @@ int vp_table_stats_get(vp_ctx *c, int table, vp_table_stats *out) {
   if (!c || !out || table < 0 || table > 1 || (table == 1 && c->kind != KIND_LB))
     return VP_EINVAL;
   if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+  VP_TRY(serve_stop(c));
   const vp::FlowTable &t = table ? c->ft2 : c->ft;
   VP_HIP(hipStreamSynchronize(c->stream));
   Ctl h{};

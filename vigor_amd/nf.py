@@ -231,8 +231,13 @@ class NfBase:
         return step
 
     def process(self, device: int, buffer: bytearray, now: int) -> int:
-        """nf_process for one packet (nf.h:13)."""
-        return int(self.process_mbufs([buffer], [device], [now])[0])
+        """nf_process for one packet (nf.h:13): vp_process_one (vignat on one
+        GPU: the persistent kernel's mailbox, no launch per packet)."""
+        a = (C.c_uint8 * len(buffer)).from_buffer(buffer)
+        out = C.c_uint16(device)
+        self._ck(self.L.vp_process_one(self.h, device, C.cast(a, C.c_void_p), len(buffer),
+                                       now, C.byref(out)), "vp_process_one")
+        return int(out.value)
 
 
 class Nat(NfBase):
