@@ -949,8 +949,9 @@ def main():
                                                         base + 4 * MBUF_BATCH, imix=True)
         pp = per_packet_drop_in()
         pp.update({"path": "host/nf_loop (nf.c's loop) over libvignat_nf.so: nf_process "
-                           "per packet (vp_process_batch of 1), and the batched loop for "
-                           "comparison; frames in pageable host memory",
+                           "per packet (vp_process_one: vignat's persistent kernel polling a "
+                           "host-coherent mailbox), and the batched loop (vp_process_batch) "
+                           "for comparison; frames in pageable host memory",
                    "packets": 20000, "flows": 1024})
         extra["per_packet_drop_in"] = pp
     if (world == 1 and not args.no_extra and slot == SLOT and args.order == "rr"
