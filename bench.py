@@ -731,6 +731,8 @@ def main():
                     help="profiling: one GPU running the owner-mode pipeline "
                          "with every LAN key sent through the (single-rank "
                          "RCCL) exchange (VIGPATH_ROUTE_ALL=1)")
+    ap.add_argument("--port-array", action="store_true",
+                    help="pass a per-packet port array instead of the burst's one port")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the host-resident end-to-end rate")
@@ -746,7 +748,10 @@ def main():
         B = 1 << 24
         while B * slot > (1 << 31):
             B >>= 1
-    alg_bytes = slot + 28  # R = slot(len) + 28 (92 at 64 B)
+    # R = slot(len) + 28 (92 at 64 B), of which 2 B are the
+    # per-packet port; a burst from one port (vp_dev_batch.in_port, nf.c's
+    # rx bursts, nf.c:150-153) reads none: R = slot + 26
+    alg_bytes = slot + 28 - (0 if args.port_array else 2)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -790,7 +795,9 @@ def main():
     dev = torch.device("cuda", local)
     bank = FlowBank(args.flows, 0, dev, slot)
     lens = torch.full((B,), bank.frame_len, dtype=torch.int16, device=dev)
-    in_dev = torch.zeros(B, dtype=torch.int16, device=dev)
+    # every packet of the workload arrives on LAN port 0: one port per burst
+    # (--port-array: a per-packet port array, as before round 5)
+    in_dev = torch.zeros(B, dtype=torch.int16, device=dev) if args.port_array else 0
     out = torch.zeros(B, dtype=torch.int16, device=dev)
 
     def make_nat(mode):
@@ -1015,6 +1022,8 @@ def main():
                        "global_batch_packets": B * world,
                        "frame_bytes": flen, "slot_bytes": slot,
                        "order": args.order,
+                       "port": "per-packet array" if args.port_array
+                               else "one per burst (vp_dev_batch.in_port)",
                        "parallelism": ("%s%d" % (mode, world))
                        if world > 1 else "single"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),

@@ -147,6 +147,11 @@ typedef struct vp_dev_batch {
   int64_t now0;
   int64_t now_step;
   uint16_t *out_dev; /* nf_process's return value, stored as u16 (nf.c:156) */
+  /* in_dev == NULL: every packet arrived on port in_port (nf.c receives each
+   * burst from one device, nf.c:150-153 / 186-190), and no per-packet port
+   * array is read. vp_process_device only; the host entry points need
+   * in_dev. */
+  uint32_t in_port;
 } vp_dev_batch;
 
 /* Process one device-resident batch on HIP stream `stream` (a hipStream_t,

@@ -181,6 +181,21 @@ def test_process_one_server(seed, slot, max_flows, expire_us):
     check_state(nat, o, max_flows)
 
 
+@pytest.mark.parametrize("slot", [64, 128])
+def test_burst_port(slot):
+    """vp_dev_batch.in_port: batches whose packets all arrived on one port
+    (nf.c's rx bursts) pass that port instead of a per-packet array; 64-byte
+    slots read it in the kernels, wider slots get an array made for them.
+    Bursts alternate LAN and WAN as the trace's ports change."""
+    rng = np.random.default_rng(21 + slot)
+    n = 1500
+    fr, ln, dv, now = mixed_nat_trace(rng, n, 60, slot=slot, max_idx=64)
+    cuts = [i for i in range(1, n) if dv[i] != dv[i - 1]]
+    nat, o = make_pair(max_flows=64, expire_us=50)
+    check_batches(nat, o, fr, ln, dv, now, slot, cuts, one_port=True)
+    check_state(nat, o, 64)
+
+
 def test_config2_1m_flows_full_size():
     """BASELINE config 2 at its full table size (1M flows, cap 2^20): a
     warm-up batch creating every flow, then steady-state batches, checked

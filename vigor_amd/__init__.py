@@ -108,7 +108,7 @@ class DevBatchC(C.Structure):
     _fields_ = [("frames", C.c_void_p), ("slot", C.c_uint32), ("n", C.c_uint32),
                 ("len", C.c_void_p), ("in_dev", C.c_void_p),
                 ("now", C.c_void_p), ("now0", C.c_int64),
-                ("now_step", C.c_int64), ("out_dev", C.c_void_p)]
+                ("now_step", C.c_int64), ("out_dev", C.c_void_p), ("in_port", C.c_uint32)]
 
 
 class MbufBatchC(C.Structure):

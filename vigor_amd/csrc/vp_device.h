@@ -605,13 +605,24 @@ __device__ __forceinline__ void wave_scatter64(uint8_t *base, size_t stride,
 // request per row; finish() answering kReprobe again asks for the next bucket
 // (it must leave no other trace in that case). Up to 64 packets per wave
 // (act); wave-uniform call. Returns the lane's touch (kNone if none).
+// Packet p's input port: in_dev[p] + in0, where exactly one of the two is
+// live: a batch without a port array (vp_dev_batch.in_port) has in_dev null,
+// read as zeros through a buffer of no records (branch-free, no register
+// more than the load), and in0 = its port; otherwise in0 = 0.
+__device__ __forceinline__ uint32_t port_of(const uint16_t *in_dev, uint32_t in0, uint32_t p) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(in_dev), 0,
+                                                    in_dev ? 0x7FFFFFFF : 0, 0x00020000);
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rs, (int)(2 * p), 0, 0) + in0;
+}
+
 template <class Issue, class Finish>
 __device__ __forceinline__ uint32_t reprobe_wave(uint8_t *frames, uint32_t slot,
                                                  const uint16_t *len,
                                                  const uint16_t *in_dev,
                                                  const uint8_t *buckets, uint32_t bmask,
                                                  uint32_t p, bool act, uint4 *S,
-                                                 Issue issue, Finish finish) {
+                                                 Issue issue, Finish finish,
+                                                 uint32_t in0 = 0) {
   uint4 fr[4];
   wave_gather64(frames, slot, act ? p : kNone, S, fr);
   RFrame f;
@@ -622,7 +633,7 @@ __device__ __forceinline__ uint32_t reprobe_wave(uint8_t *frames, uint32_t slot,
     f.w[4 * k + 2] = fr[k].z;
     f.w[4 * k + 3] = fr[k].w;
   }
-  const uint32_t in = act ? in_dev[p] : 0u, ln = act ? len[p] : 0u;
+  const uint32_t in = act ? port_of(in_dev, in0, p) : 0u, ln = act ? len[p] : 0u;
   const auto pend = issue(p, f, in, ln, act);
   uint32_t want = act ? pend.row : kNone;
   bool live = act, mod = false;

@@ -168,6 +168,8 @@ struct Workspace {
   uint32_t *missq = nullptr;  // phase-A misses per classify block (the reprobe slices' layout)
   uint32_t *mkey = nullptr;  // 4 words per miss
   uint32_t *pairs = nullptr;  // tbl_touch_reduce's scattered (position, index) words
+  uint16_t *in_fill = nullptr;  // a batch's one port as an array (vp_dev_batch.in_port)
+  size_t in_fill_n = 0;
   // tbl_new_keys_unsorted: the tagged key set (3 x u64 per slot, never
   // reset: a slot of an older tag is empty), its tag, first-sighting bits
   // per position and their scan, the first sightings' miss ordinals and

@@ -159,7 +159,8 @@ constexpr uint32_t kAnswered = 0xFFFFFFF9u;  // route_answer: answered by an ear
 struct NatArgs {
   uint8_t *frames;
   const uint16_t *len;
-  const uint16_t *in_dev;
+  const uint16_t *in_dev;  // null: every packet on port in0 (vp_dev_batch.in_port)
+  uint32_t in0;
   uint16_t *out;
   uint32_t *log;
   NowSpec now;
@@ -544,7 +545,7 @@ __device__ __forceinline__ uint32_t nat_lane(const NatArgs &a, const uint32_t *T
   f.w[4] = c1.x; f.w[5] = c1.y; f.w[6] = c1.z; f.w[7] = c1.w;
   f.w[8] = c2.x; f.w[9] = c2.y; f.w[10] = c2.z; f.w[11] = c2.w;
   f.w[12] = c3.x; f.w[13] = c3.y; f.w[14] = c3.z; f.w[15] = c3.w;
-  const uint32_t in = a.in_dev[p], len = a.len[p];
+  const uint32_t in = port_of(a.in_dev, a.in0, p), len = a.len[p];
   uint32_t touch = kNone;
   const NatPend P = nat_issue(a, T, p, f, in, len, true, nat_lim64(a));
   uint4 row[4] = {};
@@ -744,7 +745,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       const uint32_t bytes = min(64u, n_all - tb) * slot;
 #pragma unroll
       for (uint32_t j = 0; j < 4; j++) r[j] = buf_ld16(g8, bytes, chunk_at(64 * j + lane));
-      m_in = p < n_all ? a.in_dev[p] : 0u;
+      m_in = p < n_all ? port_of(a.in_dev, a.in0, p) : 0u;
       m_len = p < n_all ? a.len[p] : 0u;
       return;
     }
@@ -752,7 +753,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
 #pragma unroll
       for (uint32_t j = 0; j < 4; j++)
         r[j] = tile_ld(reinterpret_cast<const uint4 *>(g8 + chunk_at(64 * j + lane)));
-      m_in = a.in_dev[p];
+      m_in = port_of(a.in_dev, a.in0, p);
       m_len = a.len[p];
       return;
     }
@@ -763,7 +764,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       r[j] = (c >> 2) < avail ? tile_ld(reinterpret_cast<const uint4 *>(g8 + chunk_at(c)))
                               : make_uint4(0, 0, 0, 0);
     }
-    m_in = p < n_all ? a.in_dev[p] : 0u;
+    m_in = p < n_all ? port_of(a.in_dev, a.in0, p) : 0u;
     m_len = p < n_all ? a.len[p] : 0u;
   };
   const uint32_t rb = a.vb0 + blockIdx.x;  // (virtual blocks: the chunked pipeline)
@@ -803,7 +804,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
 #pragma unroll
       for (uint32_t j = 0; j < 8; j++) d8[j] = buf_ld16(g8, bytes, (64 * j + lane) * 16);
       const uint32_t pp = tb + lane;
-      m_in = pp < n_all ? a.in_dev[pp] : 0u;
+      m_in = pp < n_all ? a.in_dev[pp] : 0u;  // (wide slots: always an array)
       m_len = pp < n_all ? a.len[pp] : 0u;
 #pragma unroll
       for (uint32_t j = 0; j < 8; j++)
@@ -1299,7 +1300,7 @@ __global__ __launch_bounds__(256) void nat_miss_keys(NatArgs a, const uint32_t *
     const uint32_t j = j0 + lane;
     const bool v = j < n;
     const uint32_t p = v ? list[j] : kNone;
-    const uint32_t in = v ? a.in_dev[p] : 0u, len = v ? a.len[p] : 0u;
+    const uint32_t in = v ? port_of(a.in_dev, a.in0, p) : 0u, len = v ? a.len[p] : 0u;
     RFrame r;
     bool reg;
     if (a.slot == 64) {
@@ -1367,14 +1368,14 @@ __global__ __launch_bounds__(256) void nat_miss_finish(NatArgs a, const uint32_t
     const uint32_t idx = !v ? kNone : nkord ? (uint32_t)nkord[rep[j]] : assign[scratch[rep[j]]];
     if (v) {
       if (!nkord) a.log[p] = idx;
-      if (idx == kNone) a.out[p] = a.in_dev[p];  // nat_main.c:87-91
+      if (idx == kNone) a.out[p] = port_of(a.in_dev, a.in0, p);  // nat_main.c:87-91
     }
     const bool live = v && idx != kNone;
     bool fast = false;
     if (a.slot == 64) {
       RFrame f;
       gather_slots64(a.frames, live ? p : kNone, S, f);
-      fast = live && nat_lan_fast_ok(a, f, a.in_dev[p], a.len[p], nat_lim64(a));
+      fast = live && nat_lan_fast_ok(a, f, port_of(a.in_dev, a.in0, p), a.len[p], nat_lim64(a));
       if (fast) {
         const uint32_t proto = f.w[5] >> 24;
         f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
@@ -1415,7 +1416,8 @@ __global__ __launch_bounds__(256) void nat_reprobe(NatArgs a, const uint32_t *li
         [&](const NatPend &P, const uint4 *row, uint32_t q, RFrame &f, uint32_t in,
             uint32_t len, uint32_t &touch) {
           return nat_finish(a, T, P, row, q, f, in, len, touch, nat_tail(a, q));
-        });
+        },
+        a.in0);
   });
 }
 
@@ -1819,7 +1821,7 @@ __global__ void nat_defer_finish(NatArgs a, const uint32_t *list, uint32_t n) {
        j += gridDim.x * blockDim.x) {
     const uint32_t p = list[j];
     const uint64_t q = a.seq_base + p;
-    const uint32_t in = a.in_dev[p];
+    const uint32_t in = port_of(a.in_dev, a.in0, p);
     GFrame f{a.frames + (size_t)p * a.slot, a.slot};
     const L34 h = parse_l34(f, a.len[p]);
     const uint32_t proto = f.r8(h.ip + 9);
@@ -2650,6 +2652,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.frames = b->frames;
   a.len = b->len;
   a.in_dev = b->in_dev;
+  a.in0 = b->in_dev ? 0u : b->in_port;  // (port_of: exactly one is live)
   a.out = b->out_dev;
   a.log = w.log;
   a.now = now;

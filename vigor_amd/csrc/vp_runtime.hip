@@ -211,7 +211,7 @@ static void free_all(vp_ctx *c) {
                   w.route,   w.sendk,    w.recvk,  w.reply,  w.rreply,
                   w.cnt_t,   w.rcnt_t,   w.dneed,  w.xsend, w.sendk2, w.recvk2,
                   w.reply2,  w.rreply2,  w.lcnt, w.nkset, w.nkbits, w.nkpre,
-                  w.nkfirst, w.nkcnt};
+                  w.nkfirst, w.nkcnt, w.in_fill};
   for (void *p : ptrs) hipFree(p);
   for (int i = 0; i < 2; i++) {
     if (w.ev_p1[i]) hipEventDestroy(w.ev_p1[i]);
@@ -656,6 +656,24 @@ int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
     VP_HIP(hipEventCreateWithFlags(&dep, hipEventDisableTiming));
     VP_HIP(hipEventRecord(dep, user));
     VP_HIP(hipStreamWaitEvent(c->stream, dep, 0));
+  }
+  // one port for the whole batch (in_dev == NULL): vignat's 64-byte slots on
+  // one GPU read in_port itself; elsewhere the port array is made here
+  vp_dev_batch one;
+  if (!b->in_dev && b->n && (c->kind != KIND_NAT || c->comm || b->slot != 64)) {
+    Workspace &w = c->ws;
+    if (w.in_fill_n < b->n) {
+      VP_HIP(hipStreamSynchronize(c->stream));
+      hipFree(w.in_fill);
+      w.in_fill = nullptr;
+      w.in_fill_n = 0;
+      VP_HIP(hipMalloc((void **)&w.in_fill, 2ull * b->n));
+      w.in_fill_n = b->n;
+    }
+    VP_HIP(hipMemsetD16Async(w.in_fill, (uint16_t)b->in_port, b->n, c->stream));
+    one = *b;
+    one.in_dev = w.in_fill;
+    b = &one;
   }
   int rc = VP_ENOTSUP;
   switch (c->kind) {

@@ -45,14 +45,17 @@ class NfBase:
     def process_device(self, frames, lens, in_dev, out, slot: int, now=None,
                        now0: int = 0, now_step: int = 0, stream=None):
         """frames: uint8 CUDA tensor of n*slot bytes (mutated in place);
-        lens/in_dev/out: int16/uint16-sized CUDA tensors of n; now: int64
-        CUDA tensor of n, or None for now0 + i*now_step."""
+        lens/in_dev/out: int16/uint16-sized CUDA tensors of n (in_dev an int:
+        every packet on that port, vp_dev_batch.in_port); now: int64 CUDA
+        tensor of n, or None for now0 + i*now_step."""
         n = lens.numel()
         assert frames.numel() == n * slot and frames.is_cuda
+        port = isinstance(in_dev, int)
         b = DevBatchC(frames=frames.data_ptr(), slot=slot, n=n,
-                      len=lens.data_ptr(), in_dev=in_dev.data_ptr(),
+                      len=lens.data_ptr(), in_dev=None if port else in_dev.data_ptr(),
                       now=now.data_ptr() if now is not None else None,
-                      now0=now0, now_step=now_step, out_dev=out.data_ptr())
+                      now0=now0, now_step=now_step, out_dev=out.data_ptr(),
+                      in_port=in_dev if port else 0)
         s = C.c_void_p(stream.cuda_stream) if stream is not None else None
         self._ck(self.L.vp_process_device(self.h, C.byref(b), s),
                "vp_process_device")
@@ -62,12 +65,15 @@ class NfBase:
         affine time: returns f(now0, now_step). The batch descriptor and its
         pointers are built once (a C caller's per-burst cost), so a loop of
         calls pays only the C-ABI call itself. The callable keeps the tensors
-        alive: the descriptor holds their raw device pointers."""
+        alive: the descriptor holds their raw device pointers. in_dev: as for
+        process_device (an int: the burst's one port)."""
         n = lens.numel()
         assert frames.numel() == n * slot and frames.is_cuda
+        port = isinstance(in_dev, int)
         b = DevBatchC(frames=frames.data_ptr(), slot=slot, n=n,
-                      len=lens.data_ptr(), in_dev=in_dev.data_ptr(), now=None,
-                      now0=0, now_step=0, out_dev=out.data_ptr())
+                      len=lens.data_ptr(), in_dev=None if port else in_dev.data_ptr(),
+                      now=None, now0=0, now_step=0, out_dev=out.data_ptr(),
+                      in_port=in_dev if port else 0)
         ref, fn, h, L = C.byref(b), self.L.vp_process_device, self.h, self.L
         keep = (frames, lens, in_dev, out)
 
