@@ -373,7 +373,7 @@ def golden_configs():
 
 
 def steady_workload(nf, batch_of, warm: int, steps: int, B: int, dev, golden=None,
-                    kernel="", times=None, state=None, repeats=False):
+                    kernel="", times=None, state=None, repeats=False, alg_bytes=ALG_BYTES):
     """Batches 0 .. warm-1 untimed (allocation), then `steps` timed calls
     (batches warm ..) without timing events, each from its own buffer filled
     before the timed region; the last timed batch's digest against golden[k]
@@ -425,7 +425,7 @@ def steady_workload(nf, batch_of, warm: int, steps: int, B: int, dev, golden=Non
     del last
     _, kms, last = run(warm + steps, steps, True)
     del last
-    per_launch_s, pkts, achieved = kernel_rate(kms, B, steps, ALG_BYTES)
+    per_launch_s, pkts, achieved = kernel_rate(kms, B, steps, alg_bytes)
     mpps = B * steps / el / 1e6
     line = {"value": round(mpps, 1), "unit": "Mpps", "ms_per_step": round(el / steps * 1e3, 4),
             "batch_packets": B, "steps": steps, "warm_batches": warm,
@@ -433,8 +433,10 @@ def steady_workload(nf, batch_of, warm: int, steps: int, B: int, dev, golden=Non
             "kernel": kernel, "kernel_ms_per_launch": round(per_launch_s * 1e3, 4),
             "kernel_mpps": round(pkts / per_launch_s / 1e6, 1),
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "frac_step": round(mpps * 1e6 * ALG_BYTES / 1e9 / HBM_PEAK_GBS, 4),
-            "frac_basis": "92 B per packet (SURVEY.md §8(d) vignat basis), 8 TB/s",
+            "frac_step": round(mpps * 1e6 * alg_bytes / 1e9 / HBM_PEAK_GBS, 4),
+            "frac_basis": "%d B per packet (SURVEY.md §8(d) vignat basis%s), 8 TB/s"
+                          % (alg_bytes, "" if alg_bytes == ALG_BYTES
+                             else ", no per-packet port: one per burst"),
             "parity": parity}
     if times is not None:
         line.update(times)
@@ -485,12 +487,14 @@ def bench_lb_c4(dev, B, steps, golden):
     fr, ln, dv, _ = T.lb_traffic(B, N)
     src, lens, ind = host_batch(dev, fr, ln, dv)
     del fr
+    # every packet arrives on the WAN port: one port per burst (in_port)
+    port = int(dv[0]) if (dv == dv[0]).all() else ind
 
     def batch_of(k, buf):
         buf.copy_(src)
-        return lens, ind, T.NOW0 + k * B, 1
+        return lens, port, T.NOW0 + k * B, 1
     r = steady_workload(lb, batch_of, 1, steps, B, dev, golden, "lb_classify64",
-                        repeats=True)
+                        repeats=True, alg_bytes=ALG_BYTES - (2 if isinstance(port, int) else 0))
     lb.close()
     r["workload"] = "viglb 64B, 256 backends / 1M flows (BASELINE configs[3])"
     return r

@@ -72,6 +72,18 @@ def test_mixed_traces(seed, fcap, fexp, bexp, quiet, cuts):
     check_state(lb, o)
 
 
+def test_burst_port():
+    """vp_dev_batch.in_port: bursts of heartbeats (LAN ports) and WAN
+    traffic, each passed with its one port instead of a port array (the
+    64-byte tile and the queue rounds read it), state compared at the end."""
+    rng = np.random.default_rng(31)
+    fr, ln, dv, now = mixed_lb_trace(rng, 3000, 200, 20)
+    cuts = [i for i in range(1, len(dv)) if dv[i] != dv[i - 1]]
+    lb, o = make_pair(flow_cap=256, fexp=40)
+    check_batches(lb, o, fr, ln, dv, now, 64, cuts, one_port=True)
+    check_state(lb, o)
+
+
 def test_backend_table_full_and_generic_slots():
     rng = np.random.default_rng(8)
     fr, ln, dv, now = mixed_lb_trace(rng, 4000, 200, 40, hb_frac=0.1,

@@ -438,7 +438,20 @@ __device__ __forceinline__ void bins_publish(const TouchBins &bins, const uint32
 // launch is blocks vb0 .. vb0 + gridDim.x - 1 of a grid whose every block
 // owns vper tiles of [p0, p1); the per-block slices (bins, rq) are indexed by
 // the virtual block.
-template <uint32_t kOvf = kCurOverflow, class Issue, class Finish>
+// Packet p's input port: in_dev[p] + in0, where exactly one of the two is
+// live: a batch without a port array (vp_dev_batch.in_port) has in_dev null,
+// read as zeros through a buffer of no records (branch-free, no register
+// more than the load), and in0 = its port; otherwise in0 = 0.
+__device__ __forceinline__ uint32_t port_of(const uint16_t *in_dev, uint32_t in0, uint32_t p) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(in_dev), 0,
+                                                    in_dev ? 0x7FFFFFFF : 0, 0x00020000);
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rs, (int)(2 * p), 0, 0) + in0;
+}
+
+// PR: the issue half, the row requests and the next tile's prefetch at a
+// raised wave priority (as vignat's lean tile: the SIMD issues them ahead of
+// other waves' arithmetic, more requests in flight).
+template <uint32_t kOvf = kCurOverflow, bool PR = false, class Issue, class Finish>
 __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
                                                const uint16_t *len,
                                                const uint16_t *in_dev,
@@ -449,7 +462,7 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
                                                const TouchBins &bins,
                                                const TileQueue &rq,
                                                uint32_t *cur, uint32_t vb0 = 0,
-                                               uint32_t vper = 0) {
+                                               uint32_t vper = 0, uint32_t in0 = 0) {
   // (the wave index as a scalar: the tile stores' buffer resources are
   // provably uniform, no waterfall loops)
   const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -467,7 +480,7 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
       r[j] = (c >> 2) < avail ? tile_ld(g + c) : make_uint4(0, 0, 0, 0);
     }
     const uint32_t p = tb + lane;
-    m_in = p < n_all ? in_dev[p] : 0u;
+    m_in = p < n_all ? port_of(in_dev, in0, p) : 0u;
     m_len = p < n_all ? len[p] : 0u;
   };
   const uint32_t rb = vb0 + blockIdx.x;
@@ -494,23 +507,44 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
       f.w[4 * k + 3] = v.w;
     }
     const uint32_t in = m_in, ln = m_len;
+    if constexpr (PR) __builtin_amdgcn_s_setprio(1);
     auto pend = issue(p, f, in, ln, mine);
-    // piece j of lane L: part L % 4 of the row of packet 16 j + L / 4
-    uint4 q[4];
+    // piece j of lane L: part L % 4 of the row of packet 16 j + L / 4; the
+    // four row numbers come in by ds_bpermute, issued together and waited for
+    // once, and the four loads go out unconditionally (a packet without a row
+    // reads bucket 0, an L1 hit, and gets zeros): a load under a branch waited
+    // for its own permute
+    // (named registers: an array here stays in scratch memory)
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
     if (rows) {
-#pragma unroll
-      for (uint32_t j = 0; j < 4; j++) {
-        const uint32_t row = __shfl(pend.row, 16 * j + (lane >> 2));
-        q[j] = row != kNone ? rows[4 * (size_t)row + (lane & 3)]
-                            : make_uint4(0, 0, 0, 0);
-      }
+      uint32_t b0, b1, b2, b3;
+      const uint32_t src = lane & ~3u;  // byte address of lane L / 4
+      const uint32_t want = pend.row;
+      asm volatile("ds_bpermute_b32 %0, %1, %2" : "=v"(b0) : "v"(src), "v"(want));
+      asm volatile("ds_bpermute_b32 %0, %1, %2 offset:64" : "=v"(b1) : "v"(src), "v"(want));
+      asm volatile("ds_bpermute_b32 %0, %1, %2 offset:128" : "=v"(b2) : "v"(src), "v"(want));
+      asm volatile("ds_bpermute_b32 %0, %1, %2 offset:192" : "=v"(b3) : "v"(src), "v"(want));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
+      const uint32_t part = lane & 3;
+      const uint4 z = q0;
+      const uint4 r0 = rows[4 * (size_t)(b0 != kNone ? b0 : 0u) + part];
+      const uint4 r1 = rows[4 * (size_t)(b1 != kNone ? b1 : 0u) + part];
+      const uint4 r2 = rows[4 * (size_t)(b2 != kNone ? b2 : 0u) + part];
+      const uint4 r3 = rows[4 * (size_t)(b3 != kNone ? b3 : 0u) + part];
+      q0 = b0 != kNone ? r0 : z;
+      q1 = b1 != kNone ? r1 : z;
+      q2 = b2 != kNone ? r2 : z;
+      q3 = b3 != kNone ? r3 : z;
     }
     if (tile + tstep < tend) fetch(tile + tstep);
+    if constexpr (PR) __builtin_amdgcn_s_setprio(0);
     uint4 row[4] = {};
     if (rows) {  // S is free: f is in registers
       wave_lds_sync();
-#pragma unroll
-      for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = q[j];
+      S[chunk_swz(lane)] = q0;
+      S[chunk_swz(64 + lane)] = q1;
+      S[chunk_swz(128 + lane)] = q2;
+      S[chunk_swz(192 + lane)] = q3;
       wave_lds_sync();
 #pragma unroll
       for (uint32_t k = 0; k < 4; k++) row[k] = S[chunk_swz(4 * lane + k)];
@@ -605,16 +639,6 @@ __device__ __forceinline__ void wave_scatter64(uint8_t *base, size_t stride,
 // request per row; finish() answering kReprobe again asks for the next bucket
 // (it must leave no other trace in that case). Up to 64 packets per wave
 // (act); wave-uniform call. Returns the lane's touch (kNone if none).
-// Packet p's input port: in_dev[p] + in0, where exactly one of the two is
-// live: a batch without a port array (vp_dev_batch.in_port) has in_dev null,
-// read as zeros through a buffer of no records (branch-free, no register
-// more than the load), and in0 = its port; otherwise in0 = 0.
-__device__ __forceinline__ uint32_t port_of(const uint16_t *in_dev, uint32_t in0, uint32_t p) {
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(in_dev), 0,
-                                                    in_dev ? 0x7FFFFFFF : 0, 0x00020000);
-  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rs, (int)(2 * p), 0, 0) + in0;
-}
-
 template <class Issue, class Finish>
 __device__ __forceinline__ uint32_t reprobe_wave(uint8_t *frames, uint32_t slot,
                                                  const uint16_t *len,
@@ -822,6 +846,38 @@ __device__ inline void fast_checksums(RFrame &f, uint32_t proto, uint32_t tl,
 }
 
 // ------------------------------------------------------------------ CRC --
+// The XOR of 13 position tables' entries (table j = 256 words at T + 256 j,
+// T an LDS array), byte b_j for table j: the reads issued back to back and
+// waited for once. (Compiled from an expression, each read waits for the one
+// before it: 13 LDS round trips per packet.) viglb's and vigfw's flow hashes.
+#define VP_CRC_RD(t, a, off) asm volatile("ds_read_b32 %0, %1 offset:" #off : "=v"(t) : "v"(a))
+__device__ __forceinline__ uint32_t crc13_lds(const uint32_t *T, uint32_t b0, uint32_t b1,
+                                              uint32_t b2, uint32_t b3, uint32_t b4,
+                                              uint32_t b5, uint32_t b6, uint32_t b7,
+                                              uint32_t b8, uint32_t b9, uint32_t b10,
+                                              uint32_t b11, uint32_t b12) {
+  const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)T;
+  uint32_t t0, t1, t2, t3, t4, t5, t6, t7, t8, t9, t10, t11, t12;
+  VP_CRC_RD(t0, base + (b0 << 2), 0);
+  VP_CRC_RD(t1, base + (b1 << 2), 1024);
+  VP_CRC_RD(t2, base + (b2 << 2), 2048);
+  VP_CRC_RD(t3, base + (b3 << 2), 3072);
+  VP_CRC_RD(t4, base + (b4 << 2), 4096);
+  VP_CRC_RD(t5, base + (b5 << 2), 5120);
+  VP_CRC_RD(t6, base + (b6 << 2), 6144);
+  VP_CRC_RD(t7, base + (b7 << 2), 7168);
+  VP_CRC_RD(t8, base + (b8 << 2), 8192);
+  VP_CRC_RD(t9, base + (b9 << 2), 9216);
+  VP_CRC_RD(t10, base + (b10 << 2), 10240);
+  VP_CRC_RD(t11, base + (b11 << 2), 11264);
+  VP_CRC_RD(t12, base + (b12 << 2), 12288);
+  // (the results as operands: nothing reads them before this wait)
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(t0), "+v"(t1), "+v"(t2), "+v"(t3), "+v"(t4), "+v"(t5), "+v"(t6),
+                 "+v"(t7), "+v"(t8), "+v"(t9), "+v"(t10), "+v"(t11), "+v"(t12));
+  return (t0 ^ t1 ^ t2) ^ (t3 ^ t4 ^ t5) ^ (t6 ^ t7 ^ t8) ^ (t9 ^ t10 ^ t11) ^ t12;
+}
+#undef VP_CRC_RD
 // CRC-32C as SSE4.2 `crc32 r32` computes it (boilerplate-util.h:9): reflected
 // polynomial 0x82F63B78, the operand's 4 LE bytes, no pre/post inversion.
 __host__ __device__ inline uint32_t crc32c_byte(uint32_t crc, uint8_t b) {

@@ -170,8 +170,13 @@ __device__ __forceinline__ FwPend fw_issue(const FwArgs &a, const uint32_t *T,
   }
   const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
   const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
-  const uint32_t hh = in == a.wan ? fw_hash(T, dp, sp, dip, sip, proto)
-                                  : fw_hash(T, sp, dp, sip, dip, proto);
+  // (WAN packets hash the reversed FlowId; the 13 reads batched, crc13_lds)
+  const bool w = in == a.wan;
+  const uint32_t s0 = w ? dp : sp, d0 = w ? sp : dp, si = w ? dip : sip, di = w ? sip : dip;
+  const uint32_t hh = crc13_lds(T, s0 & 0xFF, (s0 >> 8) & 0xFF, d0 & 0xFF, (d0 >> 8) & 0xFF,
+                                si & 0xFF, (si >> 8) & 0xFF, (si >> 16) & 0xFF, si >> 24,
+                                di & 0xFF, (di >> 8) & 0xFF, (di >> 16) & 0xFF, di >> 24,
+                                proto & 0xFF);
   P.kind = kFwProbe;
   P.row = home_bucket(hh, a.t.bmask, a.t.mix, fw_lin(T));
   return P;
@@ -250,7 +255,7 @@ __global__ __launch_bounds__(256, 4) void fw_classify64(FwArgs a, uint32_t n_all
   __shared__ uint32_t cur[kCurs];
   for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
   fw_load_tables(T, a);  // (its barrier also covers cur)
-  frames64_tiles(
+  frames64_tiles<kCurOverflow, true>(
       a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
       reinterpret_cast<const uint4 *>(a.t.bk),
       [&](uint32_t p, const RFrame &f, uint32_t in, uint32_t len, bool mine) {

@@ -70,6 +70,15 @@ __device__ __forceinline__ uint32_t lbflow_hash(const uint32_t *T, uint32_t sip,
          T[10 * 256 + (dp & 0xFF)] ^ T[11 * 256 + ((dp >> 8) & 0xFF)] ^
          T[12 * 256 + (proto & 0xFF)];
 }
+// lbflow_hash for the 64-byte tile, its 13 table reads batched (crc13_lds).
+__device__ __forceinline__ uint32_t lbflow_hash_batched(const uint32_t *T, uint32_t sip,
+                                                        uint32_t dip, uint32_t sp,
+                                                        uint32_t dp, uint32_t proto) {
+  return crc13_lds(T, sip & 0xFF, (sip >> 8) & 0xFF, (sip >> 16) & 0xFF, sip >> 24, dip & 0xFF,
+                   (dip >> 8) & 0xFF, (dip >> 16) & 0xFF, dip >> 24, sp & 0xFF,
+                   (sp >> 8) & 0xFF, dp & 0xFF, (dp >> 8) & 0xFF, proto & 0xFF);
+}
+
 __device__ __forceinline__ uint32_t ip_hash(const uint32_t *I, uint32_t ip) {
   return I[0 * 256 + (ip & 0xFF)] ^ I[1 * 256 + ((ip >> 8) & 0xFF)] ^
          I[2 * 256 + ((ip >> 16) & 0xFF)] ^ I[3 * 256 + (ip >> 24)];
@@ -110,7 +119,8 @@ __device__ __forceinline__ uint32_t flow_probe(const TableDev &t, uint32_t h,
 struct LbArgs {
   uint8_t *frames;
   const uint16_t *len;
-  const uint16_t *in_dev;
+  const uint16_t *in_dev;  // null: every packet on port in0 (vp_dev_batch.in_port)
+  uint32_t in0;
   uint16_t *out;
   uint32_t *log, *log2;  // flow / backend touch logs
   uint32_t slot, p0, p1;
@@ -205,29 +215,18 @@ __device__ __forceinline__ void lb_heartbeat(const LbArgs &a, const uint32_t *I,
 // A WAN packet after its flow lookup (fi, and the entry's word 3): a flow
 // with a live backend is handed to `rw` with the backend record; the rest
 // are queued (M: no flow, S: its backend is gone).
-// `brec`: the backends staged in LDS by lb_classify64 (record, .w = live),
-// or null: their liveness and record from global memory.
 template <class Rw>
 __device__ __forceinline__ bool lb_flow_found(const LbArgs &a, uint32_t p, uint32_t fi,
-                                              uint32_t w3, Rw rw, uint32_t *touch,
-                                              const uint4 *brec = nullptr) {
+                                              uint32_t w3, Rw rw, uint32_t *touch) {
   if (fi == kNone) {
     if (!a.binned) a.log[p] = kNone;
     a.miss[wave_append(&a.ft.ctl->miss_count, true)] = p;
     return false;
   }
   const uint32_t bi = w3 >> 8;
-  // the backend's liveness and record: one LDS read, or one global round trip
   // (both depend on bi only; the record of a dead backend is read and ignored)
-  uint4 rec;
-  bool live;
-  if (brec) {
-    rec = brec[bi];
-    live = rec.w != 0;
-  } else {
-    live = a.bt.slot_of[bi] != kNone;
-    rec = a.be_rec[bi];
-  }
+  const bool live = a.bt.slot_of[bi] != kNone;
+  const uint4 rec = a.be_rec[bi];
   if (!live) {  // backend gone: erase + re-lookup
     if (!a.binned) a.log[p] = kNone;
     a.stale[wave_append(&a.ft.ctl->defer_count, true)] = p;
@@ -265,7 +264,7 @@ __device__ __forceinline__ void lb_generic_a(const LbArgs &a, const uint32_t *T,
                                              const uint32_t *I,
                                              uint32_t p) {
   const GFrame f{a.frames + (size_t)p * a.slot, a.slot};
-  const uint32_t in = a.in_dev[p];
+  const uint32_t in = port_of(a.in_dev, a.in0, p);
   const L34 h = parse_l34(f, a.len[p]);
   if (!h.ok) {
     a.out[p] = (uint16_t)in;
@@ -302,6 +301,11 @@ struct LbPend {
 // hit's backend costs one LDS read instead of a dependent global round trip.
 // To make room, the tile loop keeps only the cursors of 256 touch bins and
 // the overflow queue's (lb_segment keeps the flow table's bins at 256).
+// Each staged backend is what a hit's rewrite needs, ready: bhdr[b] = {ip,
+// the three MAC header words (backend_macs, the NIC's source MAC folded
+// in)}, bnic[b] = its NIC | live << 16. The NIC's MAC was a global load that
+// depended on the backend the row named (row -> backend -> NIC -> MAC): one
+// more dependent round trip per packet.
 constexpr uint32_t kLbLdsBackends = 256;
 constexpr uint32_t kLbCurs = 257;  // bins 0..255, the overflow queue at 256
 __global__ __launch_bounds__(256, 4) void lb_classify64(LbArgs a, uint32_t n_all,
@@ -309,7 +313,8 @@ __global__ __launch_bounds__(256, 4) void lb_classify64(LbArgs a, uint32_t n_all
   __shared__ uint32_t T[kLbFlowTabs * 256 + 1024];  // + the layout's byte tables
   __shared__ uint4 stage[4][256];
   __shared__ uint32_t cur[kLbCurs];
-  __shared__ uint4 brec[kLbLdsBackends];
+  __shared__ uint4 bhdr[kLbLdsBackends];
+  __shared__ uint32_t bnic[kLbLdsBackends];
   for (uint32_t i = threadIdx.x; i < kLbCurs; i += blockDim.x) cur[i] = 0;
   for (uint32_t i = threadIdx.x; i < kLbFlowTabs * 256; i += blockDim.x) T[i] = a.crc_tab[i];
   const uint32_t *lin = T + kLbFlowTabs * 256;
@@ -318,13 +323,16 @@ __global__ __launch_bounds__(256, 4) void lb_classify64(LbArgs a, uint32_t n_all
   const bool lds_be = a.bcap <= kLbLdsBackends;
   if (lds_be)
     for (uint32_t b = threadIdx.x; b < a.bcap; b += blockDim.x) {
-      uint4 r = a.be_rec[b];
-      r.w = a.bt.slot_of[b] != kNone ? 1u : 0u;
-      brec[b] = r;
+      const uint4 r = a.be_rec[b];
+      const uint32_t nic = r.z >> 16;
+      uint32_t mw[3];
+      backend_macs(a, r, nic, mw);
+      bhdr[b] = make_uint4(r.x, mw[0], mw[1], mw[2]);
+      bnic[b] = nic | (a.bt.slot_of[b] != kNone ? 1u << 16 : 0u);
     }
   __syncthreads();
   const uint32_t *I = a.crc_tab + kLbFlowTabs * 256;  // ip_addr tables (global)
-  frames64_tiles<kLbCurs - 1>(
+  frames64_tiles<kLbCurs - 1, true>(
       a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
       reinterpret_cast<const uint4 *>(a.ft.bk),
       [&](uint32_t p, const RFrame &f, uint32_t in, uint32_t len, bool mine) {
@@ -352,7 +360,7 @@ __global__ __launch_bounds__(256, 4) void lb_classify64(LbArgs a, uint32_t n_all
         }
         const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
         P.kind = 2;
-        P.row = home_bucket(lbflow_hash(T, f.u32at2(26), f.u32at2(30), sp, dp, proto),
+        P.row = home_bucket(lbflow_hash_batched(T, f.u32at2(26), f.u32at2(30), sp, dp, proto),
                             a.ft.bmask, a.ft.mix, lin);
         return P;
       },
@@ -379,15 +387,34 @@ __global__ __launch_bounds__(256, 4) void lb_classify64(LbArgs a, uint32_t n_all
         uint32_t fi = bucket_match<0xFFu>(row[0], row[1], row[2], row[3], key, &done, &w3);
         if (!done)
           fi = tbl_probe_from<0xFFu>(a.ft, (P.row + 1) & a.ft.bmask, key, a.ft.bmask, &w3);
+        if (lds_be && fi != kNone) {  // a flow: its backend from LDS
+          const uint32_t bi = w3 >> 8;
+          const uint32_t meta = bnic[bi];
+          const uint4 h = bhdr[bi];
+          if (meta >> 16) {  // live: lb_main.c:56-65
+            if (!a.binned) a.log[p] = fi;
+            touch = fi;
+            const uint32_t nic = meta & 0xFFFF;
+            a.out[p] = (uint16_t)nic;
+            if (nic == a.wan) return 0u;
+            f.set32at2(30, h.x);  // dst_addr = backend.ip
+            f.w[0] = h.y;
+            f.w[1] = h.z;
+            f.w[2] = h.w;
+            fast_checksums(f, proto, tl);
+            return 0xFu;
+          }
+        }
+        // (no flow, a backend gone, or backends not staged: the queues)
         const bool rw = lb_flow_found(a, p, fi, w3, [&](uint4 rec) {
           return lb_rewrite_fast(a, f, rec, proto, tl, p);
-        }, &touch, lds_be ? brec : nullptr);
+        }, &touch);
         // dst address, MACs and checksums change bytes 0-47 (and the TCP
         // checksum 50-51): the whole 64-byte slot is stored back, since a
         // partial-line write costs more than a whole one
         return rw ? 0xFu : 0u;
       },
-      bins, TileQueue{}, cur);
+      bins, TileQueue{}, cur, 0, 0, a.in0);
 }
 
 __global__ __launch_bounds__(256) void lb_classify(LbArgs a) {
@@ -455,7 +482,7 @@ __global__ void lb_stale_free_seq(LbArgs a, const uint32_t *list, uint32_t n) {
     uint32_t w3 = 0;
     const uint32_t fi =
         flow_probe(a.ft, h, q.sip, q.dip, q.sp | (q.dp << 16), q.proto, &w3);
-    a.out[p] = a.in_dev[p];  // backend.nic = wan device = in
+    a.out[p] = port_of(a.in_dev, a.in0, p);  // backend.nic = wan device = in
     a.log[p] = kNone;
     if (fi == kNone) continue;  // freed by an earlier packet of the flow
     const uint32_t e = a.ft.slot_of[fi];
@@ -509,7 +536,7 @@ __global__ void lb_drop_list(LbArgs a, const uint32_t *list, uint32_t n) {
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n;
        j += gridDim.x * blockDim.x) {
     const uint32_t p = list[j];
-    a.out[p] = a.in_dev[p];
+    a.out[p] = port_of(a.in_dev, a.in0, p);
     a.log[p] = kNone;
   }
 }
@@ -541,7 +568,7 @@ __global__ void lb_hb_finish(LbArgs a, const uint32_t *list, uint32_t n,
     const GFrame f{a.frames + (size_t)p * a.slot, a.slot};
     const L34 h = parse_l34(f, a.len[p]);
     const uint32_t m0 = f.r32(6), m1 = f.r16(10);
-    a.be_rec[idx] = make_uint4(f.r32(h.ip + 12), m0, m1 | ((uint32_t)a.in_dev[p] << 16), 0);
+    a.be_rec[idx] = make_uint4(f.r32(h.ip + 12), m0, m1 | (port_of(a.in_dev, a.in0, p) << 16), 0);
   }
 }
 
@@ -628,6 +655,7 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   a.frames = b->frames;
   a.len = b->len;
   a.in_dev = b->in_dev;
+  a.in0 = b->in_dev ? 0u : b->in_port;  // (port_of: exactly one is live)
   a.out = b->out_dev;
   a.log = w.log;
   a.log2 = w.log2;

@@ -657,10 +657,12 @@ int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
     VP_HIP(hipEventRecord(dep, user));
     VP_HIP(hipStreamWaitEvent(c->stream, dep, 0));
   }
-  // one port for the whole batch (in_dev == NULL): vignat's 64-byte slots on
-  // one GPU read in_port itself; elsewhere the port array is made here
+  // one port for the whole batch (in_dev == NULL): vignat's and viglb's
+  // 64-byte slots on one GPU read in_port themselves; elsewhere the port
+  // array is made here
   vp_dev_batch one;
-  if (!b->in_dev && b->n && (c->kind != KIND_NAT || c->comm || b->slot != 64)) {
+  if (!b->in_dev && b->n &&
+      ((c->kind != KIND_NAT && c->kind != KIND_LB) || c->comm || b->slot != 64)) {
     Workspace &w = c->ws;
     if (w.in_fill_n < b->n) {
       VP_HIP(hipStreamSynchronize(c->stream));

@@ -1601,7 +1601,7 @@ int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
   c->last_launches = 0;
   if (n == 0) return 0;
   if (b->slot < 64 || (b->slot & 15) || !b->frames || ((uintptr_t)b->frames & 15) ||
-      !b->len || (!b->in_dev && (c->kind != KIND_NAT || b->slot != 64)) || !b->out_dev)
+      !b->len || (!b->in_dev && ((c->kind != KIND_NAT && c->kind != KIND_LB) || b->slot != 64)) || !b->out_dev)
     return VP_EINVAL;  // (frames are read as aligned 16-byte chunks; in_dev: see vp_process_device)
   VP_TRY(ws_reserve(c, n));
 
