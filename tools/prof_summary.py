@@ -22,6 +22,11 @@ import statistics
 import sys
 
 KERNEL = os.environ.get("PROF_KERNEL", "nat_classify64")
+# PROF_LAUNCHES=a:b: only launches a..b-1 of each kernel, in dispatch order
+# (one workload's launches when a bench run holds several: bench.py's
+# headline comes first, its extras after it)
+_LR = os.environ.get("PROF_LAUNCHES")
+LAUNCHES = slice(*[int(x) if x else None for x in _LR.split(":")]) if _LR else None
 
 
 def _rows(d, suffix):
@@ -57,6 +62,8 @@ def trace(d, out, skip):
     for name, v in sorted(per.items()):
         v.sort()
         us = [round(x, 3) for _, x in v]
+        if LAUNCHES is not None:
+            us = us[LAUNCHES]
         tail = us[skip:] if len(us) > skip else us
         kernels[name] = {"launches": len(us), "us_all_launches": us[:64],
                          "us_avg_after_warmup": round(statistics.mean(tail), 3)
@@ -91,9 +98,11 @@ def pmc(out, pkts, dirs):
             vals.setdefault(c, {}).setdefault(disp, 0.0)
             vals[c][disp] += float(_col(r, "Counter_Value", "Counter-Value"))
     launches = {c: [round(v[k], 2) for k in sorted(v)] for c, v in vals.items()}
+    if LAUNCHES is not None:
+        launches = {c: v[LAUNCHES] for c, v in launches.items()}
     res = {"kernel": "vp::" + KERNEL, "packets_per_launch": pkts,
-           "launches": launches}
-    med = {c: statistics.median(v[1:] if len(v) > 1 else v)
+           "launches": launches, "launch_range": _LR}
+    med = {c: statistics.median(v if LAUNCHES is not None or len(v) < 2 else v[1:])
            for c, v in launches.items()}
     for c, m in med.items():
         res[c + "_median"] = m
