@@ -755,7 +755,8 @@ def main():
     # R = slot(len) + 28 (92 at 64 B), of which 2 B are the
     # per-packet port; a burst from one port (vp_dev_batch.in_port, nf.c's
     # rx bursts, nf.c:150-153) reads none: R = slot + 26
-    alg_bytes = slot + 28 - (0 if args.port_array else 2)
+    port_array = args.port_array or args.gpus > 1 or args.route_all
+    alg_bytes = slot + 28 - (0 if port_array else 2)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -800,8 +801,9 @@ def main():
     bank = FlowBank(args.flows, 0, dev, slot)
     lens = torch.full((B,), bank.frame_len, dtype=torch.int16, device=dev)
     # every packet of the workload arrives on LAN port 0: one port per burst
-    # (--port-array: a per-packet port array, as before round 5)
-    in_dev = torch.zeros(B, dtype=torch.int16, device=dev) if args.port_array else 0
+    # (--port-array: a per-packet port array, as before round 5; N > 1 ranks
+    # take the array, which their exchange paths read)
+    in_dev = torch.zeros(B, dtype=torch.int16, device=dev) if port_array else 0
     out = torch.zeros(B, dtype=torch.int16, device=dev)
 
     def make_nat(mode):
@@ -1026,7 +1028,7 @@ def main():
                        "global_batch_packets": B * world,
                        "frame_bytes": flen, "slot_bytes": slot,
                        "order": args.order,
-                       "port": "per-packet array" if args.port_array
+                       "port": "per-packet array" if port_array
                                else "one per burst (vp_dev_batch.in_port)",
                        "parallelism": ("%s%d" % (mode, world))
                        if world > 1 else "single"},
