@@ -196,6 +196,35 @@ def test_burst_port(slot):
     check_state(nat, o, 64)
 
 
+def test_process_one_two_contexts():
+    """Two vignat contexts served one packet at a time, alternately: each
+    has its own resident kernel and mailbox on its own stream; both agree
+    with their oracles, then one is destroyed while the other keeps
+    serving."""
+    rng = np.random.default_rng(41)
+    n = 300
+    pairs, traces = [], []
+    for k in range(2):
+        fr, ln, dv, now = mixed_nat_trace(rng, n, 80, max_idx=128)
+        nat, o = make_pair(max_flows=128)
+        exp = fr.copy()
+        exp_out = o.run(exp, ln, dv, now, 64)
+        pairs.append((nat, o))
+        traces.append((fr, ln, dv, now, exp, exp_out))
+    for i in range(n):
+        for k in range(2):
+            if k == 1 and i == n // 2:
+                pairs[0][0].close()  # the other context's kernel keeps serving
+            if k == 0 and i >= n // 2:
+                continue
+            nat = pairs[k][0]
+            fr, ln, dv, now, exp, exp_out = traces[k]
+            b = bytearray(fr[i * 64:i * 64 + int(ln[i])].tobytes())
+            assert nat.process(int(dv[i]), b, int(now[i])) == exp_out[i], (k, i)
+            assert bytes(b) == exp[i * 64:i * 64 + int(ln[i])].tobytes(), (k, i)
+    check_state(pairs[1][0], pairs[1][1], 128)
+
+
 def test_config2_1m_flows_full_size():
     """BASELINE config 2 at its full table size (1M flows, cap 2^20): a
     warm-up batch creating every flow, then steady-state batches, checked
