@@ -196,6 +196,29 @@ def test_burst_port(slot):
     check_state(nat, o, 64)
 
 
+def test_process_one_long_frame_and_empty():
+    """Frames the mailbox does not take (longer than its 2048 bytes) go
+    through the batch path, a zero-length frame drops, and the kernel
+    serves the packets around them; all against the oracle."""
+    nat, o = make_pair(max_flows=64)
+    fr, ln, dv, now = T.nat_lan_trace(6, 3)
+    slot = 4096
+    F = np.zeros((6, slot), np.uint8)
+    F[:, :64] = fr.reshape(6, 64)
+    lens = ln.astype(np.int64).copy()
+    lens[2] = 3000                          # past the mailbox: the batch path
+    lens[4] = 0                             # nothing to parse: dropped
+    # (total_length as the frame says: 46 bytes of IP; the rest is padding)
+    exp = F.reshape(-1).copy()
+    exp_out = o.run(exp, lens.astype(np.uint16), dv, now, slot)
+    E = exp.reshape(6, slot)
+    for i in range(6):
+        b = bytearray(F[i, :lens[i]].tobytes())
+        assert nat.process(int(dv[i]), b, int(now[i])) == exp_out[i], i
+        assert bytes(b) == E[i, :lens[i]].tobytes(), i
+    check_state(nat, o, 64)
+
+
 def test_process_one_two_contexts():
     """Two vignat contexts served one packet at a time, alternately: each
     has its own resident kernel and mailbox on its own stream; both agree
