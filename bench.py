@@ -372,6 +372,11 @@ def golden_configs():
         return {k: z[k] for k in z.files}
 
 
+# vignat's 64-byte classify kernel on one GPU: one 1024-thread block per CU
+# (vp_nat.hip nat_classify64w) unless VIGPATH_BLOCK_WAVES=4
+NAT64 = "nat_classify64" if os.environ.get("VIGPATH_BLOCK_WAVES") == "4" else "nat_classify64w"
+
+
 def steady_workload(nf, batch_of, warm: int, steps: int, B: int, dev, golden=None,
                     kernel="", times=None, state=None, repeats=False, alg_bytes=ALG_BYTES):
     """Batches 0 .. warm-1 untimed (allocation), then `steps` timed calls
@@ -520,7 +525,7 @@ def bench_nat_random(dev, B, steps, golden):
     def batch_of(k, buf):
         bank.fill(buf, k * B)
         return lens, ind, T.NOW0 + k * B, 1
-    r = steady_workload(nat, batch_of, 1, steps, B, dev, golden, "nat_classify64",
+    r = steady_workload(nat, batch_of, 1, steps, B, dev, golden, NAT64,
                         repeats=True)
     r["table_layout"] = nat.table_stats()["layout"]
     nat.close()
@@ -550,7 +555,7 @@ def bench_nat_churn(dev, B, steps, golden, state=None):
     def batch_of(k, buf):
         bank.fill_flows(buf, (k + slot_id % 4) // 4 * W + slot_id)
         return lens, ind, T.NOW0 + k * T.CHURN_DT, 0
-    r = steady_workload(nat, batch_of, warm, steps, B, dev, golden, "nat_classify64",
+    r = steady_workload(nat, batch_of, warm, steps, B, dev, golden, NAT64,
                         state=state)
     r["live_flows"] = nat.live_count()
     nat.close()
@@ -921,7 +926,9 @@ def main():
     else:
         workload = "vignat %dB frames in %dB slots, %d flows, %s order, 1xMI355X" % (
             flen, slot, args.flows, args.order)
-    kname = ("nat_classify64" if slot == SLOT else "nat_classify_wide")
+    owner_pass = (world > 1 and mode == "owner") or args.route_all  # (pass 1: 256-thread)
+    kname = ((NAT64 if not owner_pass else "nat_classify64") if slot == SLOT
+             else "nat_classify_wide")
     if args.route_all:
         workload = ("vignat %dB, %d flows, 1xMI355X, owner-mode pipeline with every key "
                     "routed through a one-rank RCCL exchange (profiling)" % (flen, args.flows))

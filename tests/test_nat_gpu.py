@@ -208,7 +208,10 @@ def test_process_one_long_frame_and_empty():
     lens = ln.astype(np.int64).copy()
     lens[2] = 3000                          # past the mailbox: the batch path
     lens[4] = 0                             # nothing to parse: dropped
-    # (total_length as the frame says: 46 bytes of IP; the rest is padding)
+    # (total_length as the frame says: 46 bytes of IP; the rest is padding;
+    # a frame is its buffer of len bytes, so the oracle sees zeros past len)
+    for i in range(6):
+        F[i, lens[i]:] = 0
     exp = F.reshape(-1).copy()
     exp_out = o.run(exp, lens.astype(np.uint16), dv, now, slot)
     E = exp.reshape(6, slot)

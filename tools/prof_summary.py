@@ -21,7 +21,7 @@ import os
 import statistics
 import sys
 
-KERNEL = os.environ.get("PROF_KERNEL", "nat_classify64")
+KERNEL = os.environ.get("PROF_KERNEL", "nat_classify64w")
 # PROF_LAUNCHES=a:b: only launches a..b-1 of each kernel, in dispatch order
 # (one workload's launches when a bench run holds several: bench.py's
 # headline comes first, its extras after it)

@@ -11,7 +11,7 @@ import csv
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--marker", default="nat_classify64")
+    ap.add_argument("--marker", default="nat_classify64")  # (prefix: also nat_classify64w)
     ap.add_argument("--step", type=int, default=-5, help="which marker launch (python index)")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))

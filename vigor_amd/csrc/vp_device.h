@@ -305,15 +305,16 @@ struct TouchBins {
   uint32_t nsrc;  // classify blocks (the launch's grid)
   // run entries (runs != 0): a wave whose 64 packets touch the 64
   // consecutive indices of one bin run records them as one word in its
-  // block's row of rtab ([block][bin][2], kept whole in the L2 as the block
-  // fills it), flagged in the bin's count (kBinRunFlag, kBinRunFlag2); two
-  // per block and bin
+  // block's row of rtab ([block][bin][rwords], kept whole in the L2 as the
+  // block fills it), counted in the top byte of the bin's count; rwords per
+  // block and bin (2; 8 for 1024-thread blocks, whose ranges are 4x longer)
   uint32_t *rtab;
   uint32_t runs;
+  uint32_t rwords;
 };
-constexpr uint32_t kBinRunFlag = 0x80000000u;   // run word 0 of the block's bin
-constexpr uint32_t kBinRunFlag2 = 0x40000000u;  // run word 1
-constexpr uint32_t kBinRunFlags = kBinRunFlag | kBinRunFlag2;
+constexpr uint32_t kBinRunShift = 24;            // run words claimed: a count's top byte
+constexpr uint32_t kBinRunFlags = 0xFF000000u;   // (that byte)
+constexpr uint32_t kBinRunWordsMax = 8;
 
 // Touch-log entry of packet p; `log` is null in the classify kernels that
 // bin their touches.
@@ -352,17 +353,17 @@ __device__ __forceinline__ void bins_put(const TouchBins &bins, uint32_t *cur,
                         p == q0 + lane;
     if (__ballot(in_run) == ~0ull) {
       const uint32_t b0 = bin_of(t0, bins.bbits);
-      uint32_t slot = 2;
-      if (lane == 0) {
-        if (!(atomicOr(&cur[b0], kBinRunFlag) & kBinRunFlag))
-          slot = 0;
-        else if (!(atomicOr(&cur[b0], kBinRunFlag2) & kBinRunFlag2))
-          slot = 1;
-      }
+      uint32_t slot = kBinRunWordsMax;
+      // (claims past rwords only by waves racing the check: at most the
+      // block's waves more, well inside the byte)
+      if (lane == 0 &&
+          (__hip_atomic_load(&cur[b0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >>
+           kBinRunShift) < bins.rwords)
+        slot = atomicAdd(&cur[b0], 1u << kBinRunShift) >> kBinRunShift;
       slot = __builtin_amdgcn_readfirstlane(slot);
-      if (slot < 2) {
+      if (slot < bins.rwords) {
         if (lane == 0)
-          bins.rtab[((((size_t)rb << bins.bbits) + b0) << 1) + slot] =
+          bins.rtab[(((size_t)rb << bins.bbits) + b0) * bins.rwords + slot] =
               ((bin_local(t0, bins.bbits) >> kBinRunBits) << 20) | (q0 - range0);
         return;
       }
@@ -390,8 +391,8 @@ __device__ __forceinline__ void bins_publish(const TouchBins &bins, const uint32
                                              uint32_t rb) {
   if (!bins.ent) return;
   for (uint32_t b = threadIdx.x; b < (1u << bins.bbits); b += blockDim.x) {
-    const uint32_t c = cur[b] & ~kBinRunFlags;
-    bins.cnt[(size_t)b * bins.nsrc + rb] = (c < bins.cap ? c : bins.cap) | (cur[b] & kBinRunFlags);
+    const uint32_t c = cur[b] & ~kBinRunFlags, nr = min(cur[b] >> kBinRunShift, bins.rwords);
+    bins.cnt[(size_t)b * bins.nsrc + rb] = (c < bins.cap ? c : bins.cap) | (nr << kBinRunShift);
   }
   if (threadIdx.x == 0) {
     const uint32_t o = cur[kOvf];

@@ -701,12 +701,15 @@ __device__ __forceinline__ uint32_t dense128_tail(const uint4 d[8]) {
 // phase B or the reprobe walk are stored unchanged). Any other tile runs
 // nat_issue / nat_finish per lane. Owner mode's pass 1 has a lean tile of its
 // own (keys of other ranks routed, this rank's looked up).
-template <uint32_t G, uint32_t H = 1, bool D = false, bool X = false, bool PR = G == 0>
+// W: waves per block (4: 256-thread blocks, four per CU; 16: one 1024-thread
+// block per CU, nat_classify64w).
+template <uint32_t G, uint32_t H = 1, bool D = false, bool X = false, bool PR = G == 0,
+          uint32_t W = 4>
 __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins bins,
                                           TileQueue rq) {
   static_assert(!X || G == 0, "header slots (X) are 64-byte slots");
   __shared__ uint32_t T[kNatTabWords];
-  __shared__ uint4 stage[4][256];
+  __shared__ uint4 stage[W][256];
   __shared__ uint32_t cur[kCurs];
   __shared__ uint32_t mbase;
   for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
@@ -770,7 +773,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   const uint32_t rb = a.vb0 + blockIdx.x;  // (virtual blocks: the chunked pipeline)
   const uint32_t per_b = a.vper ? a.vper : (tiles + gridDim.x - 1) / gridDim.x;
   uint32_t tile = rb * per_b + wv;
-  const uint32_t tend = min(tiles, rb * per_b + per_b), tstep = 4;
+  const uint32_t tend = min(tiles, rb * per_b + per_b), tstep = W;
   const uint32_t range0 = first + rb * per_b * 64;  // this block's first packet
   // a lean tile's misses (wave-uniform call), with their FlowIds and hashes
   // when phase B takes them unsorted (a.mkq)
@@ -1167,6 +1170,11 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
                                                         TouchBins bins, TileQueue rq) {
   nat_tiles<0>(a, n_all, bins, rq);
 }
+// One 1024-thread block per CU (the default, nat_block_waves)
+__global__ __launch_bounds__(1024, 1) void nat_classify64w(NatArgs a, uint32_t n_all,
+                                                          TouchBins bins, TileQueue rq) {
+  nat_tiles<0, 1, false, false, true, 16>(a, n_all, bins, rq);
+}
 // (diagnostics, VIGPATH_PRIO=0: the lean tile without the raised priority)
 __global__ __launch_bounds__(256, 4) void nat_classify64_p0(NatArgs a, uint32_t n_all,
                                                            TouchBins bins, TileQueue rq) {
@@ -1201,11 +1209,26 @@ __global__ __launch_bounds__(256, 4) void nat_classify128(NatArgs a, uint32_t n_
 // The classify kernel for a slot: 64 bytes, or the wide kernel whose G is the
 // tail's 16-byte chunks (slot - 64) / 16 rounded up to a power of two, at most 16.
 typedef void (*NatTileKernel)(NatArgs, uint32_t, TouchBins, TileQueue);
+// Waves per block of the 64-byte classify: 16 (one 1024-thread block per
+// CU, nat_classify64w) unless VIGPATH_BLOCK_WAVES=4 (four 256-thread blocks,
+// nat_classify64, for A/B). A block's range is then four times longer, so
+// the chip keeps a quarter of the partly written bin-slice lines (uniform
+// order 0.805 -> 0.725 ms per step, round robin unchanged with eight run
+// words per block and bin: DESIGN.md §5.1).
+static uint32_t nat_block_waves() {
+  static const uint32_t w = [] {
+    const char *e = getenv("VIGPATH_BLOCK_WAVES");
+    return e && atoi(e) == 4 ? 4u : 16u;
+  }();
+  return w;
+}
+
 static NatTileKernel nat_tile_kernel(uint32_t slot, bool hdr_tail = false) {
   static const bool p0 = [] {
     const char *e = getenv("VIGPATH_PRIO");
     return e && atoi(e) == 0;
   }();
+  if (slot == 64 && !hdr_tail && nat_block_waves() == 16) return nat_classify64w;
   if (slot == 64) return hdr_tail ? nat_classify64x : p0 ? nat_classify64_p0 : nat_classify64;
   if (slot == 128) return nat_classify128;
   const uint32_t nch = (slot - 64) / 16;
@@ -2705,13 +2728,14 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // per block (TileQueue)
   const bool tiles64 = owner ? ph.tiles64 : p1 > p0 && c->coalesced_io;
   const NatTileKernel tk = nat_tile_kernel(b->slot, a.tail != nullptr);
+  const uint32_t tw = tk == nat_classify64w ? 16u : 4u;  // waves per block
   BinsPlan bp = ph.bp;
   uint32_t grid64 = ph.grid1, range64 = ph.range1;
   TileQueue rq{};
   if (tiles64 && !owner) {
-    VP_TRY(tbl_bins_plan(c, t, (const void *)tk, p0, p1, &bp));
+    VP_TRY(tbl_bins_plan(c, t, (const void *)tk, p0, p1, &bp, tw));
     const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
-    grid64 = resident_grid((const void *)tk, (tiles + 3) / 4);
+    grid64 = resident_grid((const void *)tk, (tiles + tw - 1) / tw, 64 * (int)tw);
     range64 = (tiles + grid64 - 1) / grid64 * 64;
     rq = TileQueue{w.reprobe, w.reprobe_cnt, &t.ctl->reprobe_count};
     a.tileq = 1;
@@ -2727,10 +2751,10 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
       NatArgs a64 = a;
       if (bp.on) a64.log = nullptr;  // touches go to the bins only
       if (c->ktime) {
-        VP_HIP(launch_timed(tk, grid64, 256, c->stream, c->ev0, c->ev1, a64,
+        VP_HIP(launch_timed(tk, grid64, 64 * tw, c->stream, c->ev0, c->ev1, a64,
                             (uint32_t)b->n, bp.bins, rq));
       } else {
-        tk<<<grid64, 256, 0, c->stream>>>(a64, (uint32_t)b->n, bp.bins, rq);
+        tk<<<grid64, 64 * tw, 0, c->stream>>>(a64, (uint32_t)b->n, bp.bins, rq);
         VP_HIP(hipGetLastError());
       }
     } else {

@@ -1042,7 +1042,7 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
     const uint32_t *ent, const uint32_t *cnt, uint32_t nsrc, uint32_t cap,
     uint32_t pbits, uint32_t bbits, uint32_t range, uint32_t L, uint32_t tcap,
     uint32_t p0, NowSpec now, uint64_t seq_base, uint64_t *ts, uint64_t *tseq,
-    PubArgs pub, const uint32_t *rtab, uint32_t sbits, uint32_t maxmode) {
+    PubArgs pub, const uint32_t *rtab, uint32_t sbits, uint32_t maxmode, uint32_t rwords) {
   // 1 + position in the launch, 0 = none; L words of dynamic LDS (16 KB at
   // 1M flows: the 256 bin blocks spread over all CUs, where a 64 KB static
   // array let only two blocks share a CU and left half of them idle)
@@ -1070,12 +1070,12 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
   for (uint32_t r0 = threadIdx.x >> 6; r0 < nsrc; r0 += 64 * nw) {
     const uint32_t my = r0 + lane * nw;
     const uint32_t raw = my < nsrc ? cnt[(size_t)bin * nsrc + my] : 0;
-    const uint32_t nv = raw & ~kBinRunFlags;
-    // the slice's run words, loaded beside the count (one round trip; a word
-    // whose flag is clear is stale and ignored)
-    const size_t ri = (((size_t)my << bbits) + bin) << 1;
+    const uint32_t nv = raw & ~kBinRunFlags, nr = raw >> kBinRunShift;
+    // the slice's first two run words, loaded beside the count (one round
+    // trip; a word past the slice's count is stale and ignored)
+    const size_t ri = (((size_t)my << bbits) + bin) * rwords;
     const uint32_t re = my < nsrc ? rtab[ri] : 0u, re2 = my < nsrc ? rtab[ri + 1] : 0u;
-    const bool run = (raw & kBinRunFlag) != 0, run2 = (raw & kBinRunFlag2) != 0;
+    const bool run = nr > 0, run2 = nr > 1;
     const uint32_t ch = (nv + 63) >> 6;
     uint32_t inc = ch;  // inclusive prefix over the wave
 #pragma unroll
@@ -1107,6 +1107,14 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
       atomicMax(&grp[(re >> 20) - (lo >> kBinRunBits)], my * range + 1 + (re & 0xFFFFFu));
     if (run2 && ((re2 >> 20) << kBinRunBits) - lo < Lp)
       atomicMax(&grp[(re2 >> 20) - (lo >> kBinRunBits)], my * range + 1 + (re2 & 0xFFFFFu));
+    for (uint32_t j = 2; j < rwords; j++) {  // (1024-thread classify blocks)
+      if (__ballot(j < nr) == 0) break;
+      if (j < nr) {
+        const uint32_t rj = rtab[ri + j];
+        if (((rj >> 20) << kBinRunBits) - lo < Lp)
+          atomicMax(&grp[(rj >> 20) - (lo >> kBinRunBits)], my * range + 1 + (rj & 0xFFFFFu));
+      }
+    }
   }
   __syncthreads();
   for (uint32_t l = threadIdx.x; l < Lp; l += blockDim.x) {
@@ -1192,8 +1200,10 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   plan->range = range;
   plan->L = L;
   plan->sbits = sbits;
-  // run words: two per block and bin, positions below 2^20 within a block
-  const size_t nr = ((size_t)grid << bbits) * 2;
+  // run words per block and bin: two, eight for 1024-thread blocks (four
+  // times the range); positions below 2^20 within a block
+  const uint32_t rwords = waves >= 16 ? kBinRunWordsMax : 2u;
+  const size_t nr = ((size_t)grid << bbits) * rwords;
   if (nr > w.bins_rtab_n) {
     VP_HIP(hipStreamSynchronize(c->stream));
     hipFree(w.bins_rtab);
@@ -1208,7 +1218,8 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   }();
   const uint32_t runs = runs_env && range <= (1u << 20) && (L >> kBinRunBits) < (1u << 12);
   plan->bins = TouchBins{w.bins_ent, w.bins_cnt, &t.ctl->touch_ovf, w.ovf_q,
-                         w.ovf_cnt, w.log, cap, pbits, bbits, grid, w.bins_rtab, runs};
+                         w.ovf_cnt, w.log, cap, pbits, bbits, grid, w.bins_rtab, runs,
+                         rwords};
   return 0;
 }
 
@@ -1227,7 +1238,8 @@ static int bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p
   fold<<<1u << (plan.bins.bbits + plan.sbits), 1024, 4u * (Lp + (Lp >> kBinRunBits)),
          c->stream>>>(plan.bins.ent, plan.bins.cnt, plan.grid, plan.bins.cap, plan.bins.pbits,
                       plan.bins.bbits, plan.range, plan.L, t.cap, p0, now, seq_base, t.ts,
-                      t.tseq, pub, plan.bins.rtab, plan.sbits, plan.maxmode ? 1u : 0u);
+                      t.tseq, pub, plan.bins.rtab, plan.sbits, plan.maxmode ? 1u : 0u,
+                      plan.bins.rwords);
   VP_HIP(hipGetLastError());
   return 0;
 }
