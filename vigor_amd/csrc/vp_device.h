@@ -452,7 +452,9 @@ __device__ __forceinline__ uint32_t port_of(const uint16_t *in_dev, uint32_t in0
 // PR: the issue half, the row requests and the next tile's prefetch at a
 // raised wave priority (as vignat's lean tile: the SIMD issues them ahead of
 // other waves' arithmetic, more requests in flight).
-template <uint32_t kOvf = kCurOverflow, bool PR = false, class Issue, class Finish>
+// W: waves per block (4, or 16 for one 1024-thread block per CU).
+template <uint32_t kOvf = kCurOverflow, bool PR = false, uint32_t W = 4, class Issue,
+          class Finish>
 __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
                                                const uint16_t *len,
                                                const uint16_t *in_dev,
@@ -487,7 +489,7 @@ __device__ __forceinline__ void frames64_tiles(uint8_t *frames,
   const uint32_t rb = vb0 + blockIdx.x;
   const uint32_t per_b = vper ? vper : (tiles + gridDim.x - 1) / gridDim.x;
   uint32_t tile = rb * per_b + wv;
-  const uint32_t tend = min(tiles, rb * per_b + per_b), tstep = 4;
+  const uint32_t tend = min(tiles, rb * per_b + per_b), tstep = W;
   const uint32_t range0 = first + rb * per_b * 64;  // this block's first packet
   if (tile < tend) fetch(tile);
   for (; tile < tend; tile += tstep) {

@@ -308,10 +308,10 @@ struct LbPend {
 // more dependent round trip per packet.
 constexpr uint32_t kLbLdsBackends = 256;
 constexpr uint32_t kLbCurs = 257;  // bins 0..255, the overflow queue at 256
-__global__ __launch_bounds__(256, 4) void lb_classify64(LbArgs a, uint32_t n_all,
-                                                       TouchBins bins) {
+template <uint32_t W>  // waves per block
+__device__ __forceinline__ void lb_tiles(LbArgs a, uint32_t n_all, TouchBins bins) {
   __shared__ uint32_t T[kLbFlowTabs * 256 + 1024];  // + the layout's byte tables
-  __shared__ uint4 stage[4][256];
+  __shared__ uint4 stage[W][256];
   __shared__ uint32_t cur[kLbCurs];
   __shared__ uint4 bhdr[kLbLdsBackends];
   __shared__ uint32_t bnic[kLbLdsBackends];
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(256, 4) void lb_classify64(LbArgs a, uint32_t n_all
     }
   __syncthreads();
   const uint32_t *I = a.crc_tab + kLbFlowTabs * 256;  // ip_addr tables (global)
-  frames64_tiles<kLbCurs - 1, true>(
+  frames64_tiles<kLbCurs - 1, true, W>(
       a.frames, a.len, a.in_dev, a.p0, a.p1, n_all, stage[threadIdx.x >> 6],
       reinterpret_cast<const uint4 *>(a.ft.bk),
       [&](uint32_t p, const RFrame &f, uint32_t in, uint32_t len, bool mine) {
@@ -415,6 +415,15 @@ __global__ __launch_bounds__(256, 4) void lb_classify64(LbArgs a, uint32_t n_all
         return rw ? 0xFu : 0u;
       },
       bins, TileQueue{}, cur, 0, 0, a.in0);
+}
+__global__ __launch_bounds__(256, 4) void lb_classify64(LbArgs a, uint32_t n_all,
+                                                       TouchBins bins) {
+  lb_tiles<4>(a, n_all, bins);
+}
+// one 1024-thread block per CU (as vignat's nat_classify64w; VIGPATH_LB_WAVES)
+__global__ __launch_bounds__(1024, 1) void lb_classify64w(LbArgs a, uint32_t n_all,
+                                                         TouchBins bins) {
+  lb_tiles<16>(a, n_all, bins);
 }
 
 __global__ __launch_bounds__(256) void lb_classify(LbArgs a) {
@@ -691,14 +700,21 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   if (tiles64) {
     // the flow touches go to the touch bins (256 of them: lb_classify64 keeps
     // 256 bin cursors; a larger table logs every touch and refolds the log)
-    VP_TRY(tbl_bins_plan(c, c->ft, (const void *)lb_classify64, p0, p1, &bp));
+    static const uint32_t lw = [] {  // waves per block (VIGPATH_LB_WAVES: 4 or 16)
+      const char *e = getenv("VIGPATH_LB_WAVES");
+      return e && atoi(e) == 16 ? 16u : 4u;
+    }();
+    const void *k = lw == 16 ? (const void *)lb_classify64w : (const void *)lb_classify64;
+    VP_TRY(tbl_bins_plan(c, c->ft, k, p0, p1, &bp, lw));
     if (bp.on && bp.bins.bbits > 8) bp = BinsPlan{};
     const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
-    const uint32_t grid =
-        bp.on ? bp.grid : resident_grid((const void *)lb_classify64, (tiles + 3) / 4);
+    const uint32_t grid = bp.on ? bp.grid : resident_grid(k, (tiles + lw - 1) / lw, 64 * (int)lw);
     LbArgs a64 = a;
     a64.binned = bp.on;
-    lb_classify64<<<grid, 256, 0, c->stream>>>(a64, b->n, bp.bins);
+    if (lw == 16)
+      lb_classify64w<<<grid, 1024, 0, c->stream>>>(a64, b->n, bp.bins);
+    else
+      lb_classify64<<<grid, 256, 0, c->stream>>>(a64, b->n, bp.bins);
   } else {
     lb_classify<<<grid_for(p1 - p0), 256, 0, c->stream>>>(a);
   }
