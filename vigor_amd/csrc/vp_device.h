@@ -385,6 +385,112 @@ __device__ __forceinline__ void bins_put(const TouchBins &bins, uint32_t *cur,
   }
 }
 
+// Whole-line bin entries (1024-thread vignat blocks, up to 128 bins): a
+// block stages each bin's entries in an LDS ring of kStageLines lines of 16
+// entries (64 bytes) and stores a line only once all 16 are written, as one
+// 64-byte piece, so no partly written slice line sits in the L2 (uniform
+// order). Entry k of bin b goes to line k / 16, ring
+// position (k / 16) % kStageLines; a position is free for line L once line
+// L - kStageLines has been stored (gen[] holds the next line it may take),
+// the lane whose write completes a line stores it. Every reserved entry
+// belongs to a wave inside bins_put_staged's loop, and the oldest unstored
+// line of a bin always has its position, so the loop always progresses (no
+// block barrier inside it). The last partial line of each bin is stored by
+// bins_flush_staged after the block's final barrier.
+constexpr uint32_t kStageLines = 4, kStageBins = 128;
+struct BinStage {
+  uint32_t *ring;  // [bin][kStageLines][16] entries
+  uint32_t *wc;    // [bin][kStageLines] entries written into the line
+  uint32_t *gen;   // [bin][kStageLines] the line the position may take next
+};
+__device__ __forceinline__ void bins_stage_init(const BinStage &st) {
+  for (uint32_t i = threadIdx.x; i < kStageBins * kStageLines; i += blockDim.x) {
+    st.wc[i] = 0;
+    st.gen[i] = i % kStageLines;
+  }
+}
+
+template <uint32_t kOvf = kCurOverflow>
+__device__ __forceinline__ void bins_put_staged(const TouchBins &bins, const BinStage &st,
+                                                uint32_t *cur, uint32_t rb, uint32_t range,
+                                                uint32_t range0, uint32_t p, uint32_t touch) {
+  if (!bins.ent) return;
+  if (bins.runs) {  // the whole wave one run of 64 indices: one word (as bins_put)
+    const uint32_t lane = __lane_id();
+    const uint32_t t0 = __builtin_amdgcn_readfirstlane(touch);
+    const uint32_t q0 = __builtin_amdgcn_readfirstlane(p);
+    const bool in_run = t0 != kNone && (t0 & (kBinRun - 1)) == 0 && touch == t0 + lane &&
+                        p == q0 + lane;
+    if (__ballot(in_run) == ~0ull) {
+      const uint32_t b0 = bin_of(t0, bins.bbits);
+      uint32_t slot = kBinRunWordsMax;
+      if (lane == 0 &&
+          (__hip_atomic_load(&cur[b0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >>
+           kBinRunShift) < bins.rwords)
+        slot = atomicAdd(&cur[b0], 1u << kBinRunShift) >> kBinRunShift;
+      slot = __builtin_amdgcn_readfirstlane(slot);
+      if (slot < bins.rwords) {
+        if (lane == 0)
+          bins.rtab[(((size_t)rb << bins.bbits) + b0) * bins.rwords + slot] =
+              ((bin_local(t0, bins.bbits) >> kBinRunBits) << 20) | (q0 - range0);
+        return;
+      }
+    }
+  }
+  const bool v = touch != kNone;
+  const uint32_t b = v ? bin_of(touch, bins.bbits) : 0;
+  const uint32_t k = group_reserve(cur, b, v) & ~kBinRunFlags;
+  const bool fits = k < bins.cap;
+  const uint32_t e = (bin_local(touch, bins.bbits) << bins.pbits) | (p - range0);
+  const uint32_t line = k >> 4, pos = b * kStageLines + (line % kStageLines);
+  bool pend = v && fits;
+  while (__ballot(pend)) {
+    bool full = false;
+    if (pend && __hip_atomic_load(&st.gen[pos], __ATOMIC_ACQUIRE,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP) == line) {
+      st.ring[pos * 16 + (k & 15)] = e;
+      full = __hip_atomic_fetch_add(&st.wc[pos], 1u, __ATOMIC_ACQ_REL,
+                                    __HIP_MEMORY_SCOPE_WORKGROUP) == 15;
+      pend = false;
+    }
+    if (full) {  // this lane's write completed the line: store it whole
+      const uint4 *src = reinterpret_cast<const uint4 *>(st.ring + pos * 16);
+      uint4 *dst = reinterpret_cast<uint4 *>(
+          bins.ent + ((size_t)b * bins.nsrc + rb) * bins.cap + (size_t)line * 16);
+      const uint4 x0 = src[0], x1 = src[1], x2 = src[2], x3 = src[3];
+      dst[0] = x0;
+      dst[1] = x1;
+      dst[2] = x2;
+      dst[3] = x3;
+      __hip_atomic_store(&st.wc[pos], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(&st.gen[pos], line + kStageLines, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (__ballot(pend)) __builtin_amdgcn_s_sleep(1);
+  }
+  const bool spill = v && !fits;
+  const uint32_t o = group_reserve(cur, kOvf, spill);
+  if (spill) {
+    bins.olog[p] = touch;
+    bins.oent[(size_t)rb * range + o] = p;
+  }
+}
+
+// After the block's final barrier: each bin's last, partial line (the full
+// ones were stored by the lanes that completed them).
+__device__ __forceinline__ void bins_flush_staged(const TouchBins &bins, const BinStage &st,
+                                                  const uint32_t *cur, uint32_t rb) {
+  if (!bins.ent) return;
+  for (uint32_t b = threadIdx.x; b < (1u << bins.bbits); b += blockDim.x) {
+    const uint32_t c = min(cur[b] & ~kBinRunFlags, bins.cap);
+    const uint32_t line = c >> 4, n = c & 15;
+    if (!n) continue;
+    const uint32_t pos = b * kStageLines + (line % kStageLines);
+    uint32_t *dst = bins.ent + ((size_t)b * bins.nsrc + rb) * bins.cap + (size_t)line * 16;
+    for (uint32_t i = 0; i < n; i++) dst[i] = st.ring[pos * 16 + i];
+  }
+}
+
 // After the block's last bins_put and a barrier: publish its slice sizes.
 template <uint32_t kOvf = kCurOverflow>
 __device__ __forceinline__ void bins_publish(const TouchBins &bins, const uint32_t *cur,

@@ -197,6 +197,9 @@ struct NatArgs {
   uint32_t *mhash;
   uint4 *mkq;
   uint32_t *mhq;
+  // 1024-thread tiles: bin entries staged in LDS and stored a whole line at
+  // a time (bins_put_staged; VIGPATH_BIN_STAGE=0 off, for A/B)
+  uint32_t bstage;
 };
 
 // Queue packet p (FlowId key, hash h) as a phase-B miss.
@@ -712,6 +715,14 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   __shared__ uint4 stage[W][256];
   __shared__ uint32_t cur[kCurs];
   __shared__ uint32_t mbase;
+  // (1024-thread blocks: whole-line bin entries, bins_put_staged)
+  constexpr bool kStaged = W == 16;
+  __shared__ uint32_t sring[kStaged ? kStageBins * kStageLines * 16 : 1];
+  __shared__ uint32_t swc[kStaged ? kStageBins * kStageLines : 1];
+  __shared__ uint32_t sgen[kStaged ? kStageBins * kStageLines : 1];
+  const BinStage bst{sring, swc, sgen};
+  const bool staged = kStaged && bins.ent && bins.bbits <= 7 && a.bstage;
+  if (kStaged) bins_stage_init(bst);
   for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
   a.own.cur = cur + kCurDest;
   load_nat_tables(T, a);  // (its barrier also covers cur)
@@ -1135,7 +1146,10 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
         wave_lds_sync();  // the next tile overwrites S
       }
     }
-    bins_put(bins, cur, rb, per_b * 64, range0, p, touch);
+    if (staged)
+      bins_put_staged(bins, bst, cur, rb, per_b * 64, range0, p, touch);
+    else
+      bins_put(bins, cur, rb, per_b * 64, range0, p, touch);
     if (store_all) {
 #pragma unroll
       for (uint32_t k = 0; k < 4; k++)
@@ -1148,6 +1162,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
     }
   }
   __syncthreads();
+  if (staged) bins_flush_staged(bins, bst, cur, rb);
   bins_publish(bins, cur, rb);
   if (rq.ent && threadIdx.x == 0) {
     const uint32_t c = cur[kCurReprobe];
@@ -2706,6 +2721,11 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     return e && atoi(e);
   }();
   const bool nku = !c->comm && !nk_sorted;
+  static const bool bin_stage = [] {
+    const char *e = getenv("VIGPATH_BIN_STAGE");
+    return !e || atoi(e) != 0;
+  }();
+  a.bstage = bin_stage ? 1u : 0u;
   if (nku) {
     a.mkey = reinterpret_cast<uint4 *>(w.mkey);
     a.mhash = w.mhash;
