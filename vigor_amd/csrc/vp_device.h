@@ -340,10 +340,12 @@ __device__ __forceinline__ uint32_t bin_index(uint32_t bin, uint32_t local,
 // packet). A full slice logs the touch alone on the block's overflow queue.
 // kOvf: the overflow queue's LDS cursor (a kernel whose tables stay at 256
 // bins keeps only cursors 0..256, kOvf = 256, to make room in LDS).
+// (runcnt: an LDS counter of the block's run tiles, or null)
 template <uint32_t kOvf = kCurOverflow>
 __device__ __forceinline__ void bins_put(const TouchBins &bins, uint32_t *cur,
                                          uint32_t rb, uint32_t range, uint32_t range0,
-                                         uint32_t p, uint32_t touch) {
+                                         uint32_t p, uint32_t touch,
+                                         uint32_t *runcnt = nullptr) {
   if (!bins.ent) return;
   if (bins.runs) {  // the whole wave one run of 64 indices: one word
     const uint32_t lane = __lane_id();
@@ -353,6 +355,7 @@ __device__ __forceinline__ void bins_put(const TouchBins &bins, uint32_t *cur,
                         p == q0 + lane;
     if (__ballot(in_run) == ~0ull) {
       const uint32_t b0 = bin_of(t0, bins.bbits);
+      if (runcnt && lane == 0) atomicAdd(runcnt, 1u);
       uint32_t slot = kBinRunWordsMax;
       // (claims past rwords only by waves racing the check: at most the
       // block's waves more, well inside the byte)
@@ -413,7 +416,8 @@ __device__ __forceinline__ void bins_stage_init(const BinStage &st) {
 template <uint32_t kOvf = kCurOverflow>
 __device__ __forceinline__ void bins_put_staged(const TouchBins &bins, const BinStage &st,
                                                 uint32_t *cur, uint32_t rb, uint32_t range,
-                                                uint32_t range0, uint32_t p, uint32_t touch) {
+                                                uint32_t range0, uint32_t p, uint32_t touch,
+                                                uint32_t *runcnt = nullptr) {
   if (!bins.ent) return;
   if (bins.runs) {  // the whole wave one run of 64 indices: one word (as bins_put)
     const uint32_t lane = __lane_id();
@@ -423,6 +427,7 @@ __device__ __forceinline__ void bins_put_staged(const TouchBins &bins, const Bin
                         p == q0 + lane;
     if (__ballot(in_run) == ~0ull) {
       const uint32_t b0 = bin_of(t0, bins.bbits);
+      if (runcnt && lane == 0) atomicAdd(runcnt, 1u);
       uint32_t slot = kBinRunWordsMax;
       if (lane == 0 &&
           (__hip_atomic_load(&cur[b0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >>

@@ -98,7 +98,8 @@ struct Ctl {
   uint32_t disp_count;  // inserts that passed their home bucket (since rebuild)
   uint32_t sh_live;     // entries in this rank's buckets (= n_live unless owner mode)
   uint32_t own_new;     // owner mode: union keys this rank will insert (upper bound)
-  uint32_t pad_;
+  uint32_t run_tiles;   // vignat's 64-byte tiles whose 64 touches were one run
+                        // (cumulative, never reset: the host takes differences)
 };
 
 // The control block as a fold kernel publishes it into page-locked host
@@ -146,6 +147,10 @@ struct FlowTable {
   uint32_t pub_epoch = 0;          // last epoch asked of the fold
   uint32_t *ttotal = nullptr;  // touch-reduce entry count (device)
   uint64_t ts_floor = UINT64_MAX;  // lower bound of min ts over live indices
+  // vignat: the last segment's tiles were mostly runs (Ctl::run_tiles), so
+  // the next one takes the 1024-thread tile without staged bin lines
+  bool runs_seen = true;
+  uint32_t last_run_tiles = 0;
   // the segment counters (miss_count .. reprobe_count) are known to be zero on
   // the device: the next segment needs no reset (vignat steady state)
   bool ctl_clean = false;

@@ -707,7 +707,7 @@ __device__ __forceinline__ uint32_t dense128_tail(const uint4 d[8]) {
 // W: waves per block (4: 256-thread blocks, four per CU; 16: one 1024-thread
 // block per CU, nat_classify64w).
 template <uint32_t G, uint32_t H = 1, bool D = false, bool X = false, bool PR = G == 0,
-          uint32_t W = 4>
+          uint32_t W = 4, bool ST = false>
 __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins bins,
                                           TileQueue rq) {
   static_assert(!X || G == 0, "header slots (X) are 64-byte slots");
@@ -715,14 +715,16 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   __shared__ uint4 stage[W][256];
   __shared__ uint32_t cur[kCurs];
   __shared__ uint32_t mbase;
-  // (1024-thread blocks: whole-line bin entries, bins_put_staged)
-  constexpr bool kStaged = W == 16;
+  // (ST, 1024-thread blocks: whole-line bin entries, bins_put_staged)
+  constexpr bool kStaged = ST && W == 16;
+  __shared__ uint32_t nruns;  // this block's run tiles (Ctl::run_tiles)
   __shared__ uint32_t sring[kStaged ? kStageBins * kStageLines * 16 : 1];
   __shared__ uint32_t swc[kStaged ? kStageBins * kStageLines : 1];
   __shared__ uint32_t sgen[kStaged ? kStageBins * kStageLines : 1];
   const BinStage bst{sring, swc, sgen};
   const bool staged = kStaged && bins.ent && bins.bbits <= 7 && a.bstage;
   if (kStaged) bins_stage_init(bst);
+  if (threadIdx.x == 0) nruns = 0;
   for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
   a.own.cur = cur + kCurDest;
   load_nat_tables(T, a);  // (its barrier also covers cur)
@@ -1147,9 +1149,9 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       }
     }
     if (staged)
-      bins_put_staged(bins, bst, cur, rb, per_b * 64, range0, p, touch);
+      bins_put_staged(bins, bst, cur, rb, per_b * 64, range0, p, touch, &nruns);
     else
-      bins_put(bins, cur, rb, per_b * 64, range0, p, touch);
+      bins_put(bins, cur, rb, per_b * 64, range0, p, touch, &nruns);
     if (store_all) {
 #pragma unroll
       for (uint32_t k = 0; k < 4; k++)
@@ -1163,6 +1165,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   }
   __syncthreads();
   if (staged) bins_flush_staged(bins, bst, cur, rb);
+  if (threadIdx.x == 0 && nruns) atomicAdd(&a.t.ctl->run_tiles, nruns);
   bins_publish(bins, cur, rb);
   if (rq.ent && threadIdx.x == 0) {
     const uint32_t c = cur[kCurReprobe];
@@ -1185,10 +1188,17 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
                                                         TouchBins bins, TileQueue rq) {
   nat_tiles<0>(a, n_all, bins, rq);
 }
-// One 1024-thread block per CU (the default, nat_block_waves)
+// One 1024-thread block per CU (the default, nat_block_waves); the ws
+// variant stages its bin entries in LDS (traffic without runs: the host
+// picks it when the last segment's tiles were mostly not runs, since its
+// extra registers cost round robin 2.5 %)
 __global__ __launch_bounds__(1024, 1) void nat_classify64w(NatArgs a, uint32_t n_all,
                                                           TouchBins bins, TileQueue rq) {
   nat_tiles<0, 1, false, false, true, 16>(a, n_all, bins, rq);
+}
+__global__ __launch_bounds__(1024, 1) void nat_classify64ws(NatArgs a, uint32_t n_all,
+                                                           TouchBins bins, TileQueue rq) {
+  nat_tiles<0, 1, false, false, true, 16, true>(a, n_all, bins, rq);
 }
 // (diagnostics, VIGPATH_PRIO=0: the lean tile without the raised priority)
 __global__ __launch_bounds__(256, 4) void nat_classify64_p0(NatArgs a, uint32_t n_all,
@@ -1238,12 +1248,14 @@ static uint32_t nat_block_waves() {
   return w;
 }
 
-static NatTileKernel nat_tile_kernel(uint32_t slot, bool hdr_tail = false) {
+static NatTileKernel nat_tile_kernel(uint32_t slot, bool hdr_tail = false,
+                                     bool staged = false) {
   static const bool p0 = [] {
     const char *e = getenv("VIGPATH_PRIO");
     return e && atoi(e) == 0;
   }();
-  if (slot == 64 && !hdr_tail && nat_block_waves() == 16) return nat_classify64w;
+  if (slot == 64 && !hdr_tail && nat_block_waves() == 16)
+    return staged ? nat_classify64ws : nat_classify64w;
   if (slot == 64) return hdr_tail ? nat_classify64x : p0 ? nat_classify64_p0 : nat_classify64;
   if (slot == 128) return nat_classify128;
   const uint32_t nch = (slot - 64) / 16;
@@ -2747,8 +2759,9 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // classify launch also bins its touches (TouchBins) and queues reprobes
   // per block (TileQueue)
   const bool tiles64 = owner ? ph.tiles64 : p1 > p0 && c->coalesced_io;
-  const NatTileKernel tk = nat_tile_kernel(b->slot, a.tail != nullptr);
-  const uint32_t tw = tk == nat_classify64w ? 16u : 4u;  // waves per block
+  // (staged bin lines unless the last segment's tiles were mostly runs)
+  const NatTileKernel tk = nat_tile_kernel(b->slot, a.tail != nullptr, !t.runs_seen);
+  const uint32_t tw = tk == nat_classify64w || tk == nat_classify64ws ? 16u : 4u;
   BinsPlan bp = ph.bp;
   uint32_t grid64 = ph.grid1, range64 = ph.range1;
   TileQueue rq{};
@@ -2791,6 +2804,11 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // toucher still wins).
   hostprof(2);
   VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, seq0));
+  if (tiles64 && bp.on) {  // (the run tiles of this launch: the next one's kernel)
+    const uint32_t nrun = t.h_ctl.run_tiles - t.last_run_tiles;
+    t.last_run_tiles = t.h_ctl.run_tiles;
+    t.runs_seen = 2ull * nrun >= (uint64_t)(p1 - p0) / 64;
+  }
   hostprof(4);
   VP_HIP(ev_ms(c->ktime, c->ev0, c->ev1, &ph.ms));
   hostprof(5);
