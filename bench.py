@@ -59,7 +59,7 @@ METRIC = "Mpackets/s device-resident, 64B vignat @1M flows; %HBM roofline"
 ALG_BYTES = 92          # 64 frame + 4 len/port + 16 key + 4 tag + 4 value
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SLOT = 64
-TRAFFIC_PROFILE = "r05zc_bench_traffic.json"  # rocprofv3 --pmc passes (tools/gpu_session.sh pmc)
+TRAFFIC_PROFILE = "r05zl_bench_traffic.json"  # rocprofv3 --pmc passes (tools/gpu_session.sh pmc)
 DEV_MACS = [T.mac("02:00:00:00:00:00"), T.mac("02:00:00:00:00:01")]
 NAT_ARGS = ["--expire", "60000000", "--starting-port", "0", "--wan", "1",
             "--extip", "192.168.4.2", "--eth-dest", "0,90:e2:ba:55:12:20",
