@@ -1237,9 +1237,10 @@ typedef void (*NatTileKernel)(NatArgs, uint32_t, TouchBins, TileQueue);
 // Waves per block of the 64-byte classify: 16 (one 1024-thread block per
 // CU, nat_classify64w) unless VIGPATH_BLOCK_WAVES=4 (four 256-thread blocks,
 // nat_classify64, for A/B). A block's range is then four times longer, so
-// the chip keeps a quarter of the partly written bin-slice lines (uniform
-// order 0.805 -> 0.725 ms per step, round robin unchanged with eight run
-// words per block and bin: DESIGN.md §5.1).
+// the chip keeps a quarter of the partly written bin-slice lines, and its
+// LDS has room to stage whole bin lines (nat_classify64ws): uniform order
+// 0.800 -> 0.678 ms per step, round robin 0.464-0.469 -> 0.461 with eight
+// run words per block and bin.
 static uint32_t nat_block_waves() {
   static const uint32_t w = [] {
     const char *e = getenv("VIGPATH_BLOCK_WAVES");
