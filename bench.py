@@ -926,9 +926,7 @@ def main():
     else:
         workload = "vignat %dB frames in %dB slots, %d flows, %s order, 1xMI355X" % (
             flen, slot, args.flows, args.order)
-    owner_pass = (world > 1 and mode == "owner") or args.route_all  # (pass 1: 256-thread)
-    kname = ((NAT64 if not owner_pass else "nat_classify64") if slot == SLOT
-             else "nat_classify_wide")
+    kname = NAT64 if slot == SLOT else "nat_classify_wide"
     if args.route_all:
         workload = ("vignat %dB, %d flows, 1xMI355X, owner-mode pipeline with every key "
                     "routed through a one-rank RCCL exchange (profiling)" % (flen, args.flows))

@@ -2251,7 +2251,11 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
   if (ph->tiles64) {
     first = p0 & ~63u;
     const uint32_t tiles = (p1 - first + 63) / 64;
-    ph->grid1 = resident_grid((const void *)nat_classify64, (tiles + 3) / 4);
+    // pass 1: the 1024-thread tile unless VIGPATH_BLOCK_WAVES=4 (one block
+    // per CU: four times fewer, longer key slices)
+    const uint32_t tw = nat_block_waves();
+    ph->grid1 = tw == 16 ? resident_grid((const void *)nat_classify64w, (tiles + 15) / 16, 1024)
+                         : resident_grid((const void *)nat_classify64, (tiles + 3) / 4);
     ph->range1 = (tiles + ph->grid1 - 1) / ph->grid1 * 64;
     VP_TRY(tbl_bins_plan(c, t, (const void *)nat_remote64, p0, p1, &ph->bp));
   } else {
@@ -2301,8 +2305,11 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
       a1.tileq = 1;
       a1.mq = w.missq;
       if (ph->bp.on) a1.log = nullptr;  // pass 2 bins every touch
-      nat_classify64<<<ph->grid1, 256, 0, c->stream>>>(
-          a1, b->n, TouchBins{}, TileQueue{w.reprobe, w.reprobe_cnt, &t.ctl->reprobe_count});
+      const TileQueue rq1{w.reprobe, w.reprobe_cnt, &t.ctl->reprobe_count};
+      if (nat_block_waves() == 16)
+        nat_classify64w<<<ph->grid1, 1024, 0, c->stream>>>(a1, b->n, TouchBins{}, rq1);
+      else
+        nat_classify64<<<ph->grid1, 256, 0, c->stream>>>(a1, b->n, TouchBins{}, rq1);
     } else {
       nat_classify<<<ph->grid1, 256, 0, c->stream>>>(a);
     }
