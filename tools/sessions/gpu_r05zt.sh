@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5 session zt: owner-mode pass 1 on the 1024-thread tile -- owner
+# round 5 session zt: owner-mode pass 1 (and, rerun as zt2, pass 2) on the 1024-thread tile -- owner
 # tests, then --route-all with its stages, 1024- vs 256-thread, twice
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out; mkdir -p $O
