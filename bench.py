@@ -209,6 +209,59 @@ def cpu_baseline(n_flows: int, sample: int):
     return float(np.median(rates)), rates, per * CPU_SAMPLES, core, warm
 
 
+CONFIG1_FLOWS, CONFIG1_MAX_FLOWS, CONFIG1_PACKETS = 1000, 65536, 10_000_000
+
+
+def cpu_config1():
+    """BASELINE configs[0]: vignat over the 64 B
+    trace of 1,000 flows round robin, --max-flows 65536, 10M packets, on one
+    pinned core -- the oracle restatement of nf.c's loop (nf.c:150-176), as
+    cpu_baseline. The flows are allocated by an untimed first pass; then
+    CPU_SAMPLES + 1 samples of CONFIG1_PACKETS / CPU_SAMPLES packets (the
+    first discarded as a warm-up). A sample's frames are the same 2,000
+    rounds over the flows each time (a fresh copy: the loop rewrites them),
+    its times continue the trace's. Returns the line's dict."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import orc
+
+    cfg = orc.nat_cfg(wan=1, ext_ip=T.ip4(192, 168, 4, 2),
+                      expire_us=60_000_000, max_flows=CONFIG1_MAX_FLOWS,
+                      device_macs=DEV_MACS,
+                      endpoint_macs=[T.mac("90:e2:ba:55:12:20"),
+                                     T.mac("90:e2:ba:55:12:21")])
+    o = orc.Oracle("nat", cfg, ref="native")
+    N = CONFIG1_FLOWS
+    per = CONFIG1_PACKETS // CPU_SAMPLES // N * N
+    fr0, ln0, dv0, now0 = T.nat_lan_trace(N, N)
+    frs, ln, dv, nows = T.nat_lan_trace(per, N, start=N)
+    mask = os.sched_getaffinity(0)
+    core = min(mask)
+    os.sched_setaffinity(0, {core})
+    rates = []
+    try:
+        o.run(fr0, ln0, dv0, now0, SLOT)
+        for k in range(CPU_SAMPLES + 1):
+            fr = frs.copy()
+            now = nows + k * per
+            t0 = time.perf_counter()
+            out = o.run(fr, ln, dv, now, SLOT)
+            rates.append(per / (time.perf_counter() - t0) / 1e6)
+            assert (out == 1).all()
+    finally:
+        os.sched_setaffinity(0, mask)
+    warm, rates = rates[0], rates[1:]
+    med = float(np.median(rates))
+    return {"value": round(med, 3), "unit": "Mpps", "cores": 1, "kind": "port",
+            "samples": [round(r, 3) for r in rates], "warmup_sample": round(warm, 3),
+            "spread": round((max(rates) - min(rates)) / med, 4),
+            "workload": "vignat 64B synthetic trace, %d flows round robin, --max-flows %d, "
+                        "CPU nf.c loop (BASELINE configs[0])" % (N, CONFIG1_MAX_FLOWS),
+            "sample": "median of %d samples of %d packets after one discarded warm-up "
+                      "sample (%d packets timed in all); oracle restatement -O3 "
+                      "-march=native, 1 thread pinned to cpu %d (%s)"
+                      % (len(rates), per, per * len(rates), core, cpu_model())}
+
+
 def golden_batch_digest(flows: int, batch: int):
     """The reference's digest of one steady-state batch of this exact shape
     (tests/golden/nat_bench_shape.npz, made by tests/golden/make_golden.py
@@ -219,6 +272,8 @@ def golden_batch_digest(flows: int, batch: int):
     with np.load(path, allow_pickle=False) as z:
         return int(z["batch_digest"][-1])
 
+
+OWN_CHUNK = 1 << 21  # packets per rank and chunk of the chunked owner pipeline (N > 1)
 
 E2E_BATCH = 1 << 24
 E2E_CHUNK = 1 << 21
@@ -378,7 +433,8 @@ NAT64 = "nat_classify64" if os.environ.get("VIGPATH_BLOCK_WAVES") == "4" else "n
 
 
 def steady_workload(nf, batch_of, warm: int, steps: int, B: int, dev, golden=None,
-                    kernel="", times=None, state=None, repeats=False, alg_bytes=ALG_BYTES):
+                    kernel="", times=None, state=None, repeats=False, alg_bytes=ALG_BYTES,
+                    basis=None):
     """Batches 0 .. warm-1 untimed (allocation), then `steps` timed calls
     (batches warm ..) without timing events, each from its own buffer filled
     before the timed region; the last timed batch's digest against golden[k]
@@ -389,6 +445,8 @@ def steady_workload(nf, batch_of, warm: int, steps: int, B: int, dev, golden=Non
     times, same outputs), so the last golden digest stands for them all.
     Returns the line's dict."""
     out = torch.zeros(B, dtype=torch.int16, device=dev)
+
+    knames = {}
 
     def run(k0, n, events):
         nf.kernel_timing(events)
@@ -404,6 +462,8 @@ def steady_workload(nf, batch_of, warm: int, steps: int, B: int, dev, golden=Non
             nf.process_device(b, ln, ind, out, SLOT, now0=n0, now_step=st)
             if events:
                 kms.append(nf.last_kernel_ms())
+                kn = nf.last_kernel()
+                knames[kn] = knames.get(kn, 0) + 1
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         nf.kernel_timing(False)
@@ -435,13 +495,15 @@ def steady_workload(nf, batch_of, warm: int, steps: int, B: int, dev, golden=Non
     line = {"value": round(mpps, 1), "unit": "Mpps", "ms_per_step": round(el / steps * 1e3, 4),
             "batch_packets": B, "steps": steps, "warm_batches": warm,
             "warm_s": round(warm_s, 2),
-            "kernel": kernel, "kernel_ms_per_launch": round(per_launch_s * 1e3, 4),
+            "kernel": kernel_label(knames, kernel),
+            "kernel_ms_per_launch": round(per_launch_s * 1e3, 4),
             "kernel_mpps": round(pkts / per_launch_s / 1e6, 1),
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "frac_step": round(mpps * 1e6 * alg_bytes / 1e9 / HBM_PEAK_GBS, 4),
-            "frac_basis": "%d B per packet (SURVEY.md §8(d) vignat basis%s), 8 TB/s"
+            "frac_basis": basis or "%d B per packet (SURVEY.md §8(d) vignat basis%s), 8 TB/s"
                           % (alg_bytes, "" if alg_bytes == ALG_BYTES
                              else ", no per-packet port: one per burst"),
+            "alg_bytes_per_packet": alg_bytes,
             "parity": parity}
     if times is not None:
         line.update(times)
@@ -453,6 +515,12 @@ def host_batch(dev, frames, lens, in_dev):
     return (torch.from_numpy(frames).to(dev),
             torch.from_numpy(lens.astype(np.uint16).view(np.int16)).to(dev),
             torch.from_numpy(in_dev.astype(np.uint16).view(np.int16)).to(dev))
+
+
+# vigbridge per packet (bridge_main.c:39-62,272-290): the two MACs (one
+# 16-byte chunk of the slot), the port, and two map lookups (src learn, dst
+# forward) of key + tag + value each
+BRIDGE_ALG_BYTES = 16 + 2 + 2 * (8 + 4 + 4)
 
 
 def bench_bridge_c3(dev, B, steps, golden):
@@ -471,7 +539,12 @@ def bench_bridge_c3(dev, B, steps, golden):
         buf.copy_(src)
         return lens, ind, T.NOW0 + k * B, 1
     r = steady_workload(br, batch_of, 1, steps, B, dev, golden, "bridge_classify",
-                        repeats=True)
+                        repeats=True, alg_bytes=BRIDGE_ALG_BYTES,
+                        basis="%d B per packet, vigbridge's own reads: 16 B (the frame's "
+                              "first chunk: both MACs) + 2 B port + 2 lookups x (8 B MAC key "
+                              "+ 4 B tag + 4 B value); it writes no frame (2 B out port), "
+                              "so its ceiling is the read-only shape (shape_read_ms); 8 TB/s"
+                              % BRIDGE_ALG_BYTES)
     br.close()
     r["workload"] = "vigbridge 64B, 1M MACs, learn + lookup (BASELINE configs[2])"
     return r
@@ -564,7 +637,8 @@ def bench_nat_churn(dev, B, steps, golden, state=None):
     return r
 
 
-def per_packet_drop_in(packets: int = 20000, flows: int = 1024, batches=(0, 32, 1024)):
+def per_packet_drop_in(packets: int = 20000, flows: int = 1024, batches=(0, 32, 1024),
+                       mark=lambda name: None):
     """north_star's "drops into nf.c's main loop unchanged", timed: host/nf_loop
     (nf.c:143-216 restated over a trace file, linked against
     libvignat_nf.so) with every packet through nf_process one at a time
@@ -587,6 +661,7 @@ def per_packet_drop_in(packets: int = 20000, flows: int = 1024, batches=(0, 32, 
             f.write(dv.astype(np.uint16).tobytes() + ln.astype(np.uint16).tobytes())
             f.write(now.astype(np.int64).tobytes() + fr.tobytes())
         for bt in batches:
+            mark("per-packet drop-in: batch %d" % bt)
             cmd = [exe, tin, tout, "--warm", str(flows)] + (["--batch", str(bt)] if bt else [])
             r = subprocess.run(cmd + ["--"] + NAT_ARGS + ["--max-flows", str(flows)],
                                capture_output=True, text=True, timeout=300)
@@ -631,12 +706,15 @@ def cpu_model() -> str:
 
 
 def timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank, first, steps,
-                order="rr", host_comm=False, stages=None, wd=None, label="timed"):
+                order="rr", host_comm=False, stages=None, wd=None, label="timed",
+                knames=None):
     """Fill one buffer per step (batches first .. first + steps - 1 of this
     rank's slices, `order`), then time exactly `steps` prepared
     vp_process_device calls between barriers + synchronisations. Returns
     (elapsed s, max over ranks; [(kernel ms, launches)] per step; buffers).
-    wd: the N > 1 watchdog (vigor_amd.watchdog), one marker per step."""
+    wd: the N > 1 watchdog (vigor_amd.watchdog), one marker per step.
+    knames: a dict counting the tile kernel each step launched last
+    (vp_last_kernel)."""
     mark = wd.stage if wd is not None else (lambda name: None)
     def gstart(k):  # global position of this rank's slice of global batch k
         return (k * world + rank) * B
@@ -657,6 +735,9 @@ def timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank, first, 
         mark("%s: step %d/%d" % (label, k + 1, steps))
         calls[k](T.NOW0 + gstart(first + k), 1)
         kms.append(nat.last_kernel_ms())
+        if knames is not None:
+            kn = nat.last_kernel()
+            knames[kn] = knames.get(kn, 0) + 1
         if stages is not None:  # owner mode's phase-A stages (timing pass)
             for name, ms in nat.last_stage_ms().items():
                 stages[name] = stages.get(name, 0.0) + ms / steps
@@ -674,33 +755,52 @@ def timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank, first, 
     return elapsed, kms, bufs
 
 
-def shape_ceiling(L, B, slot, dev, reps=10):
-    """vp_probe_slots over a scratch batch of B slots: (read+write ms, read
-    ms) per pass, each the mean of `reps` launches timed like the classify
-    kernel (its dispatch's own timestamps)."""
+def shape_ceiling(L, B, slot, dev, reps=10, waves=4):
+    """vp_probe_slots_w over a scratch batch of B slots with the tile
+    kernel's block shape (`waves` per block): (read+write ms, read ms) per
+    pass, each the mean of `reps` launches timed like the classify kernel
+    (its dispatch's own timestamps)."""
     import ctypes
     buf = torch.zeros(B * slot, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     out = []
     for store in (1, 0):
         ms = ctypes.c_float()
-        vigor_amd._check(L.vp_probe_slots(ctypes.c_void_p(buf.data_ptr()), B, slot, store, reps,
-                                          ctypes.byref(ms)), "vp_probe_slots", L)
+        vigor_amd._check(L.vp_probe_slots_w(ctypes.c_void_p(buf.data_ptr()), B, slot, store,
+                                            waves, reps, ctypes.byref(ms)), "vp_probe_slots_w", L)
         out.append(float(ms.value))
+    out.append(waves)
     del buf
     torch.cuda.empty_cache()
     return out
 
 
 def ceiling_fields(ceiling, kernel_s, step_s):
-    rw, rd = ceiling
+    rw, rd, waves = ceiling
     return {"shape_ceiling_ms": round(rw, 4), "shape_read_ms": round(rd, 4),
             "kernel_over_ceiling": round(kernel_s * 1e3 / rw, 4),
             "step_over_ceiling": round(step_s * 1e3 / rw, 4),
-            "shape_ceiling_source": "vp_probe_slots on this box: nat_classify64's grid and "
-                                    "1 KiB access shape, every slot read and written back "
-                                    "whole (write-through), no other work; shape_read_ms "
-                                    "the same without the stores"}
+            "shape_ceiling_source": "vp_probe_slots_w on this box: the tile kernel's "
+                                    "persistent grid (%d-thread blocks, %d per CU) and 1 KiB "
+                                    "access shape, every slot read and written back whole "
+                                    "(write-through), no other work; shape_read_ms the same "
+                                    "without the stores" % (64 * waves, 16 // waves)}
+
+
+def kernel_label(knames, default):
+    """The tile kernel(s) a pass ran: one name, or "a x3 + b x17" when the
+    per-segment choice changed within the pass."""
+    knames = {k: v for k, v in (knames or {}).items() if k}
+    if not knames:
+        return default
+    if len(knames) == 1:
+        return next(iter(knames))
+    return " + ".join("%s x%d" % kv for kv in sorted(knames.items(), key=lambda kv: -kv[1]))
+
+
+def probe_waves(kernel: str) -> int:
+    """Waves per block of the tile kernel's grid (vp_probe_slots_w)."""
+    return 16 if kernel.startswith("nat_classify64w") or kernel.endswith("64w") else 4
 
 
 def kernel_rate(kms, B, steps, alg_bytes):
@@ -884,9 +984,10 @@ def main():
     nat.kernel_timing(True)
     owner_run = (world > 1 and mode == "owner") or args.route_all
     stages = {} if owner_run else None
+    knames = {}
     el_k, kms, bufs = timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank,
                                   args.warmup + args.steps, args.steps, args.order, host_comm,
-                                  stages, wd=wd, label="kernel timing")
+                                  stages, wd=wd, label="kernel timing", knames=knames)
     del bufs
     stages_max = None
     if stages and world > 1:  # the slowest rank per stage
@@ -900,10 +1001,12 @@ def main():
     # the classify tile's memory-shape ceiling on this box (vp_probe_slots:
     # the same grid and 1 KiB access shape, every slot read and written back
     # whole, nothing else), beside the kernel it bounds
+    kname = kernel_label(knames, NAT64 if slot == SLOT else "nat_classify_wide")
     ceiling = None
     if world == 1 and slot in (64, 128) and not args.route_all:
         mark("shape ceiling probe")
-        ceiling = shape_ceiling(nat.L, B, slot, dev)
+        ceiling = shape_ceiling(nat.L, B, slot, dev, waves=probe_waves(kname) if slot == SLOT
+                                else 4)
     traffic = None  # PMC bytes of the same kernel (profiles/, per launch)
     tpath = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE)
     if (os.path.exists(tpath) and B == 1 << 24 and args.flows == 1 << 20
@@ -926,7 +1029,6 @@ def main():
     else:
         workload = "vignat %dB frames in %dB slots, %d flows, %s order, 1xMI355X" % (
             flen, slot, args.flows, args.order)
-    kname = NAT64 if slot == SLOT else "nat_classify_wide"
     if args.route_all:
         workload = ("vignat %dB, %d flows, 1xMI355X, owner-mode pipeline with every key "
                     "routed through a one-rank RCCL exchange (profiling)" % (flen, args.flows))
@@ -935,12 +1037,15 @@ def main():
     extra = {}
     if not args.no_extra and world == 1 and args.order == "rr":
         # SURVEY.md §8(d) secondary order on the same warm table
+        mark("secondary order")
+        kn2 = {}
         el2, kms2, bufs2 = timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world,
                                        rank, args.warmup + 2 * args.steps, args.steps,
-                                       "uniform", host_comm)
+                                       "uniform", host_comm, knames=kn2)
         del bufs2
         pl2, pk2, ach2 = kernel_rate(kms2, B, args.steps, alg_bytes)
         extra["secondary_order"] = {
+            "kernel": kernel_label(kn2, NAT64),
             "kernel_over_ceiling": round(pl2 * 1e3 / ceiling[0], 4) if ceiling else None,
             "order": "uniform (flow = splitmix64(0x5EED, p) mod N)",
             "value": round(B * args.steps / el2 / 1e6, 2), "unit": "Mpps",
@@ -952,6 +1057,7 @@ def main():
     nat.kernel_timing(False)
     e2e = None
     if world == 1 and not args.no_e2e and slot == SLOT and args.order == "rr":
+        mark("end to end")
         e2e = {"value": round(end_to_end(nat, bank, dev, (args.warmup + 3 * args.steps) * B), 1),
                "unit": "Mpps",
                "path": "page-locked host frames and per-packet arrays -> "
@@ -962,10 +1068,13 @@ def main():
                "batch_packets": E2E_BATCH,
                "pcie_bytes_per_packet": SLOT + 4 + SLOT + 2}
         base = (args.warmup + 3 * args.steps) * B + 4 * E2E_BATCH
+        mark("end to end (mbufs)")
         extra["end_to_end_mbuf"] = end_to_end_mbuf(nat, bank, dev, base)
+        mark("end to end (mbufs, IMIX)")
         extra["end_to_end_mbuf_imix"] = end_to_end_mbuf(nat, bank, dev,
                                                         base + 4 * MBUF_BATCH, imix=True)
-        pp = per_packet_drop_in()
+        mark("per-packet drop-in")
+        pp = per_packet_drop_in(mark=mark)
         pp.update({"path": "host/nf_loop (nf.c's loop) over libvignat_nf.so: nf_process "
                            "per packet (vp_process_one: vignat's persistent kernel polling a "
                            "host-coherent mailbox), and the batched loop (vp_process_batch) "
@@ -974,20 +1083,66 @@ def main():
         extra["per_packet_drop_in"] = pp
     if (world == 1 and not args.no_extra and slot == SLOT and args.order == "rr"
             and not args.route_all and args.flows == 1 << 20):
+        L0 = nat.L
         nat.close()
         bank = None
         torch.cuda.empty_cache()
         gold = golden_configs()
         steps_x = min(args.steps, EXTRA_STEPS)
+        mark("config 3 (vigbridge)")
         extra["config3_bridge"] = bench_bridge_c3(dev, B, steps_x, gold.get("bridge"))
+        mark("config 4 (viglb)")
         extra["config4_lb"] = bench_lb_c4(dev, B, steps_x, gold.get("lb"))
+        mark("random keys")
         extra["nat_random_keys"] = bench_nat_random(dev, B, steps_x, gold.get("random"))
+        mark("churn")
         extra["nat_churn"] = bench_nat_churn(dev, B, steps_x, gold.get("churn"),
                                              gold.get("churn_state"))
-        if ceiling:  # (the same 64-byte read+write shape bounds every classify kernel)
+        if ceiling:  # the 64-byte read(+write) shape at each kernel's own block shape
+            probes = {ceiling[2]: ceiling}
             for k in ("config3_bridge", "config4_lb", "nat_random_keys", "nat_churn"):
-                extra[k]["kernel_over_ceiling"] = round(
-                    extra[k]["kernel_ms_per_launch"] / ceiling[0], 4)
+                w = probe_waves(extra[k]["kernel"])
+                if w not in probes:
+                    mark("shape ceiling probe (%d waves)" % w)
+                    probes[w] = shape_ceiling(L0, B, SLOT, dev, waves=w)
+                rw, rd, _ = probes[w]
+                if k == "config3_bridge":  # (writes no frame: the read-only shape)
+                    extra[k]["shape_read_ms"] = round(rd, 4)
+                    extra[k]["kernel_over_read_ceiling"] = round(
+                        extra[k]["kernel_ms_per_launch"] / rd, 4)
+                else:
+                    extra[k]["shape_ceiling_ms"] = round(rw, 4)
+                    extra[k]["kernel_over_ceiling"] = round(
+                        extra[k]["kernel_ms_per_launch"] / rw, 4)
+    if owner_run and world > 1 and not args.no_extra:
+        # the chunked owner pipeline (VIGPATH_OWN_CHUNK, read per call; the
+        # same on every rank), same context and workload, the next batches:
+        # one pass for the rate, one with events for its stages
+        os.environ["VIGPATH_OWN_CHUNK"] = str(OWN_CHUNK)
+        try:
+            nat.kernel_timing(False)
+            el4, _, b4 = timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank,
+                                     args.warmup + 2 * args.steps, args.steps, args.order,
+                                     host_comm, wd=wd, label="owner chunked")
+            del b4
+            nat.kernel_timing(True)
+            st4 = {}
+            _, _, b4 = timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank,
+                                   args.warmup + 3 * args.steps, args.steps, args.order,
+                                   host_comm, st4, wd=wd, label="owner chunked, stages")
+            del b4
+            nat.kernel_timing(False)
+        finally:
+            os.environ.pop("VIGPATH_OWN_CHUNK", None)
+        extra["owner_chunked"] = {
+            "mode": "owner", "chunk_packets": OWN_CHUNK,
+            "value": round(B * args.steps * world / el4 / 1e6, 2), "unit": "Mpps",
+            "ms_per_step": round(el4 / args.steps * 1e3, 4),
+            "stages_ms_rank0": {k: round(v, 4) for k, v in st4.items()},
+            "note": "the owner pipeline in chunks of %d packets per rank (exchange of "
+                    "one chunk beside the next chunk's pass 1 and the last one's probe "
+                    "and pass 2); the headline value stays the unchunked owner "
+                    "pipeline" % OWN_CHUNK}
     if world > 1 and not args.no_extra:
         # the other dictionary placement, same workload
         other = "replicated" if mode == "owner" else "owner"
@@ -1003,6 +1158,10 @@ def main():
         extra["other_shard_mode"] = {
             "mode": other, "value": round(B * args.steps * world / el3 / 1e6, 2),
             "unit": "Mpps", "ms_per_step": round(el3 / args.steps * 1e3, 4)}
+        extra["shard_modes"] = {  # every candidate of the same run, side by side
+            mode: round(mpps, 2), other: extra["other_shard_mode"]["value"],
+            **({"owner_chunked": extra["owner_chunked"]["value"]}
+               if "owner_chunked" in extra else {})}
         nat_ref.clear()
         nat2.close()
     mark("report")
@@ -1072,6 +1231,9 @@ def main():
                           "pipeline's stages of every segment (vp_last_stage_ms), "
                           "mean per step on rank 0; that pass's step: %.4f ms"
                           % (el_k / args.steps * 1e3)}
+        if cpu is not None:
+            mark("cpu config 1")
+            line["cpu_config1"] = cpu_config1()
         line.update(extra)
         if wd is not None:
             line["stages_done"] = len(wd.done) + 1

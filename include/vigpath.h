@@ -150,7 +150,8 @@ typedef struct vp_dev_batch {
   /* in_dev == NULL: every packet arrived on port in_port (nf.c receives each
    * burst from one device, nf.c:150-153 / 186-190), and no per-packet port
    * array is read. vp_process_device only; the host entry points need
-   * in_dev. */
+   * in_dev. A port above 0xFFFF (nf_process's uint16_t device, nf.h:14) is
+   * VP_EINVAL. */
   uint32_t in_port;
 } vp_dev_batch;
 
@@ -362,6 +363,12 @@ int vp_kernel_timing(vp_ctx *ctx, int on);
  * vp_kernel_timing is off), and the number of launches. */
 int vp_last_kernel_ms(vp_ctx *ctx, float *ms, int *launches);
 
+/* The name of the tile kernel the last vp_process_device call launched for
+ * its 64-byte slots (vignat picks nat_classify64w or nat_classify64ws per
+ * segment; viglb lb_classify64[w]); "" when none was. The
+ * string is static. */
+const char *vp_last_kernel(vp_ctx *ctx);
+
 /* Owner-sharded multi-GPU contexts (VP_SHARD_OWNER) with kernel timing on:
  * the last vp_process_device call's phase-A stage times in ms, summed over
  * its segments, from HIP events between the stages: ms[0] pass 1 (classify,
@@ -369,8 +376,12 @@ int vp_last_kernel_ms(vp_ctx *ctx, float *ms, int *launches);
  * ms[2] keys all-to-all, ms[3] owner probe, ms[4] answers all-to-all,
  * ms[5] pass 2 (routed packets rewritten, touches binned), ms[6] fold;
  * the chunked pipeline records ms[7], its chunks' passes,
- * exchanges and probes together (they overlap), and ms[6] only. *stages = 7
- * or 8, or 0 when nothing was recorded. ms must hold 8 floats. */
+ * exchanges and probes together (they overlap), and ms[6] only.
+ * vp_stage_ms writes at most `cap` floats and sets *stages to the number of
+ * stages recorded (0..VP_STAGES, may exceed cap). vp_last_stage_ms is the
+ * 0.2 entry point: exactly 7 floats (ms[0..6]), *stages at most 7. */
+#define VP_STAGES 8
+int vp_stage_ms(vp_ctx *ctx, float *ms, int cap, int *stages);
 int vp_last_stage_ms(vp_ctx *ctx, float *ms, int *stages);
 
 /* Diagnostics (bench.py): the memory-shape ceiling of the classify tile --
@@ -378,8 +389,13 @@ int vp_last_stage_ms(vp_ctx *ctx, float *ms, int *stages);
  * multiple of 64) streamed with nat_classify64's grid and access shape, each
  * slot read and, store != 0, written back unchanged (write-through). *ms =
  * the mean duration of `reps` launches, each timed by its own dispatch's
- * timestamps. DESIGN.md §5.1. */
+ * timestamps. DESIGN.md §5.1. vp_probe_slots_w: the same with `waves` (4,
+ * 8 or 16) waves per block, one block of 64 x waves threads per 4 waves of
+ * a CU's capacity (16: nat_classify64w's one 1024-thread block per CU);
+ * vp_probe_slots is waves = 4. */
 int vp_probe_slots(void *frames, uint32_t n, uint32_t slot, int store, int reps, float *ms);
+int vp_probe_slots_w(void *frames, uint32_t n, uint32_t slot, int store, int waves, int reps,
+                     float *ms);
 
 /* Build identification (e.g. "vigpath gfx950"). */
 const char *vp_version(void);

@@ -196,6 +196,21 @@ def test_burst_port(slot):
     check_state(nat, o, 64)
 
 
+def test_burst_port_out_of_range():
+    """A burst's port is nf_process's uint16_t device (nf.h:14): a larger
+    vp_dev_batch.in_port is rejected before anything runs."""
+    import torch
+    nat, _ = make_pair(max_flows=64)
+    n = 64
+    d = torch.device("cuda:0")
+    f = torch.zeros(n * 64, dtype=torch.uint8, device=d)
+    ln = torch.full((n,), 60, dtype=torch.int16, device=d)
+    out = torch.zeros(n, dtype=torch.int16, device=d)
+    with pytest.raises(vigor_amd.VigpathError):
+        nat.process_device(f, ln, 0x10000, out, 64, now0=T.NOW0, now_step=1)
+    nat.process_device(f, ln, 0xFFFF, out, 64, now0=T.NOW0, now_step=1)  # (accepted)
+
+
 def test_process_one_long_frame_and_empty():
     """Frames the mailbox does not take (longer than its 2048 bytes) go
     through the batch path, a zero-length frame drops, and the kernel
@@ -237,6 +252,8 @@ def test_process_one_two_contexts():
         exp_out = o.run(exp, ln, dv, now, 64)
         pairs.append((nat, o))
         traces.append((fr, ln, dv, now, exp, exp_out))
+    import time
+    t0 = time.perf_counter()
     for i in range(n):
         for k in range(2):
             if k == 1 and i == n // 2:
@@ -248,6 +265,10 @@ def test_process_one_two_contexts():
             b = bytearray(fr[i * 64:i * 64 + int(ln[i])].tobytes())
             assert nat.process(int(dv[i]), b, int(now[i])) == exp_out[i], (k, i)
             assert bytes(b) == exp[i * 64:i * 64 + int(ln[i])].tobytes(), (k, i)
+    # no context waits out the other's idle exit (20 ms) at a switch: a
+    # server launch stops the other context's server first (serve_yield)
+    per = (time.perf_counter() - t0) / (n + n // 2)
+    assert per < 5e-3, "%.2f ms per packet" % (per * 1e3)
     check_state(pairs[1][0], pairs[1][1], 128)
 
 

@@ -43,7 +43,7 @@ for step in "$@"; do
     bench) run bench 600 python3 bench.py $BA > $O/${TAG}_bench.log 2>&1 || exit $? ;;
     trace) rm -rf $O/${TAG}_kt
            run trace 400 rocprofv3 --kernel-trace --stats --output-format csv \
-             -d $O/${TAG}_kt -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-e2e $BA \
+             -d $O/${TAG}_kt -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-e2e --no-extra $BA \
              > $O/${TAG}_kt.log 2>&1 || exit $? ;;
     pmc) rm -rf $O/${TAG}_fetch $O/${TAG}_write
          run pmc_fetch 180 rocprofv3 --pmc FETCH_SIZE --output-format csv \

@@ -126,7 +126,8 @@ EXPORTS = ["vp_nat_create", "vp_bridge_create", "vp_lb_create", "vp_fw_create",
            "vp_attach_comm", "vp_shard_mode", "vp_sync_state", "vp_live_count",
            "vp_kernel_timing", "vp_last_kernel_ms", "vp_version", "vp_table_stats_get",
            "vp_last_error", "vp_register_host", "vp_unregister_host", "vp_process_mbufs",
-           "vp_last_stage_ms", "vp_comm_abort", "vp_probe_slots", "vp_process_one"]
+           "vp_last_stage_ms", "vp_stage_ms", "vp_comm_abort", "vp_probe_slots",
+           "vp_probe_slots_w", "vp_process_one", "vp_last_kernel"]
 
 _libs = {}
 
@@ -205,6 +206,9 @@ def lib(path: str | None = None):
     L.vp_probe_slots.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int,
                                  C.POINTER(C.c_float)]
     L.vp_probe_slots.restype = C.c_int
+    L.vp_probe_slots_w.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int,
+                                   C.POINTER(C.c_float)]
+    L.vp_probe_slots_w.restype = C.c_int
     L.vp_live_count.argtypes = [C.c_void_p]
     L.vp_live_count.restype = C.c_int64
     L.vp_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float),
@@ -212,6 +216,10 @@ def lib(path: str | None = None):
     L.vp_last_kernel_ms.restype = C.c_int
     L.vp_last_stage_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int)]
     L.vp_last_stage_ms.restype = C.c_int
+    L.vp_stage_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]
+    L.vp_stage_ms.restype = C.c_int
+    L.vp_last_kernel.argtypes = [C.c_void_p]
+    L.vp_last_kernel.restype = C.c_char_p
     L.vp_kernel_timing.argtypes = [C.c_void_p, C.c_int]
     L.vp_kernel_timing.restype = C.c_int
     L.vp_table_stats_get.argtypes = [C.c_void_p, C.c_int, C.POINTER(TableStatsC)]

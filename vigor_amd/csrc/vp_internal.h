@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
 #include <tuple>
 #include <vector>
 
@@ -343,6 +344,9 @@ struct vp_ctx {
   // (results complete): run_batch returns without waiting for it.
   bool fold_pending = false;
   float last_ms = 0.f;
+  // the classification kernel the last vp_process_device call launched last
+  // (vp_last_kernel; "" before any)
+  const char *last_kernel = "";
   bool ktime = false;  // vp_kernel_timing: events around the classify launch
   // owner mode with ktime: the last call's phase-A stage times (ms, summed
   // over its segments; vp_last_stage_ms)
@@ -408,5 +412,9 @@ struct vp_ctx {
   bool srv_on = false;
   uint32_t srv_req = 0;
   uint64_t srv_idle = 0, srv_idle_ms = 1;
+  // held by the thread serving (nat_process_one, serve_stop); another
+  // context's server launch on the same GPU stops this one only if it can
+  // take it (serve_launch: resident kernels share the hardware queues)
+  std::recursive_mutex srv_mu;
   double srv_prof[10] = {};  // VIGPATH_SERVE_PROF: summed stage times (us), counts
 };

@@ -711,6 +711,7 @@ static int lb_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     const uint32_t grid = bp.on ? bp.grid : resident_grid(k, (tiles + lw - 1) / lw, 64 * (int)lw);
     LbArgs a64 = a;
     a64.binned = bp.on;
+    c->last_kernel = lw == 16 ? "lb_classify64w" : "lb_classify64";
     if (lw == 16)
       lb_classify64w<<<grid, 1024, 0, c->stream>>>(a64, b->n, bp.bins);
     else

@@ -1249,6 +1249,16 @@ static uint32_t nat_block_waves() {
   return w;
 }
 
+static const char *nat_tile_kernel_name(NatTileKernel k) {
+  return k == nat_classify64w    ? "nat_classify64w"
+         : k == nat_classify64ws ? "nat_classify64ws"
+         : k == nat_classify64   ? "nat_classify64"
+         : k == nat_classify64x  ? "nat_classify64x"
+         : k == nat_classify64_p0 ? "nat_classify64_p0"
+         : k == nat_classify128  ? "nat_classify128"
+                                 : "nat_classify_wide";
+}
+
 static NatTileKernel nat_tile_kernel(uint32_t slot, bool hdr_tail = false,
                                      bool staged = false) {
   static const bool p0 = [] {
@@ -2791,6 +2801,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     if (tiles64) {
       NatArgs a64 = a;
       if (bp.on) a64.log = nullptr;  // touches go to the bins only
+      c->last_kernel = nat_tile_kernel_name(tk);
       if (c->ktime) {
         VP_HIP(launch_timed(tk, grid64, 64 * tw, c->stream, c->ev0, c->ev1, a64,
                             (uint32_t)b->n, bp.bins, rq));
@@ -2935,8 +2946,9 @@ static const bool g_srv_prof = [] {
   const char *e = getenv("VIGPATH_SERVE_PROF");
   return e && atoi(e);
 }();
-int serve_stop(vp_ctx *c) {
-  if (!c || !c->srv_on) return 0;
+// The server of c leaves (a leave request, then the stream drains); the
+// caller holds c->srv_mu. Does not touch g_srv.
+static hipError_t serve_halt(vp_ctx *c) {
   ServeBox *bx = c->sbox;
   const uint32_t req = ++c->srv_req;
   __atomic_store_n(&bx->bell, (uint64_t)req | ((uint64_t)kServeLeave << 32), __ATOMIC_RELEASE);
@@ -2944,10 +2956,6 @@ int serve_stop(vp_ctx *c) {
   // (the kernel is gone: the leave request counts as answered for the next one)
   __atomic_store_n(&bx->ans, (uint64_t)req, __ATOMIC_RELEASE);
   c->srv_on = false;
-  {
-    std::lock_guard<std::mutex> g(g_srv_mu);
-    g_srv.erase(std::remove(g_srv.begin(), g_srv.end(), c), g_srv.end());
-  }
   if (g_srv_prof && c->srv_prof[5] > 0) {
     const double n = c->srv_prof[5];
     fprintf(stderr,
@@ -2960,6 +2968,18 @@ int serve_stop(vp_ctx *c) {
             c->srv_prof[8] / std::max(1.0, c->srv_prof[9]), c->srv_prof[4] / n);
     for (double &x : c->srv_prof) x = 0;
   }
+  return e;
+}
+
+int serve_stop(vp_ctx *c) {
+  if (!c) return 0;
+  std::lock_guard<std::recursive_mutex> sg(c->srv_mu);
+  if (!c->srv_on) return 0;
+  const hipError_t e = serve_halt(c);
+  {
+    std::lock_guard<std::mutex> g(g_srv_mu);
+    g_srv.erase(std::remove(g_srv.begin(), g_srv.end(), c), g_srv.end());
+  }
   VP_HIP(e);
   return 0;
 }
@@ -2970,7 +2990,28 @@ void serve_free(vp_ctx *c) {
   c->sbox = nullptr;
 }
 
+// Another context's resident server on this GPU may share a hardware queue
+// with c->stream (GPU_MAX_HW_QUEUES streams' worth): c's server would then
+// wait behind it until its idle exit. Stop those first (contexts served by
+// another thread right now keep theirs: try_lock).
+static void serve_yield(vp_ctx *c) {
+  // (under g_srv_mu throughout: a listed context is not destroyed meanwhile,
+  // as vp_destroy's serve_stop unlists it under the same lock first)
+  std::lock_guard<std::mutex> g(g_srv_mu);
+  for (size_t i = 0; i < g_srv.size();) {
+    vp_ctx *x = g_srv[i];
+    if (x == c || x->gpu != c->gpu || !x->srv_mu.try_lock()) {
+      i++;
+      continue;
+    }
+    if (x->srv_on) serve_halt(x);  // (an error shows at x's next call)
+    x->srv_mu.unlock();
+    g_srv.erase(g_srv.begin() + (ptrdiff_t)i);
+  }
+}
+
 static int serve_launch(vp_ctx *c) {
+  serve_yield(c);
   const FlowTable &t = c->ft;
   NatArgs a{};
   a.t = tbl_dev(t);
@@ -3000,6 +3041,7 @@ static int serve_launch(vp_ctx *c) {
 
 int nat_process_one(vp_ctx *c, uint16_t in_dev, uint8_t *frame, uint16_t len, int64_t now,
                     uint16_t *out) {
+  std::lock_guard<std::recursive_mutex> sg(c->srv_mu);
   static const bool off = [] {
     const char *e = getenv("VIGPATH_SERVE");
     return e && !atoi(e);

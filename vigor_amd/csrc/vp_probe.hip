@@ -1,6 +1,7 @@
-// Memory-shape ceiling of the 64-byte classify tile (vp_probe_slots,
+// Memory-shape ceiling of the 64-byte classify tile (vp_probe_slots[_w],
 // include/vigpath.h): the same persistent grid and access shape as
-// nat_classify64 -- 4 blocks of 256 threads per CU, each block a contiguous
+// nat_classify64 -- 4 blocks of 256 threads per CU (or one of 1024 threads,
+// as nat_classify64w; or two of 512), each block a contiguous
 // range of 64-slot tiles, its four waves interleaved over it, every load and
 // store instruction 1 KiB contiguous through a buffer resource, write-through
 // (sc1) stores as the tile stores -- with none of its work: each slot is read
@@ -18,15 +19,17 @@ namespace vp {
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
-// N = 16-byte chunks per slot; ST: store the slot back
-template <uint32_t N, bool ST>
-__global__ __launch_bounds__(256, 4) void probe_slots(uint4 *buf, uint32_t tiles,
-                                                      uint32_t *sink) {
+// N = 16-byte chunks per slot; ST: store the slot back; W waves per block
+// (4: nat_classify64's four 256-thread blocks per CU; 16: nat_classify64w's
+// one 1024-thread block; 8: two 512-thread waves per SIMD)
+template <uint32_t N, bool ST, uint32_t W = 4>
+__global__ __launch_bounds__(64 * W, 16 / W) void probe_slots(uint4 *buf, uint32_t tiles,
+                                                             uint32_t *sink) {
   const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t per_b = (tiles + gridDim.x - 1) / gridDim.x;
   const uint32_t tend = min(tiles, blockIdx.x * per_b + per_b);
   v4u acc = {0, 0, 0, 0};
-  for (uint32_t tile = blockIdx.x * per_b + wv; tile < tend; tile += 4) {
+  for (uint32_t tile = blockIdx.x * per_b + wv; tile < tend; tile += W) {
     uint4 *g = buf + (size_t)tile * 64 * N;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(g, 0, 64 * N * 16, 0x00020000);
     v4u d[N];
@@ -49,18 +52,27 @@ __global__ __launch_bounds__(256, 4) void probe_slots(uint4 *buf, uint32_t tiles
 
 using namespace vp;
 
-extern "C" int vp_probe_slots(void *frames, uint32_t n, uint32_t slot, int store, int reps,
-                              float *ms) {
+typedef void (*ProbeKernel)(uint4 *, uint32_t, uint32_t *);
+template <uint32_t W>
+static ProbeKernel probe_kernel(uint32_t slot, int store) {
+  return slot == 64 ? (store ? probe_slots<4, true, W> : probe_slots<4, false, W>)
+                    : (store ? probe_slots<8, true, W> : probe_slots<8, false, W>);
+}
+
+extern "C" int vp_probe_slots_w(void *frames, uint32_t n, uint32_t slot, int store, int waves,
+                                int reps, float *ms) {
   if (!frames || !ms || reps < 1 || (n & 63) || n == 0 || (slot != 64 && slot != 128) ||
-      ((uintptr_t)frames & 15))
+      ((uintptr_t)frames & 15) || (waves != 4 && waves != 8 && waves != 16))
     return VP_EINVAL;
-  auto k = slot == 64 ? (store ? probe_slots<4, true> : probe_slots<4, false>)
-                      : (store ? probe_slots<8, true> : probe_slots<8, false>);
+  const ProbeKernel k = waves == 16  ? probe_kernel<16>(slot, store)
+                        : waves == 8 ? probe_kernel<8>(slot, store)
+                                     : probe_kernel<4>(slot, store);
+  const int threads = 64 * waves, cap = 16 / waves;  // blocks per CU at most
   int dev = 0, cus = 0, per = 0;
   VP_HIP(hipGetDevice(&dev));
   VP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  VP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)k, 256, 0));
-  const uint32_t grid = (uint32_t)(cus * (per > 4 ? 4 : per));
+  VP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)k, threads, 0));
+  const uint32_t grid = (uint32_t)(cus * (per > cap ? cap : per < 1 ? 1 : per));
   hipStream_t s = nullptr;
   hipEvent_t a = nullptr, b = nullptr;
   uint32_t *sink = nullptr;
@@ -74,13 +86,13 @@ extern "C" int vp_probe_slots(void *frames, uint32_t n, uint32_t slot, int store
     rc = fail(e, __LINE__);
     goto out;
   }
-  for (int i = 0; i < 2; i++) k<<<grid, 256, 0, s>>>((uint4 *)frames, n / 64, sink);  // warm
+  for (int i = 0; i < 2; i++) k<<<grid, threads, 0, s>>>((uint4 *)frames, n / 64, sink);  // warm
   // each launch timed by its own dispatch's timestamps, as the classify
   // kernel is (launch_timed, vp_internal.h)
   for (int i = 0; i < reps; i++) {
     float one = 0.f;
-    if ((e = launch_timed(k, dim3(grid), dim3(256), s, a, b, (uint4 *)frames, n / 64, sink)) !=
-            hipSuccess ||
+    if ((e = launch_timed(k, dim3(grid), dim3(threads), s, a, b, (uint4 *)frames, n / 64,
+                          sink)) != hipSuccess ||
         (e = hipEventSynchronize(b)) != hipSuccess ||
         (e = hipEventElapsedTime(&one, a, b)) != hipSuccess) {
       rc = fail(e, __LINE__);
@@ -96,4 +108,9 @@ out:
   if (b) hipEventDestroy(b);
   if (s) hipStreamDestroy(s);
   return rc;
+}
+
+extern "C" int vp_probe_slots(void *frames, uint32_t n, uint32_t slot, int store, int reps,
+                              float *ms) {
+  return vp_probe_slots_w(frames, n, slot, store, 4, reps, ms);
 }

@@ -529,7 +529,7 @@ using namespace vp;
 
 extern "C" {
 
-const char *vp_version(void) { return "vigpath 0.2 gfx950"; }
+const char *vp_version(void) { return "vigpath 0.3 gfx950"; }
 
 int vp_nat_create(const vp_nat_config *cfg, int gpu, vp_ctx **out) {
   if (!cfg || !out) return VP_EINVAL;
@@ -644,6 +644,9 @@ void hostprof(int k) {
 
 int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
   if (!c || !b) return VP_EINVAL;
+  // (nf_process's device is a uint16_t, nf.h:14: the kernels that read the
+  // burst's port directly and the port arrays made below must agree)
+  if (!b->in_dev && b->in_port > 0xFFFFu) return VP_EINVAL;
   if (vp::g_hostprof) {
     for (double &x : vp::g_hp) x = 0;
     vp::hostprof(0);
@@ -849,12 +852,23 @@ int vp_kernel_timing(vp_ctx *c, int on) {
   return 0;
 }
 
-int vp_last_stage_ms(vp_ctx *c, float *ms, int *stages) {
-  if (!c || !ms || !stages) return VP_EINVAL;
-  for (int i = 0; i < kStages; i++) ms[i] = c->stage_ms[i];
+int vp_stage_ms(vp_ctx *c, float *ms, int cap, int *stages) {
+  static_assert(kStages == VP_STAGES, "include/vigpath.h VP_STAGES");
+  if (!c || !stages || cap < 0 || (cap > 0 && !ms)) return VP_EINVAL;
+  for (int i = 0; i < kStages && i < cap; i++) ms[i] = c->stage_ms[i];
   *stages = c->stage_n;
   return 0;
 }
+
+// (the 0.2 contract: seven floats; the chunked pipeline's ms[7] only through
+// vp_stage_ms)
+int vp_last_stage_ms(vp_ctx *c, float *ms, int *stages) {
+  const int rc = vp_stage_ms(c, ms, 7, stages);
+  if (rc == 0 && *stages > 7) *stages = 7;
+  return rc;
+}
+
+const char *vp_last_kernel(vp_ctx *c) { return c ? c->last_kernel : ""; }
 
 int vp_last_kernel_ms(vp_ctx *c, float *ms, int *launches) {
   if (!c || !ms || !launches) return VP_EINVAL;

@@ -103,17 +103,22 @@ class NfBase:
         self._ck(self.L.vp_last_kernel_ms(self.h, rms, rk), "vp_last_kernel_ms")
         return ms.value, k.value
 
+    def last_kernel(self) -> str:
+        """vp_last_kernel: the tile kernel the last call launched ("" if none)."""
+        return (self.L.vp_last_kernel(self.h) or b"").decode()
+
     STAGES = ("pass1", "offsets", "a2a_keys", "probe", "a2a_answers", "pass2", "fold",
               "pipeline")
 
     def last_stage_ms(self) -> dict:
-        """vp_last_stage_ms: owner mode with kernel timing on, the last
-        call's phase-A stage times (ms) by stage name ({} if none); the
-        chunked pipeline reports "pipeline" (its overlapped chunks) and
-        "fold" only."""
-        ms, k = (C.c_float * 8)(), C.c_int()
-        self._ck(self.L.vp_last_stage_ms(self.h, ms, C.byref(k)), "vp_last_stage_ms")
-        d = {self.STAGES[i]: ms[i] for i in range(k.value)}
+        """vp_stage_ms: owner mode with kernel timing on, the last call's
+        phase-A stage times (ms) by stage name ({} if none); the chunked
+        pipeline reports "pipeline" (its overlapped chunks) and "fold"
+        only."""
+        cap = len(self.STAGES)
+        ms, k = (C.c_float * cap)(), C.c_int()
+        self._ck(self.L.vp_stage_ms(self.h, ms, cap, C.byref(k)), "vp_stage_ms")
+        d = {self.STAGES[i]: ms[i] for i in range(min(cap, k.value))}
         if d.get("pipeline"):
             d = {"pipeline": d["pipeline"], "fold": d["fold"]}
         return d
