@@ -1200,9 +1200,10 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
   plan->range = range;
   plan->L = L;
   plan->sbits = sbits;
-  // run words per block and bin: two, eight for 1024-thread blocks (four
-  // times the range); positions below 2^20 within a block
-  const uint32_t rwords = waves >= 16 ? kBinRunWordsMax : 2u;
+  // run words per block and bin: two, eight for one block per CU (512- to
+  // 1024-thread blocks: four times the range); positions below 2^20 within
+  // a block
+  const uint32_t rwords = waves >= 8 ? kBinRunWordsMax : 2u;
   const size_t nr = ((size_t)grid << bbits) * rwords;
   if (nr > w.bins_rtab_n) {
     VP_HIP(hipStreamSynchronize(c->stream));
