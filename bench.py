@@ -781,10 +781,12 @@ def ceiling_fields(ceiling, kernel_s, step_s):
             "kernel_over_ceiling": round(kernel_s * 1e3 / rw, 4),
             "step_over_ceiling": round(step_s * 1e3 / rw, 4),
             "shape_ceiling_source": "vp_probe_slots_w on this box: the tile kernel's "
-                                    "persistent grid (%d-thread blocks, %d per CU) and 1 KiB "
-                                    "access shape, every slot read and written back whole "
-                                    "(write-through), no other work; shape_read_ms the same "
-                                    "without the stores" % (64 * waves, 16 // waves)}
+                                    "persistent grid (%d-thread blocks, %d per CU; tile "
+                                    "order VIGPATH_SPLIT=%s) and 1 KiB access shape, every "
+                                    "slot read and written back whole (write-through), no "
+                                    "other work; shape_read_ms the same without the stores"
+                                    % (64 * waves, max(1, 16 // waves),
+                                       os.environ.get("VIGPATH_SPLIT", "1"))}
 
 
 def kernel_label(knames, default):
@@ -800,7 +802,12 @@ def kernel_label(knames, default):
 
 def probe_waves(kernel: str) -> int:
     """Waves per block of the tile kernel's grid (vp_probe_slots_w)."""
-    return 16 if kernel.startswith("nat_classify64w") or kernel.endswith("64w") else 4
+    k = kernel.split(" ")[0]
+    if k.startswith("nat_classify64w") or k.endswith("64w"):
+        return 16
+    if k.startswith("nat_classify64p"):
+        return 12 if k.endswith("12") else 8
+    return 4
 
 
 def kernel_rate(kms, B, steps, alg_bytes):

@@ -390,9 +390,9 @@ int vp_last_stage_ms(vp_ctx *ctx, float *ms, int *stages);
  * slot read and, store != 0, written back unchanged (write-through). *ms =
  * the mean duration of `reps` launches, each timed by its own dispatch's
  * timestamps. DESIGN.md §5.1. vp_probe_slots_w: the same with `waves` (4,
- * 8 or 16) waves per block, one block of 64 x waves threads per 4 waves of
- * a CU's capacity (16: nat_classify64w's one 1024-thread block per CU);
- * vp_probe_slots is waves = 4. */
+ * 8, 12 or 16) waves per block, as many blocks per CU as 16 waves make (16:
+ * nat_classify64w's one 1024-thread block per CU, its tile order as
+ * VIGPATH_SPLIT sets it); vp_probe_slots is waves = 4. */
 int vp_probe_slots(void *frames, uint32_t n, uint32_t slot, int store, int reps, float *ms);
 int vp_probe_slots_w(void *frames, uint32_t n, uint32_t slot, int store, int waves, int reps,
                      float *ms);

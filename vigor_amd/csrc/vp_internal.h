@@ -4,6 +4,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <mutex>
 #include <tuple>
@@ -63,6 +64,18 @@ hipError_t launch_timed(void (*k)(P...), dim3 grid, dim3 block, hipStream_t s,
     ((ptrs[i++] = (void *)&x), ...);
   }, t);
   return hipExtLaunchKernel((const void *)k, grid, block, ptrs, 0, s, e0, e1, 0);
+}
+
+// 1024-thread vignat tiles (nat_tiles) and their memory-shape probe
+// (vp_probe_slots_w): each block's range in VIGPATH_SPLIT (1, 2 or 4)
+// contiguous sub-ranges, 16 / split waves interleaved over each.
+inline uint32_t tile_split() {
+  static const uint32_t s = [] {
+    const char *e = getenv("VIGPATH_SPLIT");
+    const int v = e ? atoi(e) : 1;
+    return v == 2 || v == 4 ? (uint32_t)v : 1u;
+  }();
+  return s;
 }
 
 // Owner-mode phase A stages (vp_last_stage_ms).

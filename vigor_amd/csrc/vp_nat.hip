@@ -200,6 +200,10 @@ struct NatArgs {
   // 1024-thread tiles: bin entries staged in LDS and stored a whole line at
   // a time (bins_put_staged; VIGPATH_BIN_STAGE=0 off, for A/B)
   uint32_t bstage;
+  // 1024-thread tiles: the block's range cut into `split` contiguous
+  // sub-ranges, W / split waves interleaved over each (tile_split(); 0 or 1:
+  // all W waves over the whole range)
+  uint32_t split;
 };
 
 // Queue packet p (FlowId key, hash h) as a phase-B miss.
@@ -785,8 +789,12 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   };
   const uint32_t rb = a.vb0 + blockIdx.x;  // (virtual blocks: the chunked pipeline)
   const uint32_t per_b = a.vper ? a.vper : (tiles + gridDim.x - 1) / gridDim.x;
-  uint32_t tile = rb * per_b + wv;
-  const uint32_t tend = min(tiles, rb * per_b + per_b), tstep = W;
+  // (split: sub-range wv / (W / split) of the block's range, W / split waves
+  // interleaved over it -- the streams of `split` smaller blocks)
+  const uint32_t ks = W == 16 && (a.split == 2 || a.split == 4) ? a.split : 1u;
+  const uint32_t tstep = W / ks, per_s = (per_b + ks - 1) / ks, sub = wv / tstep;
+  uint32_t tile = rb * per_b + sub * per_s + (wv - sub * tstep);
+  const uint32_t tend = min(tiles, rb * per_b + min(per_b, (sub + 1) * per_s));
   const uint32_t range0 = first + rb * per_b * 64;  // this block's first packet
   // a lean tile's misses (wave-uniform call), with their FlowIds and hashes
   // when phase B takes them unsorted (a.mkq)
@@ -3056,6 +3064,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     return !e || atoi(e) != 0;
   }();
   a.bstage = bin_stage ? 1u : 0u;
+  a.split = tile_split();
   if (nku) {
     a.mkey = reinterpret_cast<uint4 *>(w.mkey);
     a.mhash = w.mhash;

@@ -11,6 +11,7 @@
 // (tools/slot_probe.hip is the stand-alone form with more variants.)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "vp_internal.h"
@@ -22,14 +23,18 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 // N = 16-byte chunks per slot; ST: store the slot back; W waves per block
 // (4: nat_classify64's four 256-thread blocks per CU; 16: nat_classify64w's
 // one 1024-thread block; 8: two 512-thread waves per SIMD)
+// (split: as the 1024-thread vignat tiles, tile_split(), vp_internal.h)
 template <uint32_t N, bool ST, uint32_t W = 4>
 __global__ __launch_bounds__(64 * W, 16 / W) void probe_slots(uint4 *buf, uint32_t tiles,
-                                                             uint32_t *sink) {
+                                                             uint32_t *sink, uint32_t split) {
   const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t per_b = (tiles + gridDim.x - 1) / gridDim.x;
-  const uint32_t tend = min(tiles, blockIdx.x * per_b + per_b);
+  const uint32_t ks = W == 16 && (split == 2 || split == 4) ? split : 1u;
+  const uint32_t tstep = W / ks, per_s = (per_b + ks - 1) / ks, sub = wv / tstep;
+  const uint32_t tend = min(tiles, blockIdx.x * per_b + min(per_b, (sub + 1) * per_s));
   v4u acc = {0, 0, 0, 0};
-  for (uint32_t tile = blockIdx.x * per_b + wv; tile < tend; tile += W) {
+  for (uint32_t tile = blockIdx.x * per_b + sub * per_s + (wv - sub * tstep); tile < tend;
+       tile += tstep) {
     uint4 *g = buf + (size_t)tile * 64 * N;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(g, 0, 64 * N * 16, 0x00020000);
     v4u d[N];
@@ -52,7 +57,7 @@ __global__ __launch_bounds__(64 * W, 16 / W) void probe_slots(uint4 *buf, uint32
 
 using namespace vp;
 
-typedef void (*ProbeKernel)(uint4 *, uint32_t, uint32_t *);
+typedef void (*ProbeKernel)(uint4 *, uint32_t, uint32_t *, uint32_t);
 template <uint32_t W>
 static ProbeKernel probe_kernel(uint32_t slot, int store) {
   return slot == 64 ? (store ? probe_slots<4, true, W> : probe_slots<4, false, W>)
@@ -62,17 +67,19 @@ static ProbeKernel probe_kernel(uint32_t slot, int store) {
 extern "C" int vp_probe_slots_w(void *frames, uint32_t n, uint32_t slot, int store, int waves,
                                 int reps, float *ms) {
   if (!frames || !ms || reps < 1 || (n & 63) || n == 0 || (slot != 64 && slot != 128) ||
-      ((uintptr_t)frames & 15) || (waves != 4 && waves != 8 && waves != 16))
+      ((uintptr_t)frames & 15) || (waves != 4 && waves != 8 && waves != 12 && waves != 16))
     return VP_EINVAL;
-  const ProbeKernel k = waves == 16  ? probe_kernel<16>(slot, store)
-                        : waves == 8 ? probe_kernel<8>(slot, store)
-                                     : probe_kernel<4>(slot, store);
-  const int threads = 64 * waves, cap = 16 / waves;  // blocks per CU at most
+  const ProbeKernel k = waves == 16   ? probe_kernel<16>(slot, store)
+                        : waves == 12 ? probe_kernel<12>(slot, store)
+                        : waves == 8  ? probe_kernel<8>(slot, store)
+                                      : probe_kernel<4>(slot, store);
+  const int threads = 64 * waves, cap = std::max(1, 16 / waves);  // blocks per CU at most
   int dev = 0, cus = 0, per = 0;
   VP_HIP(hipGetDevice(&dev));
   VP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   VP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)k, threads, 0));
   const uint32_t grid = (uint32_t)(cus * (per > cap ? cap : per < 1 ? 1 : per));
+  const uint32_t split = tile_split();
   hipStream_t s = nullptr;
   hipEvent_t a = nullptr, b = nullptr;
   uint32_t *sink = nullptr;
@@ -86,13 +93,13 @@ extern "C" int vp_probe_slots_w(void *frames, uint32_t n, uint32_t slot, int sto
     rc = fail(e, __LINE__);
     goto out;
   }
-  for (int i = 0; i < 2; i++) k<<<grid, threads, 0, s>>>((uint4 *)frames, n / 64, sink);  // warm
+  for (int i = 0; i < 2; i++) k<<<grid, threads, 0, s>>>((uint4 *)frames, n / 64, sink, split);
   // each launch timed by its own dispatch's timestamps, as the classify
   // kernel is (launch_timed, vp_internal.h)
   for (int i = 0; i < reps; i++) {
     float one = 0.f;
     if ((e = launch_timed(k, dim3(grid), dim3(threads), s, a, b, (uint4 *)frames, n / 64,
-                          sink)) != hipSuccess ||
+                          sink, split)) != hipSuccess ||
         (e = hipEventSynchronize(b)) != hipSuccess ||
         (e = hipEventElapsedTime(&one, a, b)) != hipSuccess) {
       rc = fail(e, __LINE__);
