@@ -318,17 +318,26 @@ constexpr int kMaxHostMaps = 16;
 
 // vp_process_one's mailbox (vp_nat.hip nat_serve): page-locked, host-coherent
 // memory the host and a persistent one-wave kernel poll. The host writes the
-// packet's time and frame, then the doorbell; the kernel rewrites the frame in
-// place, then sets the answer word.
+// request (below); the kernel writes the rewritten frame to `frame`, then
+// sets the answer word.
 constexpr uint32_t kServeFrame = 2048;  // longest frame served (others: the batch path)
-constexpr uint32_t kServeLeave = 0xFFFFFFFFu;  // doorbell high word: leave
+constexpr uint32_t kServeLeave = 0xFFFFFFFFu;  // message word 0: leave
+// The request travels in kServeChunks tagged 16-byte chunks that every poll
+// of the server reads whole (one PCIe read per poll, no second round trip for
+// the frame): chunk k holds bytes 12k .. 12k + 11 of the message (len |
+// in_dev << 16 as 4 bytes -- kServeLeave: leave --, the time as 8, then the
+// frame's first kServeInline bytes) and, as its last word, the request
+// number. The host writes a chunk's payload before its tag, and a chunk lies
+// within one cache line, which a device read sees whole: a chunk whose tag is
+// the request's carries the request's bytes. Frames past kServeInline bytes
+// also go whole through `frame`, read after the chunks.
+constexpr uint32_t kServeChunks = 8;
+constexpr uint32_t kServeInline = 12 * kServeChunks - 12;  // 84 frame bytes
 struct ServeBox {
-  uint64_t bell;     // host: request number | (len | in_dev << 16) << 32
+  alignas(128) uint32_t msg[kServeChunks][4];  // host: the tagged request chunks
   uint64_t ans;      // device: request number | (out | fresh << 16) << 32
   uint64_t prof[8];  // device: wall-clock stamps of the last request (VIGPATH_SERVE_PROF)
-  alignas(16) int64_t now;  // host: the packet's time (read with the frame's first bytes)
-  uint64_t pad_;
-  uint8_t frame[kServeFrame];
+  alignas(16) uint8_t frame[kServeFrame];  // longer frames in; every result out
 };
 // One packet through the persistent kernel (vignat, one GPU, no expiry due):
 // 0 done; 1 not eligible (the caller takes the batch path, the server is

@@ -2339,7 +2339,7 @@ __device__ __forceinline__ uint32_t nat_one_reg(const NatArgs &a, const uint32_t
     dst = k.w & 0xFFFF;
   } else {
     const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
-    const uint32_t hh = flowid_hash(T, sp, dp, sip, dip, in, proto);
+    const uint32_t hh = flowid_hash_batched(T, sp, dp, sip, dip, in, proto);
     if (prof) mk0 = wall_clock64();
     const uint32_t idx = one_lan(a.t, hh, key, now, seq, fresh);
     if (prof) mk1 = wall_clock64();
@@ -2356,20 +2356,22 @@ __device__ __forceinline__ uint32_t nat_one_reg(const NatArgs &a, const uint32_t
   return dst;
 }
 
-// The server: one wave. It polls the doorbell (one PCIe read a turn); on a
-// request the frame and time cross PCIe into LDS together (16-byte
-// system-coherent loads, one per lane per 1 KiB), the wave sums the L4 bytes
-// past byte 64, lane 0 runs the packet, the frame goes back the same way,
-// and the answer word follows once every store has completed. Packets take
-// global sequence numbers seq, seq + 1, ... It leaves on the leave doorbell
-// or after `idle` wall-clock ticks without a request; a request posted as it
-// leaves finds the stream idle and the host launches it again
-// (nat_process_one). flags: bit 0, the stage clock (VIGPATH_SERVE_PROF).
+// The server: one wave. Every poll reads the request chunks whole (ServeBox,
+// vp_internal.h: one PCIe read brings the doorbell, the time and a frame of up
+// to kServeInline bytes), four polls in flight, staggered, so a request is
+// seen about a quarter of a round trip sooner than by one poll at a time;
+// longer frames are read from `frame` afterwards. The frame goes into LDS, the
+// wave sums the L4 bytes past byte 64, lane 0 runs the packet, the frame goes
+// back (16-byte system-coherent stores) and the answer word follows once
+// every store has completed. Packets take global sequence numbers seq, seq +
+// 1, ... It leaves on the leave request or after `idle` wall-clock ticks
+// without a request; a request posted as it leaves finds the stream idle and
+// the host launches it again (nat_process_one). flags: bit 0, the stage
+// clock (VIGPATH_SERVE_PROF).
 __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64_t seq,
                                                 uint64_t idle, uint32_t flags) {
   __shared__ uint32_t T[kNatTabWords];
   __shared__ uint4 fr[kServeFrame / 16];
-  __shared__ int64_t now_s;
   load_nat_tables(T, a);
   const uint32_t lane = threadIdx.x;
   const bool prof = flags & 1u;
@@ -2378,32 +2380,42 @@ __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64
   done = __builtin_amdgcn_readfirstlane(done);
   typedef unsigned v4u __attribute__((ext_vector_type(4)));
   constexpr int kSys = 17;  // sc0 | sc1: system-coherent (bypasses the GPU caches)
-  // 16-byte chunk 0: the time; chunk 1 + i: the frame's chunk i
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc(&box->now, 0, 16 + kServeFrame, 0x00020000);
+  const auto ms = __builtin_amdgcn_make_buffer_rsrc(box->msg, 0, 16 * kServeChunks, 0x00020000);
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(box->frame, 0, kServeFrame, 0x00020000);
+  // (lanes past the chunks read nothing: an offset past the resource)
+  const int moff = lane < kServeChunks ? (int)(16 * lane) : (int)(16 * kServeChunks);
+  auto poll = [&]() -> v4u { return __builtin_amdgcn_raw_buffer_load_b128(ms, moff, 0, kSys); };
+  uint32_t *fw = reinterpret_cast<uint32_t *>(fr);
   uint64_t t0 = wall_clock64();
-  for (;;) {
-    const uint64_t bell =
-        __hip_atomic_load(&box->bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint32_t req = __builtin_amdgcn_readfirstlane((uint32_t)bell);
-    if (req == done) {
-      if (wall_clock64() - t0 > idle) break;
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    // The frame and time are read with system-coherent loads issued after
-    // the doorbell's came back (the host wrote them before it), so no
-    // acquire fence: one would also drop the table's lines from the L2.
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(bell >> 32));
-    if (hi == kServeLeave) break;
-    const uint64_t s0 = wall_clock64();
+  bool leave = false;
+  // one poll's chunks: -1 nothing new (or not yet whole), 0 a request served,
+  // 1 leave
+  auto serve = [&](const v4u &c) -> int {
+    const uint32_t want = done + 1;
+    const uint32_t tag0 = __builtin_amdgcn_readfirstlane(c[3]);
+    if (tag0 != want) return -1;
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(c[0]);
+    if (hi == kServeLeave) return 1;
     const uint32_t len = min(hi & 0xFFFFu, kServeFrame), in = hi >> 16;
+    const bool inl = len <= kServeInline;
+    const uint32_t need = inl ? (12 + len + 11) / 12 : 1u;  // chunks carrying it
+    if (__ballot(lane < need && c[3] != want)) return -1;  // not whole yet: poll again
+    const uint64_t s0 = wall_clock64();
+    const int64_t now =
+        (int64_t)((uint64_t)__builtin_amdgcn_readfirstlane(c[1]) |
+                  ((uint64_t)__builtin_amdgcn_readfirstlane(c[2]) << 32));
     const uint32_t nch = (len + 15) / 16;
-    for (uint32_t i = lane; i <= nch; i += 64) {
-      const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16 * i), 0, kSys);
-      if (i == 0)
-        now_s = (int64_t)((uint64_t)v[0] | ((uint64_t)v[1] << 32));
-      else
-        fr[i - 1] = make_uint4(v[0], v[1], v[2], v[3]);
+    if (inl) {  // chunk k >= 1: frame bytes 12k - 12 .. 12k - 1
+      if (lane >= 1 && lane < need) {
+        fw[3 * lane - 3] = c[0];
+        fw[3 * lane - 2] = c[1];
+        fw[3 * lane - 1] = c[2];
+      }
+    } else {  // the whole frame from `frame` (the host wrote it before the chunks)
+      for (uint32_t i = lane; i < nch; i += 64) {
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16 * i), 0, kSys);
+        fr[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
     }
     __syncthreads();
     // the L4 checksum's bytes past 64: [64, min(14 + total_length, len))
@@ -2412,8 +2424,8 @@ __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64
       const uint8_t *fb = reinterpret_cast<const uint8_t *>(fr);
       const uint32_t tl = ((uint32_t)fb[16] << 8) | fb[17];
       const uint32_t end = min(14 + tl, len);
-      for (uint32_t c = 64 + 16 * lane; c < end; c += 1024)
-        tail = sum16x4(chunk_keep(fr[c / 16], 0, (int)end - (int)c), tail);
+      for (uint32_t cc = 64 + 16 * lane; cc < end; cc += 1024)
+        tail = sum16x4(chunk_keep(fr[cc / 16], 0, (int)end - (int)cc), tail);
       for (int o = 32; o > 0; o >>= 1) tail += __shfl_xor(tail, o);
     }
     const uint64_t s1 = wall_clock64();
@@ -2430,11 +2442,11 @@ __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64
         f.w[4 * j + 2] = v.z;
         f.w[4 * j + 3] = v.w;
       }
-      uint32_t out = nat_one_reg(a, T, f, in, len, tail, now_s, seq, &fresh, prof, mk0, mk1);
+      uint32_t out = nat_one_reg(a, T, f, in, len, tail, now, seq, &fresh, prof, mk0, mk1);
       if (prof) mk2 = wall_clock64();
       if (out == kNone) {
         const GFrame g{reinterpret_cast<uint8_t *>(fr), len};
-        out = nat_one(a, T, g, in, len, now_s, seq, &fresh);
+        out = nat_one(a, T, g, in, len, now, seq, &fresh);
       } else {
 #pragma unroll
         for (int j = 0; j < 4; j++)
@@ -2446,8 +2458,8 @@ __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64
     const uint64_t s2 = wall_clock64();
     for (uint32_t i = lane; i < nch; i += 64) {
       const uint4 v = fr[i];
-      __builtin_amdgcn_raw_buffer_store_b128((v4u){v.x, v.y, v.z, v.w}, rs, (int)(16 * (i + 1)),
-                                             0, kSys);
+      __builtin_amdgcn_raw_buffer_store_b128((v4u){v.x, v.y, v.z, v.w}, rs, (int)(16 * i), 0,
+                                             kSys);
     }
     if (lane == 0) {
       if (prof) {
@@ -2463,7 +2475,7 @@ __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64
         put(6, s2);
         put(7, wall_clock64());
       }
-      const uint64_t ans = (uint64_t)req | ((uint64_t)res << 32);
+      const uint64_t ans = (uint64_t)want | ((uint64_t)res << 32);
       // every store of the wave complete first (its counter covers all
       // lanes); no release fence, which would write back the whole L2
       __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (no compiler reordering either)
@@ -2471,10 +2483,32 @@ __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       __hip_atomic_store(&box->ans, ans, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    done = req;
+    done = want;
     seq += 1;
     t0 = wall_clock64();
+    return 0;
+  };
+  // four polls in flight, a quarter of a round trip apart (the first
+  // round trips set the spacing; each slot re-polls when its result is in)
+  constexpr uint32_t kGap = 12;  // s_sleep units (64 clocks): ~0.3 us
+  v4u q0 = poll();
+  __builtin_amdgcn_s_sleep(kGap);
+  v4u q1 = poll();
+  __builtin_amdgcn_s_sleep(kGap);
+  v4u q2 = poll();
+  __builtin_amdgcn_s_sleep(kGap);
+  v4u q3 = poll();
+  auto slot = [&](v4u &q) -> bool {  // false: leave
+    const int st = serve(q);
+    if (st == 1) return false;
+    if (st < 0 && wall_clock64() - t0 > idle) return false;
+    q = poll();
+    return true;
+  };
+  while (!leave) {
+    if (!slot(q0) || !slot(q1) || !slot(q2) || !slot(q3)) leave = true;
   }
+  __builtin_amdgcn_s_waitcnt(0);  // (no poll left in flight)
 }
 
 // =============================================================== host ==
@@ -3260,7 +3294,8 @@ static const bool g_srv_prof = [] {
 static hipError_t serve_halt(vp_ctx *c) {
   ServeBox *bx = c->sbox;
   const uint32_t req = ++c->srv_req;
-  __atomic_store_n(&bx->bell, (uint64_t)req | ((uint64_t)kServeLeave << 32), __ATOMIC_RELEASE);
+  bx->msg[0][0] = kServeLeave;
+  __atomic_store_n(&bx->msg[0][3], req, __ATOMIC_RELEASE);
   const hipError_t e = hipStreamSynchronize(c->stream);
   // (the kernel is gone: the leave request counts as answered for the next one)
   __atomic_store_n(&bx->ans, (uint64_t)req, __ATOMIC_RELEASE);
@@ -3381,11 +3416,26 @@ int nat_process_one(vp_ctx *c, uint16_t in_dev, uint8_t *frame, uint16_t len, in
   }
   ServeBox *bx = c->sbox;
   const auto h0 = std::chrono::steady_clock::now();
-  bx->now = now;
-  memcpy(bx->frame, frame, len);
+  // the request chunks (ServeBox): payload words first, then each chunk's
+  // tag; chunk 0 last; a longer frame whole through `frame` before them
   const uint32_t req = ++c->srv_req;
-  __atomic_store_n(&bx->bell, (uint64_t)req | ((uint64_t)(len | ((uint32_t)in_dev << 16)) << 32),
-                   __ATOMIC_RELEASE);
+  uint32_t m[3 * kServeChunks] = {};
+  m[0] = len | ((uint32_t)in_dev << 16);
+  m[1] = (uint32_t)(uint64_t)now;
+  m[2] = (uint32_t)((uint64_t)now >> 32);
+  uint32_t need = 1;
+  if (len <= kServeInline) {
+    memcpy(&m[3], frame, len);
+    need = (12 + len + 11) / 12;
+  } else {
+    memcpy(bx->frame, frame, len);
+  }
+  for (uint32_t k = need; k-- > 0;) {
+    bx->msg[k][0] = m[3 * k];
+    bx->msg[k][1] = m[3 * k + 1];
+    bx->msg[k][2] = m[3 * k + 2];
+    __atomic_store_n(&bx->msg[k][3], req, __ATOMIC_RELEASE);
+  }
   auto last = h0;
   uint64_t ans;
   while ((uint32_t)(ans = __atomic_load_n(&bx->ans, __ATOMIC_ACQUIRE)) != req) {
