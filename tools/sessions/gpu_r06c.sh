@@ -7,9 +7,9 @@ O=gpurun_out; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_nat_gpu.py tests/test_nf_shim_gpu.py -x -v --timeout 200 \
   --timeout-method thread -k "process_one or nf_loop or shim" > $O/r06c_pytest.log 2>&1 || { tail -40 $O/r06c_pytest.log; exit 1; }
 grep -E "passed|failed" $O/r06c_pytest.log | tail -2
-for prof in 0 1 0; do
+for pp in "1 0" "1 1" "2 1" "4 1" "2 0" "1 0"; do set -- $pp; prof=$2; export VIGPATH_SERVE_POLLS=$1
   VIGPATH_SERVE_PROF=$prof timeout -k 10 300 python3 -c "
 import bench, json
-print(json.dumps(bench.per_packet_drop_in()))" > $O/r06c_pp_$prof.json 2> $O/r06c_pp_$prof.err || { tail -20 $O/r06c_pp_$prof.err; exit 1; }
-  cat $O/r06c_pp_$prof.json
+print(json.dumps(bench.per_packet_drop_in()))" > $O/r06c_pp_$1_$prof.json 2> $O/r06c_pp_$1_$prof.err || { tail -20 $O/r06c_pp_$1_$prof.err; exit 1; }
+  cat $O/r06c_pp_$1_$prof.json
 done

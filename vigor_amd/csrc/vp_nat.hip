@@ -2358,16 +2358,16 @@ __device__ __forceinline__ uint32_t nat_one_reg(const NatArgs &a, const uint32_t
 
 // The server: one wave. Every poll reads the request chunks whole (ServeBox,
 // vp_internal.h: one PCIe read brings the doorbell, the time and a frame of up
-// to kServeInline bytes), four polls in flight, staggered, so a request is
-// seen about a quarter of a round trip sooner than by one poll at a time;
-// longer frames are read from `frame` afterwards. The frame goes into LDS, the
+// to kServeInline bytes), one poll in flight (or, VIGPATH_SERVE_POLLS, two
+// or four, staggered); longer frames are read from `frame` afterwards. The frame goes into LDS, the
 // wave sums the L4 bytes past byte 64, lane 0 runs the packet, the frame goes
 // back (16-byte system-coherent stores) and the answer word follows once
 // every store has completed. Packets take global sequence numbers seq, seq +
 // 1, ... It leaves on the leave request or after `idle` wall-clock ticks
 // without a request; a request posted as it leaves finds the stream idle and
 // the host launches it again (nat_process_one). flags: bit 0, the stage
-// clock (VIGPATH_SERVE_PROF).
+// clock (VIGPATH_SERVE_PROF); bits 1-2: log2 of the polls in flight, plus 1;
+// bits 3-9: their spacing in wall-clock ticks.
 __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64_t seq,
                                                 uint64_t idle, uint32_t flags) {
   __shared__ uint32_t T[kNatTabWords];
@@ -2387,7 +2387,6 @@ __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64
   auto poll = [&]() -> v4u { return __builtin_amdgcn_raw_buffer_load_b128(ms, moff, 0, kSys); };
   uint32_t *fw = reinterpret_cast<uint32_t *>(fr);
   uint64_t t0 = wall_clock64();
-  bool leave = false;
   // one poll's chunks: -1 nothing new (or not yet whole), 0 a request served,
   // 1 leave
   auto serve = [&](const v4u &c) -> int {
@@ -2488,25 +2487,41 @@ __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64
     t0 = wall_clock64();
     return 0;
   };
-  // four polls in flight, a quarter of a round trip apart (the first
-  // round trips set the spacing; each slot re-polls when its result is in)
-  constexpr uint32_t kGap = 12;  // s_sleep units (64 clocks): ~0.3 us
-  v4u q0 = poll();
-  __builtin_amdgcn_s_sleep(kGap);
-  v4u q1 = poll();
-  __builtin_amdgcn_s_sleep(kGap);
-  v4u q2 = poll();
-  __builtin_amdgcn_s_sleep(kGap);
-  v4u q3 = poll();
+  // polls in flight (flags bits 1-2: 1, 2 or 4), a fraction of a round trip
+  // apart (the first round trips set the spacing; each slot re-polls when its
+  // result is in)
+  const uint32_t np = (flags >> 1) & 3u ? 1u << (((flags >> 1) & 3u) - 1) : 1u;
+  const uint32_t gap = (flags >> 3) & 0x7Fu;  // wall-clock ticks (10 ns) between polls
+  auto pause = [&]() {
+    const uint64_t w = wall_clock64();
+    while (wall_clock64() - w < gap) __builtin_amdgcn_s_sleep(1);
+  };
   auto slot = [&](v4u &q) -> bool {  // false: leave
     const int st = serve(q);
     if (st == 1) return false;
     if (st < 0 && wall_clock64() - t0 > idle) return false;
+    if (st < 0 && np == 1) __builtin_amdgcn_s_sleep(1);
     q = poll();
     return true;
   };
-  while (!leave) {
-    if (!slot(q0) || !slot(q1) || !slot(q2) || !slot(q3)) leave = true;
+  v4u q0 = poll();
+  if (np == 1) {
+    while (slot(q0)) {
+    }
+  } else if (np == 2) {
+    pause();
+    v4u q1 = poll();
+    while (slot(q0) && slot(q1)) {
+    }
+  } else {
+    pause();
+    v4u q1 = poll();
+    pause();
+    v4u q2 = poll();
+    pause();
+    v4u q3 = poll();
+    while (slot(q0) && slot(q1) && slot(q2) && slot(q3)) {
+    }
   }
   __builtin_amdgcn_s_waitcnt(0);  // (no poll left in flight)
 }
@@ -3370,8 +3385,19 @@ static int serve_launch(vp_ctx *c) {
   a.n_dev = c->nat.n_devices;
   ServeBox *dbox = nullptr;
   VP_HIP(hipHostGetDevicePointer((void **)&dbox, c->sbox, 0));
+  // polls in flight (VIGPATH_SERVE_POLLS: 1, 2 or 4) and their spacing
+  // (VIGPATH_SERVE_GAP, wall-clock ticks of 10 ns)
+  static const uint32_t polls = [] {
+    const char *e = getenv("VIGPATH_SERVE_POLLS");
+    const int v = e ? atoi(e) : 1;
+    return v == 4 ? 3u : v == 2 ? 2u : 1u;
+  }();
+  static const uint32_t gap = [] {
+    const char *e = getenv("VIGPATH_SERVE_GAP");
+    return e ? (uint32_t)std::min(127, std::max(0, atoi(e))) : 35u;
+  }();
   nat_serve<<<1, 64, 0, c->stream>>>(a, dbox, c->seq, c->srv_idle,
-                                     g_srv_prof ? 1u : 0u);
+                                     (g_srv_prof ? 1u : 0u) | (polls << 1) | (gap << 3));
   VP_HIP(hipGetLastError());
   if (!c->srv_on) {
     static std::once_flag once;
