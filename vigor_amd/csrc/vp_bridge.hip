@@ -61,6 +61,40 @@ __device__ __forceinline__ uint32_t static_hash(const uint32_t *T, uint32_t eh,
          S[4 * 256 + (dev & 0xFF)] ^ S[5 * 256 + ((dev >> 8) & 0xFF)];
 }
 
+// eth_hash of two MACs, the 12 table reads issued back to back and waited
+// for once (as vignat's flowid_hash_batched; T must be the kernel's LDS
+// tables): *hs of src {s0, s1}, *hd of dst {d0, d1}.
+__device__ __forceinline__ uint32_t bridge_lds_addr(const void *p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+#define VP_ETH_RD(t, a, off) \
+  asm volatile("ds_read_b32 %0, %1 offset:" #off : "=v"(t) : "v"(a))
+__device__ __forceinline__ void eth_hash2(const uint32_t *T, uint32_t s0, uint32_t s1,
+                                          uint32_t d0, uint32_t d1, uint32_t *hs,
+                                          uint32_t *hd) {
+  const uint32_t base = bridge_lds_addr(T);
+  auto at = [&](uint32_t byte) { return base + (byte << 2); };
+  uint32_t a0, a1, a2, a3, a4, a5, b0, b1, b2, b3, b4, b5;
+  VP_ETH_RD(a0, at(s0 & 0xFF), 0);
+  VP_ETH_RD(a1, at((s0 >> 8) & 0xFF), 1024);
+  VP_ETH_RD(a2, at((s0 >> 16) & 0xFF), 2048);
+  VP_ETH_RD(a3, at(s0 >> 24), 3072);
+  VP_ETH_RD(a4, at(s1 & 0xFF), 4096);
+  VP_ETH_RD(a5, at((s1 >> 8) & 0xFF), 5120);
+  VP_ETH_RD(b0, at(d0 & 0xFF), 0);
+  VP_ETH_RD(b1, at((d0 >> 8) & 0xFF), 1024);
+  VP_ETH_RD(b2, at((d0 >> 16) & 0xFF), 2048);
+  VP_ETH_RD(b3, at(d0 >> 24), 3072);
+  VP_ETH_RD(b4, at(d1 & 0xFF), 4096);
+  VP_ETH_RD(b5, at((d1 >> 8) & 0xFF), 5120);
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(b0),
+                 "+v"(b1), "+v"(b2), "+v"(b3), "+v"(b4), "+v"(b5));
+  *hs = (a0 ^ a1 ^ a2) ^ (a3 ^ a4 ^ a5);
+  *hd = (b0 ^ b1 ^ b2) ^ (b3 ^ b4 ^ b5);
+}
+#undef VP_ETH_RD
+
 // map_get on the dynamic table keyed by words 0-1, from bucket b on;
 // *port = entry word 2.
 __device__ __forceinline__ uint32_t mac_probe_from(const TableDev &t, uint32_t b,
@@ -174,18 +208,28 @@ __global__ __launch_bounds__(256) void bridge_classify(BridgeArgs a, TouchBins b
   const uint32_t tend = min(tiles, rb * per_b + per_b);
   const uint32_t range0 = first + rb * per_b * 64;
   const uint8_t *bk = reinterpret_cast<const uint8_t *>(a.t.bk);
-  for (uint32_t tile = rb * per_b + wv; tile < tend; tile += 4) {  // wave-uniform
+  // the next tile's header chunk and port, requested behind this tile's rows
+  // (prefetch: the header load's latency under this tile's work)
+  uint4 hn = make_uint4(0, 0, 0, 0);
+  uint32_t inn = 0;
+  auto hfetch = [&](uint32_t tile) {
+    const uint32_t p = first + tile * 64 + lane;
+    if (p >= a.p0 && p < a.p1) {
+      hn = eth_words(a, p);
+      inn = a.in_dev[p];
+    }
+  };
+  uint32_t tile = rb * per_b + wv;
+  if (tile < tend) hfetch(tile);
+  for (; tile < tend; tile += 4) {  // wave-uniform
     const uint32_t p = first + tile * 64 + lane;
     const bool mine = p >= a.p0 && p < a.p1;
-    uint4 h = make_uint4(0, 0, 0, 0);
-    uint32_t in = 0;
-    if (mine) {
-      h = eth_words(a, p);
-      in = a.in_dev[p];
-    }
+    const uint4 h = mine ? hn : make_uint4(0, 0, 0, 0);
+    const uint32_t in = mine ? inn : 0u;
     const uint32_t d0 = h.x, d1 = h.y & 0xFFFF;
     const uint32_t s0 = (h.y >> 16) | (h.z << 16), s1 = h.z >> 16;
-    const uint32_t sh = eth_hash(T, s0, s1), dh = eth_hash(T, d0, d1);
+    uint32_t sh, dh;
+    eth_hash2(T, s0, s1, d0, d1, &sh, &dh);
     // bridge_get_device: the static table first (bridge_main.c:38-61)
     int32_t st_fwd = 0;
     bool st_hit = false;
@@ -197,20 +241,33 @@ __global__ __launch_bounds__(256) void bridge_classify(BridgeArgs a, TouchBins b
         st_fwd = a.st_val[k];
       }
     }
-    // both home rows in flight at once
-    uint32_t sb = home_bucket(sh, a.t.bmask, a.t.mix, lin),
-             db = home_bucket(dh, a.t.bmask, a.t.mix, lin);
-    uint4 q[8];
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
-      const uint32_t src_l = 16 * j + (lane >> 2);
-      const uint32_t r0 = __shfl(mine ? sb : kNone, src_l);
-      const uint32_t r1 = __shfl(mine && !st_hit ? db : kNone, src_l);
-      q[j] = r0 != kNone ? reinterpret_cast<const uint4 *>(bk + (size_t)r0 * 64)[lane & 3]
-                         : make_uint4(0, 0, 0, 0);
-      q[4 + j] = r1 != kNone ? reinterpret_cast<const uint4 *>(bk + (size_t)r1 * 64)[lane & 3]
-                             : make_uint4(0, 0, 0, 0);
-    }
+    // both home rows in flight at once: lane L fetches part L % 4 of the rows
+    // of packet 16 j + L / 4, the row numbers by ds_bpermute issued together
+    // and waited for once (as vignat's lean tile); kNone reads nothing
+    const uint32_t sb = home_bucket(sh, a.t.bmask, a.t.mix, lin),
+                   db = home_bucket(dh, a.t.bmask, a.t.mix, lin);
+    const uint32_t vs = mine ? sb : kNone, vd = mine && !st_hit ? db : kNone;
+    uint32_t r0, r1, r2, r3, r4, r5, r6, r7;
+    const uint32_t src = lane & ~3u;  // byte address of lane L / 4
+    asm volatile("ds_bpermute_b32 %0, %1, %2" : "=v"(r0) : "v"(src), "v"(vs));
+    asm volatile("ds_bpermute_b32 %0, %1, %2 offset:64" : "=v"(r1) : "v"(src), "v"(vs));
+    asm volatile("ds_bpermute_b32 %0, %1, %2 offset:128" : "=v"(r2) : "v"(src), "v"(vs));
+    asm volatile("ds_bpermute_b32 %0, %1, %2 offset:192" : "=v"(r3) : "v"(src), "v"(vs));
+    asm volatile("ds_bpermute_b32 %0, %1, %2" : "=v"(r4) : "v"(src), "v"(vd));
+    asm volatile("ds_bpermute_b32 %0, %1, %2 offset:64" : "=v"(r5) : "v"(src), "v"(vd));
+    asm volatile("ds_bpermute_b32 %0, %1, %2 offset:128" : "=v"(r6) : "v"(src), "v"(vd));
+    asm volatile("ds_bpermute_b32 %0, %1, %2 offset:192" : "=v"(r7) : "v"(src), "v"(vd));
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6),
+                   "+v"(r7));
+    const uint32_t part = lane & 3;
+    auto rowq = [&](uint32_t r) {
+      return r != kNone ? reinterpret_cast<const uint4 *>(bk + (size_t)r * 64)[part]
+                        : make_uint4(0, 0, 0, 0);
+    };
+    uint4 q[8] = {rowq(r0), rowq(r1), rowq(r2), rowq(r3),
+                  rowq(r4), rowq(r5), rowq(r6), rowq(r7)};
+    if (tile + 4 < tend) hfetch(tile + 4);
     uint4 srow[4], drow[4];
     wave_lds_sync();
 #pragma unroll

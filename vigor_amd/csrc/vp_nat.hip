@@ -710,11 +710,18 @@ __device__ __forceinline__ uint32_t dense128_tail(const uint4 d[8]) {
 // own (keys of other ranks routed, this rank's looked up).
 // W: waves per block (4: 256-thread blocks, four per CU; 16: one 1024-thread
 // block per CU, nat_classify64w).
+// O: owner mode compiled in (false: the single-table kernels, whose owner
+// paths -- pass 1's routing tile, nat_issue's remote keys, route notes --
+// fold away with own.n a constant 0, fewer registers for the lean tile).
 template <uint32_t G, uint32_t H = 1, bool D = false, bool X = false, bool PR = G == 0,
-          uint32_t W = 4, bool ST = false>
+          uint32_t W = 4, bool ST = false, bool O = true>
 __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins bins,
                                           TileQueue rq) {
   static_assert(!X || G == 0, "header slots (X) are 64-byte slots");
+  if constexpr (!O) {
+    a.own.n = 0;
+    a.own.all = 0;
+  }
   __shared__ uint32_t T[kNatTabWords];
   __shared__ uint4 stage[W][256];
   __shared__ uint32_t cur[kCurs];
@@ -1476,11 +1483,16 @@ __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_a
 // extra registers cost round robin 2.5 %)
 __global__ __launch_bounds__(1024, 1) void nat_classify64w(NatArgs a, uint32_t n_all,
                                                           TouchBins bins, TileQueue rq) {
-  nat_tiles<0, 1, false, false, true, 16>(a, n_all, bins, rq);
+  nat_tiles<0, 1, false, false, true, 16, false, false>(a, n_all, bins, rq);
 }
 __global__ __launch_bounds__(1024, 1) void nat_classify64ws(NatArgs a, uint32_t n_all,
                                                            TouchBins bins, TileQueue rq) {
-  nat_tiles<0, 1, false, false, true, 16, true>(a, n_all, bins, rq);
+  nat_tiles<0, 1, false, false, true, 16, true, false>(a, n_all, bins, rq);
+}
+// owner mode's pass 1 on the 1024-thread tile (nat_phase_a_owner)
+__global__ __launch_bounds__(1024, 1) void nat_classify64wo(NatArgs a, uint32_t n_all,
+                                                           TouchBins bins, TileQueue rq) {
+  nat_tiles<0, 1, false, false, true, 16>(a, n_all, bins, rq);
 }
 // (diagnostics, VIGPATH_PRIO=0: the lean tile without the raised priority)
 __global__ __launch_bounds__(256, 4) void nat_classify64_p0(NatArgs a, uint32_t n_all,
@@ -2358,26 +2370,32 @@ __device__ __forceinline__ uint32_t nat_one_reg(const NatArgs &a, const uint32_t
 
 // The server: one wave. Every poll reads the request chunks whole (ServeBox,
 // vp_internal.h: one PCIe read brings the doorbell, the time and a frame of up
-// to kServeInline bytes), one poll in flight (or, VIGPATH_SERVE_POLLS, two
-// or four, staggered); longer frames are read from `frame` afterwards. The frame goes into LDS, the
+// to kServeInline bytes), one poll in flight per wave (VIGPATH_SERVE_WAVES
+// waves poll, staggered; the first to claim a request serves it); longer frames are read from `frame` afterwards. The frame goes into LDS, the
 // wave sums the L4 bytes past byte 64, lane 0 runs the packet, the frame goes
 // back (16-byte system-coherent stores) and the answer word follows once
 // every store has completed. Packets take global sequence numbers seq, seq +
 // 1, ... It leaves on the leave request or after `idle` wall-clock ticks
 // without a request; a request posted as it leaves finds the stream idle and
 // the host launches it again (nat_process_one). flags: bit 0, the stage
-// clock (VIGPATH_SERVE_PROF); bits 1-2: log2 of the polls in flight, plus 1;
-// bits 3-9: their spacing in wall-clock ticks.
-__global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64_t seq,
-                                                uint64_t idle, uint32_t flags) {
+// clock (VIGPATH_SERVE_PROF); bits 3-9: the waves' stagger in wall-clock ticks.
+__global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint64_t seq0,
+                                                 uint64_t idle, uint32_t flags) {
   __shared__ uint32_t T[kNatTabWords];
   __shared__ uint4 fr[kServeFrame / 16];
-  load_nat_tables(T, a);
-  const uint32_t lane = threadIdx.x;
+  __shared__ uint32_t done_s, claim_s;  // the last answered / claimed request
+  __shared__ uint64_t t0_s;             // the last answer's wall clock
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    const uint32_t d = (uint32_t)__hip_atomic_load(&box->ans, __ATOMIC_ACQUIRE,
+                                                   __HIP_MEMORY_SCOPE_SYSTEM);
+    done_s = d;
+    claim_s = d;
+    t0_s = wall_clock64();
+  }
+  load_nat_tables(T, a);  // (its barrier covers the words above)
+  const uint32_t done0 = done_s;
   const bool prof = flags & 1u;
-  uint32_t done = (uint32_t)__hip_atomic_load(&box->ans, __ATOMIC_ACQUIRE,
-                                              __HIP_MEMORY_SCOPE_SYSTEM);
-  done = __builtin_amdgcn_readfirstlane(done);
   typedef unsigned v4u __attribute__((ext_vector_type(4)));
   constexpr int kSys = 17;  // sc0 | sc1: system-coherent (bypasses the GPU caches)
   const auto ms = __builtin_amdgcn_make_buffer_rsrc(box->msg, 0, 16 * kServeChunks, 0x00020000);
@@ -2385,12 +2403,14 @@ __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64
   // (lanes past the chunks read nothing: an offset past the resource)
   const int moff = lane < kServeChunks ? (int)(16 * lane) : (int)(16 * kServeChunks);
   auto poll = [&]() -> v4u { return __builtin_amdgcn_raw_buffer_load_b128(ms, moff, 0, kSys); };
+  auto lds_ld = [](uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
   uint32_t *fw = reinterpret_cast<uint32_t *>(fr);
-  uint64_t t0 = wall_clock64();
-  // one poll's chunks: -1 nothing new (or not yet whole), 0 a request served,
-  // 1 leave
+  // one poll's chunks: -1 nothing new (not yet whole, or another wave's),
+  // 0 a request served, 1 leave
   auto serve = [&](const v4u &c) -> int {
-    const uint32_t want = done + 1;
+    const uint32_t want = __builtin_amdgcn_readfirstlane(lds_ld(&done_s)) + 1;
     const uint32_t tag0 = __builtin_amdgcn_readfirstlane(c[3]);
     if (tag0 != want) return -1;
     const uint32_t hi = __builtin_amdgcn_readfirstlane(c[0]);
@@ -2399,7 +2419,12 @@ __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64
     const bool inl = len <= kServeInline;
     const uint32_t need = inl ? (12 + len + 11) / 12 : 1u;  // chunks carrying it
     if (__ballot(lane < need && c[3] != want)) return -1;  // not whole yet: poll again
+    // one wave serves it: the first to claim it
+    uint32_t won = 0;
+    if (lane == 0) won = atomicCAS(&claim_s, want - 1, want) == want - 1;
+    if (!__builtin_amdgcn_readfirstlane(won)) return -1;
     const uint64_t s0 = wall_clock64();
+    const uint64_t seq = seq0 + (want - done0 - 1);
     const int64_t now =
         (int64_t)((uint64_t)__builtin_amdgcn_readfirstlane(c[1]) |
                   ((uint64_t)__builtin_amdgcn_readfirstlane(c[2]) << 32));
@@ -2416,7 +2441,7 @@ __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64
         fr[i] = make_uint4(v[0], v[1], v[2], v[3]);
       }
     }
-    __syncthreads();
+    wave_lds_sync();
     // the L4 checksum's bytes past 64: [64, min(14 + total_length, len))
     uint32_t tail = 0;
     if (len > 64) {
@@ -2453,7 +2478,7 @@ __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64
       }
       res = out | (fresh << 16);
     }
-    __syncthreads();
+    wave_lds_sync();
     const uint64_t s2 = wall_clock64();
     for (uint32_t i = lane; i < nch; i += 64) {
       const uint4 v = fr[i];
@@ -2465,7 +2490,7 @@ __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64
         auto put = [&](int k, uint64_t v) {
           __hip_atomic_store(&box->prof[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         };
-        put(0, t0);
+        put(0, t0_s);
         put(1, s0);
         put(2, s1);
         put(3, mk0);
@@ -2481,49 +2506,35 @@ __global__ __launch_bounds__(64) void nat_serve(NatArgs a, ServeBox *box, uint64
       __builtin_amdgcn_s_waitcnt(0);
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       __hip_atomic_store(&box->ans, ans, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      t0_s = wall_clock64();
+      // (the table writes of this request before the next request's wave
+      // reads them: the waves share the CU, workgroup scope; an agent-scope
+      // release would write the XCD's L2 back)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __hip_atomic_store(&done_s, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    done = want;
-    seq += 1;
-    t0 = wall_clock64();
+    wave_lds_sync();
     return 0;
   };
-  // polls in flight (flags bits 1-2: 1, 2 or 4), a fraction of a round trip
-  // apart (the first round trips set the spacing; each slot re-polls when its
-  // result is in)
-  const uint32_t np = (flags >> 1) & 3u ? 1u << (((flags >> 1) & 3u) - 1) : 1u;
-  const uint32_t gap = (flags >> 3) & 0x7Fu;  // wall-clock ticks (10 ns) between polls
-  auto pause = [&]() {
+  // every wave polls on its own (flags bits 3-9: the waves' stagger, in
+  // wall-clock ticks), one poll in flight per wave: a wave's polls return in
+  // order, so polls queued behind a stale one would see a request late
+  const uint32_t gap = (flags >> 3) & 0x7Fu;
+  {
     const uint64_t w = wall_clock64();
-    while (wall_clock64() - w < gap) __builtin_amdgcn_s_sleep(1);
-  };
-  auto slot = [&](v4u &q) -> bool {  // false: leave
+    while (wall_clock64() - w < (uint64_t)gap * wv) __builtin_amdgcn_s_sleep(1);
+  }
+  for (;;) {
+    const v4u q = poll();
     const int st = serve(q);
-    if (st == 1) return false;
-    if (st < 0 && wall_clock64() - t0 > idle) return false;
-    if (st < 0 && np == 1) __builtin_amdgcn_s_sleep(1);
-    q = poll();
-    return true;
-  };
-  v4u q0 = poll();
-  if (np == 1) {
-    while (slot(q0)) {
-    }
-  } else if (np == 2) {
-    pause();
-    v4u q1 = poll();
-    while (slot(q0) && slot(q1)) {
-    }
-  } else {
-    pause();
-    v4u q1 = poll();
-    pause();
-    v4u q2 = poll();
-    pause();
-    v4u q3 = poll();
-    while (slot(q0) && slot(q1) && slot(q2) && slot(q3)) {
+    if (st == 1) break;
+    if (st < 0) {
+      if (wall_clock64() - __hip_atomic_load(&t0_s, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP) > idle)
+        break;
+      __builtin_amdgcn_s_sleep(1);
     }
   }
-  __builtin_amdgcn_s_waitcnt(0);  // (no poll left in flight)
 }
 
 // =============================================================== host ==
@@ -2621,7 +2632,7 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
     // pass 1: the 1024-thread tile unless VIGPATH_BLOCK_WAVES=4 (one block
     // per CU: four times fewer, longer key slices)
     const uint32_t tw = nat_block_waves();
-    ph->grid1 = tw == 16 ? resident_grid((const void *)nat_classify64w, (tiles + 15) / 16, 1024)
+    ph->grid1 = tw == 16 ? resident_grid((const void *)nat_classify64wo, (tiles + 15) / 16, 1024)
                          : resident_grid((const void *)nat_classify64, (tiles + 3) / 4);
     ph->range1 = (tiles + ph->grid1 - 1) / ph->grid1 * 64;
     VP_TRY(tbl_bins_plan(c, t, (const void *)nat_remote64, p0, p1, &ph->bp));
@@ -2674,7 +2685,7 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
       if (ph->bp.on) a1.log = nullptr;  // pass 2 bins every touch
       const TileQueue rq1{w.reprobe, w.reprobe_cnt, &t.ctl->reprobe_count};
       if (nat_block_waves() == 16)
-        nat_classify64w<<<ph->grid1, 1024, 0, c->stream>>>(a1, b->n, TouchBins{}, rq1);
+        nat_classify64wo<<<ph->grid1, 1024, 0, c->stream>>>(a1, b->n, TouchBins{}, rq1);
       else
         nat_classify64<<<ph->grid1, 256, 0, c->stream>>>(a1, b->n, TouchBins{}, rq1);
     } else {
@@ -3385,19 +3396,19 @@ static int serve_launch(vp_ctx *c) {
   a.n_dev = c->nat.n_devices;
   ServeBox *dbox = nullptr;
   VP_HIP(hipHostGetDevicePointer((void **)&dbox, c->sbox, 0));
-  // polls in flight (VIGPATH_SERVE_POLLS: 1, 2 or 4) and their spacing
+  // polling waves (VIGPATH_SERVE_WAVES: 1, 2 or 4) and their stagger
   // (VIGPATH_SERVE_GAP, wall-clock ticks of 10 ns)
-  static const uint32_t polls = [] {
-    const char *e = getenv("VIGPATH_SERVE_POLLS");
+  static const uint32_t waves = [] {
+    const char *e = getenv("VIGPATH_SERVE_WAVES");
     const int v = e ? atoi(e) : 1;
-    return v == 4 ? 3u : v == 2 ? 2u : 1u;
+    return v == 4 ? 4u : v == 2 ? 2u : 1u;
   }();
   static const uint32_t gap = [] {
     const char *e = getenv("VIGPATH_SERVE_GAP");
     return e ? (uint32_t)std::min(127, std::max(0, atoi(e))) : 35u;
   }();
-  nat_serve<<<1, 64, 0, c->stream>>>(a, dbox, c->seq, c->srv_idle,
-                                     (g_srv_prof ? 1u : 0u) | (polls << 1) | (gap << 3));
+  nat_serve<<<1, 64 * waves, 0, c->stream>>>(a, dbox, c->seq, c->srv_idle,
+                                             (g_srv_prof ? 1u : 0u) | (gap << 3));
   VP_HIP(hipGetLastError());
   if (!c->srv_on) {
     static std::once_flag once;
