@@ -1369,6 +1369,8 @@ __device__ __forceinline__ void nat_tiles_pipe(NatArgs a, uint32_t n_all, TouchB
     if (more) take(tile + tstep, ns);  // (retires tile's row DMA)
     uint4 row[4];
     if (cs.lean) {
+      // (the last tile: no frames were waited for after its row DMA)
+      if (!more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       wave_lds_sync();
 #pragma unroll
       for (uint32_t k = 0; k < 4; k++) row[k] = R[chunk_swz(4 * lane + k)];
