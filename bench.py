@@ -803,11 +803,7 @@ def kernel_label(knames, default):
 def probe_waves(kernel: str) -> int:
     """Waves per block of the tile kernel's grid (vp_probe_slots_w)."""
     k = kernel.split(" ")[0]
-    if k.startswith("nat_classify64w") or k.endswith("64w"):
-        return 16
-    if k.startswith("nat_classify64p"):
-        return 12 if k.endswith("12") else 8
-    return 4
+    return 16 if k.startswith("nat_classify64w") or k.endswith("64w") else 4
 
 
 def kernel_rate(kms, B, steps, alg_bytes):

@@ -1199,293 +1199,6 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
   route_publish(a, cur + kCurDest, rb);
 }
 
-// Phase A over 64-byte slots, software-pipelined across two tiles (DESIGN.md
-// §5.1, round 6): while a wave matches, rewrites and stores tile t, the
-// bucket rows of tile t + 1 and the frames of tile t + 2 are in flight.
-// nat_tiles<0> waits for a tile's rows right after it requests them (only
-// the other waves of its SIMD hide that latency: traffic whose rows miss the
-// L2s -- uniform order, random 5-tuples -- runs well below its memory
-// shape's speed). The rows come in by LDS-DMA (global_load_lds_dwordx4,
-// MI355X_MICROARCH.md; a lane's source address is its row piece, the LDS
-// image lane-linear with the swizzle on the source side), so the rows in
-// flight hold no registers; each wave has a row tile R beside its frame tile
-// S (8 KiB of LDS per wave). Each iteration:
-//   1. the frames of tile t + 1 (fetched an iteration ago) to registers
-//      through S (waiting for them also retires tile t's row DMA, issued
-//      before them);
-//   2. tile t + 1 lean (every lane a fast-path LAN packet): its hash and
-//      home buckets; tile t's rows out of R into registers; tile t + 1's row
-//      DMA into R; the frames of tile t + 2 requested;
-//   3. the back half of tile t: match, rewrite, bins, store -- or, a tile
-//      that is not lean, nat_issue / rows / nat_finish as in nat_tiles.
-// W = 16 (128 VGPRs; LDS leaves no room for staged bin lines) or 12 (three
-// waves per SIMD, 168 VGPRs, ST: whole-line bin entries as
-// nat_classify64ws). Single-table vignat only (owner mode keeps nat_tiles).
-template <uint32_t W, bool ST>
-__device__ __forceinline__ void nat_tiles_pipe(NatArgs a, uint32_t n_all, TouchBins bins,
-                                               TileQueue rq) {
-  a.own.n = 0;  // (single table: the owner paths fold away)
-  a.own.all = 0;
-  __shared__ uint32_t T[kNatTabWords];
-  __shared__ uint4 stage[W][256];
-  __shared__ uint4 rowbuf[W][256];
-  __shared__ uint32_t cur[kCurs];
-  __shared__ uint32_t mbase;
-  __shared__ uint32_t nruns;  // this block's run tiles (Ctl::run_tiles)
-  __shared__ uint32_t sring[ST ? kStageBins * kStageLines * 16 : 1];
-  __shared__ uint32_t swc[ST ? kStageBins * kStageLines : 1];
-  __shared__ uint32_t sgen[ST ? kStageBins * kStageLines : 1];
-  const BinStage bst{sring, swc, sgen};
-  const bool staged = ST && bins.ent && bins.bbits <= 7 && a.bstage;
-  if (ST) bins_stage_init(bst);
-  if (threadIdx.x == 0) nruns = 0;
-  for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
-  load_nat_tables(T, a);  // (its barrier also covers cur)
-  const uint4 *rows = reinterpret_cast<const uint4 *>(a.t.bk);
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint4 *S = stage[wv];
-  uint4 *R = rowbuf[wv];
-  // the row piece a lane's DMA fetches: lane L of instruction j lands at
-  // chunk 64 j + L of R, which chunk_swz maps to packet 16 j + L / 4, part
-  // (L ^ L >> 4) & 3
-  const uint32_t pk = (lane ^ (lane >> 4)) & 3u;
-  const uint32_t first = a.p0 & ~63u;
-  const uint32_t tiles = (a.p1 - first + 63) / 64;
-  const bool lean_ok = rq.ent != nullptr;
-  const uint32_t rb = blockIdx.x;
-  const uint32_t per_b = (tiles + gridDim.x - 1) / gridDim.x;
-  const uint32_t tend = min(tiles, rb * per_b + per_b);
-  const uint32_t range0 = first + rb * per_b * 64;
-  uint4 r[4];  // the prefetched frames of the next tile
-  uint32_t r_in = 0, r_len = 0;
-  auto fetch = [&](uint32_t tile) {
-    const uint32_t tb = first + tile * 64;
-    const uint4 *g = reinterpret_cast<const uint4 *>(a.frames + (size_t)tb * 64);
-    const uint32_t p = tb + lane;
-    if (tb + 64 <= n_all) {  // (wave-uniform) a whole tile
-#pragma unroll
-      for (uint32_t j = 0; j < 4; j++) r[j] = tile_ld(g + 64 * j + lane);
-      r_in = port_of(a.in_dev, a.in0, p);
-      r_len = a.len[p];
-      return;
-    }
-    const uint32_t avail = n_all - tb;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
-      const uint32_t c = 64 * j + lane;
-      r[j] = (c >> 2) < avail ? tile_ld(g + c) : make_uint4(0, 0, 0, 0);
-    }
-    r_in = p < n_all ? port_of(a.in_dev, a.in0, p) : 0u;
-    r_len = p < n_all ? a.len[p] : 0u;
-  };
-  struct TileSt {
-    RFrame f;
-    uint32_t in, ln, lh, b;
-    bool lean;
-  };
-  // step 1 for `tile` (its frames in r)
-  auto take = [&](uint32_t tile, TileSt &s) {
-    wave_lds_sync();
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = r[j];
-    wave_lds_sync();
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-      const uint4 v = S[chunk_swz(4 * lane + k)];
-      s.f.w[4 * k] = v.x;
-      s.f.w[4 * k + 1] = v.y;
-      s.f.w[4 * k + 2] = v.z;
-      s.f.w[4 * k + 3] = v.w;
-    }
-    s.in = r_in;
-    s.ln = r_len;
-    const uint32_t p = first + tile * 64 + lane;
-    const bool mine = p >= a.p0 && p < a.p1;
-    s.lean = lean_ok && __ballot(mine && nat_lan_fast_ok(a, s.f, s.in, s.ln, 50u)) == ~0ull;
-  };
-  // step 2's hash and row DMA for a lean tile (R free: the rows it held are
-  // in registers)
-  auto rows_dma = [&](TileSt &s) {
-    __builtin_amdgcn_s_setprio(1);
-    const uint32_t proto = s.f.w[5] >> 24;
-    s.lh = flowid_hash_batched(T, s.f.w[8] >> 16, s.f.w[9] & 0xFFFF, s.f.u32at2(26),
-                               s.f.u32at2(30), s.in, proto);
-    s.b = home_bucket(s.lh, a.t.bmask, a.t.mix, nat_lin(T));
-    uint32_t b0, b1, b2, b3;
-    const uint32_t src = lane & ~3u;  // byte address of lane L / 4
-    asm volatile("ds_bpermute_b32 %0, %1, %2" : "=v"(b0) : "v"(src), "v"(s.b));
-    asm volatile("ds_bpermute_b32 %0, %1, %2 offset:64" : "=v"(b1) : "v"(src), "v"(s.b));
-    asm volatile("ds_bpermute_b32 %0, %1, %2 offset:128" : "=v"(b2) : "v"(src), "v"(s.b));
-    asm volatile("ds_bpermute_b32 %0, %1, %2 offset:192" : "=v"(b3) : "v"(src), "v"(s.b));
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
-    typedef __attribute__((address_space(3))) void *lds_ptr;
-    __builtin_amdgcn_global_load_lds(rows + 4 * (size_t)b0 + pk, (lds_ptr)(R), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(rows + 4 * (size_t)b1 + pk, (lds_ptr)(R + 64), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(rows + 4 * (size_t)b2 + pk, (lds_ptr)(R + 128), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(rows + 4 * (size_t)b3 + pk, (lds_ptr)(R + 192), 16, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  auto miss_put = [&](uint32_t tile, bool miss, const uint32_t key[4], uint32_t h) {
-    if (!a.mq) {
-      if (miss) miss_add(a, first + tile * 64 + lane, key, h);
-      return;
-    }
-    const uint32_t k = group_reserve(cur, kCurMiss, miss);
-    const size_t at = (size_t)rb * per_b * 64 + k;
-    if (miss) a.mq[at] = tile * 64 + first + lane;
-    if (miss && a.mkq) {
-      a.mkq[at] = make_uint4(key[0], key[1], key[2], key[3]);
-      a.mhq[at] = h;
-    }
-  };
-  auto store_tile = [&](uint4 *g, const RFrame &f, uint64_t mm) {
-    wave_lds_sync();
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++)
-      S[chunk_swz(4 * lane + k)] =
-          make_uint4(f.w[4 * k], f.w[4 * k + 1], f.w[4 * k + 2], f.w[4 * k + 3]);
-    wave_lds_sync();
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
-      const uint32_t c = 64 * j + lane;
-      if ((mm >> (c >> 2)) & 1ull) tile_st(g, c, S[chunk_swz(c)]);
-    }
-  };
-  uint32_t tile = rb * per_b + wv;
-  const uint32_t tstep = W;
-  TileSt cs;
-  if (tile < tend) {
-    fetch(tile);
-    take(tile, cs);
-    if (cs.lean) rows_dma(cs);
-    if (tile + tstep < tend) fetch(tile + tstep);
-  }
-  for (; tile < tend; tile += tstep) {
-    // ---- steps 1 and 2: the next tile's frames and row requests
-    TileSt ns;
-    ns.lean = false;
-    const bool more = tile + tstep < tend;
-    if (more) take(tile + tstep, ns);  // (retires tile's row DMA)
-    uint4 row[4];
-    if (cs.lean) {
-      // (the last tile: no frames were waited for after its row DMA)
-      if (!more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      wave_lds_sync();
-#pragma unroll
-      for (uint32_t k = 0; k < 4; k++) row[k] = R[chunk_swz(4 * lane + k)];
-      // (R is read before the next rows' DMA overwrites it)
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(row[0].x), "+v"(row[0].y), "+v"(row[0].z), "+v"(row[0].w),
-                     "+v"(row[1].x), "+v"(row[1].y), "+v"(row[1].z), "+v"(row[1].w),
-                     "+v"(row[2].x), "+v"(row[2].y), "+v"(row[2].z), "+v"(row[2].w),
-                     "+v"(row[3].x), "+v"(row[3].y), "+v"(row[3].z), "+v"(row[3].w));
-      wave_lds_sync();
-    }
-    if (more) {
-      if (ns.lean) rows_dma(ns);
-      if (tile + 2 * tstep < tend) fetch(tile + 2 * tstep);
-    }
-    // ---- step 3: the back half of this tile
-    const uint32_t tb = first + tile * 64;
-    uint4 *g = reinterpret_cast<uint4 *>(a.frames + (size_t)tb * 64);
-    const uint32_t p = tb + lane;
-    uint32_t touch = kNone;
-    if (cs.lean) {
-      const uint32_t proto = cs.f.w[5] >> 24;
-      const uint32_t key[4] = {(cs.f.w[8] >> 16) | ((cs.f.w[9] & 0xFFFF) << 16),
-                               cs.f.u32at2(26), cs.f.u32at2(30), cs.in | (proto << 16)};
-      bool done;
-      const uint32_t idx =
-          lean_walk(a, rows, cs.b, key, bucket_match_sel(row, key, &done), &done);
-      const bool hit = done & (idx != kNone);
-      log_put(a.log, p, hit ? idx : kNone);  // (null while the bins are on)
-      if (__ballot(!hit)) {  // misses (phase B) and longer walks (reprobes)
-        miss_put(tile, done & !hit, key, cs.lh);
-        const uint32_t k = group_reserve(cur, kCurReprobe, !done);
-        if (!done) rq.ent[(size_t)rb * per_b * 64 + k] = p;
-      }
-      if (hit) {
-        touch = idx;
-        cs.f.set32at2(26, a.ext_ip);                     // src_addr = external_addr
-        cs.f.set16(34, (uint16_t)(a.start_port + idx));  // src_port = external port
-        fast_checksums(cs.f, proto, bswap16((uint16_t)(cs.f.w[4] & 0xFFFF)), 0u);
-        cs.f.w[0] = a.wan_macw0;
-        cs.f.w[1] = a.wan_macw1;
-        cs.f.w[2] = a.wan_macw2;
-        a.out[p] = (uint16_t)a.wan;
-      }
-      store_tile(g, cs.f, ~0ull);  // (misses stored unchanged)
-    } else {
-      // ---- per-lane tile (nat_issue / nat_finish), its rows waited for here
-      const bool mine = p >= a.p0 && p < a.p1;
-      const NatPend pend = nat_issue(a, T, p, cs.f, cs.in, cs.ln, mine, 50u);
-      uint4 q[4];
-#pragma unroll
-      for (uint32_t j = 0; j < 4; j++) {
-        const uint32_t rw = __shfl(pend.row, 16 * j + (lane >> 2));
-        q[j] = rw != kNone ? rows[4 * (size_t)rw + (lane & 3)] : make_uint4(0, 0, 0, 0);
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (uint32_t j = 0; j < 4; j++) S[chunk_swz(64 * j + lane)] = q[j];
-      wave_lds_sync();
-      uint4 prow[4];
-#pragma unroll
-      for (uint32_t k = 0; k < 4; k++) prow[k] = S[chunk_swz(4 * lane + k)];
-      bool m = false;
-      if (mine) m = nat_finish(a, T, pend, prow, p, cs.f, cs.in, cs.ln, touch, 0u);
-      {  // queue on this block's reprobe slice
-        const bool v = touch == kReprobe;
-        const uint32_t k = group_reserve(cur, kCurReprobe, v);
-        if (v) rq.ent[(size_t)rb * per_b * 64 + k] = p;
-      }
-      if (touch == kReprobe) touch = kNone;
-      const uint64_t mm = __ballot(m);
-      if (mm) store_tile(g, cs.f, mm);
-    }
-    if (staged)
-      bins_put_staged(bins, bst, cur, rb, per_b * 64, range0, p, touch, &nruns);
-    else
-      bins_put(bins, cur, rb, per_b * 64, range0, p, touch, &nruns);
-    if (more) cs = ns;
-  }
-  __builtin_amdgcn_s_waitcnt(0);  // (no row DMA left in flight)
-  __syncthreads();
-  if (staged) bins_flush_staged(bins, bst, cur, rb);
-  if (threadIdx.x == 0 && nruns) atomicAdd(&a.t.ctl->run_tiles, nruns);
-  bins_publish(bins, cur, rb);
-  if (threadIdx.x == 0) {
-    const uint32_t c = cur[kCurReprobe];
-    rq.cnt[rb] = c;
-    if (c) atomicAdd(rq.total, c);
-  }
-  if (a.mq) {  // the block's lean-tile misses onto the phase-B list (one atomic)
-    const uint32_t c = cur[kCurMiss];
-    if (threadIdx.x == 0 && c) mbase = atomicAdd(&a.t.ctl->miss_count, c);
-    __syncthreads();
-    const size_t s0 = (size_t)rb * per_b * 64;
-    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x)
-      a.miss[mbase + i] = a.mkq ? (uint32_t)(s0 + i) | kMissSlice : a.mq[s0 + i];
-  }
-}
-
-// The pipelined tiles (nat_tiles_pipe): 16 waves per block (one 1024-thread
-// block per CU), and 12 (768 threads, three waves per SIMD) with or without
-// whole-line bin entries.
-__global__ __launch_bounds__(1024, 1) void nat_classify64p(NatArgs a, uint32_t n_all,
-                                                          TouchBins bins, TileQueue rq) {
-  nat_tiles_pipe<16, false>(a, n_all, bins, rq);
-}
-__global__ __launch_bounds__(768, 1) void nat_classify64p12(NatArgs a, uint32_t n_all,
-                                                           TouchBins bins, TileQueue rq) {
-  nat_tiles_pipe<12, false>(a, n_all, bins, rq);
-}
-__global__ __launch_bounds__(768, 1) void nat_classify64ps12(NatArgs a, uint32_t n_all,
-                                                            TouchBins bins, TileQueue rq) {
-  nat_tiles_pipe<12, true>(a, n_all, bins, rq);
-}
-
 __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_all,
                                                         TouchBins bins, TileQueue rq) {
   nat_tiles<0>(a, n_all, bins, rq);
@@ -1559,9 +1272,6 @@ static uint32_t nat_block_waves() {
 static const char *nat_tile_kernel_name(NatTileKernel k) {
   return k == nat_classify64w    ? "nat_classify64w"
          : k == nat_classify64ws ? "nat_classify64ws"
-         : k == nat_classify64p  ? "nat_classify64p"
-         : k == nat_classify64p12 ? "nat_classify64p12"
-         : k == nat_classify64ps12 ? "nat_classify64ps12"
          : k == nat_classify64   ? "nat_classify64"
          : k == nat_classify64x  ? "nat_classify64x"
          : k == nat_classify64_p0 ? "nat_classify64_p0"
@@ -1569,33 +1279,16 @@ static const char *nat_tile_kernel_name(NatTileKernel k) {
                                  : "nat_classify_wide";
 }
 
-// The pipelined tiles (nat_tiles_pipe) for single-table vignat:
-// VIGPATH_PIPE = 16 or 12 waves per block (0: off).
-static uint32_t nat_pipe_waves() {
-  static const uint32_t w = [] {
-    const char *e = getenv("VIGPATH_PIPE");
-    const int v = e ? atoi(e) : 0;
-    return v == 16 || v == 12 ? (uint32_t)v : 0u;
-  }();
-  return w;
-}
-
 static uint32_t nat_tile_waves(NatTileKernel k) {
-  return k == nat_classify64w || k == nat_classify64ws || k == nat_classify64p  ? 16u
-         : k == nat_classify64p12 || k == nat_classify64ps12                     ? 12u
-                                                                                 : 4u;
+  return k == nat_classify64w || k == nat_classify64ws ? 16u : 4u;
 }
 
 static NatTileKernel nat_tile_kernel(uint32_t slot, bool hdr_tail = false,
-                                     bool staged = false, bool single = true) {
+                                     bool staged = false) {
   static const bool p0 = [] {
     const char *e = getenv("VIGPATH_PRIO");
     return e && atoi(e) == 0;
   }();
-  if (slot == 64 && !hdr_tail && single && nat_pipe_waves() == 16)
-    return staged ? nat_classify64ws : nat_classify64p;
-  if (slot == 64 && !hdr_tail && single && nat_pipe_waves() == 12)
-    return staged ? nat_classify64ps12 : nat_classify64p12;
   if (slot == 64 && !hdr_tail && nat_block_waves() == 16)
     return staged ? nat_classify64ws : nat_classify64w;
   if (slot == 64) return hdr_tail ? nat_classify64x : p0 ? nat_classify64_p0 : nat_classify64;
@@ -3158,7 +2851,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // per block (TileQueue)
   const bool tiles64 = owner ? ph.tiles64 : p1 > p0 && c->coalesced_io;
   // (staged bin lines unless the last segment's tiles were mostly runs)
-  const NatTileKernel tk = nat_tile_kernel(b->slot, a.tail != nullptr, !t.runs_seen, !owner);
+  const NatTileKernel tk = nat_tile_kernel(b->slot, a.tail != nullptr, !t.runs_seen);
   const uint32_t tw = nat_tile_waves(tk);
   BinsPlan bp = ph.bp;
   uint32_t grid64 = ph.grid1, range64 = ph.range1;
