@@ -47,10 +47,10 @@ for step in "$@"; do
              > $O/${TAG}_kt.log 2>&1 || exit $? ;;
     pmc) rm -rf $O/${TAG}_fetch $O/${TAG}_write
          run pmc_fetch 180 rocprofv3 --pmc FETCH_SIZE --output-format csv \
-           -d $O/${TAG}_fetch -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-e2e $BA \
+           -d $O/${TAG}_fetch -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-e2e --no-extra $BA \
            > $O/${TAG}_fetch.log 2>&1 || exit $?
          run pmc_write 180 rocprofv3 --pmc WRITE_SIZE --output-format csv \
-           -d $O/${TAG}_write -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-e2e $BA \
+           -d $O/${TAG}_write -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-e2e --no-extra $BA \
            > $O/${TAG}_write.log 2>&1 || exit $? ;;
     pmcnf:*) nf=${step#pmcnf:}
          rm -rf $O/${TAG}_${nf}_fetch $O/${TAG}_${nf}_write
