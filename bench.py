@@ -59,7 +59,7 @@ METRIC = "Mpackets/s device-resident, 64B vignat @1M flows; %HBM roofline"
 ALG_BYTES = 92          # 64 frame + 4 len/port + 16 key + 4 tag + 4 value
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SLOT = 64
-TRAFFIC_PROFILE = "r05zl_bench_traffic.json"  # rocprofv3 --pmc passes (tools/gpu_session.sh pmc)
+TRAFFIC_PROFILE = "r06g_bench_traffic.json"  # rocprofv3 --pmc passes (tools/gpu_session.sh pmc)
 DEV_MACS = [T.mac("02:00:00:00:00:00"), T.mac("02:00:00:00:00:01")]
 NAT_ARGS = ["--expire", "60000000", "--starting-port", "0", "--wan", "1",
             "--extip", "192.168.4.2", "--eth-dest", "0,90:e2:ba:55:12:20",
@@ -1035,7 +1035,7 @@ def main():
     if args.route_all:
         workload = ("vignat %dB, %d flows, 1xMI355X, owner-mode pipeline with every key "
                     "routed through a one-rank RCCL exchange (profiling)" % (flen, args.flows))
-    if (world > 1 and mode == "owner") or args.route_all:
+    if ((world > 1 and mode == "owner") or args.route_all) and "+" not in kname:
         kname += "+nat_remote64"
     extra = {}
     if not args.no_extra and world == 1 and args.order == "rr":
