@@ -2388,12 +2388,13 @@ static int nat_phase_a_owner(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
       a1.mq = w.missq;
       if (ph->bp.on) a1.log = nullptr;  // pass 2 bins every touch
       const TileQueue rq1{w.reprobe, w.reprobe_cnt, &t.ctl->reprobe_count};
-      if (nat_block_waves() == 16)
+      if (nat_block_waves() == 16) {
         c->last_kernel = "nat_classify64wo+nat_remote64";
         nat_classify64wo<<<ph->grid1, 1024, 0, c->stream>>>(a1, b->n, TouchBins{}, rq1);
-      else
+      } else {
         c->last_kernel = "nat_classify64+nat_remote64";
         nat_classify64<<<ph->grid1, 256, 0, c->stream>>>(a1, b->n, TouchBins{}, rq1);
+      }
     } else {
       nat_classify<<<ph->grid1, 256, 0, c->stream>>>(a);
     }
