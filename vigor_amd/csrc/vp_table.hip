@@ -370,9 +370,13 @@ __global__ void nku_dedup(NkuArgs m) {
     const uint4 kj = nku_key(m, j);
     const uint32_t h = nku_hash(m, j);
     uint32_t s = home_bucket(h, m.smask, kMixMul);
+    // (plain loads, which the XCD's L2 may serve stale: a slot word is
+    // written once per call, from an older tag to this call's by the CAS, so
+    // a stale word is an older tag, the CAS fails and returns the real one;
+    // a stale fp / lp only costs an atomicMax that was not needed. Device-
+    // scope loads bypassed the L2 on every probe.)
     for (;;) {
-      unsigned long long cur = __hip_atomic_load(&ord[s], __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
+      unsigned long long cur = ord[s];
       if ((cur >> 32) != m.tag) {  // an empty slot (an older tag): claim it
         const unsigned long long old = atomicCAS(&ord[s], cur, tg | j);
         if (old == cur) break;
@@ -389,10 +393,8 @@ __global__ void nku_dedup(NkuArgs m) {
     // (read first: a key's packets mostly arrive after its earliest and
     // before its latest was seen, and a load is cheaper than an atomic)
     const unsigned long long f = tg | (unsigned long long)(~p), l = tg | (unsigned long long)p;
-    if (f > __hip_atomic_load(&fp[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-      atomicMax(&fp[s], f);
-    if (l > __hip_atomic_load(&lp[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-      atomicMax(&lp[s], l);
+    if (f > fp[s]) atomicMax(&fp[s], f);
+    if (l > lp[s]) atomicMax(&lp[s], l);
   }
 }
 
