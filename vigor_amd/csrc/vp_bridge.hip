@@ -188,9 +188,12 @@ __device__ __forceinline__ uint32_t mac_match(const uint4 *row, uint32_t m0, uin
 // dst home buckets are fetched together, four lanes per 64-byte row
 // (wave-cooperative, one request per row), then handed to their lanes
 // through LDS; a probe that continues past its home bucket walks on alone.
-__global__ __launch_bounds__(256) void bridge_classify(BridgeArgs a, TouchBins bins) {
+// W: waves per block (4; 16, one 1024-thread block per CU sharing one copy
+// of the tables, bridge_classify_w: VIGPATH_BRIDGE_WAVES=16).
+template <uint32_t W>
+__device__ __forceinline__ void bridge_tiles(BridgeArgs a, TouchBins bins) {
   __shared__ uint32_t T[kBridgeTabs * 256 + 1024];  // + the layout's tables
-  __shared__ uint4 stage[4][256];
+  __shared__ uint4 stage[W][256];
   __shared__ uint32_t cur[kCurs];
   for (uint32_t i = threadIdx.x; i < kCurs; i += blockDim.x) cur[i] = 0;
   for (uint32_t i = threadIdx.x; i < kBridgeTabs * 256; i += blockDim.x)
@@ -221,7 +224,7 @@ __global__ __launch_bounds__(256) void bridge_classify(BridgeArgs a, TouchBins b
   };
   uint32_t tile = rb * per_b + wv;
   if (tile < tend) hfetch(tile);
-  for (; tile < tend; tile += 4) {  // wave-uniform
+  for (; tile < tend; tile += W) {  // wave-uniform
     const uint32_t p = first + tile * 64 + lane;
     const bool mine = p >= a.p0 && p < a.p1;
     const uint4 h = mine ? hn : make_uint4(0, 0, 0, 0);
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(256) void bridge_classify(BridgeArgs a, TouchBins b
     };
     uint4 q[8] = {rowq(r0), rowq(r1), rowq(r2), rowq(r3),
                   rowq(r4), rowq(r5), rowq(r6), rowq(r7)};
-    if (tile + 4 < tend) hfetch(tile + 4);
+    if (tile + W < tend) hfetch(tile + W);
     uint4 srow[4], drow[4];
     wave_lds_sync();
 #pragma unroll
@@ -310,6 +313,13 @@ __global__ __launch_bounds__(256) void bridge_classify(BridgeArgs a, TouchBins b
   }
   __syncthreads();
   bins_publish(bins, cur, rb);
+}
+
+__global__ __launch_bounds__(256) void bridge_classify(BridgeArgs a, TouchBins bins) {
+  bridge_tiles<4>(a, bins);
+}
+__global__ __launch_bounds__(1024, 1) void bridge_classify_w(BridgeArgs a, TouchBins bins) {
+  bridge_tiles<16>(a, bins);
 }
 
 // Keys + hashes of the queued src MACs (packet order).
@@ -403,17 +413,25 @@ static int bridge_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // the classify launch bins its touches when it can (TouchBins; no touch
   // log then), else logs them and the log is folded
   BinsPlan bp{};
-  VP_TRY(tbl_bins_plan(c, t, (const void *)bridge_classify, p0, p1, &bp, 4, 8));
+  static const uint32_t bw = [] {  // waves per block (VIGPATH_BRIDGE_WAVES: 4 or 16)
+    const char *e = getenv("VIGPATH_BRIDGE_WAVES");
+    return e && atoi(e) == 16 ? 16u : 4u;
+  }();
+  const void *bk = bw == 16 ? (const void *)bridge_classify_w : (const void *)bridge_classify;
+  VP_TRY(tbl_bins_plan(c, t, bk, p0, p1, &bp, bw, 8));
   const uint32_t tiles = (p1 - (p0 & ~63u) + 63) / 64;
-  const uint32_t grid = bp.on ? bp.grid : resident_grid((const void *)bridge_classify,
-                                                        (tiles + 3) / 4);
+  const uint32_t grid = bp.on ? bp.grid : resident_grid(bk, (tiles + bw - 1) / bw, 64 * (int)bw);
   // (still zero after a segment that learned nothing: no reset launch)
   if (!t.ctl_clean) VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. touch_ovf
   t.ctl_clean = false;
   VP_HIP(ev_record(c->ktime, c->ev0, c->stream));
   BridgeArgs a1 = a;
   if (bp.on) a1.log = nullptr;
-  bridge_classify<<<grid, 256, 0, c->stream>>>(a1, bp.bins);
+  c->last_kernel = bw == 16 ? "bridge_classify_w" : "bridge_classify";
+  if (bw == 16)
+    bridge_classify_w<<<grid, 1024, 0, c->stream>>>(a1, bp.bins);
+  else
+    bridge_classify<<<grid, 256, 0, c->stream>>>(a1, bp.bins);
   VP_HIP(hipGetLastError());
   VP_HIP(ev_record(c->ktime, c->ev1, c->stream));
   VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, c->seq));
