@@ -227,6 +227,23 @@ def _worker_route_all(outdir, env, n, cuts):
     np.testing.assert_array_equal(ga, oa)
     np.testing.assert_array_equal(gts[oa == 1], ots[oa == 1])
     np.testing.assert_array_equal(gk[oa == 1], ok[oa == 1])
+    # ABI 0.3 on a chunked step with kernel timing on: vp_stage_ms reports
+    # the pipeline's eighth stage into a caller-sized array, the 0.2 entry
+    # point vp_last_stage_ms writes exactly seven floats (a canary after them
+    # survives), and vp_last_kernel names owner pass 1's kernels
+    from gpuh import run_gpu
+    nat.kernel_timing(True)
+    f2, l2, d2, n2 = T.nat_lan_trace(2048, 1024, start=int(now[-1]) - T.NOW0 + 1)
+    run_gpu(nat, f2, l2, d2, n2, 64)
+    ms8, k8 = (C.c_float * 8)(), C.c_int()
+    assert nat.L.vp_stage_ms(nat.h, ms8, 8, C.byref(k8)) == 0
+    assert k8.value == 8 and ms8[7] > 0, (k8.value, list(ms8))
+    ms7 = (C.c_float * 8)(*([0.0] * 7 + [-1.0]))
+    k7 = C.c_int()
+    assert nat.L.vp_last_stage_ms(nat.h, ms7, C.byref(k7)) == 0
+    assert k7.value == 7 and ms7[7] == -1.0 and list(ms7[:7]) == list(ms8[:7])
+    assert nat.L.vp_stage_ms(nat.h, None, 0, C.byref(k8)) == 0 and k8.value == 8
+    assert "nat_remote64" in nat.last_kernel()
     open(os.path.join(outdir, "ok"), "w").write("ok")
 
 

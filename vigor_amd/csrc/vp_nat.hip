@@ -2587,6 +2587,7 @@ static OwnChunks own_chunks_plan(vp_ctx *c, const vp_dev_batch *b) {
 static int nat_phase_a_owner_chunked(vp_ctx *c, const vp_dev_batch *b, NatArgs &a,
                                      const NowSpec &now, uint32_t p0, uint32_t p1,
                                      uint64_t seq0, const OwnChunks &oc, PhaseA *ph) {
+  c->last_kernel = "nat_classify64+nat_remote64 (chunked)";
   FlowTable &t = c->ft;
   Workspace &w = c->ws;
   Comm &m = *c->comm;
