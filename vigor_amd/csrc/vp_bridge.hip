@@ -38,6 +38,9 @@
 
 namespace vp {
 
+VP_PRELOAD_UNIT(bridge)
+
+
 // rte_ether_addr_hash: crc32c_u32 of each byte in turn, so the non-zero byte
 // positions of the 24-byte CRC message are 0, 4, 8, 12, 16, 20.
 constexpr int kEthTabs = 6;

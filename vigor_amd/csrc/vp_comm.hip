@@ -13,6 +13,9 @@
 
 namespace vp {
 
+VP_PRELOAD_UNIT(comm)
+
+
 static int nccl_fail(ncclResult_t e, const char *what) {
   state_fail("RCCL %s failed: %s", what, ncclGetErrorString(e));  // (the message)
   return VP_EIO;

@@ -30,6 +30,9 @@
 
 namespace vp {
 
+VP_PRELOAD_UNIT(fw)
+
+
 // FlowId_hash for vigfw's FlowId (generated, codegen/main.ml:328-401): five
 // CRC steps src_port, dst_port, src_ip, dst_ip, protocol; non-zero byte
 // positions of the 20-byte CRC message.

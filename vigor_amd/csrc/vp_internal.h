@@ -78,6 +78,26 @@ inline uint32_t tile_split() {
   return s;
 }
 
+// One empty kernel per translation unit: launching it makes HIP load the
+// unit's device code, which it otherwise does at the unit's first kernel
+// launch (5-30 ms for vp_nat.hip's variants): ctx_common pays it once per
+// GPU, at context creation (nf_init), not the first batch.
+#define VP_PRELOAD_UNIT(name)                                     \
+  __global__ void preload_k_##name() {}                           \
+  hipError_t preload_##name(hipStream_t s) {                      \
+    preload_k_##name<<<1, 64, 0, s>>>();                          \
+    return hipGetLastError();                                     \
+  }
+hipError_t preload_runtime(hipStream_t s);
+hipError_t preload_table(hipStream_t s);
+hipError_t preload_nat(hipStream_t s);
+hipError_t preload_bridge(hipStream_t s);
+hipError_t preload_lb(hipStream_t s);
+hipError_t preload_fw(hipStream_t s);
+hipError_t preload_pol(hipStream_t s);
+hipError_t preload_comm(hipStream_t s);
+hipError_t preload_mbuf(hipStream_t s);
+
 // Owner-mode phase A stages (vp_last_stage_ms).
 constexpr int kStages = 8;
 inline constexpr const char *kStageNames[kStages] = {

@@ -51,6 +51,9 @@
 
 namespace vp {
 
+VP_PRELOAD_UNIT(lb)
+
+
 // LoadBalancedFlow_hash (generated, 5 CRC steps: src_ip, dst_ip, src_port,
 // dst_port, protocol): non-zero byte positions of the 20-byte CRC message.
 static const int kLbFlowPos[13] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 13, 16};

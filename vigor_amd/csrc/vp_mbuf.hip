@@ -47,6 +47,9 @@
 
 namespace vp {
 
+VP_PRELOAD_UNIT(mbuf)
+
+
 // Registered host ranges as the kernels see them: frame bytes [p, p + len)
 // inside [hbase, hend) are at device address p + delta.
 struct MapTab {

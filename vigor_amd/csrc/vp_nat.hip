@@ -32,6 +32,9 @@
 
 namespace vp {
 
+VP_PRELOAD_UNIT(nat)
+
+
 // FlowId (vignat/flow.h:3-10) is hashed as 6 CRC steps (generated FlowId_hash,
 // codegen/main.ml:328-401); the non-zero byte positions of that 24-byte CRC
 // message: src_port 0,1  dst_port 4,5  src_ip 8-11  dst_ip 12-15

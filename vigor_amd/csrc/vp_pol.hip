@@ -39,6 +39,9 @@
 
 namespace vp {
 
+VP_PRELOAD_UNIT(pol)
+
+
 int ws_reserve(vp_ctx *c, uint32_t n);  // vp_runtime.hip
 
 // ip_addr_hash (generated for vigpol/ip_addr.h:6-8): crc32c_u32(0, addr);

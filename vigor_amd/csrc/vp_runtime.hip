@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 #include <cstdarg>
 #include <chrono>
 #include <cstdio>
@@ -14,6 +15,9 @@
 #include "vp_table.h"
 
 namespace vp {
+
+VP_PRELOAD_UNIT(runtime)
+
 
 // vp_last_error(): the calling thread's last failure
 static thread_local char g_last_error[256];
@@ -165,12 +169,28 @@ static void mac_words(const uint8_t d[6], const uint8_t s[6], uint32_t w[3]) {
            ((uint32_t)b[4 * k + 3] << 24);
 }
 
+// Every unit's device code loaded on `gpu` (VP_PRELOAD_UNIT), once per
+// process and GPU.
+static int preload_units(int gpu, hipStream_t s) {
+  static std::mutex mu;
+  static std::vector<int> done;
+  std::lock_guard<std::mutex> g(mu);
+  if (std::find(done.begin(), done.end(), gpu) != done.end()) return 0;
+  for (auto f : {preload_runtime, preload_table, preload_nat, preload_bridge, preload_lb,
+                 preload_fw, preload_pol, preload_comm, preload_mbuf})
+    VP_HIP(f(s));
+  VP_HIP(hipStreamSynchronize(s));
+  done.push_back(gpu);
+  return 0;
+}
+
 static int ctx_common(vp_ctx *c, int gpu) {
   c->gpu = gpu;
   const char *co = getenv("VIGPATH_COALESCED");
   c->coalesced_io = !co || atoi(co) != 0;  // default on (tools/ablate.py)
   VP_HIP(hipSetDevice(gpu));
   VP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  VP_TRY(preload_units(gpu, c->stream));
   VP_HIP(hipEventCreate(&c->ev0));
   VP_HIP(hipEventCreate(&c->ev1));
   VP_HIP(hipEventCreateWithFlags(&c->evc, hipEventDisableTiming));

@@ -23,6 +23,9 @@
 
 namespace vp {
 
+VP_PRELOAD_UNIT(table)
+
+
 uint32_t grid_for(uint64_t n, uint32_t block, uint32_t max_blocks) {
   uint64_t g = (n + block - 1) / block;
   if (g == 0) g = 1;
