@@ -196,6 +196,42 @@ def test_burst_port(slot):
     check_state(nat, o, 64)
 
 
+def test_first_sighting_cut():
+    """The churn shape (traces.churn_trace: a quarter of the flow slots start
+    new flows every batch, each flow seen many times per batch): once a
+    batch's misses are mostly repeats of flows first seen in its opening
+    packets, the next batches start with a segment of that many packets
+    (FlowTable::fs_hint, run_batch), then the rest hits. Every batch's out
+    ports and frames, and the final flow state, against the oracle; the cut
+    batches run two classify launches; batches without new flows drop the
+    cut again."""
+    W, B = 4096, 1 << 17
+    nat, o = make_pair(max_flows=1 << 14, expire_us=T.CHURN_EXPIRE_US)
+    launches = []
+    for k in range(10):
+        fr, ln, dv, now = T.churn_trace(k, B, w=W)
+        exp = fr.copy()
+        exp_out = o.run(exp, ln, dv, now, 64)
+        got, out = run_gpu(nat, fr, ln, dv, now, 64, affine=(int(now[0]), 0))
+        assert np.array_equal(out, exp_out), k
+        assert np.array_equal(got, exp), k
+        launches.append(nat.last_kernel_ms()[1])
+    check_state(nat, o, 1 << 14)
+    assert launches[0] == 1 and all(x == 2 for x in launches[2:]), launches
+    # steady batches (the flows of batch 9 again, no new flow): one cut
+    # batch that finds no new flow, then single segments
+    for j in range(3):
+        fr, ln, dv, now = T.churn_trace(9, B, w=W)
+        now = now + (j + 1)  # (later times, same flows)
+        exp = fr.copy()
+        exp_out = o.run(exp, ln, dv, now, 64)
+        got, out = run_gpu(nat, fr, ln, dv, now, 64, affine=(int(now[0]), 0))
+        assert np.array_equal(out, exp_out) and np.array_equal(got, exp), j
+        launches.append(nat.last_kernel_ms()[1])
+    assert launches[-2:] == [1, 1], launches
+    check_state(nat, o, 1 << 14)
+
+
 def test_burst_port_out_of_range():
     """A burst's port is nf_process's uint16_t device (nf.h:14): a larger
     vp_dev_batch.in_port is rejected before anything runs."""

@@ -134,6 +134,8 @@ struct Ctl {
   uint32_t own_new;     // owner mode: union keys this rank will insert (upper bound)
   uint32_t run_tiles;   // vignat's 64-byte tiles whose 64 touches were one run
                         // (cumulative, never reset: the host takes differences)
+  uint32_t last_first;  // unsorted new keys: 1 + the last first sighting's
+                        // position in the segment (nku_firsts)
 };
 
 // The control block as a fold kernel publishes it into page-locked host
@@ -181,6 +183,10 @@ struct FlowTable {
   uint32_t pub_epoch = 0;          // last epoch asked of the fold
   uint32_t *ttotal = nullptr;  // touch-reduce entry count (device)
   uint64_t ts_floor = UINT64_MAX;  // lower bound of min ts over live indices
+  // first-sighting cut (vignat, one GPU; run_batch): the packets at the start
+  // of a batch that held the last batch's first sightings of new flows when
+  // most of its misses were repeats of them; 0: no cut
+  uint32_t fs_hint = 0;
   // vignat: the last segment's tiles were mostly runs (Ctl::run_tiles), so
   // the next one takes the 1024-thread tile without staged bin lines
   bool runs_seen = true;
@@ -385,6 +391,7 @@ struct vp_ctx {
   // The last segment left only its timestamp fold running on `stream`
   // (results complete): run_batch returns without waiting for it.
   bool fold_pending = false;
+  bool seg_fs = false;  // the segment run_batch is running is a first-sighting cut
   float last_ms = 0.f;
   // the classification kernel the last vp_process_device call launched last
   // (vp_last_kernel; "" before any)

@@ -2932,6 +2932,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   *ms += ph.ms;
   *launches += 1;
   const uint32_t nmiss = t.h_ctl.miss_count, ndefer = t.h_ctl.defer_count;
+  if (c->seg_fs && !nmiss) t.fs_hint = 0;  // the cut met no new flow: stop cutting
 
   uint32_t union_n = nmiss, union_off = 0;  // this rank's misses in the union
   if (c->comm) VP_TRY(union_sizes(c, nmiss, &union_n, &union_off));
@@ -2945,6 +2946,13 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     VP_TRY(tbl_new_keys_done(c, t));
     a.t = tbl_dev(t);  // a rebuild may have moved the buckets
     *allocated |= 1u;
+    // the first-sighting cut for the next batch (run_batch): set when most
+    // misses repeated flows first seen in the segment's opening half
+    const uint64_t nnew = t.h_ctl.new_count, span = t.h_ctl.last_first;
+    const uint64_t rep = nmiss > nnew ? nmiss - nnew : 0;
+    if (!c->seg_fs && p0 == 0 && rep >= (1u << 16) && rep >= 4 * nnew && span &&
+        2 * span <= (uint64_t)(p1 - p0))
+      t.fs_hint = (uint32_t)((span + 63) & ~63ull);
   } else if (nmiss) {
     size_t need = 0;
     hipcub::DeviceRadixSort::SortKeys(nullptr, need, w.miss, w.miss_sorted,

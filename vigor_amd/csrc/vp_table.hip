@@ -414,6 +414,7 @@ __global__ void nku_firsts(NkuArgs m) {
       const uint32_t bit = 1u << ((p - m.p0) & 31);
       f = !(atomicOr(&m.bits[(p - m.p0) >> 5], bit) & bit);
     }
+    if (f) atomicMax(&m.t.ctl->last_first, p - m.p0 + 1);  // (run_batch's cut)
     const uint32_t k = wave_append(m.cnt, f);
     if (f) m.first[k] = j;
   }
@@ -557,6 +558,7 @@ int tbl_new_keys_unsorted(vp_ctx *c, FlowTable &t, uint32_t n, uint32_t p0, uint
   VP_TRY(cub_reserve(c, need));
   VP_HIP(hipMemsetAsync(w.nkbits, 0, 4ull * nwords, c->stream));
   VP_HIP(hipMemsetAsync(w.nkcnt, 0, 4, c->stream));
+  VP_HIP(hipMemsetAsync(&t.ctl->last_first, 0, 4, c->stream));
   const uint32_t g = grid_for(n);
   nku_dedup<<<g, 256, 0, c->stream>>>(m);
   nku_firsts<<<g, 256, 0, c->stream>>>(m);
@@ -1651,11 +1653,29 @@ int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
   int launches = 0;
   uint32_t a0 = 0;
   const uint32_t ne = std::min(n, exp_end);  // packets that may expire
+  // The first-sighting cut (FlowTable::fs_hint, vignat's unsorted new keys):
+  // when most of the last batch's misses were repeats of flows it first saw
+  // in its opening packets, this batch starts with a segment of that many
+  // packets; its new flows are in the table when the rest is classified, so
+  // their later packets are phase-A hits rather than misses to deduplicate
+  // and rewrite. Segments are exact wherever they are cut (§3).
+  const uint32_t fs = ntabs ? tabs[0].t->fs_hint : 0u;
+  auto fs_cut = [&](uint32_t a, uint32_t e) {
+    c->seg_fs = a == 0 && fs && fs < e && e - fs >= 64;
+    return c->seg_fs ? fs : e;
+  };
   while (a0 < n) {
     if (a0 >= ne) {  // the rest runs no expiry: one segment
+      const uint32_t e = fs_cut(a0, n);
       uint32_t allocated = 0;
       c->fold_pending = false;
-      VP_TRY(seg(c, b, now, a0, n, &ms, &launches, &allocated));
+      VP_TRY(seg(c, b, now, a0, e, &ms, &launches, &allocated));
+      if (e < n) {  // (the rest after the cut: its flows' stamps as below)
+        if (allocated & 1u)
+          tabs[0].t->ts_floor = std::min<uint64_t>(tabs[0].t->ts_floor, (uint64_t)at(a0));
+        a0 = e;
+        continue;
+      }
       break;
     }
     const int64_t ta = at(a0);
@@ -1680,6 +1700,7 @@ int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
       }
       b1 = lo;
     }
+    b1 = fs_cut(a0, b1);
     uint32_t allocated = 0;
     c->fold_pending = false;
     VP_TRY(seg(c, b, now, a0, b1, &ms, &launches, &allocated));
@@ -1688,6 +1709,7 @@ int run_batch(vp_ctx *c, const vp_dev_batch *b, ExpiringTable *tabs, int ntabs,
         tabs[i].t->ts_floor = std::min<uint64_t>(tabs[i].t->ts_floor, (uint64_t)ta);
     a0 = b1;
   }
+  c->seg_fs = false;
   // Results are complete once every segment's work is; a trailing timestamp
   // fold alone may keep running (ordered before any later call on the
   // stream, and before the caller's stream through vp_process_device).
