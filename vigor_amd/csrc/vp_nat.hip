@@ -2085,7 +2085,8 @@ __device__ __forceinline__ uint32_t nat_one_reg(const NatArgs &a, const uint32_t
 // 1, ... It leaves on the leave request or after `idle` wall-clock ticks
 // without a request; a request posted as it leaves finds the stream idle and
 // the host launches it again (nat_process_one). flags: bit 0, the stage
-// clock (VIGPATH_SERVE_PROF); bits 3-9: the waves' stagger in wall-clock ticks.
+// clock (VIGPATH_SERVE_PROF); bits 3-9: the waves' stagger in wall-clock
+// ticks; bits 10-17: the first poll's delay after an answer.
 __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint64_t seq0,
                                                  uint64_t idle, uint32_t flags) {
   __shared__ uint32_t T[kNatTabWords];
@@ -2231,6 +2232,14 @@ __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint6
     const uint64_t w = wall_clock64();
     while (wall_clock64() - w < (uint64_t)gap * wv) __builtin_amdgcn_s_sleep(1);
   }
+  // After an answer the next request cannot come before the answer has
+  // crossed to the host and the host's loop has turned round (about half a
+  // round trip plus its own time): a poll issued at once reads the mailbox
+  // too early and the request waits for the poll after it, a whole round
+  // trip later. The first poll after an answer waits `after` wall-clock ticks
+  // (flags bits 10-17; VIGPATH_SERVE_AFTER) so that it reads about when the
+  // request lands.
+  const uint32_t after = (flags >> 10) & 0xFFu;
   for (;;) {
     const v4u q = poll();
     const int st = serve(q);
@@ -2240,6 +2249,9 @@ __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint6
                                               __HIP_MEMORY_SCOPE_WORKGROUP) > idle)
         break;
       __builtin_amdgcn_s_sleep(1);
+    } else if (after) {
+      const uint64_t w = wall_clock64();
+      while (wall_clock64() - w < after) __builtin_amdgcn_s_sleep(1);
     }
   }
 }
@@ -3126,8 +3138,13 @@ static int serve_launch(vp_ctx *c) {
     const char *e = getenv("VIGPATH_SERVE_GAP");
     return e ? (uint32_t)std::min(127, std::max(0, atoi(e))) : 35u;
   }();
+  static const uint32_t after = [] {  // (wall-clock ticks of 10 ns, < 256)
+    const char *e = getenv("VIGPATH_SERVE_AFTER");
+    return e ? (uint32_t)std::min(255, std::max(0, atoi(e))) : 0u;
+  }();
   nat_serve<<<1, 64 * waves, 0, c->stream>>>(a, dbox, c->seq, c->srv_idle,
-                                             (g_srv_prof ? 1u : 0u) | (gap << 3));
+                                             (g_srv_prof ? 1u : 0u) | (gap << 3) |
+                                                 (after << 10));
   VP_HIP(hipGetLastError());
   if (!c->srv_on) {
     static std::once_flag once;
