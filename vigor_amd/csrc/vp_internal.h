@@ -361,7 +361,13 @@ constexpr uint32_t kServeChunks = 8;
 constexpr uint32_t kServeInline = 12 * kServeChunks - 12;  // 84 frame bytes
 struct ServeBox {
   alignas(128) uint32_t msg[kServeChunks][4];  // host: the tagged request chunks
-  uint64_t ans;      // device: request number | (out | fresh << 16) << 32
+  // device: the answer the same way -- chunk k = bytes 12k .. 12k + 11 of
+  // (out | fresh << 16, 8 unused bytes, the rewritten frame's first
+  // kServeInline bytes) and the request number; one store instruction, no
+  // wait between the frame and the answer word (a longer frame goes through
+  // `frame` first, then chunk 0 alone)
+  alignas(128) uint32_t amsg[kServeChunks][4];
+  uint64_t ans;      // device: request number | (out | fresh << 16) << 32 (relaunch state)
   uint64_t prof[8];  // device: wall-clock stamps of the last request (VIGPATH_SERVE_PROF)
   alignas(16) uint8_t frame[kServeFrame];  // longer frames in; every result out
 };

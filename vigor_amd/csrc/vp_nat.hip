@@ -2108,6 +2108,7 @@ __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint6
   constexpr int kSys = 17;  // sc0 | sc1: system-coherent (bypasses the GPU caches)
   const auto ms = __builtin_amdgcn_make_buffer_rsrc(box->msg, 0, 16 * kServeChunks, 0x00020000);
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(box->frame, 0, kServeFrame, 0x00020000);
+  const auto as = __builtin_amdgcn_make_buffer_rsrc(box->amsg, 0, 16 * kServeChunks, 0x00020000);
   // (lanes past the chunks read nothing: an offset past the resource)
   const int moff = lane < kServeChunks ? (int)(16 * lane) : (int)(16 * kServeChunks);
   auto poll = [&]() -> v4u { return __builtin_amdgcn_raw_buffer_load_b128(ms, moff, 0, kSys); };
@@ -2188,10 +2189,25 @@ __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint6
     }
     wave_lds_sync();
     const uint64_t s2 = wall_clock64();
-    for (uint32_t i = lane; i < nch; i += 64) {
-      const uint4 v = fr[i];
-      __builtin_amdgcn_raw_buffer_store_b128((v4u){v.x, v.y, v.z, v.w}, rs, (int)(16 * i), 0,
-                                             kSys);
+    res = __builtin_amdgcn_readfirstlane(res);
+    if (inl) {  // the answer chunks: the result and the frame in one store
+      if (lane < need) {
+        const v4u v = lane == 0 ? (v4u){res, 0u, 0u, want}
+                                : (v4u){fw[3 * lane - 3], fw[3 * lane - 2], fw[3 * lane - 1], want};
+        __builtin_amdgcn_raw_buffer_store_b128(v, as, (int)(16 * lane), 0, kSys);
+      }
+    } else {
+      for (uint32_t i = lane; i < nch; i += 64) {
+        const uint4 v = fr[i];
+        __builtin_amdgcn_raw_buffer_store_b128((v4u){v.x, v.y, v.z, v.w}, rs, (int)(16 * i), 0,
+                                               kSys);
+      }
+      // (the frame complete before the answer chunk that announces it)
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      __builtin_amdgcn_s_waitcnt(0);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      if (lane == 0)
+        __builtin_amdgcn_raw_buffer_store_b128((v4u){res, 0u, 0u, want}, as, 0, 0, kSys);
     }
     if (lane == 0) {
       if (prof) {
@@ -2207,12 +2223,10 @@ __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint6
         put(6, s2);
         put(7, wall_clock64());
       }
+      // (the answer word: where a relaunched server starts counting; the
+      // host reads the answer chunks. No release fence, which would write
+      // back the whole L2)
       const uint64_t ans = (uint64_t)want | ((uint64_t)res << 32);
-      // every store of the wave complete first (its counter covers all
-      // lanes); no release fence, which would write back the whole L2
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (no compiler reordering either)
-      __builtin_amdgcn_s_waitcnt(0);
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
       __hip_atomic_store(&box->ans, ans, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       t0_s = wall_clock64();
       // (the table writes of this request before the next request's wave
@@ -3211,9 +3225,16 @@ int nat_process_one(vp_ctx *c, uint16_t in_dev, uint8_t *frame, uint16_t len, in
     bx->msg[k][2] = m[3 * k + 2];
     __atomic_store_n(&bx->msg[k][3], req, __ATOMIC_RELEASE);
   }
+  // the answer: chunk 0's tag, then (frames of up to kServeInline bytes) the
+  // other chunks' tags, each chunk's bytes final once its tag is the request's
   auto last = h0;
-  uint64_t ans;
-  while ((uint32_t)(ans = __atomic_load_n(&bx->ans, __ATOMIC_ACQUIRE)) != req) {
+  const uint32_t need = len <= kServeInline ? (12 + len + 11) / 12 : 1u;
+  auto answered = [&]() {
+    for (uint32_t k = 0; k < need; k++)
+      if (__atomic_load_n(&bx->amsg[k][3], __ATOMIC_ACQUIRE) != req) return false;
+    return true;
+  };
+  while (!answered()) {
     __builtin_ia32_pause();
     const auto nw = std::chrono::steady_clock::now();
     if (nw - last < std::chrono::microseconds(200)) continue;
@@ -3222,10 +3243,22 @@ int nat_process_one(vp_ctx *c, uint16_t in_dev, uint8_t *frame, uint16_t len, in
     const hipError_t q = hipStreamQuery(c->stream);
     if (q == hipErrorNotReady) continue;
     VP_HIP(q);
-    if ((uint32_t)__atomic_load_n(&bx->ans, __ATOMIC_ACQUIRE) == req) continue;
+    if (answered()) continue;
     VP_TRY(serve_launch(c));
   }
-  memcpy(frame, bx->frame, len);
+  const uint32_t res = bx->amsg[0][0];
+  if (len <= kServeInline) {
+    uint32_t m2[3 * kServeChunks];
+    for (uint32_t k = 1; k < need; k++) {
+      m2[3 * k] = bx->amsg[k][0];
+      m2[3 * k + 1] = bx->amsg[k][1];
+      m2[3 * k + 2] = bx->amsg[k][2];
+    }
+    memcpy(frame, &m2[3], len);
+  } else {
+    memcpy(frame, bx->frame, len);
+  }
+  const uint64_t ans = (uint64_t)req | ((uint64_t)res << 32);
   *out = (uint16_t)(ans >> 32);
   if ((ans >> 48) & 1u) t.ts_floor = std::min<uint64_t>(t.ts_floor, (uint64_t)now);
   c->seq += 1;
