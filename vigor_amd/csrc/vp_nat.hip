@@ -3154,9 +3154,9 @@ static int serve_launch(vp_ctx *c) {
   }();
   static const uint32_t after = [] {  // (wall-clock ticks of 10 ns, < 256)
     const char *e = getenv("VIGPATH_SERVE_AFTER");
-    // (60: 4.73-4.82 us per packet against 5.53-5.61 at 0 through nf.c's
-    // loop, profiles/r06o_serve_after.txt)
-    return e ? (uint32_t)std::min(255, std::max(0, atoi(e))) : 60u;
+    // (45: 4.59-4.65 us per packet, 60: 4.73-4.83, 0: 5.41-5.80 through
+    // nf.c's loop, profiles/r06o_serve_after.txt, r06p_serve_after_sweep.txt)
+    return e ? (uint32_t)std::min(255, std::max(0, atoi(e))) : 45u;
   }();
   nat_serve<<<1, 64 * waves, 0, c->stream>>>(a, dbox, c->seq, c->srv_idle,
                                              (g_srv_prof ? 1u : 0u) | (gap << 3) |
@@ -3227,8 +3227,7 @@ int nat_process_one(vp_ctx *c, uint16_t in_dev, uint8_t *frame, uint16_t len, in
   }
   // the answer: chunk 0's tag, then (frames of up to kServeInline bytes) the
   // other chunks' tags, each chunk's bytes final once its tag is the request's
-  auto last = h0;
-  const uint32_t need = len <= kServeInline ? (12 + len + 11) / 12 : 1u;
+  auto last = h0;  // (need: the chunks the request took, as many as the answer takes)
   auto answered = [&]() {
     for (uint32_t k = 0; k < need; k++)
       if (__atomic_load_n(&bx->amsg[k][3], __ATOMIC_ACQUIRE) != req) return false;
