@@ -2086,7 +2086,7 @@ __device__ __forceinline__ uint32_t nat_one_reg(const NatArgs &a, const uint32_t
 // without a request; a request posted as it leaves finds the stream idle and
 // the host launches it again (nat_process_one). flags: bit 0, the stage
 // clock (VIGPATH_SERVE_PROF); bits 3-9: the waves' stagger in wall-clock
-// ticks; bits 10-17: the first poll's delay after an answer.
+// ticks; bits 10-17: the first poll's delay after an answer; bit 18: adapt it.
 __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint64_t seq0,
                                                  uint64_t idle, uint32_t flags) {
   __shared__ uint32_t T[kNatTabWords];
@@ -2253,17 +2253,29 @@ __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint6
   // trip later. The first poll after an answer waits `after` wall-clock ticks
   // (flags bits 10-17; VIGPATH_SERVE_AFTER) so that it reads about when the
   // request lands.
-  const uint32_t after = (flags >> 10) & 0xFFu;
+  // The delay adapts (flags bit 18): a request the first poll caught takes
+  // a tick off it, one that needed a later poll adds eight -- a late poll
+  // costs a round trip, an early one only its excess -- so it settles just
+  // past where the caller's requests land, whatever the caller's loop.
+  uint32_t after = (flags >> 10) & 0xFFu;
+  const bool adapt = (flags >> 18) & 1u;
+  uint32_t polls = 0;  // polls since the last answer
   for (;;) {
     const v4u q = poll();
     const int st = serve(q);
     if (st == 1) break;
+    polls++;
     if (st < 0) {
       if (wall_clock64() - __hip_atomic_load(&t0_s, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_WORKGROUP) > idle)
         break;
       __builtin_amdgcn_s_sleep(1);
-    } else if (after) {
+      continue;
+    }
+    if (adapt && polls == 1 && after > 0) after--;
+    if (adapt && polls > 1 && polls < 64) after = min(after + 8u, 200u);
+    polls = 0;
+    if (after) {
       const uint64_t w = wall_clock64();
       while (wall_clock64() - w < after) __builtin_amdgcn_s_sleep(1);
     }
@@ -3158,9 +3170,13 @@ static int serve_launch(vp_ctx *c) {
     // nf.c's loop, profiles/r06o_serve_after.txt, r06p_serve_after_sweep.txt)
     return e ? (uint32_t)std::min(255, std::max(0, atoi(e))) : 45u;
   }();
+  static const uint32_t adapt = [] {  // VIGPATH_SERVE_ADAPT=0: a fixed delay
+    const char *e = getenv("VIGPATH_SERVE_ADAPT");
+    return e && !atoi(e) ? 0u : 1u;
+  }();
   nat_serve<<<1, 64 * waves, 0, c->stream>>>(a, dbox, c->seq, c->srv_idle,
                                              (g_srv_prof ? 1u : 0u) | (gap << 3) |
-                                                 (after << 10));
+                                                 (after << 10) | (adapt << 18));
   VP_HIP(hipGetLastError());
   if (!c->srv_on) {
     static std::once_flag once;
