@@ -59,6 +59,9 @@ METRIC = "Mpackets/s device-resident, 64B vignat @1M flows; %HBM roofline"
 ALG_BYTES = 92          # 64 frame + 4 len/port + 16 key + 4 tag + 4 value
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SLOT = 64
+# VIGPATH_BENCH_PYLOOP=1: the headline's calls from Python, one ctypes call a
+# step (A/B against the C loop, host/steps.c)
+PY_LOOP = os.environ.get("VIGPATH_BENCH_PYLOOP") == "1"
 TRAFFIC_PROFILE = "r06n_bench_traffic.json"  # rocprofv3 --pmc passes (tools/gpu_session.sh pmc)
 DEV_MACS = [T.mac("02:00:00:00:00:00"), T.mac("02:00:00:00:00:01")]
 NAT_ARGS = ["--expire", "60000000", "--starting-port", "0", "--wan", "1",
@@ -724,7 +727,14 @@ def timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank, first, 
         b = torch.empty(B * slot, dtype=torch.uint8, device=dev)
         bank.fill(b, gstart(first + k), order)
         bufs.append(b)
-    calls = [nat.device_step(b, lens, in_dev, out, slot) for b in bufs]
+    # the headline pass: the calls in a C loop (host/steps.c), as nf.c makes
+    # them; the timing pass reads per-step values back between calls (Python)
+    c_loop = knames is None and stages is None and not PY_LOOP
+    if c_loop:
+        run = nat.device_steps(bufs, lens, in_dev, out, slot)
+        nows = [T.NOW0 + gstart(first + k) for k in range(steps)]
+    else:
+        calls = [nat.device_step(b, lens, in_dev, out, slot) for b in bufs]
     torch.cuda.synchronize()
     kms = []
     mark("%s: barrier" % label)
@@ -732,7 +742,10 @@ def timed_steps(nat, bank, dev, lens, in_dev, out, B, slot, world, rank, first, 
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(steps):
+    if c_loop:
+        mark("%s: %d steps (C loop)" % (label, steps))
+        run(nows, 1)
+    for k in range(0 if c_loop else steps):
         mark("%s: step %d/%d" % (label, k + 1, steps))
         calls[k](T.NOW0 + gstart(first + k), 1)
         kms.append(nat.last_kernel_ms())
@@ -1193,6 +1206,9 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "u8", "data": "synthetic",
+            "timed_loop": "python (one ctypes call a step)" if PY_LOOP else
+                          "C (host/steps.c: one vp_process_device call a batch, as "
+                          "nf.c's loop; descriptors prepared before the timed region)",
             "config": {"workload": workload, "flows": args.flows,
                        "batch_packets_per_gpu": B,
                        "global_batch_packets": B * world,

@@ -41,6 +41,13 @@ def test_library_exports_every_declared_symbol():
     vigor_amd.lib()  # loads (resolves every ctypes binding)
 
 
+def test_bench_step_loop_library():
+    # bench.py's timed loop in C (host/steps.c): loads against libvigpath.so
+    path = os.path.join(ROOT, "vigor_amd", "libvp_steps.so")
+    assert "vp_steps_device" in exported(path)
+    C.CDLL(path).vp_steps_device
+
+
 @pytest.mark.parametrize("nf", sorted(SHIMS))
 def test_shim_exports_nf_h_surface(nf):
     syms = exported(SHIMS[nf])

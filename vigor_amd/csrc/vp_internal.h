@@ -136,10 +136,12 @@ struct Ctl {
                         // (cumulative, never reset: the host takes differences)
   uint32_t last_first;  // unsorted new keys: 1 + the last first sighting's
                         // position in the segment (nku_firsts)
+  uint32_t arrive;      // classify blocks finished (tile_publish; 0 between launches)
 };
 
-// The control block as a fold kernel publishes it into page-locked host
-// memory (tbl_fold_read_ctl, vp_table.hip); the host polls `epoch`.
+// The control block as a fold kernel (or, one GPU, the classify's last
+// block: tile_publish) publishes it into page-locked host memory
+// (tbl_fold_read_ctl, vp_table.hip); the host polls `epoch`.
 // Multi-GPU: the fold also publishes every rank's segment counters
 // (miss, defer, touch_ovf, reprobe: gathered on the device before the fold)
 // and, owner mode, this rank's key count per owner.
@@ -368,7 +370,7 @@ struct ServeBox {
   // `frame` first, then chunk 0 alone)
   alignas(128) uint32_t amsg[kServeChunks][4];
   uint64_t ans;      // device: request number | (out | fresh << 16) << 32 (relaunch state)
-  uint64_t prof[8];  // device: wall-clock stamps of the last request (VIGPATH_SERVE_PROF)
+  uint64_t prof[10];  // device: wall-clock stamps of the last request (VIGPATH_SERVE_PROF)
   alignas(16) uint8_t frame[kServeFrame];  // longer frames in; every result out
 };
 // One packet through the persistent kernel (vignat, one GPU, no expiry due):
@@ -471,5 +473,5 @@ struct vp_ctx {
   // context's server launch on the same GPU stops this one only if it can
   // take it (serve_launch: resident kernels share the hardware queues)
   std::recursive_mutex srv_mu;
-  double srv_prof[10] = {};  // VIGPATH_SERVE_PROF: summed stage times (us), counts
+  double srv_prof[11] = {};  // VIGPATH_SERVE_PROF: summed stage times (us), counts
 };

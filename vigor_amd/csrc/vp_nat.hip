@@ -207,7 +207,43 @@ struct NatArgs {
   // sub-ranges, W / split waves interleaved over each (tile_split(); 0 or 1:
   // all W waves over the whole range)
   uint32_t split;
+  // one GPU, touch bins: the launch's last block publishes phase A's control
+  // block (tile_publish; pub.pub null: the fold does)
+  PubArgs pub;
 };
+
+// The end of a 64-byte tile block: every block releases its counters (its
+// XCD's L2 written back, so plain stores such as TouchBins' overflow flag
+// reach memory too) and counts itself in Ctl::arrive; the last one acquires
+// and publishes the control block to the host (ctl_publish), which then
+// learns phase A's counts a fold-kernel dispatch earlier and launches the
+// next batch while the fold still runs.
+// Off by default (VIGPATH_TILE_PUB=1: on): every block's release lengthened
+// the headline kernel by 6 us and the step by 5 (profiles/r06s_tile_pub.txt)
+// -- the host is not on the step's critical path; the fold and the two
+// dispatches around it are.
+static bool tile_pub_on() {
+  static const bool on = [] {
+    const char *e = getenv("VIGPATH_TILE_PUB");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+__device__ __forceinline__ void tile_publish(const NatArgs &a) {
+  if (!a.pub.pub) return;
+  // every wave's stores and atomics acknowledged (in its XCD's L2) before the
+  // barrier, so thread 0's release writes them back with its own
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  Ctl *ctl = const_cast<Ctl *>(a.pub.ctl);
+  const uint32_t n =
+      __hip_atomic_fetch_add(&ctl->arrive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (n != gridDim.x - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the other blocks' releases)
+  __hip_atomic_store(&ctl->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ctl_publish(a.pub);
+}
 
 // Queue packet p (FlowId key, hash h) as a phase-B miss.
 __device__ __forceinline__ void miss_add(const NatArgs &a, uint32_t p, const uint32_t key[4],
@@ -1200,6 +1236,7 @@ __device__ __forceinline__ void nat_tiles(NatArgs a, uint32_t n_all, TouchBins b
       a.miss[mbase + i] = a.mkq ? (uint32_t)(s0 + i) | kMissSlice : a.mq[s0 + i];
   }
   route_publish(a, cur + kCurDest, rb);
+  tile_publish(a);
 }
 
 __global__ __launch_bounds__(256, 4) void nat_classify64(NatArgs a, uint32_t n_all,
@@ -1951,9 +1988,32 @@ __global__ void nat_defer_finish(NatArgs a, const uint32_t *list, uint32_t n) {
 // flow_manager_get_internal / allocate_flow (nat_main.c:68-97) for one LAN
 // key at global sequence seq: its index, allocated when new (*fresh = 1), and
 // stamped; kNone when the table is full (drop).
+// map_get for the server: the home bucket through the kernel's LDS copy of
+// the linear layout's byte tables (lin: nat_lin(T)), and each bucket's four
+// 16-byte words requested together (compiled from bucket_match alone, the
+// first key word's load waited behind the index word's: two HBM round trips
+// per bucket, in a path that is all latency).
+__device__ __forceinline__ uint32_t serve_probe(const TableDev &t, uint32_t hh,
+                                                const uint32_t key[4], const uint32_t *lin) {
+  uint32_t b = home_bucket(hh, t.bmask, t.mix, lin);
+  for (uint32_t i = 0; i <= t.bmask; i++) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(t.bk + b);
+    uint4 k0 = q[0], k1 = q[1], k2 = q[2], ix = q[3];
+    asm volatile("" : "+v"(k0.x), "+v"(k0.y), "+v"(k0.z), "+v"(k0.w), "+v"(k1.x), "+v"(k1.y),
+                      "+v"(k1.z), "+v"(k1.w), "+v"(k2.x), "+v"(k2.y), "+v"(k2.z), "+v"(k2.w),
+                      "+v"(ix.x), "+v"(ix.y), "+v"(ix.z), "+v"(ix.w));
+    bool done;
+    const uint32_t r = bucket_match(k0, k1, k2, ix, key, &done);
+    if (done) return r;
+    b = (b + 1) & t.bmask;
+  }
+  return kNone;
+}
+
 __device__ __forceinline__ uint32_t one_lan(const TableDev &t, uint32_t hh, const uint32_t key[4],
-                                            int64_t now, uint64_t seq, uint32_t *fresh) {
-  uint32_t idx = tbl_probe(t, hh, key);
+                                            int64_t now, uint64_t seq, uint32_t *fresh,
+                                            const uint32_t *lin) {
+  uint32_t idx = serve_probe(t, hh, key, lin);
   if (idx == kNone) {  // dchain_allocate_new_index: the freed stack, then fresh
     Ctl *c = t.ctl;
     const uint32_t st = c->stack_top, fn = c->fresh_next;
@@ -1978,22 +2038,29 @@ __device__ __forceinline__ uint32_t one_lan(const TableDev &t, uint32_t hh, cons
     t.birth[idx] = seq;
     *fresh = 1;
   }
+  return idx;  // (the caller stamps it: one_stamp)
+}
+
+// The touch of index idx at (now, seq), right behind the lookup: stamped
+// after the answer instead, the stores' acknowledgement held the wave from
+// its next poll (4.6-4.8 against 4.3-4.4 us per packet,
+// profiles/r06z_serve_stamp.txt).
+__device__ __forceinline__ void one_stamp(const TableDev &t, uint32_t idx, int64_t now,
+                                          uint64_t seq) {
   t.ts[idx] = (uint64_t)now;
   t.tseq[idx] = seq;
-  return idx;
 }
 
 // flow_manager_get_external (nat_main.c:42-67) for external port dp: false
 // when no flow holds it; else the flow's key in *k, stamped (rejuvenated
 // before the anti-spoof check).
 __device__ __forceinline__ bool one_wan(const NatArgs &a, uint32_t dp, int64_t now,
-                                        uint64_t seq, uint4 *k) {
+                                        uint64_t seq, uint4 *k, uint32_t *ix) {
   const TableDev &t = a.t;
   const int idx = (int)dp - (int)a.start_port;
   if (idx < 0 || idx >= (int)t.cap || t.slot_of[idx] == kNone) return false;
   *k = tbl_key_of(t, (uint32_t)idx);
-  t.ts[idx] = (uint64_t)now;
-  t.tseq[idx] = seq;
+  *ix = (uint32_t)idx;  // (the caller stamps it, before the anti-spoof check)
   return true;
 }
 
@@ -2010,7 +2077,9 @@ __device__ __forceinline__ uint32_t nat_one(const NatArgs &a, const uint32_t *T,
   uint32_t dst;
   if (in == a.wan) {
     uint4 k;
-    if (!one_wan(a, dp, now, seq, &k)) return in;
+    uint32_t ix;
+    if (!one_wan(a, dp, now, seq, &k, &ix)) return in;
+    one_stamp(a.t, ix, now, seq);
     if ((k.z != sip) | ((k.x >> 16) != sp) | (((k.w >> 16) & 0xFF) != proto)) return in;
     f.w32(h.ip + 16, k.y);
     f.w16(h.l4 + 2, (uint16_t)(k.x & 0xFFFF));
@@ -2018,8 +2087,9 @@ __device__ __forceinline__ uint32_t nat_one(const NatArgs &a, const uint32_t *T,
   } else {
     const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
     const uint32_t idx = one_lan(a.t, flowid_hash(T, sp, dp, sip, dip, in, proto), key, now,
-                                 seq, fresh);
+                                 seq, fresh, nat_lin(T));
     if (idx == kNone) return in;
+    one_stamp(a.t, idx, now, seq);
     f.w32(h.ip + 12, a.ext_ip);
     f.w16(h.l4, (uint16_t)(a.start_port + idx));
     dst = a.wan;
@@ -2048,10 +2118,11 @@ __device__ __forceinline__ uint32_t nat_one_reg(const NatArgs &a, const uint32_t
     return in;
   const uint32_t sp = f.w[8] >> 16, dp = f.w[9] & 0xFFFF;
   const uint32_t sip = f.u32at2(26), dip = f.u32at2(30);
-  uint32_t dst, mw[3];
+  uint32_t dst, mw[3], ix;
   if (in == a.wan) {
     uint4 k;
-    if (!one_wan(a, dp, now, seq, &k)) return in;
+    if (!one_wan(a, dp, now, seq, &k, &ix)) return in;
+    one_stamp(a.t, ix, now, seq);  // (rejuvenated before the anti-spoof check)
     if ((k.z != sip) | ((k.x >> 16) != sp) | (((k.w >> 16) & 0xFF) != proto)) return in;
     f.set32at2(30, k.y);        // dst_addr = flow.src_ip
     f.set16(36, k.x & 0xFFFF);  // dst_port = flow.src_port
@@ -2060,9 +2131,10 @@ __device__ __forceinline__ uint32_t nat_one_reg(const NatArgs &a, const uint32_t
     const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
     const uint32_t hh = flowid_hash_batched(T, sp, dp, sip, dip, in, proto);
     if (prof) mk0 = wall_clock64();
-    const uint32_t idx = one_lan(a.t, hh, key, now, seq, fresh);
+    const uint32_t idx = one_lan(a.t, hh, key, now, seq, fresh, nat_lin(T));
     if (prof) mk1 = wall_clock64();
     if (idx == kNone) return in;
+    one_stamp(a.t, idx, now, seq);
     f.set32at2(26, a.ext_ip);
     f.set16(34, (uint16_t)(a.start_port + idx));
     dst = a.wan;
@@ -2133,6 +2205,7 @@ __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint6
     if (lane == 0) won = atomicCAS(&claim_s, want - 1, want) == want - 1;
     if (!__builtin_amdgcn_readfirstlane(won)) return -1;
     const uint64_t s0 = wall_clock64();
+    const uint64_t t0_prev = prof ? t0_s : 0;  // (the last answer's clock)
     const uint64_t seq = seq0 + (want - done0 - 1);
     const int64_t now =
         (int64_t)((uint64_t)__builtin_amdgcn_readfirstlane(c[1]) |
@@ -2162,6 +2235,7 @@ __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint6
       for (int o = 32; o > 0; o >>= 1) tail += __shfl_xor(tail, o);
     }
     const uint64_t s1 = wall_clock64();
+    const uint64_t c1 = prof ? __builtin_amdgcn_s_memtime() : 0;  // (shader clock)
     uint32_t res = 0;
     uint64_t mk0 = 0, mk1 = 0, mk2 = 0;
     if (lane == 0) {
@@ -2189,6 +2263,7 @@ __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint6
     }
     wave_lds_sync();
     const uint64_t s2 = wall_clock64();
+    const uint64_t c2 = prof ? __builtin_amdgcn_s_memtime() : 0;
     res = __builtin_amdgcn_readfirstlane(res);
     if (inl) {  // the answer chunks: the result and the frame in one store
       if (lane < need) {
@@ -2210,11 +2285,17 @@ __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint6
         __builtin_amdgcn_raw_buffer_store_b128((v4u){res, 0u, 0u, want}, as, 0, 0, kSys);
     }
     if (lane == 0) {
+      // (the answer word: where a relaunched server starts counting; the
+      // host reads the answer chunks. No release fence, which would write
+      // back the whole L2)
+      const uint64_t ans = (uint64_t)want | ((uint64_t)res << 32);
+      __hip_atomic_store(&box->ans, ans, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      t0_s = wall_clock64();
       if (prof) {
         auto put = [&](int k, uint64_t v) {
           __hip_atomic_store(&box->prof[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         };
-        put(0, t0_s);
+        put(0, t0_prev);
         put(1, s0);
         put(2, s1);
         put(3, mk0);
@@ -2222,13 +2303,9 @@ __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint6
         put(5, mk2);
         put(6, s2);
         put(7, wall_clock64());
+        put(8, c1);
+        put(9, c2);
       }
-      // (the answer word: where a relaunched server starts counting; the
-      // host reads the answer chunks. No release fence, which would write
-      // back the whole L2)
-      const uint64_t ans = (uint64_t)want | ((uint64_t)res << 32);
-      __hip_atomic_store(&box->ans, ans, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      t0_s = wall_clock64();
       // (the table writes of this request before the next request's wave
       // reads them: the waves share the CU, workgroup scope; an agent-scope
       // release would write the XCD's L2 back)
@@ -2915,10 +2992,15 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
     VP_HIP(hipMemsetAsync(&t.ctl->miss_count, 0, 16, c->stream));  // .. reprobe
   t.ctl_clean = false;
   hostprof(1);
+  uint32_t pub_epoch = 0;  // (nonzero: the classify publishes, tile_publish)
   if (p1 > p0) {  // (the launch's own timestamps in ev0 / ev1)
     if (tiles64) {
       NatArgs a64 = a;
       if (bp.on) a64.log = nullptr;  // touches go to the bins only
+      if (bp.on && !c->comm && tile_pub_on()) {
+        pub_epoch = ++t.pub_epoch;
+        a64.pub = PubArgs{t.d_pub, t.ctl, pub_epoch, nullptr, nullptr, 0, 0};
+      }
       c->last_kernel = nat_tile_kernel_name(tk);
       if (c->ktime) {
         VP_HIP(launch_timed(tk, grid64, 64 * tw, c->stream, c->ev0, c->ev1, a64,
@@ -2940,7 +3022,7 @@ static int nat_segment(vp_ctx *c, const vp_dev_batch *b, const NowSpec &now,
   // applied on top of it afterwards as late touches (tbl_late_touches: last
   // toucher still wins).
   hostprof(2);
-  VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, seq0));
+  VP_TRY(tbl_fold_read_ctl(c, t, bp, w.log, p0, p1, now, seq0, nullptr, pub_epoch));
   if (tiles64 && bp.on) {  // (the run tiles of this launch: the next one's kernel)
     const uint32_t nrun = t.h_ctl.run_tiles - t.last_run_tiles;
     t.last_run_tiles = t.h_ctl.run_tiles;
@@ -3088,11 +3170,12 @@ static hipError_t serve_halt(vp_ctx *c) {
     fprintf(stderr,
             "vigpath serve: %.0f packets, us/packet: host call %.2f, bell->seen %.2f "
             "(idle poll), load %.2f, packet %.2f (LAN: hash %.2f, table %.2f, rewrite %.2f), "
-            "store+answer %.2f\n",
+            "store+answer %.2f; shader clock %.0f MHz\n",
             n, c->srv_prof[0] / n, c->srv_prof[1] / n, c->srv_prof[2] / n, c->srv_prof[3] / n,
             c->srv_prof[6] / std::max(1.0, c->srv_prof[9]),
             c->srv_prof[7] / std::max(1.0, c->srv_prof[9]),
-            c->srv_prof[8] / std::max(1.0, c->srv_prof[9]), c->srv_prof[4] / n);
+            c->srv_prof[8] / std::max(1.0, c->srv_prof[9]), c->srv_prof[4] / n,
+            c->srv_prof[10] / std::max(1e-9, c->srv_prof[3]));
     for (double &x : c->srv_prof) x = 0;
   }
   return e;
@@ -3293,6 +3376,7 @@ int nat_process_one(vp_ctx *c, uint16_t in_dev, uint8_t *frame, uint16_t len, in
     }
     c->srv_prof[3] += us_tick * (double)(p[6] - p[2]);
     c->srv_prof[4] += us_tick * (double)(p[7] - p[6]);
+    c->srv_prof[10] += (double)(p[9] - p[8]);  // (shader cycles over `packet`: MHz)
     c->srv_prof[5] += 1;
   }
   return 0;

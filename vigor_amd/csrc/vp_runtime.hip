@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <mutex>
 #include <cstdarg>
 #include <chrono>
@@ -649,11 +650,23 @@ void vp_destroy(vp_ctx *ctx) { free_all(ctx); }
 
 extern "C++" {
 namespace vp {
-static const bool g_hostprof = [] {
+// VIGPATH_HOSTPROF=1: each call's stages printed as it returns (us from
+// entry); =2: recorded as absolute steady-clock times (CLOCK_MONOTONIC, the
+// kernel trace's clock) and printed at exit, so that they line up with a
+// rocprofv3 kernel trace of the same run without a print between calls
+static const int g_hostprof = [] {
   const char *e = getenv("VIGPATH_HOSTPROF");
-  return e && atoi(e);
+  return e ? atoi(e) : 0;
 }();
 static double g_hp[8];
+static std::vector<std::array<double, 8>> g_hp_log;
+static void hostprof_dump() {
+  for (size_t i = 0; i < g_hp_log.size(); i++) {
+    fprintf(stderr, "vigpath hostprof abs %zu:", i);
+    for (int k = 0; k < 8; k++) fprintf(stderr, " %.3f", g_hp_log[i][k]);
+    fprintf(stderr, " (us, CLOCK_MONOTONIC)\n");
+  }
+}
 void hostprof(int k) {
   if (g_hostprof && k >= 0 && k < 8)
     g_hp[k] = std::chrono::duration<double, std::micro>(
@@ -725,7 +738,13 @@ int vp_process_device(vp_ctx *c, const vp_dev_batch *b, void *stream) {
     hipStreamWaitEvent(user, dep, 0);
     hipEventDestroy(dep);
   }
-  if (vp::g_hostprof) {  // entry -> classify issued -> fold issued -> ctl seen -> exit
+  if (vp::g_hostprof == 2) {
+    vp::hostprof(7);
+    if (vp::g_hp_log.empty()) atexit(vp::hostprof_dump);
+    std::array<double, 8> r;
+    for (int k = 0; k < 8; k++) r[k] = vp::g_hp[k];
+    if (vp::g_hp_log.size() < 4096) vp::g_hp_log.push_back(r);
+  } else if (vp::g_hostprof) {  // entry -> classify issued -> fold issued -> ctl seen -> exit
     vp::hostprof(7);
     fprintf(stderr, "vigpath hostprof:");
     for (int k = 1; k < 8; k++)

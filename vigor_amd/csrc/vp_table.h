@@ -56,8 +56,10 @@ __host__ __device__ __forceinline__ uint32_t owner_of(uint32_t h, uint32_t n) {
 
 // A fold kernel's publication of the control block into host-coherent
 // memory (tbl_fold_read_ctl): pub == null means off. One thread calls
-// ctl_publish after the launch that filled `ctl` has completed: device-scope
-// loads of the block, system-scope stores, the epoch last (release).
+// ctl_publish after the launch that filled `ctl` has completed (or, the
+// classify's last block, after every block's release: tile_publish):
+// device-scope loads of the block, system-scope stores, the epoch last
+// (release).
 struct PubArgs {
   CtlPub *pub;
   const Ctl *ctl;
@@ -320,7 +322,7 @@ int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
 int tbl_wait_pub(vp_ctx *c, FlowTable &t, uint32_t epoch);
 int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_t *log,
                       uint32_t p0, uint32_t p1, const NowSpec &now, uint64_t seq_base,
-                      const uint32_t *sends = nullptr);
+                      const uint32_t *sends = nullptr, uint32_t pub_epoch = 0);
 
 
 // expire_items_single_map for cutoff: free every allocated index with

@@ -1262,6 +1262,8 @@ int tbl_bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
 // (the classify launch has completed: kernel boundary) and publishes it into
 // host-coherent memory, so no copy launch and its kernel boundary sit between
 // the classify and the fold; the host polls for it while the fold runs.
+// One GPU, 64-byte tiles (pub_epoch != 0): the classify's last block has
+// published it already (tile_publish, vp_nat.hip) and the fold only folds.
 // Without bins: a copy behind phase A, then the log fold. On return h_ctl
 // holds phase A's counts; the fold may still be running.
 // Multi-GPU (every rank, every segment, so the collective always matches):
@@ -1290,7 +1292,7 @@ int tbl_wait_pub(vp_ctx *c, FlowTable &t, uint32_t epoch) {
 
 int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_t *log,
                       uint32_t p0, uint32_t p1, const NowSpec &now, uint64_t seq_base,
-                      const uint32_t *sends) {
+                      const uint32_t *sends, uint32_t pub_epoch) {
   Workspace &w = c->ws;
   const uint32_t nr = c->comm ? (uint32_t)c->comm->n : 0u;
   const uint32_t ns = sends ? nr : 0u;
@@ -1315,9 +1317,12 @@ int tbl_fold_read_ctl(vp_ctx *c, FlowTable &t, const BinsPlan &bp, const uint32_
     }
     return 0;
   }
-  const uint32_t epoch = ++t.pub_epoch;
+  // (pub_epoch != 0: the classify launch publishes the block itself, one GPU)
+  const uint32_t epoch = pub_epoch ? pub_epoch : ++t.pub_epoch;
   VP_TRY(bins_reduce(c, t, bp, p0, now, seq_base,
-                     PubArgs{t.d_pub, t.ctl, epoch, w.gath, sends, kPubGath * nr, ns}));
+                     pub_epoch ? PubArgs{}
+                               : PubArgs{t.d_pub, t.ctl, epoch, w.gath, sends, kPubGath * nr,
+                                         ns}));
   hostprof(3);
   VP_TRY(tbl_wait_pub(c, t, epoch));
   if (nr) {

@@ -85,6 +85,41 @@ class NfBase:
         step.tensors = keep
         return step
 
+    def device_steps(self, frames_list, lens, in_dev, out, slot: int):
+        """The loop of device_step calls in C (host/steps.c,
+        libvp_steps.so): one vp_process_device per buffer of frames_list, in
+        order, as nf.c's loop makes one call per burst. Returns
+        f(now0s, now_step) that runs them all (now0s: each batch's first time
+        stamp). Measurement infrastructure: no interpreter between the
+        calls."""
+        import os
+        n = lens.numel()
+        port = isinstance(in_dev, int)
+        arr = (DevBatchC * len(frames_list))()
+        for k, fr in enumerate(frames_list):
+            assert fr.numel() == n * slot and fr.is_cuda
+            arr[k] = DevBatchC(frames=fr.data_ptr(), slot=slot, n=n, len=lens.data_ptr(),
+                               in_dev=None if port else in_dev.data_ptr(), now=None,
+                               now0=0, now_step=0, out_dev=out.data_ptr(),
+                               in_port=in_dev if port else 0)
+        S = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(self.L._name)),
+                                "libvp_steps.so"))
+        S.vp_steps_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int,
+                                      C.POINTER(C.c_int)]
+        keep = (list(frames_list), lens, in_dev, out)
+
+        def run(now0s, now_step: int):
+            assert len(now0s) == len(arr)
+            for k, t0 in enumerate(now0s):
+                arr[k].now0, arr[k].now_step = t0, now_step
+            done = C.c_int()
+            rc = S.vp_steps_device(self.h, C.cast(arr, C.c_void_p), len(arr),
+                                   C.byref(done))
+            if rc:
+                _check(rc, "vp_process_device (call %d)" % done.value, self.L)
+        run.tensors = keep
+        return run
+
     def sync_state(self):
         """Multi-GPU: merge the ranks' timestamps (collective)."""
         self._ck(self.L.vp_sync_state(self.h), "vp_sync_state")
