@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out; mkdir -p $O; export TMPDIR=/tmp
 for i in 1 2 3; do
   for v in new old; do
-    if [ $v = old ]; then export LD_LIBRARY_PATH=$PWD/build_ab; else unset LD_LIBRARY_PATH; fi
+    if [ $v = old ]; then export LD_LIBRARY_PATH=$PWD/build_ab/old; else unset LD_LIBRARY_PATH; fi
     timeout -k 10 300 python3 -c "
 import bench, json
 print(json.dumps(bench.per_packet_drop_in(batches=(0,))))" > $O/r06z_pp_${v}_$i.json 2> $O/r06z_pp_${v}_$i.err || { tail -20 $O/r06z_pp_${v}_$i.err; exit 1; }
