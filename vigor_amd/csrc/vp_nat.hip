@@ -1988,32 +1988,9 @@ __global__ void nat_defer_finish(NatArgs a, const uint32_t *list, uint32_t n) {
 // flow_manager_get_internal / allocate_flow (nat_main.c:68-97) for one LAN
 // key at global sequence seq: its index, allocated when new (*fresh = 1), and
 // stamped; kNone when the table is full (drop).
-// map_get for the server: the home bucket through the kernel's LDS copy of
-// the linear layout's byte tables (lin: nat_lin(T)), and each bucket's four
-// 16-byte words requested together (compiled from bucket_match alone, the
-// first key word's load waited behind the index word's: two HBM round trips
-// per bucket, in a path that is all latency).
-__device__ __forceinline__ uint32_t serve_probe(const TableDev &t, uint32_t hh,
-                                                const uint32_t key[4], const uint32_t *lin) {
-  uint32_t b = home_bucket(hh, t.bmask, t.mix, lin);
-  for (uint32_t i = 0; i <= t.bmask; i++) {
-    const uint4 *q = reinterpret_cast<const uint4 *>(t.bk + b);
-    uint4 k0 = q[0], k1 = q[1], k2 = q[2], ix = q[3];
-    asm volatile("" : "+v"(k0.x), "+v"(k0.y), "+v"(k0.z), "+v"(k0.w), "+v"(k1.x), "+v"(k1.y),
-                      "+v"(k1.z), "+v"(k1.w), "+v"(k2.x), "+v"(k2.y), "+v"(k2.z), "+v"(k2.w),
-                      "+v"(ix.x), "+v"(ix.y), "+v"(ix.z), "+v"(ix.w));
-    bool done;
-    const uint32_t r = bucket_match(k0, k1, k2, ix, key, &done);
-    if (done) return r;
-    b = (b + 1) & t.bmask;
-  }
-  return kNone;
-}
-
 __device__ __forceinline__ uint32_t one_lan(const TableDev &t, uint32_t hh, const uint32_t key[4],
-                                            int64_t now, uint64_t seq, uint32_t *fresh,
-                                            const uint32_t *lin) {
-  uint32_t idx = serve_probe(t, hh, key, lin);
+                                            int64_t now, uint64_t seq, uint32_t *fresh) {
+  uint32_t idx = tbl_probe(t, hh, key);
   if (idx == kNone) {  // dchain_allocate_new_index: the freed stack, then fresh
     Ctl *c = t.ctl;
     const uint32_t st = c->stack_top, fn = c->fresh_next;
@@ -2087,7 +2064,7 @@ __device__ __forceinline__ uint32_t nat_one(const NatArgs &a, const uint32_t *T,
   } else {
     const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
     const uint32_t idx = one_lan(a.t, flowid_hash(T, sp, dp, sip, dip, in, proto), key, now,
-                                 seq, fresh, nat_lin(T));
+                                 seq, fresh);
     if (idx == kNone) return in;
     one_stamp(a.t, idx, now, seq);
     f.w32(h.ip + 12, a.ext_ip);
@@ -2131,7 +2108,7 @@ __device__ __forceinline__ uint32_t nat_one_reg(const NatArgs &a, const uint32_t
     const uint32_t key[4] = {sp | (dp << 16), sip, dip, in | (proto << 16)};
     const uint32_t hh = flowid_hash_batched(T, sp, dp, sip, dip, in, proto);
     if (prof) mk0 = wall_clock64();
-    const uint32_t idx = one_lan(a.t, hh, key, now, seq, fresh, nat_lin(T));
+    const uint32_t idx = one_lan(a.t, hh, key, now, seq, fresh);
     if (prof) mk1 = wall_clock64();
     if (idx == kNone) return in;
     one_stamp(a.t, idx, now, seq);
