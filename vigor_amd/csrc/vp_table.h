@@ -66,6 +66,7 @@ struct PubArgs {
   uint32_t epoch;
   const uint32_t *x0, *x1;  // extra words (CtlPub::xtra): x0[0..n0), then x1[0..n1)
   uint32_t n0, n1;
+  uint32_t rel = 0;  // the epoch stored with a system-scope release (A/B)
 };
 static_assert(sizeof(Ctl) % 8 == 0, "Ctl is published as 8-byte words");
 __device__ __forceinline__ void ctl_publish(const PubArgs &a) {
@@ -86,7 +87,16 @@ __device__ __forceinline__ void ctl_publish(const PubArgs &a) {
                        __hip_atomic_load(s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  __hip_atomic_store(&a.pub->epoch, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  // The epoch after every word above has completed. Those are system-scope
+  // stores (past the GPU's caches), so waiting for them orders them; a
+  // release would also write the XCD's L2 back (buffer_wbl2), which the fold
+  // kernel could not end before (VIGPATH_PUB_RELEASE=1: that form, for A/B)
+  if (a.rel) {
+    __hip_atomic_store(&a.pub->epoch, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&a.pub->epoch, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 struct NowSpec {

@@ -1076,12 +1076,30 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
   // at a time whatever the slices' lengths.
   for (uint32_t r0 = threadIdx.x >> 6; r0 < nsrc; r0 += 64 * nw) {
     const uint32_t my = r0 + lane * nw;
-    const uint32_t raw = my < nsrc ? cnt[(size_t)bin * nsrc + my] : 0;
-    const uint32_t nv = raw & ~kBinRunFlags, nr = raw >> kBinRunShift;
-    // the slice's first two run words, loaded beside the count (one round
-    // trip; a word past the slice's count is stale and ignored)
+    // the slice's run words, all loaded beside its count (one round trip; a
+    // word past the slice's count is stale and ignored). Loaded one by one
+    // behind the first two, eight words of 1024-thread blocks cost the fold
+    // six more round trips (profiles/r06af_fold_runs.txt); both addresses
+    // first, so no load's address registers are reused while it is in
+    // flight (a wait for it, in the compiled order)
     const size_t ri = (((size_t)my << bbits) + bin) * rwords;
-    const uint32_t re = my < nsrc ? rtab[ri] : 0u, re2 = my < nsrc ? rtab[ri + 1] : 0u;
+    const uint32_t *cp = cnt + (size_t)bin * nsrc + my;
+    uint32_t rw[kBinRunWordsMax];
+    if (rwords == kBinRunWordsMax) {  // (32-byte aligned: ri is a multiple of 8)
+      const uint4 *q = reinterpret_cast<const uint4 *>(rtab + ri);
+      const uint4 x = my < nsrc ? q[0] : make_uint4(0, 0, 0, 0);
+      const uint4 y = my < nsrc ? q[1] : make_uint4(0, 0, 0, 0);
+      rw[0] = x.x, rw[1] = x.y, rw[2] = x.z, rw[3] = x.w;
+      rw[4] = y.x, rw[5] = y.y, rw[6] = y.z, rw[7] = y.w;
+    } else {
+      rw[0] = my < nsrc ? rtab[ri] : 0u;
+      rw[1] = my < nsrc ? rtab[ri + 1] : 0u;
+#pragma unroll
+      for (uint32_t j = 2; j < kBinRunWordsMax; j++) rw[j] = 0;
+    }
+    const uint32_t raw = my < nsrc ? *cp : 0;
+    const uint32_t nv = raw & ~kBinRunFlags, nr = raw >> kBinRunShift;
+    const uint32_t re = rw[0], re2 = rw[1];
     const bool run = nr > 0, run2 = nr > 1;
     const uint32_t ch = (nv + 63) >> 6;
     uint32_t inc = ch;  // inclusive prefix over the wave
@@ -1114,13 +1132,11 @@ __global__ __launch_bounds__(1024) void touch_bins_reduce(
       atomicMax(&grp[(re >> 20) - (lo >> kBinRunBits)], my * range + 1 + (re & 0xFFFFFu));
     if (run2 && ((re2 >> 20) << kBinRunBits) - lo < Lp)
       atomicMax(&grp[(re2 >> 20) - (lo >> kBinRunBits)], my * range + 1 + (re2 & 0xFFFFFu));
-    for (uint32_t j = 2; j < rwords; j++) {  // (1024-thread classify blocks)
-      if (__ballot(j < nr) == 0) break;
-      if (j < nr) {
-        const uint32_t rj = rtab[ri + j];
-        if (((rj >> 20) << kBinRunBits) - lo < Lp)
-          atomicMax(&grp[(rj >> 20) - (lo >> kBinRunBits)], my * range + 1 + (rj & 0xFFFFFu));
-      }
+#pragma unroll
+    for (uint32_t j = 2; j < kBinRunWordsMax; j++) {  // (1024-thread classify blocks)
+      const uint32_t rj = rw[j];
+      if (j < rwords && j < nr && ((rj >> 20) << kBinRunBits) - lo < Lp)
+        atomicMax(&grp[(rj >> 20) - (lo >> kBinRunBits)], my * range + 1 + (rj & 0xFFFFFu));
     }
   }
   __syncthreads();
@@ -1233,6 +1249,11 @@ int tbl_bins_plan(vp_ctx *c, FlowTable &t, const void *kernel, uint32_t p0,
 
 static int bins_reduce(vp_ctx *c, FlowTable &t, const BinsPlan &plan, uint32_t p0,
                        const NowSpec &now, uint64_t seq_base, PubArgs pub) {
+  static const uint32_t rel = [] {  // (VIGPATH_PUB_RELEASE=1: ctl_publish's release form)
+    const char *e = getenv("VIGPATH_PUB_RELEASE");
+    return e && atoi(e) ? 1u : 0u;
+  }();
+  pub.rel = rel;
   // chunks in flight per fold wave (VIGPATH_FOLD_U: 8, 16 or 32; 16 and 32
   // measured no faster than 8, r03k)
   static const uint32_t fold_u = [] {
