@@ -2135,7 +2135,8 @@ __device__ __forceinline__ uint32_t nat_one_reg(const NatArgs &a, const uint32_t
 // without a request; a request posted as it leaves finds the stream idle and
 // the host launches it again (nat_process_one). flags: bit 0, the stage
 // clock (VIGPATH_SERVE_PROF); bits 3-9: the waves' stagger in wall-clock
-// ticks; bits 10-17: the first poll's delay after an answer; bit 18: adapt it.
+// ticks; bits 10-17: the first poll's delay after an answer; bit 18: adapt it;
+// bits 19-23: the ticks a late poll adds to it.
 __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint64_t seq0,
                                                  uint64_t idle, uint32_t flags) {
   __shared__ uint32_t T[kNatTabWords];
@@ -2312,6 +2313,7 @@ __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint6
   // costs a round trip, an early one only its excess -- so it settles just
   // past where the caller's requests land, whatever the caller's loop.
   uint32_t after = (flags >> 10) & 0xFFu;
+  const uint32_t up = (flags >> 19) & 0x1Fu;  // ticks added after a late poll
   const bool adapt = (flags >> 18) & 1u;
   uint32_t polls = 0;  // polls since the last answer
   for (;;) {
@@ -2327,7 +2329,7 @@ __global__ __launch_bounds__(256) void nat_serve(NatArgs a, ServeBox *box, uint6
       continue;
     }
     if (adapt && polls == 1 && after > 0) after--;
-    if (adapt && polls > 1 && polls < 64) after = min(after + 8u, 200u);
+    if (adapt && polls > 1 && polls < 64) after = min(after + up, 200u);
     polls = 0;
     if (after) {
       const uint64_t w = wall_clock64();
@@ -3230,13 +3232,17 @@ static int serve_launch(vp_ctx *c) {
     // nf.c's loop, profiles/r06o_serve_after.txt, r06p_serve_after_sweep.txt)
     return e ? (uint32_t)std::min(255, std::max(0, atoi(e))) : 45u;
   }();
+  static const uint32_t up = [] {  // (VIGPATH_SERVE_UP: ticks added after a late poll)
+    const char *e = getenv("VIGPATH_SERVE_UP");
+    return e ? (uint32_t)std::min(31, std::max(1, atoi(e))) : 8u;
+  }();
   static const uint32_t adapt = [] {  // VIGPATH_SERVE_ADAPT=0: a fixed delay
     const char *e = getenv("VIGPATH_SERVE_ADAPT");
     return e && !atoi(e) ? 0u : 1u;
   }();
   nat_serve<<<1, 64 * waves, 0, c->stream>>>(a, dbox, c->seq, c->srv_idle,
                                              (g_srv_prof ? 1u : 0u) | (gap << 3) |
-                                                 (after << 10) | (adapt << 18));
+                                                 (after << 10) | (adapt << 18) | (up << 19));
   VP_HIP(hipGetLastError());
   if (!c->srv_on) {
     static std::once_flag once;
@@ -3263,6 +3269,7 @@ int nat_process_one(vp_ctx *c, uint16_t in_dev, uint8_t *frame, uint16_t len, in
     VP_TRY(serve_stop(c));
     return 1;
   }
+  if (!c->sbox || !c->srv_on) VP_HIP(hipSetDevice(c->gpu));  // (HIP calls below)
   if (!c->sbox) {
     VP_HIP(hipHostMalloc((void **)&c->sbox, sizeof(ServeBox),
                          hipHostMallocCoherent | hipHostMallocMapped));
@@ -3315,6 +3322,7 @@ int nat_process_one(vp_ctx *c, uint16_t in_dev, uint8_t *frame, uint16_t len, in
     if (nw - last < std::chrono::microseconds(200)) continue;
     last = nw;
     // the kernel left (idle) before it saw the request: launch it again
+    VP_HIP(hipSetDevice(c->gpu));
     const hipError_t q = hipStreamQuery(c->stream);
     if (q == hipErrorNotReady) continue;
     VP_HIP(q);

@@ -758,9 +758,11 @@ int vp_process_one(vp_ctx *c, uint16_t in_dev, uint8_t *frame, uint16_t len, int
                    uint16_t *out_dev) {
   if (!c || !frame || !out_dev) return VP_EINVAL;
   if (c->kind == KIND_NAT) {
-    if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
+    // (no hipSetDevice here: a served packet makes no HIP call; the server's
+    // launch and stop set the device themselves)
     const int rc = nat_process_one(c, in_dev, frame, len, now, out_dev);
     if (rc <= 0) return rc;  // (1: not eligible, the batch path below)
+    if (hipSetDevice(c->gpu) != hipSuccess) return VP_EIO;
   }
   uint8_t *frames[1] = {frame};
   return vp_process_batch(c, 1, &in_dev, frames, &len, &now, out_dev);
