@@ -3316,8 +3316,10 @@ int nat_process_one(vp_ctx *c, uint16_t in_dev, uint8_t *frame, uint16_t len, in
       if (__atomic_load_n(&bx->amsg[k][3], __ATOMIC_ACQUIRE) != req) return false;
     return true;
   };
+  uint32_t spins = 0;
   while (!answered()) {
     __builtin_ia32_pause();
+    if (++spins & 255) continue;  // (the clock read every 256 spins, not each)
     const auto nw = std::chrono::steady_clock::now();
     if (nw - last < std::chrono::microseconds(200)) continue;
     last = nw;
