@@ -146,6 +146,37 @@ def test_gpu_reproduces_bench_shape():
     assert nat.live_count() == int(g["live"])
 
 
+@pytest.mark.gpu
+def test_c_step_loop_reproduces_bench_shape():
+    """The same batches through bench.py's timed loop in C (host/steps.c,
+    Nat.device_steps: one vp_process_device per batch with no interpreter
+    between them): the last batch's bytes and the table state equal the
+    reference's, as through one call at a time."""
+    import torch
+    g = _bench_golden()
+    nat = G.nat_gpu(G.BENCH_FLOWS)
+    d = torch.device("cuda:0")
+    B = G.BENCH_BATCH
+    lens = torch.full((B,), 60, dtype=torch.int16, device=d)
+    ind = torch.zeros(B, dtype=torch.int16, device=d)
+    out = torch.zeros(B, dtype=torch.int16, device=d)
+    bufs = []
+    for k in range(G.BENCH_BATCHES):
+        fr, _, _, _ = T.nat_lan_trace(B, G.BENCH_FLOWS, start=k * B)
+        bufs.append(torch.from_numpy(fr).to(d))
+        del fr
+    run = nat.device_steps(bufs, lens, ind, out, 64)
+    run([T.NOW0 + k * B for k in range(G.BENCH_BATCHES)], 1)
+    torch.cuda.synchronize()
+    k = G.BENCH_BATCHES - 1
+    dig = T.batch_digest(bufs[k].cpu().numpy(), out.cpu().numpy().view(np.uint16), 64)
+    assert dig == int(g["batch_digest"][k]), "batch %d digest" % k
+    del bufs
+    alloc, ts, _ = nat.dump()
+    assert T.state_digest(alloc, ts) == int(g["state_digest"])
+    assert nat.live_count() == int(g["live"])
+
+
 # ---- BASELINE configs[4] table size (16M flows) ---------------------------
 
 def _16m_golden():
