@@ -817,6 +817,8 @@ def kernel_label(knames, default):
 def probe_waves(kernel: str) -> int:
     """Waves per block of the tile kernel's grid (vp_probe_slots_w)."""
     k = kernel.split(" ")[0]
+    if k.startswith("nat_classify64h"):
+        return 8
     return 16 if k.startswith("nat_classify64w") or k.endswith("64w") else 4
 
 

@@ -1255,6 +1255,12 @@ __global__ __launch_bounds__(1024, 1) void nat_classify64ws(NatArgs a, uint32_t 
                                                            TouchBins bins, TileQueue rq) {
   nat_tiles<0, 1, false, false, true, 16, true, false>(a, n_all, bins, rq);
 }
+// Two 512-thread blocks per CU (VIGPATH_TILE_WAVES=8, for A/B): between the
+// 256-thread shape's faster bare pass and the 1024-thread kernel
+__global__ __launch_bounds__(512, 4) void nat_classify64h(NatArgs a, uint32_t n_all,
+                                                         TouchBins bins, TileQueue rq) {
+  nat_tiles<0, 1, false, false, true, 8, false, false>(a, n_all, bins, rq);
+}
 // owner mode's pass 1 on the 1024-thread tile (nat_phase_a_owner)
 __global__ __launch_bounds__(1024, 1) void nat_classify64wo(NatArgs a, uint32_t n_all,
                                                            TouchBins bins, TileQueue rq) {
@@ -1309,8 +1315,17 @@ static uint32_t nat_block_waves() {
   return w;
 }
 
+static uint32_t nat_tile_waves_env() {
+  static const uint32_t w = [] {
+    const char *e = getenv("VIGPATH_TILE_WAVES");
+    return e && atoi(e) == 8 ? 8u : 16u;
+  }();
+  return w;
+}
+
 static const char *nat_tile_kernel_name(NatTileKernel k) {
   return k == nat_classify64w    ? "nat_classify64w"
+         : k == nat_classify64h  ? "nat_classify64h"
          : k == nat_classify64ws ? "nat_classify64ws"
          : k == nat_classify64   ? "nat_classify64"
          : k == nat_classify64x  ? "nat_classify64x"
@@ -1320,7 +1335,7 @@ static const char *nat_tile_kernel_name(NatTileKernel k) {
 }
 
 static uint32_t nat_tile_waves(NatTileKernel k) {
-  return k == nat_classify64w || k == nat_classify64ws ? 16u : 4u;
+  return k == nat_classify64w || k == nat_classify64ws ? 16u : k == nat_classify64h ? 8u : 4u;
 }
 
 static NatTileKernel nat_tile_kernel(uint32_t slot, bool hdr_tail = false,
@@ -1330,7 +1345,7 @@ static NatTileKernel nat_tile_kernel(uint32_t slot, bool hdr_tail = false,
     return e && atoi(e) == 0;
   }();
   if (slot == 64 && !hdr_tail && nat_block_waves() == 16)
-    return staged ? nat_classify64ws : nat_classify64w;
+    return staged ? nat_classify64ws : nat_tile_waves_env() == 8 ? nat_classify64h : nat_classify64w;
   if (slot == 64) return hdr_tail ? nat_classify64x : p0 ? nat_classify64_p0 : nat_classify64;
   if (slot == 128) return nat_classify128;
   const uint32_t nch = (slot - 64) / 16;
