@@ -819,6 +819,8 @@ def probe_waves(kernel: str) -> int:
     k = kernel.split(" ")[0]
     if k.startswith("nat_classify64h"):
         return 8
+    if k.startswith("nat_classify64q"):
+        return 4
     return 16 if k.startswith("nat_classify64w") or k.endswith("64w") else 4
 
 

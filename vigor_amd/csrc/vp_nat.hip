@@ -1261,6 +1261,12 @@ __global__ __launch_bounds__(512, 4) void nat_classify64h(NatArgs a, uint32_t n_
                                                          TouchBins bins, TileQueue rq) {
   nat_tiles<0, 1, false, false, true, 8, false, false>(a, n_all, bins, rq);
 }
+// Four 256-thread blocks per CU with the owner paths compiled out
+// (VIGPATH_TILE_WAVES=4, for A/B; nat_classify64 keeps them)
+__global__ __launch_bounds__(256, 4) void nat_classify64q(NatArgs a, uint32_t n_all,
+                                                         TouchBins bins, TileQueue rq) {
+  nat_tiles<0, 1, false, false, true, 4, false, false>(a, n_all, bins, rq);
+}
 // owner mode's pass 1 on the 1024-thread tile (nat_phase_a_owner)
 __global__ __launch_bounds__(1024, 1) void nat_classify64wo(NatArgs a, uint32_t n_all,
                                                            TouchBins bins, TileQueue rq) {
@@ -1318,7 +1324,8 @@ static uint32_t nat_block_waves() {
 static uint32_t nat_tile_waves_env() {
   static const uint32_t w = [] {
     const char *e = getenv("VIGPATH_TILE_WAVES");
-    return e && atoi(e) == 8 ? 8u : 16u;
+    const int v = e ? atoi(e) : 16;
+    return v == 8 || v == 4 ? (uint32_t)v : 16u;
   }();
   return w;
 }
@@ -1326,6 +1333,7 @@ static uint32_t nat_tile_waves_env() {
 static const char *nat_tile_kernel_name(NatTileKernel k) {
   return k == nat_classify64w    ? "nat_classify64w"
          : k == nat_classify64h  ? "nat_classify64h"
+         : k == nat_classify64q  ? "nat_classify64q"
          : k == nat_classify64ws ? "nat_classify64ws"
          : k == nat_classify64   ? "nat_classify64"
          : k == nat_classify64x  ? "nat_classify64x"
@@ -1335,7 +1343,7 @@ static const char *nat_tile_kernel_name(NatTileKernel k) {
 }
 
 static uint32_t nat_tile_waves(NatTileKernel k) {
-  return k == nat_classify64w || k == nat_classify64ws ? 16u : k == nat_classify64h ? 8u : 4u;
+  return k == nat_classify64w || k == nat_classify64ws ? 16u : k == nat_classify64h ? 8u : 4u;  // (64q: 4)
 }
 
 static NatTileKernel nat_tile_kernel(uint32_t slot, bool hdr_tail = false,
@@ -1345,7 +1353,10 @@ static NatTileKernel nat_tile_kernel(uint32_t slot, bool hdr_tail = false,
     return e && atoi(e) == 0;
   }();
   if (slot == 64 && !hdr_tail && nat_block_waves() == 16)
-    return staged ? nat_classify64ws : nat_tile_waves_env() == 8 ? nat_classify64h : nat_classify64w;
+    return staged ? nat_classify64ws
+           : nat_tile_waves_env() == 8 ? nat_classify64h
+           : nat_tile_waves_env() == 4 ? nat_classify64q
+                                       : nat_classify64w;
   if (slot == 64) return hdr_tail ? nat_classify64x : p0 ? nat_classify64_p0 : nat_classify64;
   if (slot == 128) return nat_classify128;
   const uint32_t nch = (slot - 64) / 16;
