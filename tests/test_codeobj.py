@@ -33,6 +33,7 @@ NO_SCRATCH = ["bridge_classify", "lb_classify64", "fw_classify64", "pol_classify
 # registers one phase longer once cost 200 bytes and 60 % of the kernel
 # (round 3)
 SMALL_SPILLS = {"nat_classify64": 32, "nat_classify64w": 16, "nat_classify64ws": 24,
+                "nat_classify64h": 16, "nat_classify64q": 16,
                 "nat_classify64wo": 32,
                 "nat_classify128": 32,
                 "nat_classify64x": 32}
