@@ -62,7 +62,7 @@ SLOT = 64
 # VIGPATH_BENCH_PYLOOP=1: the headline's calls from Python, one ctypes call a
 # step (A/B against the C loop, host/steps.c)
 PY_LOOP = os.environ.get("VIGPATH_BENCH_PYLOOP") == "1"
-TRAFFIC_PROFILE = "r06ah_bench_traffic.json"  # rocprofv3 --pmc passes (tools/gpu_session.sh pmc)
+TRAFFIC_PROFILE = "r06ao_bench_traffic.json"  # rocprofv3 --pmc passes (tools/gpu_session.sh pmc)
 DEV_MACS = [T.mac("02:00:00:00:00:00"), T.mac("02:00:00:00:00:01")]
 NAT_ARGS = ["--expire", "60000000", "--starting-port", "0", "--wan", "1",
             "--extip", "192.168.4.2", "--eth-dest", "0,90:e2:ba:55:12:20",
